@@ -1,0 +1,96 @@
+"""ctypes / numpy mirror of include/mtr_types.h (the packed, pointer-free batch format)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+OP_INSERT = 0
+OP_REMOVE = 1
+OP_ANNOTATE = 2
+OP_SEQ = 3
+OP_LOCAL_INSERT = 8
+OP_LOCAL_REMOVE = 9
+OP_LOCAL_ANNOTATE = 10
+OP_START_COLLAB = 12
+
+F_LAST = 1
+F_MARKER = 2
+F_PROPS = 4
+F_NOREF = 8
+
+NULL_VALUE = 0xFFFFFFFF
+NOT_INDEX = 0xFFFFFFFF
+
+MTR_OK = 0
+MTR_ERR_INSERT_FAILED = 1
+MTR_ERR_BAD_OP = 2
+MTR_ERR_CAPACITY = 3
+MTR_ERR_UNSUPPORTED = 4
+MTR_ERR_ASSERT = 0x1000
+
+OP_DTYPE = np.dtype(
+    [
+        ("type", "u1"),
+        ("flags", "u1"),
+        ("client", "<u2"),
+        ("seq", "<i4"),
+        ("ref_seq", "<i4"),
+        ("min_seq", "<i4"),
+        ("pos1", "<i4"),
+        ("pos2", "<i4"),
+        ("payload", "<u4"),
+        ("payload2", "<u4"),
+    ]
+)
+assert OP_DTYPE.itemsize == 32
+
+DOC_DTYPE = np.dtype(
+    [
+        ("op_begin", "<u8"),
+        ("text_base", "<u8"),
+        ("op_count", "<u4"),
+        ("text_count", "<u4"),
+        ("client_base", "<u4"),
+        ("n_clients", "<u4"),
+    ]
+)
+assert DOC_DTYPE.itemsize == 32
+
+
+class MtrOptions(C.Structure):
+    _fields_ = [
+        ("new_length_calc", C.c_int32),
+        ("snapshot_v1", C.c_int32),
+        ("chunk_size", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+class MtrBatch(C.Structure):
+    _fields_ = [
+        ("n_docs", C.c_uint32),
+        ("n_propops", C.c_uint32),
+        ("n_keys", C.c_uint32),
+        ("n_vals", C.c_uint32),
+        ("n_ops", C.c_uint64),
+        ("n_text", C.c_uint64),
+        ("docs", C.c_void_p),
+        ("ops", C.c_void_p),
+        ("text", C.c_void_p),
+        ("propop_off", C.c_void_p),
+        ("propop_kv", C.c_void_p),
+        ("key_off", C.c_void_p),
+        ("key_bytes", C.c_void_p),
+        ("key_index", C.c_void_p),
+        ("val_off", C.c_void_p),
+        ("val_bytes", C.c_void_p),
+        ("val_eq", C.c_void_p),
+        ("client_off", C.c_void_p),
+        ("client_bytes", C.c_void_p),
+    ]
+
+
+def ptr(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data if a.size else 0

@@ -1,0 +1,306 @@
+"""Host-side packing of ISequencedDocumentMessage streams into the engine's batch format.
+
+This is the code a scribe-like summarizer runs before handing a batch to the engine; it mirrors the
+message handling the reference does on the JS thread:
+
+* ``Client.applyMsg`` registers ``msg.clientId`` (first-seen short ids, client.ts:858-860, 673-688),
+  routes ``type == "op"`` to ``applyRemoteOp`` (client.ts:802-829) and always finishes with
+  ``updateSeqNumbers(msn, seq)`` (client.ts:874-887).
+* ``specToSegment`` (packages/dds/sequence/src/sequenceFactory.ts:26-38) accepts a string, a
+  ``{text, props}`` object or a ``{marker: {refType}, props}`` object.
+* GROUP ops (ops.ts:113) become several records with one sequence number.
+
+Property keys/values are interned into global tables (see include/mtr_types.h).  Features outside
+the observer path (relative positions, combining ops, messages authored by the observer itself) make
+the document ``unsupported`` (the reference-side shim keeps such documents on the TypeScript Client).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Any, Iterable
+
+import numpy as np
+
+from . import abi
+from .jsjson import array_index, eq_key, js_key_order, js_string, js_stringify, parse, to_utf8
+
+
+class Unsupported(Exception):
+    """A message uses a feature the engine does not implement (document must fall back)."""
+
+
+class Interner:
+    """Global key / value / prop-op tables (ids are stable across batches)."""
+
+    def __init__(self) -> None:
+        self.keys: dict[str, int] = {}
+        self.key_bytes: list[bytes] = []
+        self.key_index: list[int] = []
+        self.vals: dict[str, int] = {}
+        self.val_bytes: list[bytes] = []
+        self.val_eq: list[int] = []
+        self.eq_ids: dict[str, int] = {}
+        self.propops: list[list[tuple[int, int]]] = []
+
+    def key(self, k: str) -> int:
+        i = self.keys.get(k)
+        if i is None:
+            i = len(self.key_bytes)
+            self.keys[k] = i
+            self.key_bytes.append(to_utf8(js_string(k)[1:-1]))
+            ix = array_index(k)
+            self.key_index.append(abi.NOT_INDEX if ix is None else ix)
+        return i
+
+    def value(self, v: Any) -> int:
+        if v is None:
+            return abi.NULL_VALUE
+        s = js_stringify(v)
+        i = self.vals.get(s)
+        if i is None:
+            i = len(self.val_bytes)
+            self.vals[s] = i
+            self.val_bytes.append(to_utf8(s))
+            ek = eq_key(v)
+            e = self.eq_ids.setdefault(ek, len(self.eq_ids))
+            self.val_eq.append(e)
+        return i
+
+    def propop(self, props: dict) -> int:
+        pairs = [(self.key(k), self.value(props[k])) for k in js_key_order(props.keys())]
+        self.propops.append(pairs)
+        return len(self.propops) - 1
+
+
+@dataclass
+class DocLog:
+    """Per-document host state: client registry plus the ops/text of the batch being built."""
+
+    observer_id: str | None = None
+    clients: list[str] = field(default_factory=list)
+    client_ix: dict[str, int] = field(default_factory=dict)
+    ops: list[tuple] = field(default_factory=list)
+    text: list[int] = field(default_factory=list)
+    unsupported: str | None = None
+    collaborating: bool = False
+
+    def short_id(self, long_id: str) -> int:
+        i = self.client_ix.get(long_id)
+        if i is None:
+            i = len(self.clients)
+            self.client_ix[long_id] = i
+            self.clients.append(long_id)
+        return i
+
+    def _text(self, s: str) -> tuple[int, int]:
+        u = np.frombuffer(s.encode("utf-16-le", "surrogatepass"), dtype="<u2")
+        off = len(self.text)
+        self.text.extend(u.tolist())
+        return off, len(u)
+
+    def _seg(self, spec: Any, interner: Interner) -> tuple[int, int, int, int]:
+        """-> (flags, payload, payload2, propop)"""
+        if isinstance(spec, str):
+            off, n = self._text(spec)
+            return 0, off, n, -1
+        if isinstance(spec, dict) and "text" in spec:
+            off, n = self._text(spec["text"])
+            props = spec.get("props")
+            if props is not None:  # `if (props)` in TextSegment.make: {} is truthy
+                return abi.F_PROPS, off, n, interner.propop(props)
+            return 0, off, n, -1
+        if isinstance(spec, dict) and "marker" in spec:
+            m = spec["marker"] or {}
+            flags = abi.F_MARKER
+            ref = m.get("refType")
+            if ref is None:
+                flags |= abi.F_NOREF
+                ref = 0
+            props = spec.get("props")
+            pp = -1
+            if props is not None:
+                flags |= abi.F_PROPS
+                pp = interner.propop(props)
+            return flags, int(ref), 0, pp
+        raise Unsupported("unrecognized segment spec")
+
+    # -- non-collaborating local edits (pre-attach SharedString / TestClient.insertTextLocal)
+    def local_insert(self, pos: int, spec: Any, interner: Interner) -> None:
+        flags, p1, p2, pp = self._seg(spec, interner)
+        self.ops.append((abi.OP_LOCAL_INSERT, flags, 0, 0, 0, 0, pos, pp, p1, p2))
+
+    def local_remove(self, start: int, end: int) -> None:
+        self.ops.append((abi.OP_LOCAL_REMOVE, 0, 0, 0, 0, 0, start, end, 0, 0))
+
+    def local_annotate(self, start: int, end: int, props: dict, interner: Interner) -> None:
+        self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, 0, 0, 0, start, end, interner.propop(props), 0))
+
+    def start_collab(self, long_id: str, min_seq: int = 0, current_seq: int = 0) -> None:
+        """Client.startOrUpdateCollaboration (client.ts:1133-1155)."""
+        if self.observer_id is None:
+            self.observer_id = long_id
+            self.short_id(long_id)
+            self.collaborating = True
+            self.ops.append((abi.OP_START_COLLAB, 0, 0, current_seq, 0, min_seq, 0, 0, 0, 0))
+
+    # -- sequenced messages (Client.applyMsg)
+    def message(self, msg: dict, interner: Interner) -> None:
+        cid = msg.get("clientId")
+        cid = "null" if cid is None else str(cid)
+        short = self.short_id(cid)
+        seq = int(msg["sequenceNumber"])
+        ref = int(msg["referenceSequenceNumber"])
+        msn = int(msg["minimumSequenceNumber"])
+        if msg.get("type") != "op":
+            self.ops.append((abi.OP_SEQ, abi.F_LAST, short, seq, ref, msn, 0, 0, 0, 0))
+            return
+        if cid == self.observer_id:
+            raise Unsupported("message authored by the observer (local ack path)")
+        contents = msg["contents"]
+        if isinstance(contents, str):
+            contents = parse(contents)
+        members = contents["ops"] if contents.get("type") == 3 else [contents]
+        if not members:
+            self.ops.append((abi.OP_SEQ, abi.F_LAST, short, seq, ref, msn, 0, 0, 0, 0))
+            return
+        for i, op in enumerate(members):
+            last = abi.F_LAST if i == len(members) - 1 else 0
+            t = op.get("type")
+            if "relativePos1" in op or "relativePos2" in op:
+                raise Unsupported("relative positions")
+            if t == 0:
+                seg = op.get("seg")
+                if seg is None:
+                    # applyInsertOp returns early; only updateSeqNumbers runs
+                    self.ops.append((abi.OP_SEQ, last, short, seq, ref, msn, 0, 0, 0, 0))
+                    continue
+                flags, p1, p2, pp = self._seg(seg, interner)
+                self.ops.append((abi.OP_INSERT, flags | last, short, seq, ref, msn, int(op["pos1"]), pp, p1, p2))
+            elif t == 1:
+                self.ops.append(
+                    (abi.OP_REMOVE, last, short, seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0)
+                )
+            elif t == 2:
+                if op.get("combiningOp") is not None:
+                    raise Unsupported("combining ops")
+                pp = interner.propop(op["props"])
+                self.ops.append(
+                    (abi.OP_ANNOTATE, last, short, seq, ref, msn, int(op["pos1"]), int(op["pos2"]), pp, 0)
+                )
+            else:
+                raise Unsupported(f"op type {t}")
+
+
+class Batch:
+    """Numpy-backed arrays + the ctypes MtrBatch view of them (keeps the arrays alive)."""
+
+    def __init__(self, docs, ops, text, propop_off, propop_kv, key_off, key_bytes, key_index,
+                 val_off, val_bytes, val_eq, client_off, client_bytes):
+        self.docs = np.ascontiguousarray(docs, dtype=abi.DOC_DTYPE)
+        self.ops = np.ascontiguousarray(ops, dtype=abi.OP_DTYPE)
+        self.text = np.ascontiguousarray(text, dtype="<u2")
+        self.propop_off = np.ascontiguousarray(propop_off, dtype="<u4")
+        self.propop_kv = np.ascontiguousarray(propop_kv, dtype="<u4")
+        self.key_off = np.ascontiguousarray(key_off, dtype="<u4")
+        self.key_bytes = np.ascontiguousarray(key_bytes, dtype="u1")
+        self.key_index = np.ascontiguousarray(key_index, dtype="<u4")
+        self.val_off = np.ascontiguousarray(val_off, dtype="<u4")
+        self.val_bytes = np.ascontiguousarray(val_bytes, dtype="u1")
+        self.val_eq = np.ascontiguousarray(val_eq, dtype="<u4")
+        self.client_off = np.ascontiguousarray(client_off, dtype="<u4")
+        self.client_bytes = np.ascontiguousarray(client_bytes, dtype="u1")
+        # keep a non-empty allocation behind every pointer
+        for name in ("text", "propop_kv", "key_bytes", "key_index", "val_bytes", "val_eq", "client_bytes"):
+            a = getattr(self, name)
+            if a.size == 0:
+                setattr(self, name, np.zeros(1, dtype=a.dtype))
+        self.c = abi.MtrBatch(
+            n_docs=len(self.docs),
+            n_propops=len(self.propop_off) - 1,
+            n_keys=len(self.key_off) - 1,
+            n_vals=len(self.val_off) - 1,
+            n_ops=len(self.ops),
+            n_text=len(self.text),
+            docs=abi.ptr(self.docs),
+            ops=abi.ptr(self.ops),
+            text=abi.ptr(self.text),
+            propop_off=abi.ptr(self.propop_off),
+            propop_kv=abi.ptr(self.propop_kv),
+            key_off=abi.ptr(self.key_off),
+            key_bytes=abi.ptr(self.key_bytes),
+            key_index=abi.ptr(self.key_index),
+            val_off=abi.ptr(self.val_off),
+            val_bytes=abi.ptr(self.val_bytes),
+            val_eq=abi.ptr(self.val_eq),
+            client_off=abi.ptr(self.client_off),
+            client_bytes=abi.ptr(self.client_bytes),
+        )
+
+    @property
+    def ref(self):
+        return C.byref(self.c)
+
+    @property
+    def n_docs(self) -> int:
+        return len(self.docs)
+
+
+def _offsets(chunks: Iterable[bytes]) -> tuple[np.ndarray, np.ndarray]:
+    chunks = list(chunks)
+    off = np.zeros(len(chunks) + 1, dtype="<u4")
+    if chunks:
+        off[1:] = np.cumsum([len(c) for c in chunks])
+    data = np.frombuffer(b"".join(chunks), dtype="u1").copy() if chunks else np.zeros(0, "u1")
+    return off, data
+
+
+def build_batch(logs: list[DocLog], interner: Interner) -> Batch:
+    """Pack the pending ops of every DocLog (in order) into one Batch and clear them."""
+    docs = np.zeros(len(logs), dtype=abi.DOC_DTYPE)
+    all_ops = []
+    all_text = []
+    client_chunks: list[bytes] = []
+    op_n = 0
+    text_n = 0
+    for d, log in enumerate(logs):
+        docs[d]["op_begin"] = op_n
+        docs[d]["op_count"] = len(log.ops)
+        docs[d]["text_base"] = text_n
+        docs[d]["text_count"] = len(log.text)
+        docs[d]["client_base"] = len(client_chunks)
+        docs[d]["n_clients"] = len(log.clients)
+        for c in log.clients:
+            client_chunks.append(to_utf8(js_string(c)[1:-1]))
+        all_ops.extend(log.ops)
+        all_text.extend(log.text)
+        op_n += len(log.ops)
+        text_n += len(log.text)
+        log.ops = []
+        log.text = []
+    ops = np.array(all_ops, dtype=abi.OP_DTYPE) if all_ops else np.zeros(0, abi.OP_DTYPE)
+    text = np.array(all_text, dtype="<u2")
+    po = np.zeros(len(interner.propops) + 1, dtype="<u4")
+    kv = []
+    for i, pairs in enumerate(interner.propops):
+        po[i + 1] = po[i] + len(pairs)
+        for k, v in pairs:
+            kv.extend((k, v))
+    key_off, key_bytes = _offsets(interner.key_bytes)
+    val_off, val_bytes = _offsets(interner.val_bytes)
+    client_off, client_bytes = _offsets(client_chunks)
+    return Batch(
+        docs,
+        ops,
+        text,
+        po,
+        np.array(kv, dtype="<u4"),
+        key_off,
+        key_bytes,
+        np.array(interner.key_index, dtype="<u4"),
+        val_off,
+        val_bytes,
+        np.array(interner.val_eq, dtype="<u4"),
+        client_off,
+        client_bytes,
+    )

@@ -1,0 +1,126 @@
+/*
+ * mtr_types.h -- packed, pointer-free input format shared by the HIP engine
+ * (fluidframework_amd/csrc) and the CPU oracle (oracle/).
+ *
+ * One mtr_op is one *member op* of an ISequencedDocumentMessage
+ * (common/lib/protocol-definitions/src/protocol.ts:212).  A message whose
+ * contents is a GROUP op (packages/dds/merge-tree/src/ops.ts:113) becomes
+ * several mtr_op records with the same seq; only the last one carries
+ * MTR_F_LAST, which triggers Client.updateSeqNumbers(msn, seq)
+ * (packages/dds/merge-tree/src/client.ts:858-887).  A message of any other
+ * type (join/leave/noop) becomes one MTR_OP_SEQ record.
+ *
+ * Plain C, fixed-width fields, no torch or STL types.
+ */
+#ifndef MTR_TYPES_H
+#define MTR_TYPES_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* op.type -- MergeTreeDeltaType (ops.ts:43-48) plus engine-only records */
+enum {
+    MTR_OP_INSERT = 0,          /* remote insert  (client.ts:489)  */
+    MTR_OP_REMOVE = 1,          /* remote remove  (client.ts:430)  */
+    MTR_OP_ANNOTATE = 2,        /* remote annotate(client.ts:457)  */
+    MTR_OP_SEQ = 3,             /* non-"op" message: updateSeqNumbers only */
+    MTR_OP_LOCAL_INSERT = 8,    /* non-collaborating local insert (client.ts:237, seq=0, client=-1) */
+    MTR_OP_LOCAL_REMOVE = 9,    /* non-collaborating local remove */
+    MTR_OP_LOCAL_ANNOTATE = 10, /* non-collaborating local annotate */
+    MTR_OP_START_COLLAB = 12    /* Client.startOrUpdateCollaboration (client.ts:1133): seq/min_seq = currentSeq/minSeq */
+};
+
+/* op.flags */
+enum {
+    MTR_F_LAST = 1,    /* last member op of its message: run updateSeqNumbers(min_seq, seq) after it */
+    MTR_F_MARKER = 2,  /* insert of a Marker segment (mergeTreeNodes.ts:557); payload = refType */
+    MTR_F_PROPS = 4,   /* insert carries initial props: pos2 = prop-op index */
+    MTR_F_NOREF = 8    /* marker has no refType member ({"marker":{}}) */
+};
+
+typedef struct mtr_op {
+    uint8_t  type;     /* MTR_OP_* */
+    uint8_t  flags;    /* MTR_F_* */
+    uint16_t client;   /* short client id (client.ts:673-688); 0 = the observer itself */
+    int32_t  seq;      /* sequenceNumber */
+    int32_t  ref_seq;  /* referenceSequenceNumber */
+    int32_t  min_seq;  /* minimumSequenceNumber */
+    int32_t  pos1;     /* op.pos1 */
+    int32_t  pos2;     /* remove/annotate: op.pos2; insert: prop-op index or -1 */
+    uint32_t payload;  /* insert text: UTF-16 offset relative to doc text base; marker: refType;
+                          annotate: prop-op index */
+    uint32_t payload2; /* insert text: length in UTF-16 code units */
+} mtr_op;
+
+/* Per-document slice of a batch. */
+typedef struct mtr_doc_desc {
+    uint64_t op_begin;    /* index of the first op of this document in mtr_batch.ops */
+    uint64_t text_base;   /* base index in mtr_batch.text for this document's op text */
+    uint32_t op_count;
+    uint32_t text_count;  /* UTF-16 units of op text in this batch for this document */
+    uint32_t client_base; /* index into mtr_batch.client_off of short id 0 */
+    uint32_t n_clients;   /* number of short ids registered so far (first-seen order) */
+} mtr_doc_desc;
+
+#define MTR_NULL_VALUE 0xFFFFFFFFu   /* prop-op value meaning JSON null (delete the key) */
+#define MTR_NOT_INDEX  0xFFFFFFFFu   /* key_index for keys that are not JS array indices */
+
+/*
+ * A batch: flat arrays only.  Property keys and values are interned by the host:
+ *   key k   : JSON-escaped key bytes key_bytes[key_off[k] .. key_off[k+1])
+ *             key_index[k] = integer value if the key is a canonical JS array index
+ *             (those sort first, ascending, in JS own-key order), else MTR_NOT_INDEX
+ *   value v : JSON.stringify(value) bytes val_bytes[val_off[v] .. val_off[v+1]),
+ *             val_eq[v] = equivalence class under matchProperties (properties.ts:71)
+ *   prop-op p: ordered (key, value|MTR_NULL_VALUE) pairs
+ *             propop_kv[2*propop_off[p] .. 2*propop_off[p+1]) in Object.keys order
+ *   client c of doc d: JSON-escaped long id bytes
+ *             client_bytes[client_off[docs[d].client_base + c] .. +1)
+ */
+typedef struct mtr_batch {
+    uint32_t n_docs;
+    uint32_t n_propops;
+    uint32_t n_keys;
+    uint32_t n_vals;
+    uint64_t n_ops;
+    uint64_t n_text;
+    const mtr_doc_desc* docs;
+    const mtr_op* ops;
+    const uint16_t* text;
+    const uint32_t* propop_off;   /* n_propops + 1 */
+    const uint32_t* propop_kv;    /* 2 * propop_off[n_propops] */
+    const uint32_t* key_off;      /* n_keys + 1 */
+    const uint8_t*  key_bytes;
+    const uint32_t* key_index;    /* n_keys */
+    const uint32_t* val_off;      /* n_vals + 1 */
+    const uint8_t*  val_bytes;
+    const uint32_t* val_eq;       /* n_vals */
+    const uint32_t* client_off;   /* total clients + 1 */
+    const uint8_t*  client_bytes;
+} mtr_batch;
+
+/* Engine / oracle options: IMergeTreeOptions (mergeTree.ts:400-438) */
+typedef struct mtr_options {
+    int32_t new_length_calc;   /* mergeTreeUseNewLengthCalculations (default 0) */
+    int32_t snapshot_v1;       /* newMergeTreeSnapshotFormat: 1 = SnapshotV1, 0 = SnapshotLegacy */
+    int32_t chunk_size;        /* mergeTreeSnapshotChunkSize (default 10000) */
+    int32_t reserved;
+} mtr_options;
+
+/* Status codes (a per-document status word; assert codes use the reference's hex ids) */
+enum {
+    MTR_OK = 0,
+    MTR_ERR_INSERT_FAILED = 1,     /* UsageError("MergeTree insert failed") mergeTree.ts:1671 */
+    MTR_ERR_BAD_OP = 2,            /* malformed record / unsupported op type */
+    MTR_ERR_CAPACITY = 3,          /* engine-only: per-document arena exhausted */
+    MTR_ERR_UNSUPPORTED = 4,       /* feature outside the observer path: caller falls back */
+    MTR_ERR_ASSERT = 0x1000        /* 0x1000 | reference assert id, e.g. 0x104e for 0x04e */
+};
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTR_TYPES_H */

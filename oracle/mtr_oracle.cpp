@@ -1,0 +1,1238 @@
+// mtr_oracle.cpp -- CPU oracle: scalar restatement of the merge-tree observer path.
+//
+// TEST INFRASTRUCTURE ONLY (see mtr_oracle.h).  Every function below names the
+// reference file:line it restates; paths are relative to
+// packages/dds/merge-tree/src/ of the reference unless stated otherwise.
+//
+// Differences from the reference that are deliberate and behaviour-neutral:
+//  * Block lengths seen by a remote (refSeq, clientId) view are the sum of the
+//    leaves' nodeLength (undefined counted as 0) instead of
+//    PartialSequenceLengths.getPartialLength (partialLengths.ts:698).  The
+//    reference's own tests assert the two agree (test/testUtils.ts:209-248,
+//    used by test/partialLength.spec.ts); see DESIGN.md "Oracle".
+//  * Ordinals, tiles/range stacks, local references, attribution, pending
+//    segment groups and delta/maintenance events are not modelled: none of them
+//    change the observer's text, segment boundaries or summary bytes.
+#include "mtr_oracle.h"
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int kMaxNodesInBlock = 8;          // mergeTreeNodes.ts:330
+constexpr int kTextSegmentGranularity = 256; // textSegment.ts:35
+constexpr int kZamboniSegmentsMax = 2;       // zamboni.ts:14
+constexpr int kUniversalSeq = 0;             // constants.ts:11
+constexpr int kUnassignedSeq = -1;           // constants.ts:12
+constexpr int kTreeMaintenanceSeq = -2;      // constants.ts:13
+constexpr int kLocalClientId = -1;           // constants.ts:14
+constexpr int kNonCollabClient = -2;         // constants.ts:15
+constexpr int kUndef = -1;                   // "undefined" node length
+constexpr int64_t kMaxSafe = 9007199254740991LL;
+
+struct Block;
+
+struct PropMap {
+    std::vector<std::pair<uint32_t, uint32_t>> kv;  // (key id, value id) in JS own-key order
+};
+
+struct Node {
+    Block* parent = nullptr;
+    int index = 0;
+    bool leaf = true;
+};
+
+struct Seg : Node {
+    bool marker = false;
+    bool noRef = false;
+    int refType = 0;
+    std::u16string text;
+    int len = 0;                     // cachedLength
+    int seq = kUniversalSeq;         // BaseSegment.seq  mergeTreeNodes.ts:368
+    int clientId = kLocalClientId;   // BaseSegment.clientId
+    bool removed = false;
+    int removedSeq = 0;
+    std::vector<int> removedClientIds;
+    bool hasProps = false;           // properties !== undefined
+    bool hasPropMgr = false;         // propertyManager !== undefined
+    PropMap props;
+};
+
+struct Block : Node {
+    int childCount = 0;
+    Node* children[kMaxNodesInBlock] = {};
+    int needsScour = -1;  // -1 undefined, 0 false, 1 true
+    Block() { leaf = false; }
+};
+
+struct LRUEntry {
+    Seg* segment;
+    int maxSeq;
+};
+
+// Binary heap with the exact sift rules of collections/heap.ts:11-67
+struct Heap {
+    std::vector<LRUEntry> L{{nullptr, -2}};  // L[0] = comp.min (mergeTree.ts:112-115)
+    int count() const { return int(L.size()) - 1; }
+    const LRUEntry* peek() const { return count() > 0 ? &L[1] : nullptr; }
+    LRUEntry get() {
+        LRUEntry x = L[1];
+        L[1] = L[count()];
+        L.pop_back();
+        fixDown(1);
+        return x;
+    }
+    void add(LRUEntry x) {
+        L.push_back(x);
+        fixup(count());
+    }
+    static int cmp(const LRUEntry& a, const LRUEntry& b) { return a.maxSeq - b.maxSeq; }
+    void fixup(int k) {
+        while (k > 1 && cmp(L[k >> 1], L[k]) > 0) {
+            std::swap(L[k >> 1], L[k]);
+            k >>= 1;
+        }
+    }
+    void fixDown(int k) {
+        while ((k << 1) <= count()) {
+            int j = k << 1;
+            if (j < count() && cmp(L[j], L[j + 1]) > 0) j++;
+            if (cmp(L[k], L[j]) <= 0) break;
+            std::swap(L[k], L[j]);
+            k = j;
+        }
+    }
+};
+
+struct Tables {
+    const mtr_batch* b = nullptr;
+    bool keyIsIndex(uint32_t k) const { return b->key_index[k] != MTR_NOT_INDEX; }
+    uint32_t keyIndex(uint32_t k) const { return b->key_index[k]; }
+};
+
+// JS own-key insertion: integer-like keys first in ascending order, others in insertion order.
+void propSet(PropMap& m, uint32_t key, uint32_t val, const Tables& t) {
+    for (auto& kv : m.kv)
+        if (kv.first == key) {
+            kv.second = val;
+            return;
+        }
+    if (t.keyIsIndex(key)) {
+        uint32_t ix = t.keyIndex(key);
+        size_t pos = 0;
+        while (pos < m.kv.size() && t.keyIsIndex(m.kv[pos].first) && t.keyIndex(m.kv[pos].first) < ix) pos++;
+        m.kv.insert(m.kv.begin() + pos, {key, val});
+    } else {
+        m.kv.push_back({key, val});
+    }
+}
+
+void propDelete(PropMap& m, uint32_t key) {
+    for (size_t i = 0; i < m.kv.size(); i++)
+        if (m.kv[i].first == key) {
+            m.kv.erase(m.kv.begin() + i);
+            return;
+        }
+}
+
+// matchProperties (properties.ts:71-105) with values compared by equivalence class.
+bool matchProperties(const Seg* a, const Seg* b, const mtr_batch* bt) {
+    if (a->hasProps) {
+        if (!b->hasProps) return false;
+        if (a->props.kv.size() != b->props.kv.size()) return false;
+        for (auto& ka : a->props.kv) {
+            bool found = false;
+            for (auto& kb : b->props.kv)
+                if (kb.first == ka.first) {
+                    if (bt->val_eq[kb.second] != bt->val_eq[ka.second]) return false;
+                    found = true;
+                    break;
+                }
+            if (!found) return false;
+        }
+        return true;
+    }
+    return !b->hasProps;
+}
+
+struct OpCtx {
+    int refSeq;
+    int clientId;
+    int seq;
+};
+
+class Tree {
+  public:
+    explicit Tree(const mtr_options& o) : opt(o) { root = makeBlock(); }
+
+    mtr_options opt;
+    Block* root;
+    // CollaborationWindow (mergeTreeNodes.ts:656)
+    int localClientId = kLocalClientId;
+    bool collaborating = false;
+    int minSeq = 0;
+    int currentSeq = 0;
+    Heap heap;
+    std::deque<Seg> segPool;
+    std::deque<Block> blockPool;
+    Tables tabs;
+    int status = MTR_OK;
+
+    Block* makeBlock() {
+        blockPool.emplace_back();
+        return &blockPool.back();
+    }
+    Seg* makeSeg() {
+        segPool.emplace_back();
+        return &segPool.back();
+    }
+
+    static void assignChild(Block* b, Node* child, int index) {  // mergeTreeNodes.ts:355-362
+        child->parent = b;
+        child->index = index;
+        b->children[index] = child;
+    }
+
+    // ---------------------------------------------------------------- lengths
+    // localNetLength, mergeTree.ts:613-634 (localSeq undefined)
+    int localNetLength(const Seg* s) const {
+        if (s->removed) {
+            if (!opt.new_length_calc) {
+                int64_t rs = s->removedSeq == kUnassignedSeq ? kMaxSafe : s->removedSeq;
+                if (rs > minSeq) return 0;
+                return kUndef;
+            }
+            return 0;
+        }
+        return s->len;
+    }
+
+    int blockLocalLength(const Block* b) const {  // cachedLength via blockUpdate, mergeTree.ts:2387
+        int len = 0;
+        for (int i = 0; i < b->childCount; i++) {
+            const Node* c = b->children[i];
+            int l = c->leaf ? localNetLength(static_cast<const Seg*>(c)) : blockLocalLength(static_cast<const Block*>(c));
+            if (l > 0) len += l;
+        }
+        return len;
+    }
+
+    // Remote leaf visibility, mergeTree.ts:928-1003
+    int leafRemoteLength(const Seg* s, int refSeq, int clientId) const {
+        bool isRemoved = s->removed;
+        if (opt.new_length_calc) {  // mergeTree.ts:935-965
+            int64_t seq = s->seq == kUnassignedSeq ? kMaxSafe - 1 : s->seq;
+            if (isRemoved) {
+                int64_t rs = s->removedSeq == kUnassignedSeq ? kMaxSafe : s->removedSeq;
+                if (rs <= minSeq) return kUndef;
+                if (rs <= refSeq || std::find(s->removedClientIds.begin(), s->removedClientIds.end(), clientId) !=
+                                        s->removedClientIds.end())
+                    return 0;
+            }
+            return (seq <= refSeq || s->clientId == clientId) ? s->len : 0;
+        }
+        if (isRemoved && s->removedSeq != kUnassignedSeq && s->removedSeq <= refSeq) return kUndef;  // :967-976
+        if (s->clientId == clientId || (s->seq != kUnassignedSeq && s->seq <= refSeq)) {            // :977-988
+            if (isRemoved) {
+                return std::find(s->removedClientIds.begin(), s->removedClientIds.end(), clientId) !=
+                               s->removedClientIds.end()
+                           ? 0
+                           : s->len;
+            }
+            return s->len;
+        }
+        if (isRemoved && s->removedSeq != kUnassignedSeq) return kUndef;  // :993-998
+        return 0;
+    }
+
+    int blockRemoteLength(const Block* b, int refSeq, int clientId) const {
+        int len = 0;
+        for (int i = 0; i < b->childCount; i++) {
+            const Node* c = b->children[i];
+            int l = c->leaf ? leafRemoteLength(static_cast<const Seg*>(c), refSeq, clientId)
+                            : blockRemoteLength(static_cast<const Block*>(c), refSeq, clientId);
+            if (l > 0) len += l;
+        }
+        return len;
+    }
+
+    // nodeLength, mergeTree.ts:916-1004 (localSeq undefined)
+    int nodeLength(const Node* n, int refSeq, int clientId) const {
+        if (!collaborating || localClientId == clientId) {
+            if (n->leaf) return localNetLength(static_cast<const Seg*>(n));
+            return blockLocalLength(static_cast<const Block*>(n));
+        }
+        if (!n->leaf) return blockRemoteLength(static_cast<const Block*>(n), refSeq, clientId);
+        return leafRemoteLength(static_cast<const Seg*>(n), refSeq, clientId);
+    }
+
+    // ------------------------------------------------------------ segments
+    // TextSegment.canAppend, textSegment.ts:86-93; Marker.canAppend -> false
+    static bool canAppend(const Seg* a, const Seg* b) {
+        if (a->marker || b->marker) return false;
+        if (!a->text.empty() && a->text.back() == u'\n') return false;
+        return a->len <= kTextSegmentGranularity || b->len <= kTextSegmentGranularity;
+    }
+
+    // BaseSegment.splitAt + TextSegment.createSplitSegmentAt, mergeTreeNodes.ts:481-510, textSegment.ts:121-129
+    Seg* splitAt(Seg* s, int pos) {
+        if (pos <= 0 || s->marker) return nullptr;
+        Seg* r = makeSeg();
+        r->text = s->text.substr(pos);
+        s->text.resize(pos);
+        s->len = int(s->text.size());
+        r->len = int(r->text.size());
+        if (s->hasPropMgr && s->hasProps) {  // copyPropertiesTo, mergeTreeNodes.ts:512-522
+            r->hasPropMgr = true;
+            r->hasProps = true;
+            r->props = s->props;
+        }
+        r->parent = s->parent;
+        r->removedClientIds = s->removedClientIds;
+        r->removed = s->removed;
+        r->removedSeq = s->removedSeq;
+        r->seq = s->seq;
+        r->clientId = s->clientId;
+        return r;
+    }
+
+    // ------------------------------------------------------------ walking
+    enum class LeafMode { Insert, Split };
+    struct InsertContext {
+        LeafMode mode;
+        Seg* candidate = nullptr;
+        bool hasContinue = false;
+    };
+    struct SegChanges {
+        Node* replaceCurrent = nullptr;
+        Node* next = nullptr;
+    };
+    static Block* unfinished() {
+        static Block u;
+        return &u;
+    }
+
+    SegChanges leafAction(InsertContext& ctx, Seg* segment, int pos) {
+        SegChanges ch;
+        if (ctx.mode == LeafMode::Insert) {  // onLeaf, mergeTree.ts:1638-1648
+            if (segment) {
+                ch.replaceCurrent = ctx.candidate;
+                ch.next = segment;
+            } else {
+                ch.next = ctx.candidate;
+            }
+        } else {  // splitLeafSegment, mergeTree.ts:1686-1704
+            if (!(pos > 0 && segment)) return ch;
+            ch.next = splitAt(segment, pos);
+        }
+        return ch;
+    }
+
+    // breakTie, mergeTree.ts:1719-1738
+    static bool breakTie(int pos, const Node* node, int seq) {
+        if (node->leaf) {
+            if (pos == 0) {
+                int64_t newSeq = seq == kUnassignedSeq ? kMaxSafe : seq;
+                const Seg* s = static_cast<const Seg*>(node);
+                int64_t segSeq = s->seq == kUnassignedSeq ? kMaxSafe - 1 : s->seq;
+                return newSeq > segSeq;
+            }
+            return false;
+        }
+        return true;
+    }
+
+    // first leaf after `node` in tree order (forwardExcursion, mergeTreeNodeWalk.ts:121)
+    Seg* firstLeafAfter(Node* node) {
+        Node* cur = node;
+        while (cur->parent) {
+            Block* p = cur->parent;
+            for (int i = cur->index + 1; i < p->childCount; i++) {
+                Node* c = p->children[i];
+                while (c && !c->leaf) {
+                    Block* cb = static_cast<Block*>(c);
+                    c = cb->childCount > 0 ? cb->children[0] : nullptr;
+                }
+                if (c) return static_cast<Seg*>(c);
+            }
+            cur = p;
+        }
+        return nullptr;
+    }
+    // continueFrom, mergeTree.ts:1611-1615
+    bool continuePredicate(Block* block) {
+        Seg* s = firstLeafAfter(block);
+        return s != nullptr && s->seq == kUnassignedSeq;
+    }
+
+    // split, mergeTree.ts:1858-1871
+    Block* split(Block* node) {
+        const int half = kMaxNodesInBlock / 2;
+        Block* nb = makeBlock();
+        nb->childCount = half;
+        node->childCount = half;
+        for (int i = 0; i < half; i++) {
+            assignChild(nb, node->children[half + i], i);
+            node->children[half + i] = nullptr;
+        }
+        return nb;
+    }
+
+    // insertingWalk, mergeTree.ts:1740-1856
+    Block* insertingWalk(Block* block, int pos, int refSeq, int clientId, int seq, InsertContext& ctx) {
+        int _pos = pos;
+        int childIndex;
+        Node* newNode = nullptr;
+        for (childIndex = 0; childIndex < block->childCount; childIndex++) {
+            Node* child = block->children[childIndex];
+            int len = nodeLength(child, refSeq, clientId);
+            if (len == kUndef) continue;
+            if (_pos < len || (_pos == len && breakTie(_pos, child, seq))) {
+                if (!child->leaf) {
+                    Block* splitNode = insertingWalk(static_cast<Block*>(child), _pos, refSeq, clientId, seq, ctx);
+                    if (splitNode == nullptr) return nullptr;
+                    if (splitNode == unfinished()) {
+                        _pos -= len;
+                        continue;
+                    }
+                    newNode = splitNode;
+                    childIndex++;
+                } else {
+                    SegChanges ch = leafAction(ctx, static_cast<Seg*>(child), _pos);
+                    if (ch.replaceCurrent) assignChild(block, ch.replaceCurrent, childIndex);
+                    if (ch.next) {
+                        newNode = ch.next;
+                        childIndex++;
+                    } else {
+                        return nullptr;
+                    }
+                }
+                break;
+            } else {
+                _pos -= len;
+            }
+        }
+        if (!newNode && _pos == 0) {
+            if (seq != kUnassignedSeq && ctx.hasContinue && continuePredicate(block)) return unfinished();
+            newNode = leafAction(ctx, nullptr, _pos).next;
+        }
+        if (newNode) {
+            for (int i = block->childCount; i > childIndex; i--) {
+                block->children[i] = block->children[i - 1];
+                block->children[i]->index = i;
+            }
+            assignChild(block, newNode, childIndex);
+            block->childCount++;
+            if (block->childCount < kMaxNodesInBlock) return nullptr;
+            return split(block);
+        }
+        return nullptr;
+    }
+
+    // updateRoot, mergeTree.ts:1268-1277
+    void updateRoot(Block* splitNode) {
+        if (splitNode && splitNode != unfinished()) {
+            Block* nr = makeBlock();
+            nr->childCount = 2;
+            assignChild(nr, root, 0);
+            assignChild(nr, splitNode, 1);
+            root = nr;
+        }
+    }
+
+    // ensureIntervalBoundary, mergeTree.ts:1706-1716
+    void ensureIntervalBoundary(int pos, int refSeq, int clientId) {
+        InsertContext ctx{LeafMode::Split};
+        Block* s = insertingWalk(root, pos, refSeq, clientId, kTreeMaintenanceSeq, ctx);
+        updateRoot(s);
+    }
+
+    // addToLRUSet, mergeTree.ts:741-751
+    void addToLRUSet(Seg* s, int seq) {
+        if (s->parent->needsScour != 1 && seq > currentSeq) {
+            s->parent->needsScour = 1;
+            heap.add({s, seq});
+        }
+    }
+
+    // nodeMap restricted to its leaf visits, mergeTree.ts:2526-2577 + mergeTreeNodeWalk.ts:35-115.
+    // (The post action only maintains cached/partial lengths, which this oracle recomputes.)
+    template <class F>
+    void nodeMap(int refSeq, int clientId, F&& leaf, int start, int end) {
+        int endPos = end >= 0 ? end : std::max(0, nodeLength(root, refSeq, clientId));
+        if (endPos == start) return;
+        int pos = 0;
+        bool exit = false;
+        std::vector<Seg*> visit;  // collect then apply: leaf actions never change lengths seen later
+        walkMap(root, refSeq, clientId, start, endPos, pos, exit, visit);
+        for (Seg* s : visit) leaf(s);
+    }
+    void walkMap(Block* b, int refSeq, int clientId, int start, int endPos, int& pos, bool& exit,
+                 std::vector<Seg*>& visit) {
+        for (int i = 0; i < b->childCount && !exit; i++) {
+            Node* n = b->children[i];
+            if (endPos <= pos) {
+                exit = true;
+                return;
+            }
+            int len = nodeLength(n, refSeq, clientId);
+            if (len == kUndef || len == 0) continue;
+            int nextPos = pos + len;
+            if (start >= nextPos) {
+                pos = nextPos;
+                continue;
+            }
+            if (n->leaf) {
+                visit.push_back(static_cast<Seg*>(n));
+                pos = nextPos;
+            } else {
+                walkMap(static_cast<Block*>(n), refSeq, clientId, start, endPos, pos, exit, visit);
+            }
+        }
+    }
+
+    // ------------------------------------------------------------ zamboni
+    // scourNode, zamboni.ts:122-193
+    void scourNode(Block* node, std::vector<Node*>& hold) {
+        Seg* prev = nullptr;
+        for (int k = 0; k < node->childCount; k++) {
+            Node* child = node->children[k];
+            if (child->leaf) {
+                Seg* s = static_cast<Seg*>(child);
+                if (s->removed) {
+                    if (s->removedSeq > minSeq) {
+                        hold.push_back(s);
+                    } else {
+                        s->parent = nullptr;  // UNLINK
+                    }
+                    prev = nullptr;
+                } else {
+                    if (s->seq <= minSeq) {
+                        int ln = localNetLength(s);
+                        bool ok = prev && canAppend(prev, s) && matchProperties(prev, s, tabs.b) && (ln > 0);
+                        if (ok) {
+                            prev->text += s->text;  // TextSegment.append textSegment.ts:99-103
+                            prev->len += s->len;
+                            s->parent = nullptr;
+                        } else {
+                            hold.push_back(s);
+                            prev = ln > 0 ? s : nullptr;
+                        }
+                    } else {
+                        hold.push_back(s);
+                        prev = nullptr;
+                    }
+                }
+            } else {
+                hold.push_back(child);
+                prev = nullptr;
+            }
+        }
+    }
+
+    static bool underflow(const Block* b) { return b->childCount < kMaxNodesInBlock / 2; }
+
+    // packParent, zamboni.ts:63-120
+    void packParent(Block* parent) {
+        std::vector<Node*> hold;
+        for (int ci = 0; ci < parent->childCount; ci++) {
+            Block* cb = static_cast<Block*>(parent->children[ci]);
+            scourNode(cb, hold);
+            cb->parent = nullptr;
+        }
+        if (!hold.empty()) {
+            int total = int(hold.size());
+            const int halfMax = kMaxNodesInBlock / 2;
+            int childCount = std::min(kMaxNodesInBlock - 1, total / halfMax);
+            if (childCount < 1) childCount = 1;
+            int base = total / childCount;
+            int rem = total % childCount;
+            int packed = 0;
+            std::vector<Block*> blocks;
+            for (int ni = 0; ni < childCount; ni++) {
+                int nc = base;
+                if (rem > 0) {
+                    nc++;
+                    rem--;
+                }
+                Block* pb = makeBlock();
+                pb->childCount = nc;
+                for (int pi = 0; pi < nc; pi++) assignChild(pb, hold[packed++], pi);
+                pb->parent = parent;
+                blocks.push_back(pb);
+            }
+            for (int j = 0; j < kMaxNodesInBlock; j++) parent->children[j] = nullptr;
+            for (int j = 0; j < childCount; j++) assignChild(parent, blocks[j], j);
+            parent->childCount = childCount;
+        } else {
+            for (int j = 0; j < kMaxNodesInBlock; j++) parent->children[j] = nullptr;
+            parent->childCount = 0;
+        }
+        if (underflow(parent) && parent->parent) packParent(parent->parent);
+    }
+
+    // zamboniSegments, zamboni.ts:19-60
+    void zamboniSegments() {
+        if (!collaborating) return;
+        for (int i = 0; i < kZamboniSegmentsMax; i++) {
+            const LRUEntry* top = heap.peek();
+            if (!top || top->maxSeq > minSeq) break;
+            LRUEntry e = heap.get();
+            Seg* s = e.segment;
+            if (s->parent && s->parent->needsScour != 0) {
+                Block* block = s->parent;
+                std::vector<Node*> copy;
+                scourNode(block, copy);
+                block->needsScour = 0;
+                int newCount = int(copy.size());
+                if (newCount < block->childCount) {
+                    for (int j = 0; j < kMaxNodesInBlock; j++) block->children[j] = nullptr;
+                    block->childCount = newCount;
+                    for (int j = 0; j < newCount; j++) assignChild(block, copy[j], j);
+                    if (underflow(block) && block->parent) packParent(block->parent);
+                }
+            }
+        }
+    }
+
+    // setMinSeq, mergeTree.ts:1025-1044
+    void setMinSeq(int ms) {
+        if (ms > currentSeq) {
+            status = MTR_ERR_ASSERT | 0x04e;
+            return;
+        }
+        if (minSeq > ms) {
+            status = MTR_ERR_ASSERT | 0x04f;
+            return;
+        }
+        if (ms > minSeq) {
+            minSeq = ms;
+            zamboniSegments();
+        }
+    }
+    // updateSeqNumbers, client.ts:877-887
+    void updateSeqNumbers(int ms, int seq) {
+        if (currentSeq > seq) {
+            status = MTR_ERR_ASSERT | 0x038;
+            return;
+        }
+        currentSeq = seq;
+        if (ms > seq) {
+            status = MTR_ERR_ASSERT | 0x039;
+            return;
+        }
+        setMinSeq(ms);
+    }
+
+    // ------------------------------------------------------------ ops
+    // properties: PropertiesManager.addProperties without combining ops
+    // (segmentPropertiesManager.ts:60-157), BaseSegment.addProperties (mergeTreeNodes.ts:385-406)
+    void addProperties(Seg* s, uint32_t propop) {
+        const mtr_batch* b = tabs.b;
+        s->hasPropMgr = true;
+        s->hasProps = true;
+        for (uint32_t i = b->propop_off[propop]; i < b->propop_off[propop + 1]; i++) {
+            uint32_t k = b->propop_kv[2 * i], v = b->propop_kv[2 * i + 1];
+            if (v == MTR_NULL_VALUE)
+                propDelete(s->props, k);
+            else
+                propSet(s->props, k, v, tabs);
+        }
+    }
+
+    Seg* segmentFromSpec(const mtr_op& op, const mtr_doc_desc& dd) {  // sequenceFactory.ts:26-38
+        Seg* s = makeSeg();
+        if (op.flags & MTR_F_MARKER) {
+            s->marker = true;
+            s->refType = int(op.payload);
+            s->noRef = (op.flags & MTR_F_NOREF) != 0;
+            s->len = 1;
+        } else {
+            const uint16_t* t = tabs.b->text + dd.text_base + op.payload;
+            s->text.assign(reinterpret_cast<const char16_t*>(t), op.payload2);
+            s->len = int(op.payload2);
+        }
+        if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) addProperties(s, uint32_t(op.pos2));
+        return s;
+    }
+
+    // insertSegments + blockInsert, mergeTree.ts:1397-1427,1594-1685
+    void insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(pos, refSeq, clientId);
+        if (seg->len > 0) {
+            seg->seq = seq;
+            seg->clientId = clientId;
+            InsertContext ctx{LeafMode::Insert, seg, true};
+            Block* splitNode = insertingWalk(root, pos, refSeq, clientId, seq, ctx);
+            if (seg->parent == nullptr) {
+                status = MTR_ERR_INSERT_FAILED;
+                return;
+            }
+            updateRoot(splitNode);
+            if (collaborating) {  // saveIfLocal, mergeTree.ts:1618-1637
+                if (!(seg->seq == kUnassignedSeq && clientId == localClientId) && seg->seq > minSeq)
+                    addToLRUSet(seg, seg->seq);
+            }
+        }
+        if (collaborating && seq != kUnassignedSeq) zamboniSegments();
+    }
+
+    // markRangeRemoved, mergeTree.ts:1955-2047
+    void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(start, refSeq, clientId);
+        ensureIntervalBoundary(end, refSeq, clientId);
+        nodeMap(
+            refSeq, clientId,
+            [&](Seg* s) {
+                if (s->removed) {
+                    if (s->removedSeq == kUnassignedSeq) {
+                        s->removedClientIds.insert(s->removedClientIds.begin(), clientId);
+                        s->removedSeq = seq;
+                    } else {
+                        s->removedClientIds.push_back(clientId);
+                    }
+                } else {
+                    s->removed = true;
+                    s->removedClientIds.assign(1, clientId);
+                    s->removedSeq = seq;
+                }
+                if (collaborating) {
+                    if (!(s->removedSeq == kUnassignedSeq && clientId == localClientId)) addToLRUSet(s, seq);
+                }
+            },
+            start, end);
+        if (collaborating && seq != kUnassignedSeq) zamboniSegments();
+    }
+
+    // annotateRange, mergeTree.ts:1895-1953
+    void annotateRange(int start, int end, uint32_t propop, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(start, refSeq, clientId);
+        ensureIntervalBoundary(end, refSeq, clientId);
+        nodeMap(
+            refSeq, clientId,
+            [&](Seg* s) {
+                addProperties(s, propop);
+                if (collaborating && seq != kUnassignedSeq) addToLRUSet(s, seq);
+            },
+            start, end);
+        if (collaborating && seq != kUnassignedSeq) zamboniSegments();
+    }
+
+    int apply(const mtr_op& op, const mtr_doc_desc& dd) {
+        switch (op.type) {
+            case MTR_OP_INSERT: {
+                Seg* s = segmentFromSpec(op, dd);
+                insertSegments(op.pos1, s, op.ref_seq, op.client, op.seq);
+                break;
+            }
+            case MTR_OP_REMOVE:
+                markRangeRemoved(op.pos1, op.pos2, op.ref_seq, op.client, op.seq);
+                break;
+            case MTR_OP_ANNOTATE:
+                annotateRange(op.pos1, op.pos2, op.payload, op.ref_seq, op.client, op.seq);
+                break;
+            case MTR_OP_SEQ:
+                break;
+            case MTR_OP_LOCAL_INSERT: {
+                if (collaborating) return MTR_ERR_UNSUPPORTED;
+                Seg* s = segmentFromSpec(op, dd);
+                insertSegments(op.pos1, s, currentSeq, localClientId, kUniversalSeq);
+                return status;
+            }
+            case MTR_OP_LOCAL_REMOVE:
+                if (collaborating) return MTR_ERR_UNSUPPORTED;
+                markRangeRemoved(op.pos1, op.pos2, currentSeq, localClientId, kUniversalSeq);
+                return status;
+            case MTR_OP_LOCAL_ANNOTATE:
+                if (collaborating) return MTR_ERR_UNSUPPORTED;
+                annotateRange(op.pos1, op.pos2, op.payload, currentSeq, localClientId, kUniversalSeq);
+                return status;
+            case MTR_OP_START_COLLAB:  // startOrUpdateCollaboration -> startCollaboration, client.ts:1133, mergeTree.ts:731
+                if (collaborating) return MTR_OK;
+                localClientId = 0;
+                minSeq = op.min_seq;
+                currentSeq = op.seq;
+                collaborating = true;
+                heap = Heap();
+                return status;
+            default:
+                return MTR_ERR_BAD_OP;
+        }
+        if (status == MTR_OK && (op.flags & MTR_F_LAST)) updateSeqNumbers(op.min_seq, op.seq);
+        return status;
+    }
+
+    // ------------------------------------------------------------ text
+    void gatherText(Block* b, std::u16string& out) {
+        for (int i = 0; i < b->childCount; i++) {
+            Node* n = b->children[i];
+            if (n->leaf) {
+                Seg* s = static_cast<Seg*>(n);
+                int l = localNetLength(s);
+                if (l > 0 && !s->marker) out += s->text;
+            } else {
+                gatherText(static_cast<Block*>(n), out);
+            }
+        }
+    }
+
+    void leaves(Block* b, std::vector<Seg*>& out) {  // walkAllChildSegments, mergeTreeNodeWalk.ts:170
+        for (int i = 0; i < b->childCount; i++) {
+            Node* n = b->children[i];
+            if (n->leaf)
+                out.push_back(static_cast<Seg*>(n));
+            else
+                leaves(static_cast<Block*>(n), out);
+        }
+    }
+    int height() const {
+        int h = 1;
+        const Block* b = root;
+        while (b->childCount > 0 && !b->children[0]->leaf) {
+            b = static_cast<const Block*>(b->children[0]);
+            h++;
+        }
+        return h;
+    }
+};
+
+// ---------------------------------------------------------------- JSON writer
+// JSON.stringify of strings (ES2019 well-formed): escapes, lone surrogates as \udXXX.
+struct Out {
+    std::string s;
+    void raw(const char* p) { s += p; }
+    void raw(const std::string& p) { s += p; }
+    void bytes(const uint8_t* p, size_t n) { s.append(reinterpret_cast<const char*>(p), n); }
+    void num(int64_t v) { s += std::to_string(v); }
+    void hex4(unsigned u) {
+        static const char* hx = "0123456789abcdef";
+        s += "\\u";
+        s += hx[(u >> 12) & 15];
+        s += hx[(u >> 8) & 15];
+        s += hx[(u >> 4) & 15];
+        s += hx[u & 15];
+    }
+    void utf8(uint32_t cp) {
+        if (cp < 0x80) {
+            s += char(cp);
+        } else if (cp < 0x800) {
+            s += char(0xC0 | (cp >> 6));
+            s += char(0x80 | (cp & 63));
+        } else if (cp < 0x10000) {
+            s += char(0xE0 | (cp >> 12));
+            s += char(0x80 | ((cp >> 6) & 63));
+            s += char(0x80 | (cp & 63));
+        } else {
+            s += char(0xF0 | (cp >> 18));
+            s += char(0x80 | ((cp >> 12) & 63));
+            s += char(0x80 | ((cp >> 6) & 63));
+            s += char(0x80 | (cp & 63));
+        }
+    }
+    void str16(const std::u16string& t) {
+        s += '"';
+        for (size_t i = 0; i < t.size(); i++) {
+            unsigned u = t[i];
+            switch (u) {
+                case '"': s += "\\\""; continue;
+                case '\\': s += "\\\\"; continue;
+                case '\b': s += "\\b"; continue;
+                case '\f': s += "\\f"; continue;
+                case '\n': s += "\\n"; continue;
+                case '\r': s += "\\r"; continue;
+                case '\t': s += "\\t"; continue;
+                default: break;
+            }
+            if (u < 0x20) {
+                hex4(u);
+            } else if (u >= 0xD800 && u <= 0xDBFF) {
+                if (i + 1 < t.size() && t[i + 1] >= 0xDC00 && t[i + 1] <= 0xDFFF) {
+                    uint32_t cp = 0x10000 + ((u - 0xD800) << 10) + (t[i + 1] - 0xDC00);
+                    utf8(cp);
+                    i++;
+                } else {
+                    hex4(u);
+                }
+            } else if (u >= 0xDC00 && u <= 0xDFFF) {
+                hex4(u);
+            } else {
+                utf8(u);
+            }
+        }
+        s += '"';
+    }
+};
+
+struct Emitter {
+    const mtr_batch* b;
+    const mtr_doc_desc* dd;
+    void longClientId(Out& o, int id) const {  // Client.getLongClientId, client.ts:682-684
+        o.raw("\"");
+        if (id < 0 || uint32_t(id) >= dd->n_clients) {
+            o.raw("original");
+        } else {
+            uint32_t ix = dd->client_base + uint32_t(id);
+            o.bytes(b->client_bytes + b->client_off[ix], b->client_off[ix + 1] - b->client_off[ix]);
+        }
+        o.raw("\"");
+    }
+    void props(Out& o, const PropMap& p) const {
+        o.raw("{");
+        bool first = true;
+        for (auto& kv : p.kv) {
+            if (!first) o.raw(",");
+            first = false;
+            o.raw("\"");
+            o.bytes(b->key_bytes + b->key_off[kv.first], b->key_off[kv.first + 1] - b->key_off[kv.first]);
+            o.raw("\":");
+            o.bytes(b->val_bytes + b->val_off[kv.second], b->val_off[kv.second + 1] - b->val_off[kv.second]);
+        }
+        o.raw("}");
+    }
+    // toJSONObject: textSegment.ts:73-77, mergeTreeNodes.ts:577-581
+    void segJson(Out& o, const Seg* s) const {
+        if (s->marker) {
+            o.raw("{\"marker\":{");
+            if (!s->noRef) {
+                o.raw("\"refType\":");
+                o.num(s->refType);
+            }
+            o.raw("}");
+            if (s->hasProps) {
+                o.raw(",\"props\":");
+                props(o, s->props);
+            }
+            o.raw("}");
+        } else if (s->hasProps) {
+            o.raw("{\"text\":");
+            o.str16(s->text);
+            o.raw(",\"props\":");
+            props(o, s->props);
+            o.raw("}");
+        } else {
+            o.str16(s->text);
+        }
+    }
+};
+
+struct SpecOut {
+    std::string json;
+    int len;
+};
+
+}  // namespace
+
+struct oracle_doc {
+    Tree tree;
+    explicit oracle_doc(const mtr_options& o) : tree(o) {}
+};
+
+extern "C" {
+
+oracle_doc* oracle_doc_new(const mtr_options* opt) {
+    mtr_options o{0, 1, 10000, 0};
+    if (opt) o = *opt;
+    if (o.chunk_size <= 0) o.chunk_size = 10000;
+    return new oracle_doc(o);
+}
+
+void oracle_doc_free(oracle_doc* d) { delete d; }
+
+int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint32_t op_lo, uint32_t op_hi) {
+    Tree& t = d->tree;
+    t.tabs.b = b;
+    const mtr_doc_desc& dd = b->docs[doc_index];
+    if (op_hi > dd.op_count) op_hi = dd.op_count;
+    for (uint32_t i = op_lo; i < op_hi; i++) {
+        int st = t.apply(b->ops[dd.op_begin + i], dd);
+        if (st != MTR_OK) return st;
+    }
+    return t.status;
+}
+
+int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap) {
+    std::u16string s;
+    d->tree.gatherText(d->tree.root, s);
+    int64_t n = int64_t(s.size());
+    if (out) std::memcpy(out, s.data(), size_t(std::min(n, cap)) * 2);
+    return n;
+}
+
+int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client) {
+    return d->tree.nodeLength(d->tree.root, ref_seq, client);
+}
+
+void oracle_doc_state(oracle_doc* d, int64_t* out) {
+    Tree& t = d->tree;
+    std::vector<Seg*> lv;
+    t.leaves(t.root, lv);
+    out[0] = t.minSeq;
+    out[1] = t.currentSeq;
+    out[2] = t.heap.count();
+    out[3] = int64_t(lv.size());
+}
+
+int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap, int32_t* height) {
+    Tree& t = d->tree;
+    std::vector<Seg*> lv;
+    t.leaves(t.root, lv);
+    if (height) *height = t.height();
+    if (int64_t(lv.size()) > cap) return -int64_t(lv.size());
+    for (size_t i = 0; i < lv.size(); i++) {
+        Seg* s = lv[i];
+        int bnd = 0;
+        const Node* n = s;
+        while (n->parent && n->index == 0) {
+            bnd++;
+            n = n->parent;
+        }
+        if (!n->parent) {
+            // reached the root through first children: counts every level
+        }
+        uint32_t h = 2166136261u;
+        if (s->hasProps) {
+            h ^= 1u;
+            for (auto& kv : s->props.kv) {
+                h = (h ^ kv.first) * 16777619u;
+                h = (h ^ t.tabs.b->val_eq[kv.second]) * 16777619u;
+            }
+        }
+        int32_t* r = out + 8 * i;
+        r[0] = s->len;
+        r[1] = s->seq;
+        r[2] = s->clientId;
+        r[3] = s->removed ? s->removedSeq : INT32_MIN;
+        r[4] = int32_t(s->removedClientIds.size());
+        r[5] = bnd;
+        r[6] = s->marker ? 1 : 0;
+        r[7] = int32_t(s->hasProps ? h : 0);
+    }
+    return int64_t(lv.size());
+}
+
+// Client.summarize (client.ts:966-1000) with SnapshotV1 (snapshotV1.ts:122-298) or
+// SnapshotLegacy (snapshotlegacy.ts:122-255) and the chunk serializers (snapshotChunks.ts:86-149).
+int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint8_t* out, int64_t cap,
+                             int64_t* blob_len, int32_t max_blobs) {
+    Tree& t = d->tree;
+    t.tabs.b = b;
+    Emitter em{b, &b->docs[doc_index]};
+    const int minSeq = t.minSeq;
+    const int chunk = t.opt.chunk_size;
+    std::vector<Seg*> lv;
+    t.leaves(t.root, lv);
+    std::vector<std::string> blobs;
+
+    // coalesce helper state: prev is a (clone of a) segment, text accumulated in prevText
+    struct Prev {
+        bool has = false;
+        Seg seg;  // clone
+    } prev;
+    std::vector<SpecOut> specs;
+    auto pushPrev = [&]() {
+        if (prev.has) {
+            Out o;
+            em.segJson(o, &prev.seg);
+            specs.push_back({o.s, prev.seg.len});
+        }
+    };
+    auto takePrev = [&](Seg* s) {
+        prev.has = true;
+        prev.seg = *s;
+    };
+
+    if (t.opt.snapshot_v1) {
+        for (Seg* s : lv) {  // extractSync, snapshotV1.ts:180-298
+            if (s->seq == kUnassignedSeq || (s->removed && s->removedSeq <= minSeq)) continue;
+            if (s->seq <= minSeq && (!s->removed || s->removedSeq == kUnassignedSeq)) {
+                if (!prev.has) {
+                    takePrev(s);
+                } else if (Tree::canAppend(&prev.seg, s) && matchProperties(&prev.seg, s, b)) {
+                    prev.seg.text += s->text;
+                    prev.seg.len += s->len;
+                } else {
+                    pushPrev();
+                    takePrev(s);
+                }
+            } else {
+                pushPrev();
+                prev.has = false;
+                Out o;
+                o.raw("{\"json\":");
+                em.segJson(o, s);
+                if (s->seq > minSeq) {
+                    o.raw(",\"seq\":");
+                    o.num(s->seq);
+                    o.raw(",\"client\":");
+                    em.longClientId(o, s->clientId);
+                }
+                if (s->removed) {
+                    o.raw(",\"removedSeq\":");
+                    o.num(s->removedSeq);
+                    o.raw(",\"removedClient\":");
+                    em.longClientId(o, s->removedClientIds[0]);
+                    o.raw(",\"removedClientIds\":[");
+                    for (size_t k = 0; k < s->removedClientIds.size(); k++) {
+                        if (k) o.raw(",");
+                        em.longClientId(o, s->removedClientIds[k]);
+                    }
+                    o.raw("]");
+                }
+                o.raw("}");
+                specs.push_back({o.s, s->len});
+            }
+        }
+        pushPrev();
+        // emit, snapshotV1.ts:122-178
+        struct Chunk {
+            size_t start, count;
+            int64_t length;
+        };
+        std::vector<Chunk> chunks;
+        size_t total = 0;
+        int64_t totalLen = 0;
+        do {
+            Chunk c{total, 0, 0};
+            while (c.length < chunk && c.start + c.count < specs.size()) {
+                c.length += specs[c.start + c.count].len;
+                c.count++;
+            }
+            chunks.push_back(c);
+            total += c.count;
+            totalLen += c.length;
+        } while (total < specs.size());
+        auto segList = [&](Out& o, const Chunk& c) {
+            o.raw("[");
+            for (size_t k = 0; k < c.count; k++) {
+                if (k) o.raw(",");
+                o.raw(specs[c.start + k].json);
+            }
+            o.raw("]");
+        };
+        auto chunkHead = [&](Out& o, const Chunk& c) {
+            o.raw("{\"version\":\"1\",\"segmentCount\":");
+            o.num(int64_t(c.count));
+            o.raw(",\"length\":");
+            o.num(c.length);
+            o.raw(",\"segments\":");
+            segList(o, c);
+            o.raw(",\"startIndex\":");
+            o.num(int64_t(c.start));
+        };
+        Out h;
+        chunkHead(h, chunks[0]);
+        h.raw(",\"headerMetadata\":{\"minSequenceNumber\":");
+        h.num(minSeq);
+        h.raw(",\"sequenceNumber\":");
+        h.num(t.currentSeq);
+        h.raw(",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+        for (size_t k = 1; k < chunks.size(); k++) {
+            h.raw(",{\"id\":\"body_");
+            h.num(int64_t(k - 1));
+            h.raw("\"}");
+        }
+        h.raw("],\"totalLength\":");
+        h.num(totalLen);
+        h.raw(",\"totalSegmentCount\":");
+        h.num(int64_t(total));
+        h.raw("}}");
+        blobs.push_back(h.s);
+        for (size_t k = 1; k < chunks.size(); k++) {
+            Out o;
+            chunkHead(o, chunks[k]);
+            o.raw("}");
+            blobs.push_back(o.s);
+        }
+    } else {
+        // extractSync, snapshotlegacy.ts:184-255: mapRange(minSeq, NonCollabClient)
+        std::vector<SpecOut> segs;
+        const int cid = kNonCollabClient;
+        for (Seg* s : lv) {
+            int l = t.nodeLength(s, minSeq, cid);
+            if (l == kUndef || l == 0) continue;
+            if (s->seq != kUnassignedSeq && s->seq <= minSeq &&
+                (!s->removed || s->removedSeq == kUnassignedSeq || s->removedSeq > minSeq)) {
+                if (prev.has && Tree::canAppend(&prev.seg, s) && matchProperties(&prev.seg, s, b)) {
+                    prev.seg.text += s->text;
+                    prev.seg.len += s->len;
+                } else {
+                    pushPrev();
+                    takePrev(s);
+                }
+            }
+        }
+        pushPrev();
+        int64_t totalLen = 0;
+        for (auto& sp : specs) totalLen += sp.len;
+        auto getChunk = [&](int64_t approx, size_t start, size_t& count, int64_t& length) {
+            count = 0;
+            length = 0;
+            while (length < approx && start + count < specs.size()) {
+                length += specs[start + count].len;
+                count++;
+            }
+        };
+        auto body = [&](Out& o, size_t start, size_t count, int64_t length) {
+            o.raw("{\"chunkStartSegmentIndex\":");
+            o.num(int64_t(start));
+            o.raw(",\"chunkSegmentCount\":");
+            o.num(int64_t(count));
+            o.raw(",\"chunkLengthChars\":");
+            o.num(length);
+            o.raw(",\"totalLengthChars\":");
+            o.num(totalLen);
+            o.raw(",\"totalSegmentCount\":");
+            o.num(int64_t(specs.size()));
+            o.raw(",\"chunkSequenceNumber\":");
+            o.num(minSeq);
+            o.raw(",\"segmentTexts\":[");
+            for (size_t k = 0; k < count; k++) {
+                if (k) o.raw(",");
+                o.raw(specs[start + k].json);
+            }
+            o.raw("]");
+        };
+        size_t c1n;
+        int64_t c1l;
+        getChunk(chunk, 0, c1n, c1l);
+        Out h;
+        body(h, 0, c1n, c1l);
+        h.raw(",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+        if (c1l < totalLen) h.raw(",{\"id\":\"body\"}");
+        h.raw("],\"sequenceNumber\":");
+        h.num(minSeq);
+        h.raw(",\"totalLength\":");
+        h.num(totalLen);
+        h.raw(",\"totalSegmentCount\":");
+        h.num(int64_t(specs.size()));
+        h.raw("}}");
+        blobs.push_back(h.s);
+        if (c1n < specs.size()) {
+            size_t c2n;
+            int64_t c2l;
+            getChunk(totalLen, c1n, c2n, c2l);
+            Out o;
+            body(o, c1n, c2n, c2l);
+            o.raw("}");
+            blobs.push_back(o.s);
+        }
+    }
+    int64_t need = 0;
+    for (auto& s : blobs) need += int64_t(s.size());
+    if (need > cap || int32_t(blobs.size()) > max_blobs) return -need;
+    int64_t off = 0;
+    for (size_t k = 0; k < blobs.size(); k++) {
+        std::memcpy(out + off, blobs[k].data(), blobs[k].size());
+        blob_len[k] = int64_t(blobs[k].size());
+        off += int64_t(blobs[k].size());
+    }
+    return int64_t(blobs.size());
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+/*
+ * mtr_oracle.h -- C ABI of the CPU oracle.
+ *
+ * TEST INFRASTRUCTURE ONLY.  The oracle is a scalar C++ restatement of the
+ * reference merge-tree observer path (packages/dds/merge-tree/src, see
+ * mtr_oracle.cpp for file:line citations).  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product path
+ * (fluidframework_amd) never links or calls it.
+ */
+#ifndef MTR_ORACLE_H
+#define MTR_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "../include/mtr_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_doc oracle_doc;
+
+oracle_doc* oracle_doc_new(const mtr_options* opt);
+void oracle_doc_free(oracle_doc* d);
+
+/* Apply ops [op_lo, op_hi) of document doc_index of batch b. Returns MTR_OK or an error code. */
+int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint32_t op_lo, uint32_t op_hi);
+
+/* getText of the local view (MergeTreeTextHelper.getText, MergeTreeTextHelper.ts:20).
+ * Returns the length in UTF-16 units; writes at most cap units. */
+int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap);
+
+/* Client.summarize (client.ts:966).  Writes blobs back-to-back into out (cap bytes);
+ * blob_len[i] = byte length of blob i; blob order: header, body / body_0, body_1, ...
+ * Returns the number of blobs, or -(bytes needed) if cap is too small. */
+int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_index,
+                             uint8_t* out, int64_t cap, int64_t* blob_len, int32_t max_blobs);
+
+/* Export the leaf sequence for structural parity checks.  Per leaf 8 int32:
+ * [len, seq, client, removed_seq (INT32_MIN if not removed), n_removers, bnd, is_marker, props_hash]
+ * bnd = number of tree levels at which the leaf starts a block (1 = starts its leaf block).
+ * Returns number of leaves (or -(needed) if cap too small); *height = tree height. */
+int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap_leaves, int32_t* height);
+
+/* Collaboration window state: out[0]=minSeq out[1]=currentSeq out[2]=#heap entries out[3]=#leaves */
+void oracle_doc_state(oracle_doc* d, int64_t* out);
+
+/* Length of the doc in the (ref_seq, client) view (MergeTree.getLength, mergeTree.ts:757) */
+int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,100 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, never by the product package (fluidframework_amd).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from fluidframework_amd import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle not built: run `make -C {_HERE}`")
+        L = C.CDLL(path)
+        L.oracle_doc_new.restype = C.c_void_p
+        L.oracle_doc_new.argtypes = [C.POINTER(abi.MtrOptions)]
+        L.oracle_doc_free.argtypes = [C.c_void_p]
+        L.oracle_doc_apply.restype = C.c_int
+        L.oracle_doc_apply.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.oracle_doc_text.restype = C.c_int64
+        L.oracle_doc_text.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_doc_summarize.restype = C.c_int64
+        L.oracle_doc_summarize.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64,
+                                           C.c_void_p, C.c_int32]
+        L.oracle_doc_export.restype = C.c_int64
+        L.oracle_doc_export.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
+        L.oracle_doc_state.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_doc_length.restype = C.c_int64
+        L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        _LIB = L
+    return _LIB
+
+
+def options(new_length_calc=False, snapshot_v1=True, chunk_size=10000):
+    return abi.MtrOptions(int(new_length_calc), int(snapshot_v1), int(chunk_size), 0)
+
+
+class OracleDoc:
+    def __init__(self, opts=None):
+        self.opts = opts or options()
+        self.h = lib().oracle_doc_new(C.byref(self.opts))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_doc_free(self.h)
+            self.h = None
+
+    def apply(self, batch, doc_index, lo=0, hi=None):
+        if hi is None:
+            hi = int(batch.docs[doc_index]["op_count"])
+        return lib().oracle_doc_apply(self.h, C.addressof(batch.c), doc_index, lo, hi)
+
+    def text(self) -> str:
+        n = lib().oracle_doc_text(self.h, None, 0)
+        buf = np.zeros(max(n, 1), dtype="<u2")
+        lib().oracle_doc_text(self.h, buf.ctypes.data, n)
+        return buf[:n].tobytes().decode("utf-16-le", "surrogatepass")
+
+    def summarize(self, batch, doc_index) -> list[bytes]:
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, dtype="u1")
+            lens = np.zeros(4096, dtype="<i8")
+            r = lib().oracle_doc_summarize(self.h, C.addressof(batch.c), doc_index, out.ctypes.data, cap,
+                                           lens.ctypes.data, 4096)
+            if r >= 0:
+                blobs = []
+                off = 0
+                for i in range(r):
+                    blobs.append(out[off:off + lens[i]].tobytes())
+                    off += lens[i]
+                return blobs
+            cap = -r + 16
+
+    def export(self):
+        h = C.c_int32(0)
+        n = lib().oracle_doc_export(self.h, None, 0, C.byref(h))
+        n = -n if n < 0 else n
+        out = np.zeros((max(n, 1), 8), dtype="<i4")
+        lib().oracle_doc_export(self.h, out.ctypes.data, n, C.byref(h))
+        return out[:n], h.value
+
+    def state(self):
+        out = np.zeros(4, dtype="<i8")
+        lib().oracle_doc_state(self.h, out.ctypes.data)
+        return out
+
+    def length(self, ref_seq, client):
+        return lib().oracle_doc_length(self.h, ref_seq, client)
