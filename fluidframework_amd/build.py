@@ -1,0 +1,62 @@
+"""Build the HIP engine (libmtr.so, gfx950) and the synthetic op-log generator in-tree.
+
+Only hipcc/g++ invocations -- no cmake, no JIT caches -- so the built .so files travel to the GPU
+box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+ENGINE_SRC = ["mtr_engine.hip"]
+ENGINE_DEPS = ["apply.hip.h", "summary.hip.h", "mtr_engine.hip"]
+SYNTH_SRC = ["synth.cpp"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_engine(force=False, verbose=False):
+    out = os.path.join(HERE, "libmtr.so")
+    deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", "mtr.h"),
+                                                           os.path.join(ROOT, "include", "mtr_types.h")]
+    if force or _stale(out, deps):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wno-unused-result", "-o", out] + [os.path.join(CSRC, f) for f in ENGINE_SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return out
+
+
+def build_synth(force=False, verbose=False):
+    out = os.path.join(HERE, "libmtrsynth.so")
+    deps = [os.path.join(CSRC, f) for f in SYNTH_SRC] + [os.path.join(ROOT, "include", "mtr_types.h")]
+    if not all(os.path.exists(d) for d in deps):
+        return None
+    if force or _stale(out, deps):
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", out] + \
+              [os.path.join(CSRC, f) for f in SYNTH_SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return out
+
+
+def build_all(force=False, verbose=False):
+    build_engine(force, verbose)
+    build_synth(force, verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, verbose=True)

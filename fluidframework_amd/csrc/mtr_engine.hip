@@ -1,0 +1,569 @@
+// mtr_engine.hip -- host side of the MI355X merge-tree replay engine: the C ABI of
+// include/mtr.h, device memory management and kernel launches.
+//
+// Memory layout in HBM (one slab per document, sized by mtr_caps):
+//   DocHdr                      64 B                  (collaboration window + arena cursors)
+//   leaves  [NF][segcap] u32    len seq rseq meta text props rm uid   (SoA, tree order)
+//   heap    [2][hcap]    u32    zamboni LRU heap (seq, uid), 1-based
+//   text    [tcap]       u16    UTF-16 text arena (segments hold offsets)
+//   props   [pcap]       u32    immutable property-set entries [n, k0, v0, ...]
+//   removers[rcap]       u32    cons cells of overlapping removers (client<<24 | next)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mtr.h"
+#include "apply.hip.h"
+#include "summary.hip.h"
+
+using namespace mtr;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const std::string& s) { g_err = s; }
+
+#define HIPCHK(x)                                                                  \
+    do {                                                                           \
+        hipError_t _e = (x);                                                       \
+        if (_e != hipSuccess) {                                                    \
+            set_err(std::string(#x) + ": " + hipGetErrorString(_e));               \
+            return -1;                                                             \
+        }                                                                          \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int ensure(size_t want) {
+        if (want <= n && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t bytes = std::max<size_t>(want, 1) * sizeof(T);
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            set_err("hipMalloc failed for " + std::to_string(bytes) + " bytes");
+            return -1;
+        }
+        n = std::max<size_t>(want, 1);
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+int pow2_at_least(int x) {
+    int c = 64;
+    while (c < x) c <<= 1;
+    return c;
+}
+
+}  // namespace
+
+struct mtr_engine {
+    mtr_options opt{};
+    mtr_caps caps{};
+    int device = 0;
+    uint32_t max_docs = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    // persistent document state
+    DevBuf<DocHdr> hdr;
+    DevBuf<uint32_t> seg, heap, prop, rm;
+    DevBuf<uint16_t> text;
+    // current batch (device copies)
+    uint32_t n_docs = 0;
+    uint32_t max_ops_per_doc = 0;
+    DevBuf<mtr_doc_desc> docs;
+    DevBuf<mtr_op> ops;
+    DevBuf<uint16_t> btext;
+    DevBuf<uint32_t> propop_off, propop_kv, key_off, key_index, val_off, val_eq, client_off;
+    DevBuf<uint8_t> key_bytes, val_bytes, client_bytes;
+    DevBuf<unsigned long long> stat;  // [0] ops applied
+    DevBuf<int32_t> red;              // small reduction buffer
+    DevBuf<uint32_t> scratch;         // E/V arrays for HBM-resident (global-mode) launches
+    // summaries
+    DevBuf<int64_t> out_size, out_off;
+    DevBuf<unsigned long long> out_hash;
+    DevBuf<uint8_t> out;
+    std::vector<int64_t> h_off, h_size;
+    std::vector<uint32_t> h_val_eq;  // host copy for export hashes
+    int64_t out_total = 0;
+    bool summarized = false;
+    // timing
+    double t_apply = 0, t_summary = 0;
+    int launches = 0;
+};
+
+// ------------------------------------------------------------------ small kernels
+__global__ void reset_kernel(DocHdr* h, uint32_t n) {
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n) return;
+    DocHdr z{};
+    z.height = 1;
+    z.local = -1;
+    z.fail_op = -1;
+    h[d] = z;
+}
+
+__global__ void cursor_reset_kernel(DocHdr* h, uint32_t n) {
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < n) h[d].op_cursor = 0;
+}
+
+// out[0] = max nseg, out[1] = max remaining ops, out[2] = max heapn
+__global__ void scan_state_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t n, int32_t* out) {
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n) return;
+    const DocHdr x = h[d];
+    atomicMax(&out[0], x.nseg);
+    int rem = x.status == MTR_OK ? int(docs[d].op_count) - x.op_cursor : 0;
+    atomicMax(&out[1], rem);
+    atomicMax(&out[2], x.heapn);
+}
+
+template <class T>
+static int upload(mtr_engine* e, DevBuf<T>& dst, const T* src, size_t n) {
+    if (dst.ensure(n)) return -1;
+    if (n) HIPCHK(hipMemcpyAsync(dst.p, src, n * sizeof(T), hipMemcpyHostToDevice, e->stream));
+    return 0;
+}
+
+extern "C" {
+
+const char* mtr_last_error(void) { return g_err.c_str(); }
+
+mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_docs, const mtr_caps* caps) {
+    auto* e = new mtr_engine();
+    e->opt = opt ? *opt : mtr_options{0, 1, 10000, 0};
+    if (e->opt.chunk_size <= 0) e->opt.chunk_size = 10000;
+    mtr_caps c{4096, 2048, 65536, 16384, 4096, 256};
+    if (caps) {
+        if (caps->max_segments) c.max_segments = caps->max_segments;
+        if (caps->heap_entries) c.heap_entries = caps->heap_entries;
+        if (caps->text_units) c.text_units = caps->text_units;
+        if (caps->prop_words) c.prop_words = caps->prop_words;
+        if (caps->remover_cells) c.remover_cells = caps->remover_cells;
+        if (caps->ops_per_launch) c.ops_per_launch = caps->ops_per_launch;
+    }
+    c.max_segments = (c.max_segments + 63) & ~63u;
+    c.heap_entries = (c.heap_entries + 63) & ~63u;
+    if (c.remover_cells > 0xfffffe) c.remover_cells = 0xfffffe;
+    e->caps = c;
+    e->device = device;
+    e->max_docs = max_docs;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_err("cannot open HIP device " + std::to_string(device));
+        delete e;
+        return nullptr;
+    }
+    for (auto& x : e->ev) (void)hipEventCreate(&x);
+    const size_t D = std::max<uint32_t>(max_docs, 1);
+    if (e->hdr.ensure(D) || e->seg.ensure(D * NF * c.max_segments) || e->heap.ensure(D * 2 * c.heap_entries) ||
+        e->text.ensure(D * c.text_units) || e->prop.ensure(D * c.prop_words) || e->rm.ensure(D * c.remover_cells) ||
+        e->stat.ensure(4) || e->red.ensure(4)) {
+        mtr_engine_destroy(e);
+        return nullptr;
+    }
+    if (mtr_reset(e) != MTR_OK) {
+        mtr_engine_destroy(e);
+        return nullptr;
+    }
+    return e;
+}
+
+int mtr_engine_destroy(mtr_engine* e) {
+    if (!e) return 0;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto* b : {&e->seg, &e->heap, &e->prop, &e->rm, &e->propop_off, &e->propop_kv, &e->key_off, &e->key_index,
+                    &e->val_off, &e->val_eq, &e->client_off})
+        b->release();
+    e->hdr.release();
+    e->text.release();
+    e->btext.release();
+    e->docs.release();
+    e->ops.release();
+    e->key_bytes.release();
+    e->val_bytes.release();
+    e->client_bytes.release();
+    e->stat.release();
+    e->red.release();
+    e->scratch.release();
+    e->out_size.release();
+    e->out_off.release();
+    e->out_hash.release();
+    e->out.release();
+    for (auto& x : e->ev)
+        if (x) (void)hipEventDestroy(x);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return 0;
+}
+
+int mtr_reset(mtr_engine* e) {
+    HIPCHK(hipSetDevice(e->device));
+    const uint32_t n = std::max<uint32_t>(e->max_docs, 1);
+    reset_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemsetAsync(e->stat.p, 0, 4 * sizeof(unsigned long long), e->stream));
+    e->summarized = false;
+    return MTR_OK;
+}
+
+int mtr_submit(mtr_engine* e, const mtr_batch* b) {
+    HIPCHK(hipSetDevice(e->device));
+    if (b->n_docs > e->max_docs) {
+        set_err("batch has more documents than the engine was created for");
+        return MTR_ERR_BAD_OP;
+    }
+    e->n_docs = b->n_docs;
+    uint32_t mx = 0;
+    for (uint32_t d = 0; d < b->n_docs; d++) mx = std::max(mx, b->docs[d].op_count);
+    e->max_ops_per_doc = mx;
+    const size_t nkv = b->n_propops ? size_t(b->propop_off[b->n_propops]) * 2 : 0;
+    const size_t ncl = 1 + [&] {
+        size_t m = 0;
+        for (uint32_t d = 0; d < b->n_docs; d++) m = std::max<size_t>(m, size_t(b->docs[d].client_base) + b->docs[d].n_clients);
+        return m;
+    }();
+    if (upload(e, e->docs, b->docs, b->n_docs) || upload(e, e->ops, b->ops, b->n_ops) ||
+        upload(e, e->btext, b->text, b->n_text) || upload(e, e->propop_off, b->propop_off, size_t(b->n_propops) + 1) ||
+        upload(e, e->propop_kv, b->propop_kv, nkv) || upload(e, e->key_off, b->key_off, size_t(b->n_keys) + 1) ||
+        upload(e, e->key_bytes, b->key_bytes, b->n_keys ? size_t(b->key_off[b->n_keys]) : 0) ||
+        upload(e, e->key_index, b->key_index, b->n_keys) || upload(e, e->val_off, b->val_off, size_t(b->n_vals) + 1) ||
+        upload(e, e->val_bytes, b->val_bytes, b->n_vals ? size_t(b->val_off[b->n_vals]) : 0) ||
+        upload(e, e->val_eq, b->val_eq, b->n_vals) || upload(e, e->client_off, b->client_off, ncl) ||
+        upload(e, e->client_bytes, b->client_bytes, size_t(b->client_off[ncl - 1])))
+        return -1;
+    e->h_val_eq.assign(b->val_eq, b->val_eq + b->n_vals);
+    cursor_reset_kernel<<<(b->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, b->n_docs);
+    HIPCHK(hipGetLastError());
+    e->summarized = false;
+    return MTR_OK;
+}
+
+static int read_state(mtr_engine* e, int32_t out[3]) {
+    HIPCHK(hipMemsetAsync(e->red.p, 0, 4 * sizeof(int32_t), e->stream));
+    scan_state_kernel<<<(e->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, e->n_docs, e->red.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, e->red.p, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return 0;
+}
+
+int mtr_run(mtr_engine* e) {
+    HIPCHK(hipSetDevice(e->device));
+    if (e->n_docs == 0) return MTR_OK;
+    const int K = int(e->caps.ops_per_launch ? e->caps.ops_per_launch : 0x7fffffff);
+    e->launches = 0;
+    e->t_apply = 0;
+    KParams P{};
+    P.hdr = e->hdr.p;
+    P.seg = e->seg.p;
+    P.heap = e->heap.p;
+    P.text = e->text.p;
+    P.prop = e->prop.p;
+    P.rm = e->rm.p;
+    P.segcap = int(e->caps.max_segments);
+    P.hcap = int(e->caps.heap_entries);
+    P.tcap = int(e->caps.text_units);
+    P.pcap = int(e->caps.prop_words);
+    P.rcap = int(e->caps.remover_cells);
+    P.new_length_calc = e->opt.new_length_calc;
+    P.n_docs = e->n_docs;
+    P.ops = e->ops.p;
+    P.docs = e->docs.p;
+    P.btext = e->btext.p;
+    P.propop_off = e->propop_off.p;
+    P.propop_kv = e->propop_kv.p;
+    P.key_index = e->key_index.p;
+    P.val_eq = e->val_eq.p;
+    P.stat_ops = e->stat.p;
+    P.trace = getenv("MTR_TRACE") ? 1 : 0;
+    P.trace_seq = getenv("MTR_TRACE_SEQ") ? atoi(getenv("MTR_TRACE_SEQ")) : -1;
+    int dev_lds = 0;
+    HIPCHK(hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device));
+    static std::once_flag once;
+    std::call_once(once, [&] {
+        (void)hipFuncSetAttribute((const void*)apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    for (;;) {
+        int32_t st[3];
+        if (read_state(e, st)) return -1;
+        const int maxseg = st[0], rem = st[1], maxheap = st[2];
+        if (rem <= 0) break;
+        const int k = std::min(K, rem);
+        int cap = pow2_at_least(maxseg + 2 * k + 8);
+        if (cap > P.segcap) cap = P.segcap;
+        int lhcap = std::min<int>(P.hcap, std::max(cap / 2, pow2_at_least(maxheap + 2 * k + 8)));
+        size_t lds = lds_bytes(cap, lhcap);
+        int kk = k;
+        P.global_mode = 0;
+        if (lds > size_t(160 * 1024)) {
+            // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
+            if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
+            P.global_mode = 1;
+            P.scratch = e->scratch.p;
+            cap = P.segcap;
+            lhcap = P.hcap;
+            lds = lds_bytes_global_mode();
+            kk = std::max(1, std::min(k, (cap - maxseg - 8) / 2));
+        } else {
+            kk = std::max(1, std::min(k, (cap - maxseg - 8) / 2));
+        }
+        P.cap = cap;
+        P.lhcap = lhcap;
+        P.ops_this_launch = kk;
+        HIPCHK(hipEventRecord(e->ev[0], e->stream));
+        apply_kernel<<<e->n_docs, NT, lds, e->stream>>>(P);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e->ev[1], e->stream));
+        HIPCHK(hipEventSynchronize(e->ev[1]));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+        e->t_apply += ms;
+        e->launches++;
+        if (kk < 1 || cap - maxseg - 8 < 2) {
+            set_err("document exceeds the LDS leaf capacity");
+            break;
+        }
+    }
+    e->summarized = false;
+    return MTR_OK;
+}
+
+int mtr_summarize(mtr_engine* e) {
+    HIPCHK(hipSetDevice(e->device));
+    const uint32_t n = e->n_docs;
+    if (n == 0) return MTR_OK;
+    if (e->out_size.ensure(n) || e->out_off.ensure(n) || e->out_hash.ensure(n)) return -1;
+    SParams P{};
+    P.hdr = e->hdr.p;
+    P.seg = e->seg.p;
+    P.text = e->text.p;
+    P.prop = e->prop.p;
+    P.rm = e->rm.p;
+    P.segcap = int(e->caps.max_segments);
+    P.tcap = int(e->caps.text_units);
+    P.pcap = int(e->caps.prop_words);
+    P.rcap = int(e->caps.remover_cells);
+    P.snapshot_v1 = e->opt.snapshot_v1;
+    P.chunk_size = e->opt.chunk_size;
+    P.new_length_calc = e->opt.new_length_calc;
+    P.n_docs = n;
+    P.docs = e->docs.p;
+    P.key_off = e->key_off.p;
+    P.key_bytes = e->key_bytes.p;
+    P.val_off = e->val_off.p;
+    P.val_bytes = e->val_bytes.p;
+    P.val_eq = e->val_eq.p;
+    P.client_off = e->client_off.p;
+    P.client_bytes = e->client_bytes.p;
+    P.out_size = e->out_size.p;
+    P.out_off = e->out_off.p;
+    P.out_hash = e->out_hash.p;
+    HIPCHK(hipEventRecord(e->ev[2], e->stream));
+    summary_size_kernel<<<n, 64, 0, e->stream>>>(P);
+    HIPCHK(hipGetLastError());
+    e->h_size.resize(n);
+    e->h_off.resize(n);
+    HIPCHK(hipMemcpyAsync(e->h_size.data(), e->out_size.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    int64_t tot = 0;
+    for (uint32_t d = 0; d < n; d++) {
+        e->h_off[d] = tot;
+        tot += e->h_size[d];
+    }
+    e->out_total = tot;
+    if (e->out.ensure(size_t(tot) + 16)) return -1;
+    HIPCHK(hipMemcpyAsync(e->out_off.p, e->h_off.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, e->stream));
+    P.out = e->out.p;
+    summary_write_kernel<<<n, 64, 0, e->stream>>>(P);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(e->ev[3], e->stream));
+    HIPCHK(hipEventSynchronize(e->ev[3]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[2], e->ev[3]));
+    e->t_summary = ms;
+    e->summarized = true;
+    return MTR_OK;
+}
+
+int mtr_sync(mtr_engine* e) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return MTR_OK;
+}
+
+int64_t mtr_get_summary(mtr_engine* e, uint32_t doc, uint8_t* out, int64_t cap, int64_t* blob_len, int32_t max_blobs) {
+    if (!e->summarized || doc >= e->n_docs) {
+        set_err("no summary for this document (call mtr_summarize first)");
+        return -1;
+    }
+    (void)hipSetDevice(e->device);
+    const int64_t sz = e->h_size[doc];
+    std::vector<uint8_t> buf(static_cast<size_t>(sz));
+    if (hipMemcpy(buf.data(), e->out.p + e->h_off[doc], size_t(sz), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    uint32_t nb;
+    std::memcpy(&nb, buf.data(), 4);
+    const int64_t payload = sz - 4 - 4 * int64_t(nb);
+    if (payload > cap || int32_t(nb) > max_blobs) return -payload;
+    int64_t off = 4 + 4 * int64_t(nb);
+    int64_t w = 0;
+    for (uint32_t k = 0; k < nb; k++) {
+        uint32_t len;
+        std::memcpy(&len, buf.data() + 4 + 4 * k, 4);
+        blob_len[k] = len;
+        std::memcpy(out + w, buf.data() + off, len);
+        off += len;
+        w += len;
+    }
+    return int64_t(nb);
+}
+
+int mtr_summary_hashes(mtr_engine* e, uint64_t* out, uint32_t n_docs) {
+    if (!e->summarized) return -1;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipMemcpy(out, e->out_hash.p, std::min(n_docs, e->n_docs) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return MTR_OK;
+}
+
+int64_t mtr_summary_bytes(mtr_engine* e) { return e->summarized ? e->out_total : -1; }
+
+// ---- host-side decoding of one document's slabs (parity checks, getText)
+struct HostDoc {
+    DocHdr h;
+    std::vector<uint32_t> seg;
+    std::vector<uint16_t> text;
+    std::vector<uint32_t> prop, rm;
+};
+
+static int fetch_doc(mtr_engine* e, uint32_t doc, HostDoc& hd) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(&hd.h, e->hdr.p + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
+    const size_t sc = e->caps.max_segments;
+    hd.seg.resize(NF * sc);
+    HIPCHK(hipMemcpy(hd.seg.data(), e->seg.p + size_t(doc) * NF * sc, NF * sc * 4, hipMemcpyDeviceToHost));
+    hd.text.resize(std::max(hd.h.textused, 1));
+    HIPCHK(hipMemcpy(hd.text.data(), e->text.p + size_t(doc) * e->caps.text_units, hd.text.size() * 2,
+                     hipMemcpyDeviceToHost));
+    hd.prop.resize(std::max(hd.h.propused, 1));
+    HIPCHK(hipMemcpy(hd.prop.data(), e->prop.p + size_t(doc) * e->caps.prop_words, hd.prop.size() * 4,
+                     hipMemcpyDeviceToHost));
+    hd.rm.resize(std::max(hd.h.rmused, 1));
+    HIPCHK(hipMemcpy(hd.rm.data(), e->rm.p + size_t(doc) * e->caps.remover_cells, hd.rm.size() * 4,
+                     hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int64_t mtr_get_text(mtr_engine* e, uint32_t doc, uint16_t* out, int64_t cap) {
+    HostDoc hd;
+    if (doc >= e->max_docs || fetch_doc(e, doc, hd)) return -1;
+    const size_t sc = e->caps.max_segments;
+    int64_t n = 0;
+    for (int i = 0; i < hd.h.nseg; i++) {
+        const uint32_t m = hd.seg[F_META * sc + i];
+        const int32_t rs = int32_t(hd.seg[F_RSEQ * sc + i]);
+        if (rs != RNONE || (m & M_MARKER)) continue;  // local view: removed segments are not visible
+        const uint32_t len = hd.seg[F_LEN * sc + i], t = hd.seg[F_TEXT * sc + i];
+        for (uint32_t k = 0; k < len; k++) {
+            if (out && n < cap) out[n] = hd.text[t + k];
+            n++;
+        }
+    }
+    return n;
+}
+
+int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index) {
+    if (doc >= e->max_docs) return -1;
+    DocHdr h;
+    (void)hipSetDevice(e->device);
+    if (hipStreamSynchronize(e->stream) != hipSuccess ||
+        hipMemcpy(&h, e->hdr.p + doc, sizeof(DocHdr), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    if (op_index) *op_index = h.fail_op;
+    return h.status;
+}
+
+int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32_t* height) {
+    HostDoc hd;
+    if (doc >= e->max_docs || fetch_doc(e, doc, hd)) return -1;
+    const size_t sc = e->caps.max_segments;
+    if (height) *height = hd.h.height;
+    if (hd.h.nseg > cap) return -int64_t(hd.h.nseg);
+    for (int i = 0; i < hd.h.nseg; i++) {
+        const uint32_t m = hd.seg[F_META * sc + i];
+        const int32_t rs = int32_t(hd.seg[F_RSEQ * sc + i]);
+        int nrem = 0;
+        if (rs != RNONE) {
+            nrem = 1;
+            if (m & M_OVERLAP) {
+                uint32_t c = hd.seg[F_RM * sc + i];
+                while (c != 0xffffffu) {
+                    nrem++;
+                    c = hd.rm[c] & 0xffffffu;
+                }
+            }
+        }
+        uint32_t h = 0;
+        const uint32_t pr = hd.seg[F_PROPS * sc + i];
+        if (pr != NONE32) {
+            h = 2166136261u ^ 1u;
+            for (uint32_t q = 0; q < hd.prop[pr]; q++) {  // same hash as the oracle export
+                const uint32_t v = hd.prop[pr + 2 + 2 * q];
+                h = (h ^ hd.prop[pr + 1 + 2 * q]) * 16777619u;
+                h = (h ^ (v < e->h_val_eq.size() ? e->h_val_eq[v] : v)) * 16777619u;
+            }
+        }
+        int32_t* r = out + 8 * i;
+        r[0] = int32_t(hd.seg[F_LEN * sc + i]);
+        r[1] = int32_t(hd.seg[F_SEQ * sc + i]);
+        r[2] = dec_client(m & M_CLIENT_MASK);
+        r[3] = rs == RNONE ? INT32_MIN : rs;
+        r[4] = nrem;
+        r[5] = int32_t((m & M_BND_MASK) >> M_BND_SHIFT);
+        r[6] = (m & M_MARKER) ? 1 : 0;
+        r[7] = int32_t(h);
+    }
+    return hd.h.nseg;
+}
+
+int mtr_stats(mtr_engine* e, int64_t* out, int32_t n) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    std::vector<DocHdr> h(e->n_docs);
+    if (e->n_docs) HIPCHK(hipMemcpy(h.data(), e->hdr.p, e->n_docs * sizeof(DocHdr), hipMemcpyDeviceToHost));
+    unsigned long long ops = 0;
+    HIPCHK(hipMemcpy(&ops, e->stat.p, sizeof(ops), hipMemcpyDeviceToHost));
+    int64_t v[8] = {int64_t(ops), e->n_docs, 0, 0, 0, e->launches, 0, 0};
+    for (auto& x : h) {
+        v[2] = std::max<int64_t>(v[2], x.nseg);
+        v[3] += x.nseg;
+        v[4] += x.status != MTR_OK;
+        v[6] = std::max<int64_t>(v[6], x.max_heap);
+        v[7] = std::max<int64_t>(v[7], x.textused);
+    }
+    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
+    return MTR_OK;
+}
+
+int mtr_last_timing(mtr_engine* e, double* out, int32_t n) {
+    double v[3] = {e->t_apply, e->t_summary, double(e->launches)};
+    for (int i = 0; i < n && i < 3; i++) out[i] = v[i];
+    return MTR_OK;
+}
+
+}  // extern "C"

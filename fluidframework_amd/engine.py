@@ -1,0 +1,193 @@
+"""ctypes binding of libmtr.so (include/mtr.h) and the observer-Client mirror.
+
+The product path: a batch packed by :mod:`fluidframework_amd.batch` goes to the HIP engine through
+the C ABI.  There is no CPU fallback -- if libmtr.so (gfx950 code object) cannot be loaded or no
+HIP device is present, construction fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class MtrCaps(C.Structure):
+    _fields_ = [
+        ("max_segments", C.c_uint32),
+        ("heap_entries", C.c_uint32),
+        ("text_units", C.c_uint32),
+        ("prop_words", C.c_uint32),
+        ("remover_cells", C.c_uint32),
+        ("ops_per_launch", C.c_uint32),
+    ]
+
+
+def lib():
+    """Load libmtr.so (never falls back to anything else)."""
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libmtr.so")
+        if not os.path.exists(path):
+            raise EngineError(f"{path} missing: build it with `python -m fluidframework_amd.build`")
+        L = C.CDLL(path)
+        L.mtr_engine_create.restype = C.c_void_p
+        L.mtr_engine_create.argtypes = [C.POINTER(abi.MtrOptions), C.c_int, C.c_uint32, C.POINTER(MtrCaps)]
+        L.mtr_engine_destroy.argtypes = [C.c_void_p]
+        for name in ("mtr_reset", "mtr_run", "mtr_summarize", "mtr_sync"):
+            getattr(L, name).argtypes = [C.c_void_p]
+            getattr(L, name).restype = C.c_int
+        L.mtr_submit.argtypes = [C.c_void_p, C.c_void_p]
+        L.mtr_submit.restype = C.c_int
+        L.mtr_get_summary.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]
+        L.mtr_get_summary.restype = C.c_int64
+        L.mtr_summary_hashes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
+        L.mtr_summary_hashes.restype = C.c_int
+        L.mtr_summary_bytes.argtypes = [C.c_void_p]
+        L.mtr_summary_bytes.restype = C.c_int64
+        L.mtr_get_text.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
+        L.mtr_get_text.restype = C.c_int64
+        L.mtr_doc_status.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_int32)]
+        L.mtr_doc_status.restype = C.c_int
+        L.mtr_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
+        L.mtr_export.restype = C.c_int64
+        L.mtr_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        L.mtr_stats.restype = C.c_int
+        L.mtr_last_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+        L.mtr_last_timing.restype = C.c_int
+        L.mtr_last_error.restype = C.c_char_p
+        _LIB = L
+    return _LIB
+
+
+def _err() -> str:
+    return (lib().mtr_last_error() or b"").decode(errors="replace")
+
+
+class Engine:
+    """One engine = the observer Clients of up to ``max_docs`` documents on one GPU."""
+
+    def __init__(self, max_docs, *, device=0, new_length_calc=False, snapshot_v1=True, chunk_size=10000,
+                 max_segments=0, heap_entries=0, text_units=0, prop_words=0, remover_cells=0, ops_per_launch=0):
+        self.opts = abi.MtrOptions(int(new_length_calc), int(snapshot_v1), int(chunk_size), 0)
+        self.caps = MtrCaps(max_segments, heap_entries, text_units, prop_words, remover_cells, ops_per_launch)
+        self.max_docs = int(max_docs)
+        h = lib().mtr_engine_create(C.byref(self.opts), int(device), self.max_docs, C.byref(self.caps))
+        if not h:
+            raise EngineError(f"mtr_engine_create failed: {_err()}")
+        self.h = h
+        self._batch = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mtr_engine_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise EngineError(f"{what} failed ({rc}): {_err()}")
+
+    def reset(self):
+        self._check(lib().mtr_reset(self.h), "mtr_reset")
+
+    def submit(self, batch):
+        self._batch = batch  # keep host arrays alive until the copies completed
+        self._check(lib().mtr_submit(self.h, C.addressof(batch.c)), "mtr_submit")
+
+    def run(self):
+        self._check(lib().mtr_run(self.h), "mtr_run")
+
+    def summarize(self):
+        self._check(lib().mtr_summarize(self.h), "mtr_summarize")
+
+    def sync(self):
+        self._check(lib().mtr_sync(self.h), "mtr_sync")
+
+    def apply(self, batch):
+        self.submit(batch)
+        self.run()
+        self.sync()
+
+    def summary(self, doc) -> list[bytes]:
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, dtype="u1")
+            lens = np.zeros(4096, dtype="<i8")
+            r = lib().mtr_get_summary(self.h, doc, out.ctypes.data, cap, lens.ctypes.data, 4096)
+            if r >= 0:
+                res, off = [], 0
+                for k in range(r):
+                    res.append(out[off:off + lens[k]].tobytes())
+                    off += int(lens[k])
+                return res
+            if r == -1:
+                raise EngineError(_err())
+            cap = -r + 16
+
+    def hashes(self, n=None) -> np.ndarray:
+        n = self.max_docs if n is None else n
+        out = np.zeros(n, dtype="<u8")
+        self._check(lib().mtr_summary_hashes(self.h, out.ctypes.data, n), "mtr_summary_hashes")
+        return out
+
+    def summary_bytes(self) -> int:
+        return int(lib().mtr_summary_bytes(self.h))
+
+    def text(self, doc) -> str:
+        n = lib().mtr_get_text(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(_err())
+        buf = np.zeros(max(n, 1), dtype="<u2")
+        lib().mtr_get_text(self.h, doc, buf.ctypes.data, n)
+        return buf[:n].tobytes().decode("utf-16-le", "surrogatepass")
+
+    def status(self, doc):
+        op = C.c_int32(-1)
+        st = lib().mtr_doc_status(self.h, doc, C.byref(op))
+        return st, op.value
+
+    def export(self, doc):
+        h = C.c_int32(0)
+        n = lib().mtr_export(self.h, doc, None, 0, C.byref(h))
+        n = -n if n < 0 else n
+        out = np.zeros((max(n, 1), 8), dtype="<i4")
+        lib().mtr_export(self.h, doc, out.ctypes.data, n, C.byref(h))
+        return out[:n], h.value
+
+    def stats(self) -> dict:
+        out = np.zeros(8, dtype="<i8")
+        self._check(lib().mtr_stats(self.h, out.ctypes.data, 8), "mtr_stats")
+        keys = ["ops", "docs", "max_leaves", "sum_leaves", "bad_docs", "launches", "max_heap", "max_text"]
+        return dict(zip(keys, (int(x) for x in out)))
+
+    def timing(self) -> dict:
+        out = np.zeros(3, dtype="<f8")
+        lib().mtr_last_timing(self.h, out.ctypes.data, 3)
+        return {"apply_ms": float(out[0]), "summary_ms": float(out[1]), "apply_launches": int(out[2])}
+
+
+def caps_for(batch, margin=1.25):
+    """Per-document arena capacities that a batch can never exceed (host-side bound)."""
+    ops = batch.ops
+    docs = batch.docs
+    n_ops = docs["op_count"].astype(np.int64)
+    max_ops = int(n_ops.max()) if len(docs) else 0
+    max_text = int(docs["text_count"].max()) if len(docs) else 0
+    seg = 2 * max_ops + 64
+    text = int(2 * max_text * margin) + 4096
+    npk = np.diff(batch.propop_off.astype(np.int64)) if len(batch.propop_off) > 1 else np.zeros(1, np.int64)
+    max_keys = int(npk.max()) if npk.size else 0
+    prop = int((2 * max_ops) * (1 + 2 * (max_keys + 8)) * 0.25) + 4096
+    rem = max_ops + 64
+    return dict(max_segments=seg, heap_entries=seg, text_units=text, prop_words=prop, remover_cells=rem)

@@ -1,0 +1,107 @@
+/*
+ * mtr.h -- C ABI of the MI355X batched merge-tree replay engine (libmtr.so).
+ *
+ * The engine is a drop-in for the *observer* (all-ops-remote) path of
+ * @fluidframework/merge-tree's Client (packages/dds/merge-tree/src/client.ts:98):
+ * a scribe-like summarizer or a replay tool hands it ISequencedDocumentMessage
+ * batches for many documents at once and asks for each document's summary.
+ * Paths below are relative to the reference's packages/dds/merge-tree/src/.
+ *
+ *   reference                                      | engine
+ *   -----------------------------------------------+------------------------------------------
+ *   new Client(specToSegment, logger, options)      | mtr_engine_create   (client.ts:107-131)
+ *     IMergeTreeOptions (mergeTree.ts:400-438)      |   mtr_options
+ *   Client.startOrUpdateCollaboration(id, min, cur) | MTR_OP_START_COLLAB record (client.ts:1133)
+ *   Client.applyMsg(msg) for every message          | mtr_submit + mtr_run (client.ts:858-887)
+ *   Client.updateSeqNumbers(min, seq)               | MTR_F_LAST / MTR_OP_SEQ records (client.ts:877)
+ *   Client.summarize(runtime, handle, ser, [])      | mtr_summarize + mtr_get_summary (client.ts:966)
+ *   createTextHelper().getText(...)                 | mtr_get_text (MergeTreeTextHelper.ts:20)
+ *   assert(cond, 0xNNN) / UsageError                | mtr_doc_status (per-document status word)
+ *
+ * No exceptions cross the ABI; every call returns MTR_OK (0) or an error code.
+ * All pointers are host pointers; device memory is owned by the engine.
+ */
+#ifndef MTR_H
+#define MTR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mtr_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mtr_engine mtr_engine;
+
+/* Per-document device arena capacities (0 = engine default). */
+typedef struct mtr_caps {
+    uint32_t max_segments;   /* leaf records per document */
+    uint32_t heap_entries;   /* zamboni LRU heap entries per document (heap.ts:11) */
+    uint32_t text_units;     /* UTF-16 text arena per document */
+    uint32_t prop_words;     /* property-set arena per document (u32 words) */
+    uint32_t remover_cells;  /* overlapping-remove list cells per document */
+    uint32_t ops_per_launch; /* ops applied per document per kernel launch (0 = all) */
+} mtr_caps;
+
+/* Create an engine for up to max_docs documents on HIP device `device`. */
+mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_docs, const mtr_caps* caps);
+int mtr_engine_destroy(mtr_engine* e);
+
+/* Forget every document (all state back to a fresh Client); keeps allocations. */
+int mtr_reset(mtr_engine* e);
+
+/* Copy a batch to the device (async on the engine stream).  Document i of the batch is
+ * engine document i.  The batch's host arrays may be reused after mtr_sync. */
+int mtr_submit(mtr_engine* e, const mtr_batch* b);
+
+/* Apply the submitted ops (Client.applyMsg for each message, in order, per document). Async. */
+int mtr_run(mtr_engine* e);
+
+/* Build every document's summary blobs on the device (Client.summarize). Async except for
+ * one small size read-back between the sizing and writing passes. */
+int mtr_summarize(mtr_engine* e);
+
+/* Wait for all queued work on the engine stream. */
+int mtr_sync(mtr_engine* e);
+
+/* Blobs of one document after mtr_summarize: writes them back-to-back to out (cap bytes),
+ * blob_len[k] = bytes of blob k (order: header, body / body_0, body_1, ...).
+ * Returns the number of blobs, or -(bytes needed) when cap is too small. */
+int64_t mtr_get_summary(mtr_engine* e, uint32_t doc, uint8_t* out, int64_t cap, int64_t* blob_len,
+                        int32_t max_blobs);
+
+/* 64-bit FNV-1a of every document's summary (blob lengths + bytes), n_docs entries. */
+int mtr_summary_hashes(mtr_engine* e, uint64_t* out, uint32_t n_docs);
+
+/* Total summary bytes of all documents (after mtr_summarize). */
+int64_t mtr_summary_bytes(mtr_engine* e);
+
+/* Local-view text of one document (UTF-16 units); returns length (writes <= cap units). */
+int64_t mtr_get_text(mtr_engine* e, uint32_t doc, uint16_t* out, int64_t cap);
+
+/* Per-document status: MTR_OK or an MTR_ERR_* code; *op_index = op that failed (or -1). */
+int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index);
+
+/* Leaf records of one document in the oracle's export format (8 int32 per leaf:
+ * len, seq, client, removed_seq|INT32_MIN, n_removers, bnd, is_marker, props_hash).
+ * Returns #leaves or -(needed); *height = tree height. */
+int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap_leaves, int32_t* height);
+
+/* Engine-wide counters: out[0]=ops applied, out[1]=docs, out[2]=max leaves in any doc,
+ * out[3]=sum of leaves, out[4]=docs with non-OK status, out[5]=kernel launches of the last run,
+ * out[6]=max heap entries, out[7]=max text units used. */
+int mtr_stats(mtr_engine* e, int64_t* out, int32_t n);
+
+/* Device time (ms) of the last mtr_run / mtr_summarize measured with HIP events on the
+ * engine stream: out[0]=apply, out[1]=summarize, out[2]=apply kernel launches. */
+int mtr_last_timing(mtr_engine* e, double* out, int32_t n);
+
+/* Human-readable description of the last engine-level error (static storage). */
+const char* mtr_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTR_H */

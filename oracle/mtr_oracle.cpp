@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -35,6 +37,12 @@ constexpr int kLocalClientId = -1;           // constants.ts:14
 constexpr int kNonCollabClient = -2;         // constants.ts:15
 constexpr int kUndef = -1;                   // "undefined" node length
 constexpr int64_t kMaxSafe = 9007199254740991LL;
+int g_trace = 0;
+int g_trace_seq = -1;
+#define OTRACE(...)                          \
+    do {                                     \
+        if (g_trace) printf(__VA_ARGS__);    \
+    } while (0)
 
 struct Block;
 
@@ -371,6 +379,13 @@ class Tree {
         return s != nullptr && s->seq == kUnassignedSeq;
     }
 
+    int leafIndex(Seg* x) {
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        for (size_t i = 0; i < lv.size(); i++)
+            if (lv[i] == x) return int(i);
+        return -1;
+    }
     // split, mergeTree.ts:1858-1871
     Block* split(Block* node) {
         const int half = kMaxNodesInBlock / 2;
@@ -546,6 +561,7 @@ class Tree {
             scourNode(cb, hold);
             cb->parent = nullptr;
         }
+        OTRACE("PACK items=%d\n", int(hold.size()));
         if (!hold.empty()) {
             int total = int(hold.size());
             const int halfMax = kMaxNodesInBlock / 2;
@@ -578,19 +594,35 @@ class Tree {
     }
 
     // zamboniSegments, zamboni.ts:19-60
+    void dumpLeaves(const char* tag) {
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        for (size_t i = 0; i < lv.size(); i++) {
+            Seg* s = lv[i];
+            int bnd = 0;
+            const Node* n = s;
+            while (n->parent && n->index == 0) { bnd++; n = n->parent; }
+            printf("%s %zu len=%d seq=%d rs=%d bnd=%d\n", tag, i, s->len, s->seq, s->removed ? s->removedSeq : -1, bnd);
+        }
+    }
+    int curOpSeq = -1;
     void zamboniSegments() {
         if (!collaborating) return;
+        if (g_trace && curOpSeq == g_trace_seq) dumpLeaves("DUMP");
         for (int i = 0; i < kZamboniSegmentsMax; i++) {
             const LRUEntry* top = heap.peek();
             if (!top || top->maxSeq > minSeq) break;
             LRUEntry e = heap.get();
             Seg* s = e.segment;
+            OTRACE("ZPOP seq=%d linked=%d ns=%d leaf=%d\n", e.maxSeq, s->parent ? 1 : 0,
+                   s->parent ? s->parent->needsScour : -9, leafIndex(s));
             if (s->parent && s->parent->needsScour != 0) {
                 Block* block = s->parent;
                 std::vector<Node*> copy;
                 scourNode(block, copy);
                 block->needsScour = 0;
                 int newCount = int(copy.size());
+                OTRACE("SCOUR n=%d kept=%d\n", block->childCount, newCount);
                 if (newCount < block->childCount) {
                     for (int j = 0; j < kMaxNodesInBlock; j++) block->children[j] = nullptr;
                     block->childCount = newCount;
@@ -725,6 +757,7 @@ class Tree {
     }
 
     int apply(const mtr_op& op, const mtr_doc_desc& dd) {
+        curOpSeq = op.seq;
         switch (op.type) {
             case MTR_OP_INSERT: {
                 Seg* s = segmentFromSpec(op, dd);
@@ -934,6 +967,12 @@ struct oracle_doc {
 };
 
 extern "C" {
+
+void oracle_set_trace(int on) {
+    g_trace = on;
+    const char* ts = getenv("MTR_TRACE_SEQ");
+    g_trace_seq = ts ? atoi(ts) : -1;
+}
 
 oracle_doc* oracle_doc_new(const mtr_options* opt) {
     mtr_options o{0, 1, 10000, 0};

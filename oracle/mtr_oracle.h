@@ -45,6 +45,9 @@ int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap_leaves, int32
 /* Collaboration window state: out[0]=minSeq out[1]=currentSeq out[2]=#heap entries out[3]=#leaves */
 void oracle_doc_state(oracle_doc* d, int64_t* out);
 
+/* Debug: print zamboni decisions to stdout */
+void oracle_set_trace(int on);
+
 /* Length of the doc in the (ref_seq, client) view (MergeTree.getLength, mergeTree.ts:757) */
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client);
 

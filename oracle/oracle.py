@@ -36,6 +36,7 @@ def lib():
         L.oracle_doc_export.restype = C.c_int64
         L.oracle_doc_export.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
         L.oracle_doc_state.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_set_trace.argtypes = [C.c_int]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         _LIB = L
