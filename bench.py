@@ -1,0 +1,224 @@
+"""Benchmark: sequenced merge-tree ops applied per second over C3-shaped documents, with bit-exact
+summaries (BASELINE.json metric).
+
+One step = one replay of every document's op log from an empty observer Client plus its V1 summary
+(Client.applyMsg for every message, then Client.summarize), i.e. mtr_reset + mtr_run + mtr_summarize.
+Inputs are recorded on the device before the timed region (record mode of the engine, seeded recipe
+include/mtr_synth.h), so the timed region starts with every op log resident in HBM.
+
+Single GPU:   python bench.py
+Multi GPU:    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Documents are sharded over ranks (weak scaling: every rank replays its own `--docs` documents); the only
+collective is the final RCCL reduction of counters and summary digests.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "sequenced ops applied/sec (whole node) over 100k docs, bit-exact summaries"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--docs", type=int, default=100_000, help="documents per GPU (C3: 100k)")
+    ap.add_argument("--ops", type=int, default=1_000, help="sequenced messages per document (C3: 1k)")
+    ap.add_argument("--writers", type=int, default=8)
+    ap.add_argument("--max-lag", type=int, default=32)
+    ap.add_argument("--ops-per-launch", type=int, default=256)
+    ap.add_argument("--cpu-sample-docs", type=int, default=4000)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group("nccl")
+        dist = dist_mod
+
+    from fluidframework_amd.engine import Engine
+    from fluidframework_amd.synth import make_cfg, tables
+
+    n, ops = a.docs, a.ops
+    tabs = tables(writers=a.writers)
+    cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=rank * n)
+    text_units = 2 * int(cfg.text_cap) + 1024
+    eng = Engine(n, device=local, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=text_units,
+                 prop_words=16384, remover_cells=4096, ops_per_launch=a.ops_per_launch)
+
+    t0 = time.time()
+    eng.generate(cfg, tabs)  # untimed: record the op logs on the device
+    gen_s = time.time() - t0
+    gen_stats = eng.stats()
+    if gen_stats["bad_docs"]:
+        raise SystemExit(f"record mode left {gen_stats['bad_docs']} documents in an error state")
+
+    def step():
+        eng.reset()
+        eng.run()
+        eng.summarize()
+
+    for _ in range(a.warmup):
+        step()
+    eng.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    eng.sync()
+    apply_ms = summary_ms = 0.0
+    launches = 0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        tm = eng.timing()
+        apply_ms += tm["apply_ms"]
+        summary_ms += tm["summary_ms"]
+        launches += tm["apply_launches"]
+    eng.sync()
+    elapsed = time.perf_counter() - t0
+    barrier()
+
+    st = eng.stats()  # counters of the last step
+    hashes = eng.hashes(n)
+    messages = n * ops
+    local_vals = np.array([elapsed, float(messages), float(st["bad_docs"])], dtype=np.float64)
+    digest = int(np.bitwise_xor.reduce(hashes.view(np.uint64))) if n else 0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor(local_vals, dtype=torch.float64, device=f"cuda:{local}")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0].item())
+        total_messages = float(t[1].item())
+        bad = float(t[2].item())
+        d = torch.tensor([digest & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_reduce(d, op=dist.ReduceOp.SUM)  # cross-shard checksum over RCCL/xGMI
+        digest = int(d.item())
+    else:
+        total_messages = float(messages)
+        bad = float(st["bad_docs"])
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = 1000.0 * elapsed / a.steps
+    value = total_messages * a.steps / elapsed
+    # algorithmic bytes: B_op = 16*S_d(t) + 32 + 2*L_ins, per step on this rank
+    b_step = 16.0 * st["sum_leaves_before_op"] + 32.0 * messages + 2.0 * st["text_units_inserted"]
+    apply_s = apply_ms / 1000.0 / a.steps
+    launches_per_step = max(1, launches // a.steps)
+    achieved = b_step / apply_s / 1e9 if apply_s > 0 else 0.0
+    traffic = None
+    if os.path.exists(a.traffic_file):
+        try:
+            tf = json.load(open(a.traffic_file))
+            if tf.get("docs") == n and tf.get("ops") == ops:
+                traffic = tf.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    roofline = {
+        "bound": "hbm",
+        "kernel": "mtr::apply_kernel",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "algorithmic_bytes_per_launch": b_step / launches_per_step,
+        "avg_launch_ms": apply_ms / max(1, launches),
+        "launches_per_step": launches_per_step,
+        "model": "B_op = 16*S_d(t) + 32 + 2*L_ins (SURVEY.md 8d)",
+    }
+
+    cpu = None
+    bit_exact = {"checked_docs": 0, "equal": 0}
+    if not a.no_cpu_baseline and world == 1:
+        from oracle.oracle import replay_batch
+
+        k = min(a.cpu_sample_docs, n)
+        sample = eng.download(0, k)
+        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        secs, ohash, ost = replay_batch(sample, 0, k, threads)
+        eq = int((ohash == hashes[:k]).sum())
+        bit_exact = {"checked_docs": k, "equal": eq, "oracle_errors": int((ost != 0).sum())}
+        cpu = {
+            "value": round(k * ops / secs, 1),
+            "unit": "ops/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"first {k} of the {n} documents ({k * ops} messages), replay + V1 summary, one document "
+                      f"per task on {threads} host threads (reference-algorithm C++ restatement, not Node)",
+            "seconds": round(secs, 3),
+        }
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: seeded recipe include/mtr_synth.h recorded on the device (record mode)",
+        "config": {
+            "workload": f"C3: {n} docs/GPU x {ops} ops, {a.writers} writers, lag<={a.max_lag}, V1 summaries",
+            "docs_per_gpu": n,
+            "ops_per_doc": ops,
+            "writers": a.writers,
+            "max_lag": a.max_lag,
+            "parallelism": f"doc-sharded x{world}",
+        },
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "bit_exact_sample": bit_exact,
+        "detail": {
+            "apply_ms_per_step": round(apply_ms / a.steps, 3),
+            "summary_ms_per_step": round(summary_ms / a.steps, 3),
+            "summary_bytes": eng.summary_bytes(),
+            "bad_docs": int(bad),
+            "digest": digest,
+            "generate_s": round(gen_s, 2),
+            "max_leaves": st["max_leaves"],
+            "mean_leaves_before_op": st["sum_leaves_before_op"] / max(1, messages),
+        },
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

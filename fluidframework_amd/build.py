@@ -16,7 +16,6 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 ENGINE_SRC = ["mtr_engine.hip"]
 ENGINE_DEPS = ["apply.hip.h", "summary.hip.h", "mtr_engine.hip"]
-SYNTH_SRC = ["synth.cpp"]
 
 
 def _stale(target, deps):
@@ -28,8 +27,8 @@ def _stale(target, deps):
 
 def build_engine(force=False, verbose=False):
     out = os.path.join(HERE, "libmtr.so")
-    deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", "mtr.h"),
-                                                           os.path.join(ROOT, "include", "mtr_types.h")]
+    deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", h)
+                                                           for h in ("mtr.h", "mtr_types.h", "mtr_synth.h")]
     if force or _stale(out, deps):
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-result", "-o", out] + [os.path.join(CSRC, f) for f in ENGINE_SRC]
@@ -39,23 +38,8 @@ def build_engine(force=False, verbose=False):
     return out
 
 
-def build_synth(force=False, verbose=False):
-    out = os.path.join(HERE, "libmtrsynth.so")
-    deps = [os.path.join(CSRC, f) for f in SYNTH_SRC] + [os.path.join(ROOT, "include", "mtr_types.h")]
-    if not all(os.path.exists(d) for d in deps):
-        return None
-    if force or _stale(out, deps):
-        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", out] + \
-              [os.path.join(CSRC, f) for f in SYNTH_SRC]
-        if verbose:
-            print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
-    return out
-
-
 def build_all(force=False, verbose=False):
     build_engine(force, verbose)
-    build_synth(force, verbose)
 
 
 if __name__ == "__main__":

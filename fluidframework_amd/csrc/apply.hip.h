@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "../../include/mtr_types.h"
+#include "../../include/mtr_synth.h"
 
 namespace mtr {
 
@@ -54,7 +55,7 @@ struct DocHdr {
     int32_t nseg, height, minseq, curseq;
     int32_t collab, local, heapn, uidnext;
     int32_t textused, propused, rmused, status;
-    int32_t op_cursor, fail_op, max_heap, pad;
+    int32_t op_cursor, fail_op, max_heap, texthalf;  // texthalf: active half of the text arena
 };
 
 // number of 32-bit SoA fields per leaf kept in HBM and LDS
@@ -84,6 +85,13 @@ struct KParams {
     const uint32_t* key_index;
     const uint32_t* val_eq;
     unsigned long long* stat_ops;  // ops applied (atomic)
+    // record mode (synthetic workloads): ops are drawn from include/mtr_synth.h with this
+    // engine's own exact view lengths, written to gen_ops/gen_text, then applied
+    int32_t gen;
+    mtr_synth_cfg gen_cfg;
+    mtr_synth_state* gen_state;   // [doc]
+    mtr_op* gen_ops;              // == ops, writable
+    uint16_t* gen_text;           // == btext, writable
     int32_t trace;                 // debug: printf zamboni decisions of document 0
     int32_t trace_seq;             // debug: dump leaves at zamboni of this op seq
 };
@@ -96,7 +104,8 @@ struct Sc {
     int b0, b1, b2, b3;
     int b4, b5, b6, b7;
     int red[2 * NWAVES];
-    int fail_op, max_heap, ops_done, pad;
+    int fail_op, max_heap, ops_done, texthalf;
+    unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted text units
 };
 
 struct View {
@@ -119,6 +128,7 @@ struct Lds {
     int* hseq;
     uint32_t* huid;
     Sc* sc;
+    mtr_synth_state* gst;
     // document slabs in HBM
     uint16_t* gtext;
     uint32_t* gprop;
@@ -511,8 +521,11 @@ __device__ inline bool can_append(const Lds& L, int a, int b) {  // TextSegment.
 }
 
 // prev.append(seg) (textSegment.ts:99-103): text of b follows text of a
+__device__ inline int text_end(const Sc* sc, const KParams& P) { return (P.tcap / 2) * (sc->texthalf + 1); }
+
 __device__ void text_append(Lds& L, const KParams& P, int a, int b) {
     Sc* sc = L.sc;
+    const int tend = text_end(sc, P);
     uint32_t oa = L.text[a], ob = L.text[b];
     int la = L.len[a], lb = L.len[b];
     if (oa + uint32_t(la) == ob) {
@@ -520,19 +533,51 @@ __device__ void text_append(Lds& L, const KParams& P, int a, int b) {
         return;
     }
     if (oa + uint32_t(la) == uint32_t(sc->textused)) {
-        if (sc->textused + lb > P.tcap) { sc->status = MTR_ERR_CAPACITY; return; }
+        if (sc->textused + lb > tend) { sc->status = MTR_ERR_CAPACITY; return; }
         for (int k = 0; k < lb; k++) L.gtext[sc->textused + k] = L.gtext[ob + k];
         sc->textused += lb;
         L.len[a] = la + lb;
         return;
     }
-    if (sc->textused + la + lb > P.tcap) { sc->status = MTR_ERR_CAPACITY; return; }
+    if (sc->textused + la + lb > tend) { sc->status = MTR_ERR_CAPACITY; return; }
     uint32_t d = uint32_t(sc->textused);
     for (int k = 0; k < la; k++) L.gtext[d + k] = L.gtext[oa + k];
     for (int k = 0; k < lb; k++) L.gtext[d + la + k] = L.gtext[ob + k];
     sc->textused += la + lb;
     L.text[a] = d;
     L.len[a] = la + lb;
+}
+
+// Semi-space compaction of the text arena: copy every leaf's text into the other half in leaf
+// order (block prefix scan of lengths), then switch halves.  Dead text (removed/merged leaves)
+// is dropped; split halves that shared text get their own copies.
+__device__ void text_gc(Lds& L, const KParams& P) {
+    Sc* sc = L.sc;
+    const int S = sc->nseg;
+    const int per = (S + NT - 1) / NT;
+    const int lo = min(S, int(threadIdx.x) * per), hi = min(S, lo + per);
+    int sum = 0;
+    for (int i = lo; i < hi; i++)
+        if (!(L.meta[i] & M_MARKER)) sum += L.len[i];
+    int tot;
+    int run = block_excl_scan(sc, sum, &tot);
+    const int half = P.tcap / 2;
+    const int dst0 = sc->texthalf ? 0 : half;
+    for (int i = lo; i < hi; i++) {
+        if (L.meta[i] & M_MARKER) continue;
+        const uint32_t src = L.text[i];
+        const int n = L.len[i];
+        for (int k = 0; k < n; k++) L.gtext[dst0 + run + k] = L.gtext[src + k];
+        L.text[i] = uint32_t(dst0 + run);
+        run += n;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sc->texthalf ^= 1;
+        sc->textused = dst0 + tot;
+        if (tot > half) sc->status = MTR_ERR_CAPACITY;
+    }
+    __syncthreads();
 }
 
 // ------------------------------------------------------------------ zamboni
@@ -760,7 +805,7 @@ __device__ void insert_segment(Lds& L, const KParams& P, const View& v, const mt
     // copy the op's text into the document arena (all lanes)
     const int t0 = sc->textused;
     if (!marker) {
-        if (t0 + len > P.tcap) {
+        if (t0 + len > text_end(sc, P)) {
             __syncthreads();
             if (threadIdx.x == 0) sc->status = MTR_ERR_CAPACITY;
             __syncthreads();
@@ -893,6 +938,8 @@ __device__ void load_doc(Lds& L, const KParams& P, uint32_t d) {
         sc->collab = h.collab; sc->local = h.local; sc->heapn = h.heapn; sc->uidnext = h.uidnext;
         sc->textused = h.textused; sc->propused = h.propused; sc->rmused = h.rmused; sc->status = h.status;
         sc->fail_op = h.fail_op; sc->max_heap = h.max_heap; sc->ops_done = 0;
+        sc->sum_s = 0; sc->sum_l = 0;
+        sc->texthalf = h.texthalf;
     }
     __syncthreads();
     if (P.global_mode) return;
@@ -946,15 +993,21 @@ __device__ void store_doc(Lds& L, const KParams& P, uint32_t d) {
         h.op_cursor += sc->ops_done;
         h.fail_op = sc->fail_op;
         h.max_heap = sc->max_heap;
-        if (sc->ops_done) atomicAdd(P.stat_ops, (unsigned long long)sc->ops_done);
+        h.texthalf = sc->texthalf;
+        if (sc->ops_done) {
+            atomicAdd(P.stat_ops, (unsigned long long)sc->ops_done);
+            atomicAdd(P.stat_ops + 1, sc->sum_s);
+            atomicAdd(P.stat_ops + 2, sc->sum_l);
+        }
     }
 }
 
 // LDS bytes needed for a launch of capacity cap (leaves) / lhcap (heap slots)
+constexpr size_t kScBytes = ((sizeof(Sc) + 15) & ~size_t(15)) + ((sizeof(mtr_synth_state) + 15) & ~size_t(15));
 __host__ __device__ inline size_t lds_bytes(int cap, int lhcap) {
-    return size_t(cap) * 4 * 10 + size_t(lhcap) * 4 * 2 + ((sizeof(Sc) + 15) & ~size_t(15));
+    return size_t(cap) * 4 * 10 + size_t(lhcap) * 4 * 2 + kScBytes;
 }
-__host__ __device__ inline size_t lds_bytes_global_mode() { return (sizeof(Sc) + 15) & ~size_t(15); }
+__host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
 
 // global mode: every array lives in the document's HBM slab
 __device__ inline void carve_global(Lds& L, char* smem, const KParams& P, uint32_t d) {
@@ -974,6 +1027,7 @@ __device__ inline void carve_global(Lds& L, char* smem, const KParams& P, uint32
     L.hseq = reinterpret_cast<int*>(gh);
     L.huid = gh + P.hcap;
     L.sc = reinterpret_cast<Sc*>(smem);
+    L.gst = reinterpret_cast<mtr_synth_state*>(smem + ((sizeof(Sc) + 15) & ~size_t(15)));
     L.cap = P.segcap;
     L.lhcap = P.hcap;
 }
@@ -994,8 +1048,46 @@ __device__ inline void carve(Lds& L, char* smem, int cap, int lhcap) {
     L.hseq = reinterpret_cast<int*>(take(4 * size_t(lhcap)));
     L.huid = reinterpret_cast<uint32_t*>(take(4 * size_t(lhcap)));
     L.sc = reinterpret_cast<Sc*>(take(sizeof(Sc)));
+    L.gst = reinterpret_cast<mtr_synth_state*>(take(sizeof(mtr_synth_state)));
     L.cap = cap;
     L.lhcap = lhcap;
+}
+
+// record mode: draw op `idx` of document d from the synthetic recipe using this engine's exact
+// view length, write it (and its text) into the batch buffers
+__device__ void gen_op(Lds& L, const KParams& P, uint32_t d, const mtr_doc_desc& dd, int idx) {
+    Sc* sc = L.sc;
+    mtr_op* rec = P.gen_ops + dd.op_begin + idx;
+    if (idx == 0) {
+        if (threadIdx.x == 0) {
+            mtr_op z{};
+            z.type = MTR_OP_START_COLLAB;
+            *rec = z;
+        }
+        __syncthreads();
+        return;
+    }
+    if (threadIdx.x == 0) {
+        mtr_op op;
+        mtr_synth_begin(&P.gen_cfg, L.gst, idx, &op);
+        sc->b2 = op.ref_seq;
+        sc->b3 = op.client;
+        *rec = op;
+    }
+    __syncthreads();
+    View v;
+    v.ref = sc->b2;
+    v.client = enc_client(sc->b3);
+    v.local = 0;
+    prefix(L, v, P.new_length_calc);
+    if (threadIdx.x == 0) {
+        const int S = sc->nseg;
+        const int len = S > 0 ? L.E[S - 1] : 0;
+        mtr_op op = *rec;
+        mtr_synth_finish(&P.gen_cfg, L.gst, len, &op, P.gen_text + dd.text_base);
+        *rec = op;
+    }
+    __syncthreads();
 }
 
 // ------------------------------------------------------------------ the kernel
@@ -1015,9 +1107,21 @@ __global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
     L.grm = P.rm + size_t(d) * P.rcap;
     load_doc(L, P, d);
     Sc* sc = L.sc;
+    if (P.gen && threadIdx.x == 0) *L.gst = P.gen_state[d];
     for (int k = 0; k < n_ops; k++) {
+        if (P.gen) gen_op(L, P, d, dd, cursor + k);
         const mtr_op op = P.ops[dd.op_begin + cursor + k];
-        if (threadIdx.x == 0) sc->b3 = op.seq;  // (debug trace only)
+        if (threadIdx.x == 0) {
+            sc->b3 = op.seq;  // (debug trace only)
+            sc->sum_s += (unsigned long long)sc->nseg;
+            if (op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT)
+                sc->sum_l += (op.flags & MTR_F_MARKER) ? 0ull : (unsigned long long)op.payload2;
+        }
+        // text arena: keep room for this op's text plus zamboni merge copies
+        {
+            const int need = int(op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT ? op.payload2 : 0) + 4096;
+            if (sc->textused + need > text_end(sc, P)) text_gc(L, P);
+        }
         // capacity guard: every op adds at most two leaves
         if (sc->nseg + 2 >= L.cap) {
             if (threadIdx.x == 0) sc->status = MTR_ERR_CAPACITY;
@@ -1089,6 +1193,7 @@ __global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
         __syncthreads();
         if (sc->status != MTR_OK) break;
     }
+    if (P.gen && threadIdx.x == 0) P.gen_state[d] = *L.gst;
     store_doc(L, P, d);
 }
 

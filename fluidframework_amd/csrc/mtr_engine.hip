@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/mtr.h"
+#include "../../include/mtr_synth.h"
 #include "apply.hip.h"
 #include "summary.hip.h"
 
@@ -93,6 +94,8 @@ struct mtr_engine {
     DevBuf<unsigned long long> stat;  // [0] ops applied
     DevBuf<int32_t> red;              // small reduction buffer
     DevBuf<uint32_t> scratch;         // E/V arrays for HBM-resident (global-mode) launches
+    DevBuf<mtr_synth_state> gstate;   // record mode generator state
+    mtr_synth_cfg gcfg{};
     // summaries
     DevBuf<int64_t> out_size, out_off;
     DevBuf<unsigned long long> out_hash;
@@ -263,7 +266,11 @@ static int read_state(mtr_engine* e, int32_t out[3]) {
     return 0;
 }
 
-int mtr_run(mtr_engine* e) {
+static int run_impl(mtr_engine* e, int gen);
+
+int mtr_run(mtr_engine* e) { return run_impl(e, 0); }
+
+static int run_impl(mtr_engine* e, int gen) {
     HIPCHK(hipSetDevice(e->device));
     if (e->n_docs == 0) return MTR_OK;
     const int K = int(e->caps.ops_per_launch ? e->caps.ops_per_launch : 0x7fffffff);
@@ -291,6 +298,13 @@ int mtr_run(mtr_engine* e) {
     P.key_index = e->key_index.p;
     P.val_eq = e->val_eq.p;
     P.stat_ops = e->stat.p;
+    P.gen = gen;
+    if (gen) {
+        P.gen_cfg = e->gcfg;
+        P.gen_state = e->gstate.p;
+        P.gen_ops = e->ops.p;
+        P.gen_text = e->btext.p;
+    }
     P.trace = getenv("MTR_TRACE") ? 1 : 0;
     P.trace_seq = getenv("MTR_TRACE_SEQ") ? atoi(getenv("MTR_TRACE_SEQ")) : -1;
     int dev_lds = 0;
@@ -341,6 +355,74 @@ int mtr_run(mtr_engine* e) {
         }
     }
     e->summarized = false;
+    return MTR_OK;
+}
+
+__global__ void synth_init_kernel(mtr_synth_cfg cfg, mtr_synth_state* st, uint32_t n) {
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < n) mtr_synth_init(&cfg, d, &st[d]);
+}
+__global__ void synth_text_count_kernel(const mtr_synth_state* st, mtr_doc_desc* docs, uint32_t n) {
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < n) docs[d].text_count = st[d].text_used;
+}
+
+int mtr_generate(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch* tables) {
+    HIPCHK(hipSetDevice(e->device));
+    if (cfg->n_docs > e->max_docs || cfg->writers > MTR_SYNTH_MAX_WRITERS || cfg->writers + 1 > 0xfd) {
+        set_err("mtr_generate: bad configuration");
+        return MTR_ERR_BAD_OP;
+    }
+    const uint32_t n = cfg->n_docs, per = cfg->ops_per_doc + 1;
+    std::vector<mtr_doc_desc> docs(n);
+    for (uint32_t d = 0; d < n; d++) {
+        docs[d].op_begin = uint64_t(d) * per;
+        docs[d].op_count = per;
+        docs[d].text_base = uint64_t(d) * cfg->text_cap;
+        docs[d].text_count = 0;
+        docs[d].client_base = 0;
+        docs[d].n_clients = cfg->writers + 1;
+    }
+    mtr_batch b = *tables;
+    b.n_docs = n;
+    b.docs = docs.data();
+    b.n_ops = 0;
+    b.n_text = 0;
+    if (mtr_reset(e) != MTR_OK || mtr_submit(e, &b) != MTR_OK) return -1;
+    if (e->ops.ensure(size_t(n) * per) || e->btext.ensure(size_t(n) * cfg->text_cap) || e->gstate.ensure(n)) return -1;
+    e->gcfg = *cfg;
+    synth_init_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(*cfg, e->gstate.p, n);
+    HIPCHK(hipGetLastError());
+    if (run_impl(e, 1) != MTR_OK) return -1;
+    synth_text_count_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(e->gstate.p, e->docs.p, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return MTR_OK;
+}
+
+int mtr_download_batch(mtr_engine* e, uint32_t lo, uint32_t hi, mtr_doc_desc* docs, mtr_op* ops, uint16_t* text,
+                       uint64_t text_cap) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (hi > e->n_docs || lo > hi) {
+        set_err("mtr_download_batch: bad range");
+        return -1;
+    }
+    std::vector<mtr_doc_desc> dd(hi - lo);
+    if (hi > lo) HIPCHK(hipMemcpy(dd.data(), e->docs.p + lo, (hi - lo) * sizeof(mtr_doc_desc), hipMemcpyDeviceToHost));
+    uint64_t op_at = 0, text_at = 0;
+    for (uint32_t i = 0; i < hi - lo; i++) {
+        mtr_doc_desc x = dd[i];
+        if (ops) HIPCHK(hipMemcpy(ops + op_at, e->ops.p + x.op_begin, x.op_count * sizeof(mtr_op), hipMemcpyDeviceToHost));
+        if (text && text_at + x.text_count <= text_cap && x.text_count)
+            HIPCHK(hipMemcpy(text + text_at, e->btext.p + x.text_base, x.text_count * sizeof(uint16_t),
+                             hipMemcpyDeviceToHost));
+        x.op_begin = op_at;
+        x.text_base = text_at;
+        op_at += x.op_count;
+        text_at += x.text_count;
+        if (docs) docs[i] = x;
+    }
     return MTR_OK;
 }
 
@@ -546,9 +628,9 @@ int mtr_stats(mtr_engine* e, int64_t* out, int32_t n) {
     HIPCHK(hipStreamSynchronize(e->stream));
     std::vector<DocHdr> h(e->n_docs);
     if (e->n_docs) HIPCHK(hipMemcpy(h.data(), e->hdr.p, e->n_docs * sizeof(DocHdr), hipMemcpyDeviceToHost));
-    unsigned long long ops = 0;
-    HIPCHK(hipMemcpy(&ops, e->stat.p, sizeof(ops), hipMemcpyDeviceToHost));
-    int64_t v[8] = {int64_t(ops), e->n_docs, 0, 0, 0, e->launches, 0, 0};
+    unsigned long long st[3] = {0, 0, 0};
+    HIPCHK(hipMemcpy(st, e->stat.p, sizeof(st), hipMemcpyDeviceToHost));
+    int64_t v[10] = {int64_t(st[0]), e->n_docs, 0, 0, 0, e->launches, 0, 0, int64_t(st[1]), int64_t(st[2])};
     for (auto& x : h) {
         v[2] = std::max<int64_t>(v[2], x.nseg);
         v[3] += x.nseg;
@@ -556,7 +638,7 @@ int mtr_stats(mtr_engine* e, int64_t* out, int32_t n) {
         v[6] = std::max<int64_t>(v[6], x.max_heap);
         v[7] = std::max<int64_t>(v[7], x.textused);
     }
-    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
+    for (int i = 0; i < n && i < 10; i++) out[i] = v[i];
     return MTR_OK;
 }
 

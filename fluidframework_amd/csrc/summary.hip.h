@@ -413,10 +413,7 @@ __device__ void summarize_doc(const SParams& P, uint32_t d, Writer<W>& w) {
     }
     const int64_t table = 4 + 4 * int64_t(nblobs);
     const int64_t base = w.n;
-    if (W) {
-        w_blob_len(w, base, uint32_t(nblobs));
-        w.h = (w.h ^ uint64_t(nblobs)) * 1099511628211ull;
-    }
+    if (W) w_blob_len(w, base, uint32_t(nblobs));  // hashes nblobs
     w.n += table;
     int k = 0;
     Spec sp;

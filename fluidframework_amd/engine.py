@@ -65,6 +65,11 @@ def lib():
         L.mtr_last_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.mtr_last_timing.restype = C.c_int
         L.mtr_last_error.restype = C.c_char_p
+        L.mtr_generate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mtr_generate.restype = C.c_int
+        L.mtr_download_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_uint64]
+        L.mtr_download_batch.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -119,6 +124,27 @@ class Engine:
         self.run()
         self.sync()
 
+    def generate(self, cfg, tabs):
+        """Record mode: synthesize cfg.n_docs op logs (include/mtr_synth.h) with this engine's exact
+        view lengths and apply them; the recorded batch stays on the device for replays."""
+        self._tabs = tabs
+        self._cfg = cfg
+        self._check(lib().mtr_generate(self.h, C.byref(cfg), C.addressof(tabs.c)), "mtr_generate")
+
+    def download(self, lo, hi):
+        """The recorded batch of documents [lo, hi) as a host Batch (sharing the recipe tables)."""
+        from .synth import with_docs
+        n = hi - lo
+        per = self._cfg.ops_per_doc + 1
+        docs = np.zeros(n, dtype=abi.DOC_DTYPE)
+        ops = np.zeros(n * per, dtype=abi.OP_DTYPE)
+        cap = n * int(self._cfg.text_cap)
+        text = np.zeros(max(cap, 1), dtype="<u2")
+        self._check(lib().mtr_download_batch(self.h, lo, hi, docs.ctypes.data, ops.ctypes.data, text.ctypes.data, cap),
+                    "mtr_download_batch")
+        used = int(docs["text_base"][-1] + docs["text_count"][-1]) if n else 0
+        return with_docs(self._tabs, docs, ops, text[:max(used, 1)].copy())
+
     def summary(self, doc) -> list[bytes]:
         cap = 1 << 16
         while True:
@@ -166,9 +192,10 @@ class Engine:
         return out[:n], h.value
 
     def stats(self) -> dict:
-        out = np.zeros(8, dtype="<i8")
-        self._check(lib().mtr_stats(self.h, out.ctypes.data, 8), "mtr_stats")
-        keys = ["ops", "docs", "max_leaves", "sum_leaves", "bad_docs", "launches", "max_heap", "max_text"]
+        out = np.zeros(10, dtype="<i8")
+        self._check(lib().mtr_stats(self.h, out.ctypes.data, 10), "mtr_stats")
+        keys = ["ops", "docs", "max_leaves", "sum_leaves", "bad_docs", "launches", "max_heap", "max_text",
+                "sum_leaves_before_op", "text_units_inserted"]
         return dict(zip(keys, (int(x) for x in out)))
 
     def timing(self) -> dict:

@@ -91,12 +91,24 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap_leaves
 
 /* Engine-wide counters: out[0]=ops applied, out[1]=docs, out[2]=max leaves in any doc,
  * out[3]=sum of leaves, out[4]=docs with non-OK status, out[5]=kernel launches of the last run,
- * out[6]=max heap entries, out[7]=max text units used. */
+ * out[6]=max heap entries, out[7]=max text units used, out[8]=sum over applied ops of the leaf count
+ * before the op, out[9]=UTF-16 units inserted.  Counters accumulate from mtr_reset. */
 int mtr_stats(mtr_engine* e, int64_t* out, int32_t n);
 
 /* Device time (ms) of the last mtr_run / mtr_summarize measured with HIP events on the
  * engine stream: out[0]=apply, out[1]=summarize, out[2]=apply kernel launches. */
 int mtr_last_timing(mtr_engine* e, double* out, int32_t n);
+
+/* Record mode (synthetic workloads, include/mtr_synth.h): draw cfg->n_docs documents' op logs
+ * with the engine's own exact view lengths, apply them, and keep the recorded batch on the device
+ * (mtr_reset + mtr_run then replays it).  `tables` supplies prop-op/key/value/client tables. */
+struct mtr_synth_cfg;
+int mtr_generate(mtr_engine* e, const struct mtr_synth_cfg* cfg, const mtr_batch* tables);
+
+/* Copy the recorded batch of documents [lo, hi) to the host (compacted: op_begin/text_base are
+ * rewritten relative to the copied arrays; text_cap = capacity of `text` in UTF-16 units). */
+int mtr_download_batch(mtr_engine* e, uint32_t lo, uint32_t hi, mtr_doc_desc* docs, mtr_op* ops, uint16_t* text,
+                       uint64_t text_cap);
 
 /* Human-readable description of the last engine-level error (static storage). */
 const char* mtr_last_error(void);

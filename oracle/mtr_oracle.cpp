@@ -14,6 +14,7 @@
 //    segment groups and delta/maintenance events are not modelled: none of them
 //    change the observer's text, segment boundaries or summary bytes.
 #include "mtr_oracle.h"
+#include "../include/mtr_synth.h"
 
 #include <algorithm>
 #include <climits>
@@ -23,6 +24,9 @@
 #include <deque>
 #include <memory>
 #include <string>
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -1272,6 +1276,125 @@ int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_ind
         off += int64_t(blobs[k].size());
     }
     return int64_t(blobs.size());
+}
+
+
+// FNV-1a 64 over the summary: nblobs, then per blob its bytes followed by its length
+// (the same digest the engine's summary_write_kernel computes).
+static uint64_t summary_hash(const std::vector<std::string>& blobs) {
+    const uint64_t P = 1099511628211ull;
+    uint64_t h = 14695981039346656037ull;
+    h = (h ^ uint64_t(blobs.size())) * P;
+    for (auto& b : blobs) {
+        for (unsigned char c : b) h = (h ^ c) * P;
+        h = (h ^ uint64_t(b.size())) * P;
+    }
+    return h;
+}
+
+// Replay documents [lo, hi) of a batch on `nthreads` host threads (one document per task),
+// summarize each and record its digest; returns wall-clock seconds.
+double oracle_replay_batch(const mtr_batch* b, const mtr_options* opt, uint32_t lo, uint32_t hi, int nthreads,
+                           uint64_t* hashes, int32_t* status) {
+    std::atomic<uint32_t> next{lo};
+    auto t0 = std::chrono::steady_clock::now();
+    auto work = [&]() {
+        std::vector<uint8_t> out(1 << 16);
+        std::vector<int64_t> lens(4096);
+        for (;;) {
+            uint32_t d = next.fetch_add(1);
+            if (d >= hi) break;
+            oracle_doc* doc = oracle_doc_new(opt);
+            int st = oracle_doc_apply(doc, b, d, 0, b->docs[d].op_count);
+            uint64_t h = 0;
+            if (st == MTR_OK) {
+                int64_t r;
+                while ((r = oracle_doc_summarize(doc, b, d, out.data(), int64_t(out.size()), lens.data(), 4096)) < 0)
+                    out.resize(size_t(-r) + 16);
+                std::vector<std::string> blobs;
+                int64_t off = 0;
+                for (int64_t k = 0; k < r; k++) {
+                    blobs.emplace_back(reinterpret_cast<const char*>(out.data() + off), size_t(lens[k]));
+                    off += lens[k];
+                }
+                h = summary_hash(blobs);
+            }
+            if (hashes) hashes[d - lo] = h;
+            if (status) status[d - lo] = st;
+            oracle_doc_free(doc);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+
+// Synthetic op logs (include/mtr_synth.h) with the oracle as the exact simulator.
+int oracle_generate(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
+                    uint32_t hi, int nthreads, mtr_op* ops_out, uint16_t* text_out, uint32_t* text_counts,
+                    uint64_t* hashes, int32_t* status) {
+    std::atomic<uint32_t> next{lo};
+    const uint32_t per = cfg->ops_per_doc + 1;
+    auto work = [&]() {
+        std::vector<uint8_t> out(1 << 16);
+        std::vector<int64_t> lens(4096);
+        for (;;) {
+            const uint32_t d = next.fetch_add(1);
+            if (d >= hi) break;
+            const uint32_t r = d - lo;
+            mtr_op* ops = ops_out + size_t(r) * per;
+            uint16_t* text = text_out + size_t(r) * cfg->text_cap;
+            mtr_batch b = *tables;
+            mtr_doc_desc dd{};
+            dd.op_begin = 0;
+            dd.op_count = per;
+            dd.text_base = 0;
+            dd.client_base = 0;
+            dd.n_clients = cfg->writers + 1;
+            b.n_docs = 1;
+            b.docs = &dd;
+            b.ops = ops;
+            b.text = text;
+            oracle_doc* doc = oracle_doc_new(opt);
+            doc->tree.tabs.b = &b;
+            mtr_synth_state st;
+            mtr_synth_init(cfg, d, &st);
+            std::memset(ops, 0, sizeof(mtr_op) * per);
+            ops[0].type = MTR_OP_START_COLLAB;
+            int rc = doc->tree.apply(ops[0], dd);
+            for (uint32_t k = 1; k < per && rc == MTR_OK; k++) {
+                mtr_op& op = ops[k];
+                mtr_synth_begin(cfg, &st, int32_t(k), &op);
+                const int L = std::max(0, doc->tree.nodeLength(doc->tree.root, op.ref_seq, op.client));
+                mtr_synth_finish(cfg, &st, L, &op, text);
+                rc = doc->tree.apply(op, dd);
+            }
+            dd.text_count = st.text_used;
+            if (text_counts) text_counts[r] = st.text_used;
+            uint64_t h = 0;
+            if (rc == MTR_OK && hashes) {
+                int64_t nb;
+                while ((nb = oracle_doc_summarize(doc, &b, 0, out.data(), int64_t(out.size()), lens.data(), 4096)) < 0)
+                    out.resize(size_t(-nb) + 16);
+                std::vector<std::string> blobs;
+                int64_t off = 0;
+                for (int64_t k = 0; k < nb; k++) {
+                    blobs.emplace_back(reinterpret_cast<const char*>(out.data() + off), size_t(lens[k]));
+                    off += lens[k];
+                }
+                h = summary_hash(blobs);
+            }
+            if (hashes) hashes[r] = h;
+            if (status) status[r] = rc;
+            oracle_doc_free(doc);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    return 0;
 }
 
 }  // extern "C"

@@ -45,6 +45,19 @@ int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap_leaves, int32
 /* Collaboration window state: out[0]=minSeq out[1]=currentSeq out[2]=#heap entries out[3]=#leaves */
 void oracle_doc_state(oracle_doc* d, int64_t* out);
 
+/* Replay documents [lo, hi) on nthreads host threads, summarize, digest (FNV-1a 64 of nblobs and
+ * each blob's bytes + length, as the engine's mtr_summary_hashes).  Returns wall seconds. */
+double oracle_replay_batch(const mtr_batch* b, const mtr_options* opt, uint32_t lo, uint32_t hi, int nthreads,
+                           uint64_t* hashes, int32_t* status);
+
+/* Synthetic op logs (include/mtr_synth.h) driven by the oracle: documents [lo, hi); ops_out holds
+ * (hi-lo) * (ops_per_doc+1) records, text_out (hi-lo) * cfg->text_cap units.  tables supplies the
+ * prop-op / key / value / client tables.  Also digests each document's summary. */
+struct mtr_synth_cfg;
+int oracle_generate(const struct mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
+                    uint32_t hi, int nthreads, mtr_op* ops_out, uint16_t* text_out, uint32_t* text_counts,
+                    uint64_t* hashes, int32_t* status);
+
 /* Debug: print zamboni decisions to stdout */
 void oracle_set_trace(int on);
 

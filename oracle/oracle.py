@@ -37,6 +37,12 @@ def lib():
         L.oracle_doc_export.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
         L.oracle_doc_state.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_set_trace.argtypes = [C.c_int]
+        L.oracle_generate.restype = C.c_int
+        L.oracle_generate.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32,
+                                      C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_replay_batch.restype = C.c_double
+        L.oracle_replay_batch.argtypes = [C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32, C.c_int,
+                                          C.c_void_p, C.c_void_p]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         _LIB = L
@@ -99,3 +105,57 @@ class OracleDoc:
 
     def length(self, ref_seq, client):
         return lib().oracle_doc_length(self.h, ref_seq, client)
+
+
+def replay_batch(batch, lo, hi, threads, opts=None):
+    """Replay documents [lo, hi) on `threads` host threads -> (seconds, digests, statuses)."""
+    opts = opts or options()
+    n = hi - lo
+    hashes = np.zeros(n, dtype="<u8")
+    status = np.zeros(n, dtype="<i4")
+    secs = lib().oracle_replay_batch(C.addressof(batch.c), C.byref(opts), lo, hi, threads, hashes.ctypes.data,
+                                     status.ctypes.data)
+    return secs, hashes, status
+
+
+def summary_digest(blobs):
+    """Python restatement of the summary digest (FNV-1a 64)."""
+    P = 1099511628211
+    M = (1 << 64) - 1
+    h = 14695981039346656037
+    h = ((h ^ len(blobs)) * P) & M
+    for b in blobs:
+        for c in b:
+            h = ((h ^ c) * P) & M
+        h = ((h ^ len(b)) * P) & M
+    return h
+
+
+def generate(cfg, tabs, lo, hi, threads=8, opts=None):
+    """Synthetic op logs of documents [lo, hi) recorded with the oracle as the exact simulator
+    -> (Batch, summary digests, statuses)."""
+    from fluidframework_amd.synth import with_docs
+    opts = opts or options()
+    n = hi - lo
+    per = cfg.ops_per_doc + 1
+    ops = np.zeros(n * per, dtype=abi.OP_DTYPE)
+    text = np.zeros(n * int(cfg.text_cap), dtype="<u2")
+    counts = np.zeros(n, dtype="<u4")
+    hashes = np.zeros(n, dtype="<u8")
+    status = np.zeros(n, dtype="<i4")
+    lib().oracle_generate(C.byref(cfg), C.addressof(tabs.c), C.byref(opts), lo, hi, threads, ops.ctypes.data,
+                          text.ctypes.data, counts.ctypes.data, hashes.ctypes.data, status.ctypes.data)
+    docs = np.zeros(n, dtype=abi.DOC_DTYPE)
+    docs["op_begin"] = np.arange(n, dtype=np.uint64) * per
+    docs["op_count"] = per
+    docs["text_count"] = counts
+    # compact the text regions
+    bases = np.zeros(n, dtype=np.uint64)
+    if n:
+        bases[1:] = np.cumsum(counts.astype(np.uint64))[:-1]
+    docs["text_base"] = bases
+    docs["client_base"] = 0
+    docs["n_clients"] = cfg.writers + 1
+    packed = np.concatenate([text[i * int(cfg.text_cap): i * int(cfg.text_cap) + int(counts[i])] for i in range(n)]) \
+        if n else np.zeros(0, "<u2")
+    return with_docs(tabs, docs, ops, packed), hashes, status
