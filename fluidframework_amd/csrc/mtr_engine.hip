@@ -64,11 +64,7 @@ struct DevBuf {
     }
 };
 
-int pow2_at_least(int x) {
-    int c = 64;
-    while (c < x) c <<= 1;
-    return c;
-}
+int round64(int x) { return std::max(64, (x + 63) & ~63); }
 
 }  // namespace
 
@@ -305,13 +301,14 @@ static int run_impl(mtr_engine* e, int gen) {
         P.gen_ops = e->ops.p;
         P.gen_text = e->btext.p;
     }
-    P.trace = getenv("MTR_TRACE") ? 1 : 0;
-    P.trace_seq = getenv("MTR_TRACE_SEQ") ? atoi(getenv("MTR_TRACE_SEQ")) : -1;
     int dev_lds = 0;
     HIPCHK(hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device));
     static std::once_flag once;
     std::call_once(once, [&] {
-        (void)hipFuncSetAttribute((const void*)apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
     });
     for (;;) {
         int32_t st[3];
@@ -319,9 +316,9 @@ static int run_impl(mtr_engine* e, int gen) {
         const int maxseg = st[0], rem = st[1], maxheap = st[2];
         if (rem <= 0) break;
         const int k = std::min(K, rem);
-        int cap = pow2_at_least(maxseg + 2 * k + 8);
+        int cap = round64(maxseg + 2 * k + 8);
         if (cap > P.segcap) cap = P.segcap;
-        int lhcap = std::min<int>(P.hcap, std::max(cap / 2, pow2_at_least(maxheap + 2 * k + 8)));
+        int lhcap = std::min<int>(P.hcap, std::max(cap / 2, round64(maxheap + 2 * k + 8)));
         size_t lds = lds_bytes(cap, lhcap);
         int kk = k;
         P.global_mode = 0;
@@ -341,7 +338,8 @@ static int run_impl(mtr_engine* e, int gen) {
         P.lhcap = lhcap;
         P.ops_this_launch = kk;
         HIPCHK(hipEventRecord(e->ev[0], e->stream));
-        apply_kernel<<<e->n_docs, NT, lds, e->stream>>>(P);
+        if (P.global_mode) apply_kernel<true><<<e->n_docs, NT, lds, e->stream>>>(P);
+        else apply_kernel<false><<<e->n_docs, NT, lds, e->stream>>>(P);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->ev[1], e->stream));
         HIPCHK(hipEventSynchronize(e->ev[1]));
