@@ -25,13 +25,13 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_engine(force=False, verbose=False):
-    out = os.path.join(HERE, "libmtr.so")
+def build_engine(force=False, verbose=False, prof=False):
+    out = os.path.join(HERE, "libmtr_prof.so" if prof else "libmtr.so")
     deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", h)
                                                            for h in ("mtr.h", "mtr_types.h", "mtr_synth.h")]
     if force or _stale(out, deps):
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wno-unused-result", "-o", out] + [os.path.join(CSRC, f) for f in ENGINE_SRC]
+               "-Wno-unused-result"] + (["-DMTR_PROF"] if prof else []) + ["-o", out] + [os.path.join(CSRC, f) for f in ENGINE_SRC]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
@@ -43,4 +43,7 @@ def build_all(force=False, verbose=False):
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv, verbose=True)
+    if "--prof" in sys.argv:
+        build_engine(force="--force" in sys.argv, verbose=True, prof=True)
+    else:
+        build_all(force="--force" in sys.argv, verbose=True)

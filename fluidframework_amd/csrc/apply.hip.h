@@ -12,8 +12,11 @@
 // length queries of insertingWalk / nodeMap (mergeTree.ts:1740, 2526); the one-slot shift that
 // makes room for a split or an insert (mergeTree.ts:1831-1838); the uid search for popped LRU
 // entries; and the stream compaction after zamboni (zamboni.ts:19-120).  The scan arrays stay
-// valid across the op's splits, so an op scans once.  O(1)-per-op control (tie-break, block
-// splits, heap, scour decisions) runs on lane 0.
+// valid across the op's splits, so an op scans once.  The sequential control (tie-break, block
+// splits, heap, zamboni scour/pack decisions) runs as uniform code on wave 0, whose 64 lanes turn
+// every walk over leaves (block bounds, binary search, child counts, pack relabelling) into ballots
+// and every HBM access (text copies, property sets) into one coalesced round trip; waves 1-3 wait
+// at the next barrier.
 //
 // Memory spaces are explicit: LDS arrays are address_space(3) pointers (ds_read/ds_write),
 // HBM arrays address_space(1) (global_load/store) -- never generic flat accesses.
@@ -28,7 +31,7 @@
 
 namespace mtr {
 
-constexpr int NT = 256;
+constexpr int NT = 64;
 constexpr int NWAVES = NT / 64;
 constexpr int32_t RNONE = 0x7fffffff;  // removedSeq of a live leaf
 constexpr uint32_t NONE32 = 0xffffffffu;
@@ -47,6 +50,8 @@ constexpr int M_NS_SHIFT = 22;  // needsScour of the leaf block this leaf starts
 constexpr uint32_t M_NS_MASK = 3u << M_NS_SHIFT;
 constexpr uint32_t M_NOREF = 1u << 24;
 constexpr uint32_t M_DEL = 1u << 25;
+constexpr uint32_t M_NL = 1u << 26;   // text leaf whose last unit is '\n' (TextSegment.canAppend)
+constexpr uint32_t M_NLQ = 1u << 27;  // M_NL not known yet (left half of a split): read lazily by scour
 constexpr uint32_t NS_UNDEF = 0, NS_FALSE = 1, NS_TRUE = 2;
 
 constexpr uint32_t CL_LOCAL = 0xffu;      // LocalClientId (-1)
@@ -136,6 +141,12 @@ struct KParams {
     uint16_t* gen_text;          // == btext, writable
 };
 
+// phase-timer slots (-DMTR_PROF builds)
+enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBLOCK, P_COMPACT, P_FINDUID,
+       P_TEXTGC, P_LOADSTORE, P_TEXTCOPY, P_UPDSEQ, P_NZBLOCK, P_NCOMPACT, P_SCOUR1, P_PACK, P_NLQ, P_PMATCH,
+       P_TAPPEND, P_HEAP, P_OVERFLOW, P_NPACK, P_NMERGE, P_NPMATCH, P_NNLQ, P_SPLIT1, P_INS1, P_FETCH, P_X1, P_X2,
+       P_COUNT };
+
 // scalar document state, broadcast slots and lane-0 scratch, in LDS
 struct Sc {
     int nseg, height, minseq, curseq;
@@ -148,6 +159,9 @@ struct Sc {
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
     int rs[MAXH + 1], re[MAXH + 1], topb[MAXH + 1];
     uint32_t memo_old[4], memo_new[4];
+#ifdef MTR_PROF
+    unsigned long long prof[P_COUNT];
+#endif
 };
 
 struct View {
@@ -184,6 +198,19 @@ __device__ inline int wave_incl_scan(int x) {
     }
     return x;
 }
+__device__ inline int lane_id() { return int(threadIdx.x & 63); }
+__device__ inline uint64_t lanes_below() { return (uint64_t(1) << lane_id()) - 1; }
+__device__ inline int first_lane(uint64_t m) { return __ffsll((long long)m) - 1; }
+template <class T>
+__device__ inline T rdlane(T x, int l) {  // v_readlane with a wave-uniform lane index
+    return T(__builtin_amdgcn_readlane(int(x), l));
+}
+// order this wave's LDS/HBM writes before its later reads (other lanes' addresses included)
+__device__ inline void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ inline bool wave0() { return threadIdx.x < 64; }
 __device__ inline int wave_max(int x) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) x = max(x, __shfl_xor(x, d, 64));
@@ -247,6 +274,28 @@ __host__ __device__ inline size_t lds_bytes(int cap, int lhcap) {
 }
 __host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
 
+// Phase timers (builds with -DMTR_PROF only): thread-0 clock cycles per phase, summed over
+// documents into g_prof (mtr_profile()).
+
+#ifdef MTR_PROF
+__device__ unsigned long long g_prof[P_COUNT];
+struct ProfScope {
+    lptr<Sc> sc;
+    int id;
+    long long t;
+    __device__ ProfScope(lptr<Sc> s, int i) : sc(s), id(i), t(threadIdx.x == 0 ? clock64() : 0) {}
+    __device__ ~ProfScope() {
+        if (threadIdx.x == 0) sc->prof[id] += (unsigned long long)(clock64() - t);
+    }
+};
+#define PROF(id) ProfScope _prof_scope(L.sc, id)
+#define PROF_COUNT(id) \
+    if (threadIdx.x == 0) L.sc->prof[id]++
+#else
+#define PROF(id)
+#define PROF_COUNT(id)
+#endif
+
 template <bool G>
 struct Eng {
     using D = Doc<G>;
@@ -297,6 +346,7 @@ struct Eng {
 
     // V[i] = visible length, E[i] = inclusive prefix of max(V,0).  Contiguous chunk per thread.
     static __device__ void prefix(D& L, const View& v, int newlen) {
+        PROF(P_PREFIX);
         const int S = L.sc->nseg;
         const int minseq = L.sc->minseq;
         const int per = (S + NT - 1) / NT;
@@ -319,6 +369,7 @@ struct Eng {
     // ------------------------------------------------------------ data movement
     // move leaves [at, S) (with their scan entries) to [at+1, S+1); rounds of NT from the top
     static __device__ void shift_right1(D& L, int at) {
+        PROF(P_SHIFT);
         const int S = L.sc->nseg;
         for (int hi = S; hi > at; hi -= NT) {
             const int lo = max(at, hi - NT);
@@ -342,6 +393,8 @@ struct Eng {
     // stream compaction of leaves without M_DEL (zamboni unlink / append); rounds of NT from
     // the bottom; destinations never exceed sources
     static __device__ void compact(D& L) {
+        PROF(P_COMPACT);
+        PROF_COUNT(P_NCOMPACT);
         const int S = L.sc->nseg;
         int base = 0;
         for (int lo = 0; lo < S; lo += NT) {
@@ -373,6 +426,7 @@ struct Eng {
 
     // index of the leaf with this uid, -1 if unlinked
     static __device__ int find_uid(D& L, uint32_t u) {
+        PROF(P_FINDUID);
         const int S = L.sc->nseg;
         int found = -1;
         for (int i = threadIdx.x; i < S; i += NT)
@@ -380,49 +434,76 @@ struct Eng {
         return block_max(L.sc, found);
     }
 
-    // ------------------------------------------------------------ lane-0 helpers
+    // ------------------------------------------------------------ wave-0 helpers
+    // (uniform code on wave 0: every lane holds the same scalars; the searches are ballots)
+
+    // start of the level-`level` block holding leaf x: last i <= x with i == 0 or bnd >= level
     static __device__ int block_start(const D& L, int x, int level) {
-        while (x > 0 && bnd_of(L.meta[x]) < level) x--;
-        return x;
+        for (int base = x;; base -= 64) {
+            const int i = base - lane_id();
+            const uint64_t m = __ballot(i <= 0 || bnd_of(L.meta[i]) >= level);
+            if (m) return max(0, base - first_lane(m));
+        }
     }
+    // end (exclusive) of the level-`level` block holding leaf x
     static __device__ int block_end(const D& L, int x, int level) {
         const int S = L.sc->nseg;
-        x++;
-        while (x < S && bnd_of(L.meta[x]) < level) x++;
-        return x;
-    }
-    static __device__ int lower_bound_E(const D& L, int pos) {  // first i with E[i] >= pos
-        int lo = 0, hi = L.sc->nseg;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (L.E[mid] >= pos) hi = mid;
-            else lo = mid + 1;
+        for (int base = x + 1;; base += 64) {
+            const int i = base + lane_id();
+            const uint64_t m = __ballot(i >= S || bnd_of(L.meta[i]) >= level);
+            if (m) return base + first_lane(m);
         }
-        return lo;
+    }
+    // first i with E[i] >= pos (S if none): 64-ary search
+    static __device__ int lower_bound_E(const D& L, int pos) {
+        int lo = 0, hi = L.sc->nseg;  // answer in [lo, hi]
+        const int ln = lane_id();
+        while (hi - lo > 64) {
+            const int stride = (hi - lo + 63) >> 6;
+            const int idx = lo + (ln + 1) * stride - 1;
+            const uint64_t m = __ballot(idx >= hi || L.E[idx] >= pos);
+            const int k = first_lane(m);  // lane 63 always qualifies
+            const int nlo = lo + k * stride;
+            hi = min(hi, lo + (k + 1) * stride - 1);
+            lo = nlo;
+        }
+        const int i = lo + ln;
+        const uint64_t m = __ballot(i < hi && L.E[i] >= pos);
+        return m ? lo + first_lane(m) : hi;
+    }
+    // number of leaves in [bs, be) with bnd >= minb
+    static __device__ int count_bnd(const D& L, int bs, int be, int minb) {
+        int c = 0;
+        for (int base = bs; base < be; base += 64) {
+            const int i = base + lane_id();
+            c += __popcll(__ballot(i < be && bnd_of(L.meta[i]) >= minb));
+        }
+        return c;
+    }
+    // index of the n-th (0-based) leaf in [bs, be) with bnd >= minb, -1 if none
+    static __device__ int nth_bnd(const D& L, int bs, int be, int minb, int n) {
+        for (int base = bs; base < be; base += 64) {
+            const int i = base + lane_id();
+            const bool t = i < be && bnd_of(L.meta[i]) >= minb;
+            const uint64_t m = __ballot(t);
+            const int pc = __popcll(m);
+            if (n < pc) return base + first_lane(__ballot(t && __popcll(m & lanes_below()) == n));
+            n -= pc;
+        }
+        return -1;
     }
 
     // Block overflow after a leaf was added next to x (insertingWalk split + updateRoot,
     // mergeTree.ts:1831-1871, 1268-1277).
     static __device__ void overflow_fix(D& L, int x) {
+        PROF(P_OVERFLOW);
         lptr<Sc> sc = L.sc;
         int level = 1;
         int bs = block_start(L, x, 1), be = block_end(L, x, 1);
         int cnt = be - bs;
         while (cnt >= kMaxNodesInBlock) {
-            int c5 = bs;
-            if (level == 1) {
-                c5 = bs + kMaxNodesInBlock / 2;
-            } else {
-                int k = 0;
-                for (int i = bs; i < be; i++)
-                    if (bnd_of(L.meta[i]) >= level - 1) {
-                        if (k == kMaxNodesInBlock / 2) {
-                            c5 = i;
-                            break;
-                        }
-                        k++;
-                    }
-            }
+            int c5 = bs + kMaxNodesInBlock / 2;
+            if (level > 1) c5 = nth_bnd(L, bs, be, level - 1, kMaxNodesInBlock / 2);
             uint32_t m = set_bnd(L.meta[c5], level);
             if (level == 1) m = set_ns(m, NS_UNDEF);
             L.meta[c5] = m;
@@ -434,9 +515,7 @@ struct Eng {
             level++;
             bs = block_start(L, bs, level);
             be = block_end(L, bs, level);
-            cnt = 0;
-            for (int i = bs; i < be; i++)
-                if (bnd_of(L.meta[i]) >= level - 1) cnt++;
+            cnt = count_bnd(L, bs, be, level - 1);
         }
     }
 
@@ -462,6 +541,7 @@ struct Eng {
         if (sc->heapn > sc->max_heap) sc->max_heap = sc->heapn;
     }
     static __device__ uint32_t heap_pop(D& L) {
+        PROF(P_HEAP);
         lptr<Sc> sc = L.sc;
         const uint32_t x = L.huid[1];
         int n = sc->heapn;
@@ -498,7 +578,7 @@ struct Eng {
 
     // ---- properties (PropertiesManager.addProperties without combining ops,
     //      segmentPropertiesManager.ts:60-157; JS own-key order).  Entry: [n, k0, v0, k1, v1, ...]
-    static __device__ uint32_t props_apply(D& L, const KParams& P, uint32_t old, uint32_t pp) {
+    static __device__ uint32_t props_apply_serial(D& L, const KParams& P, uint32_t old, uint32_t pp) {
         lptr<Sc> sc = L.sc;
         const gptr<const uint32_t> poff = gp(P.propop_off), pkv = gp(P.propop_kv), kix = gp(P.key_index);
         const uint32_t n_old = old == NONE32 ? 0 : L.gprop[old];
@@ -551,17 +631,123 @@ struct Eng {
         return dst;
     }
 
+    // Wave version: the old set and the op's keys are fetched once (one lane per entry) and the
+    // set is edited in registers (lane t = entry t); falls back to the serial form above 64 keys.
+    static __device__ uint32_t props_apply(D& L, const KParams& P, uint32_t old, uint32_t pp) {
+        lptr<Sc> sc = L.sc;
+        const gptr<const uint32_t> poff = gp(P.propop_off), pkv = gp(P.propop_kv), kix = gp(P.key_index);
+        const int n_old = old == NONE32 ? 0 : int(L.gprop[old]);
+        const int lo = int(poff[pp]), nq = int(poff[pp + 1]) - lo;
+        if (n_old + nq > 64) return props_apply_serial(L, P, old, pp);
+        const uint32_t need = 1 + 2 * uint32_t(n_old + nq);
+        if (uint32_t(sc->propused) + need > uint32_t(P.pcap)) {
+            sc->status = MTR_ERR_CAPACITY;
+            return old;
+        }
+        const int ln = lane_id();
+        uint32_t wk = 0, wv = 0, wx = MTR_NOT_INDEX, qk = 0, qv = 0, qx = MTR_NOT_INDEX;
+        if (ln < n_old) {
+            wk = L.gprop[old + 1 + 2 * ln];
+            wv = L.gprop[old + 2 + 2 * ln];
+        }
+        if (ln < nq) {
+            qk = pkv[2 * (lo + ln)];
+            qv = pkv[2 * (lo + ln) + 1];
+        }
+        if (ln < n_old) wx = kix[wk];
+        if (ln < nq) qx = kix[qk];
+        int n = n_old;
+        for (int q = 0; q < nq; q++) {
+            const uint32_t key = rdlane(qk, q), val = rdlane(qv, q), ix = rdlane(qx, q);
+            const uint64_t hit = __ballot(ln < n && wk == key);
+            if (val == MTR_NULL_VALUE) {
+                if (hit) {  // delete entry `at`: lanes above it move down one
+                    const int at = first_lane(hit);
+                    const uint32_t dk = __shfl(wk, min(ln + 1, 63)), dv = __shfl(wv, min(ln + 1, 63)),
+                                   dx = __shfl(wx, min(ln + 1, 63));
+                    if (ln >= at) {
+                        wk = dk;
+                        wv = dv;
+                        wx = dx;
+                    }
+                    n--;
+                }
+            } else if (hit) {
+                if (ln == first_lane(hit)) wv = val;
+            } else {
+                int pos = n;
+                if (ix != MTR_NOT_INDEX) {  // index-like keys sort first (JS own-key order)
+                    const uint64_t ge = __ballot(ln < n && !(wx != MTR_NOT_INDEX && wx < ix));
+                    pos = ge ? first_lane(ge) : n;
+                }
+                const uint32_t uk = __shfl(wk, max(ln - 1, 0)), uv = __shfl(wv, max(ln - 1, 0)),
+                               ux = __shfl(wx, max(ln - 1, 0));
+                if (ln > pos) {
+                    wk = uk;
+                    wv = uv;
+                    wx = ux;
+                } else if (ln == pos) {
+                    wk = key;
+                    wv = val;
+                    wx = ix;
+                }
+                n++;
+            }
+        }
+        const uint32_t dst = uint32_t(sc->propused);
+        const gptr<uint32_t> e = L.gprop + dst;
+        if (ln < n) {
+            e[1 + 2 * ln] = wk;
+            e[2 + 2 * ln] = wv;
+        }
+        e[0] = uint32_t(n);
+        sc->propused += 1 + 2 * n;
+        wave_fence();
+        return dst;
+    }
+
+    // matchProperties on wave 0: one lane per key of `a`, `b`'s keys broadcast by readlane
+    static __device__ bool props_match_w(const D& L, const KParams& P, uint32_t a, uint32_t b) {
+        if (a == b) return true;
+        if (a == NONE32 || b == NONE32) return false;
+        const int na = int(L.gprop[a]), nb = int(L.gprop[b]);
+        if (na != nb) return false;
+        const gptr<const uint32_t> veq = gp(P.val_eq);
+        if (na > 64) return props_match(L.gprop, veq, a, b);
+        PROF(P_PMATCH);
+        PROF_COUNT(P_NPMATCH);
+        const int ln = lane_id();
+        uint32_t ka = 0, kb = 0, ea = 0, eb = 0;
+        if (ln < na) {
+            ka = L.gprop[a + 1 + 2 * ln];
+            kb = L.gprop[b + 1 + 2 * ln];
+            ea = veq[L.gprop[a + 2 + 2 * ln]];
+            eb = veq[L.gprop[b + 2 + 2 * ln]];
+        }
+        bool ok = ln >= na;
+        for (int j = 0; j < nb; j++) {
+            const uint32_t kj = rdlane(kb, j), ej = rdlane(eb, j);
+            if (ka == kj && ln < na) ok = ea == ej;
+        }
+        return __ballot(!ok) == 0;
+    }
+
     // ---- text
-    static __device__ bool can_append(const D& L, int a, int b) {  // TextSegment.canAppend textSegment.ts:86-93
-        if ((L.meta[a] | L.meta[b]) & M_MARKER) return false;
-        const int la = L.len[a];
-        if (la > 0 && L.gtext[L.text[a] + la - 1] == u'\n') return false;
-        return la <= kGranularity || L.len[b] <= kGranularity;
+    static __device__ bool can_append(uint32_t ma, int la, uint32_t mb, int lb) {  // TextSegment.canAppend, textSegment.ts:86-93
+        if ((ma | mb) & M_MARKER) return false;
+        if (la > 0 && (ma & M_NL)) return false;
+        return la <= kGranularity || lb <= kGranularity;
+    }
+    static __device__ void copy_text(const D& L, uint32_t dst, uint32_t src, int n) {  // wave 0
+        for (int k = lane_id(); k < n; k += 64) L.gtext[dst + k] = L.gtext[src + k];
     }
     static __device__ int text_end(lptr<Sc> sc, const KParams& P) { return (P.tcap / 2) * (sc->texthalf + 1); }
 
     // prev.append(seg) (textSegment.ts:99-103): text of b follows text of a
+    // (wave 0; returns false on arena overflow).  Updates L.len/L.text of a; the caller keeps M_NL.
     static __device__ void text_append(D& L, const KParams& P, int a, int b) {
+        PROF(P_TAPPEND);
+        PROF_COUNT(P_NMERGE);
         lptr<Sc> sc = L.sc;
         const int tend = text_end(sc, P);
         const uint32_t oa = L.text[a], ob = L.text[b];
@@ -575,7 +761,7 @@ struct Eng {
                 sc->status = MTR_ERR_CAPACITY;
                 return;
             }
-            for (int k = 0; k < lb; k++) L.gtext[sc->textused + k] = L.gtext[ob + k];
+            copy_text(L, uint32_t(sc->textused), ob, lb);
             sc->textused += lb;
             L.len[a] = la + lb;
             return;
@@ -585,8 +771,8 @@ struct Eng {
             return;
         }
         const uint32_t d = uint32_t(sc->textused);
-        for (int k = 0; k < la; k++) L.gtext[d + k] = L.gtext[oa + k];
-        for (int k = 0; k < lb; k++) L.gtext[d + la + k] = L.gtext[ob + k];
+        copy_text(L, d, oa, la);
+        copy_text(L, d + uint32_t(la), ob, lb);
         sc->textused += la + lb;
         L.text[a] = d;
         L.len[a] = la + lb;
@@ -595,6 +781,7 @@ struct Eng {
     // Semi-space compaction of the text arena: copy every leaf's text into the other half in
     // leaf order (block prefix scan of lengths), then switch halves.
     static __device__ void text_gc(D& L, const KParams& P) {
+        PROF(P_TEXTGC);
         lptr<Sc> sc = L.sc;
         const int S = sc->nseg;
         const int per = (S + NT - 1) / NT;
@@ -624,30 +811,72 @@ struct Eng {
     }
 
     // ------------------------------------------------------------ zamboni
-    // scourNode over one leaf block [cs, ce) (zamboni.ts:122-193); marks M_DEL; returns #kept
-    static __device__ int scour_leaf_block(D& L, const KParams& P, int cs, int ce) {
+    // scourNode (zamboni.ts:122-193) over the child blocks in [cs, ce): a new child block starts at
+    // every leaf with bnd >= 1.  Marks M_DEL; returns #kept (used for a single block).  Wave 0:
+    // the leaves are read 64 at a time into registers and visited in order by readlane.
+    static __device__ int scour_range(D& L, const KParams& P, int cs, int ce) {
         lptr<Sc> sc = L.sc;
-        const gptr<const uint32_t> veq = gp(P.val_eq);
-        int prev = -1, kept = 0;
-        for (int k = cs; k < ce; k++) {
-            const uint32_t m = L.meta[k];
-            if (m & M_DEL) continue;
-            if (L.rseq[k] != RNONE) {
-                if (L.rseq[k] > sc->minseq) kept++;
-                else L.meta[k] = m | M_DEL;  // UNLINK
-                prev = -1;
-            } else if (L.seq[k] <= sc->minseq) {
-                if (prev >= 0 && can_append(L, prev, k) && props_match(L.gprop, veq, L.props[prev], L.props[k]) &&
-                    L.len[k] > 0) {
-                    text_append(L, P, prev, k);
-                    L.meta[k] = m | M_DEL;
+        const int minseq = sc->minseq;
+        int prev = -1, kept = 0, plen = 0;
+        uint32_t pmeta = 0, pprops = 0;
+        for (int base = cs; base < ce; base += 64) {
+            const int i = base + lane_id();
+            uint32_t vm = M_DEL, vp = 0;
+            int vr = 0, vs = 0, vl = 0;
+            if (i < ce) {
+                vm = L.meta[i];
+                vr = L.rseq[i];
+                vs = L.seq[i];
+                vl = L.len[i];
+                vp = L.props[i];
+            }
+            {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
+                const bool q = (vm & (M_NLQ | M_DEL | M_MARKER)) == M_NLQ && vl > 0 && vr == RNONE && vs <= minseq;
+                if (__ballot(q)) {
+                    PROF(P_NLQ);
+                    PROF_COUNT(P_NNLQ);
+                    if (q) {
+                        const uint16_t u = L.gtext[L.text[i] + uint32_t(vl) - 1];
+                        vm = (vm & ~(M_NLQ | M_NL)) | (u == u'\n' ? M_NL : 0u);
+                        L.meta[i] = vm;
+                    }
+                }
+            }
+            const int nk = min(64, ce - base);
+            for (int t = 0; t < nk; t++) {
+                const int k = base + t;
+                const uint32_t m = rdlane(vm, t);
+                if (k > cs && bnd_of(m) >= 1) prev = -1;  // next child block
+                if (m & M_DEL) continue;
+                const int rs = rdlane(vr, t);
+                if (rs != RNONE) {
+                    if (rs > minseq) kept++;
+                    else L.meta[k] = m | M_DEL;  // UNLINK
+                    prev = -1;
+                } else if (rdlane(vs, t) <= minseq) {
+                    const int lk = rdlane(vl, t);
+                    const uint32_t pk = rdlane(vp, t);
+                    if (prev >= 0 && lk > 0 && can_append(pmeta, plen, m, lk) && props_match_w(L, P, pprops, pk)) {
+                        text_append(L, P, prev, k);
+                        plen += lk;
+                        pmeta = (pmeta & ~(M_NL | M_NLQ)) | (m & (M_NL | M_NLQ));
+                        L.meta[prev] = pmeta;
+                        L.meta[k] = m | M_DEL;
+                    } else {
+                        kept++;
+                        if (lk > 0) {
+                            prev = k;
+                            pmeta = m;
+                            plen = lk;
+                            pprops = pk;
+                        } else {
+                            prev = -1;
+                        }
+                    }
                 } else {
                     kept++;
-                    prev = L.len[k] > 0 ? k : -1;
+                    prev = -1;
                 }
-            } else {
-                kept++;
-                prev = -1;
             }
         }
         return kept;
@@ -657,6 +886,8 @@ struct Eng {
     // (zamboni.ts:33-58 + packParent zamboni.ts:63-120).  Lane 0.  Returns 1 if leaves were
     // marked for deletion (the caller compacts).
     static __device__ int zamboni_block(D& L, const KParams& P, int x) {
+        PROF(P_ZBLOCK);
+        PROF_COUNT(P_NZBLOCK);
         lptr<Sc> sc = L.sc;
         const int H = sc->height;
         sc->rs[1] = block_start(L, x, 1);
@@ -671,61 +902,62 @@ struct Eng {
         }
         const int rs1 = sc->rs[1], re1 = sc->re[1];
         const int before = re1 - rs1;
-        const int kept = scour_leaf_block(L, P, rs1, re1);
+        int kept;
+        {
+            PROF(P_SCOUR1);
+            kept = scour_range(L, P, rs1, re1);
+        }
         int first = -1;  // block.needsScour = false, kept on the block's first surviving leaf
-        for (int k = rs1; k < re1; k++)
-            if (!(L.meta[k] & M_DEL)) {
-                first = k;
-                break;
-            }
+        {
+            const int i = rs1 + lane_id();
+            const uint64_t m = __ballot(i < re1 && !(L.meta[i] & M_DEL));
+            if (m) first = rs1 + first_lane(m);
+        }
         if (first >= 0) L.meta[first] = set_ns(set_bnd(L.meta[first], sc->topb[1]), NS_FALSE);
         if (kept >= before) return 0;
         if (kept < kMaxNodesInBlock / 2 && H > 1) {
+            PROF(P_PACK);
+            PROF_COUNT(P_NPACK);
             for (int l = 2; l <= H; l++) {  // packParent chain
                 const int ps = sc->rs[l], pe = sc->re[l];
                 if (l == 2) {
                     // packParent scours every child of P again -- including the block just
                     // scoured: scourNode is not idempotent (a dropped tombstone no longer resets
                     // the merge candidate), zamboni.ts:68-73,122-193.
-                    for (int cs = ps; cs < pe;) {
-                        int ce = cs + 1;
-                        while (ce < pe && bnd_of(L.meta[ce]) < 1) ce++;
-                        scour_leaf_block(L, P, cs, ce);
-                        cs = ce;
-                    }
+                    scour_range(L, P, ps, pe);
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
                 int T = 0;
-                for (int k = ps; k < pe; k++) {
-                    const uint32_t m = L.meta[k];
-                    if (m & M_DEL) continue;
-                    if (l == 2 || bnd_of(m) >= l - 2) T++;
+                for (int wb = ps; wb < pe; wb += 64) {
+                    const int i = wb + lane_id();
+                    const uint32_t m = i < pe ? L.meta[i] : M_DEL;
+                    T += __popcll(__ballot(!(m & M_DEL) && (l == 2 || bnd_of(m) >= l - 2)));
                 }
                 int c = 0;
-                if (T > 0) {
+                if (T > 0) {  // rebalance into c blocks: the first `rem` get base+1 items
                     c = min(kMaxNodesInBlock - 1, T / (kMaxNodesInBlock / 2));
                     if (c < 1) c = 1;
                     const int base = T / c;
                     const int rem = T % c;
-                    int item = 0, nextStart = 0, blk = 0;
-                    for (int k = ps; k < pe; k++) {
-                        uint32_t m = L.meta[k];
-                        if (m & M_DEL) continue;
-                        if (!(l == 2 || bnd_of(m) >= l - 2)) continue;
-                        const bool isStart = item == nextStart;
-                        if (isStart) {
-                            nextStart += base + (blk < rem ? 1 : 0);
-                            blk++;
+                    const int big = rem * (base + 1);
+                    const int top = sc->topb[l];
+                    int item0 = 0;
+                    for (int wb = ps; wb < pe; wb += 64) {
+                        const int i = wb + lane_id();
+                        uint32_t m = i < pe ? L.meta[i] : M_DEL;
+                        const bool it = !(m & M_DEL) && (l == 2 || bnd_of(m) >= l - 2);
+                        const uint64_t mask = __ballot(it);
+                        if (it) {
+                            const int item = item0 + __popcll(mask & lanes_below());
+                            const bool isStart = item < big ? item % (base + 1) == 0 : (item - big) % base == 0;
+                            const int nb = item == 0 ? top : (isStart ? l - 1 : (l == 2 ? 0 : l - 2));
+                            m = set_bnd(m, nb);
+                            if (l == 2 && isStart) m = set_ns(m, NS_UNDEF);
+                            L.meta[i] = m;
                         }
-                        int nb;
-                        if (item == 0) nb = sc->topb[l];
-                        else if (isStart) nb = l - 1;
-                        else nb = l == 2 ? 0 : l - 2;
-                        m = set_bnd(m, nb);
-                        if (l == 2 && isStart) m = set_ns(m, NS_UNDEF);
-                        L.meta[k] = m;
-                        item++;
+                        item0 += __popcll(mask);
                     }
+                    wave_fence();
                 }
                 if (!(c < kMaxNodesInBlock / 2 && l < H)) break;
             }
@@ -735,6 +967,7 @@ struct Eng {
 
     // zamboniSegments (zamboni.ts:19-60): all threads
     static __device__ void zamboni(D& L, const KParams& P) {
+        PROF(P_ZAMBONI);
         lptr<Sc> sc = L.sc;
         if (!sc->collab) return;
         for (int it = 0; it < 2; it++) {
@@ -742,11 +975,11 @@ struct Eng {
             if (sc->heapn == 0 || sc->status != MTR_OK) return;
             if (L.hseq[1] > sc->minseq) return;
             __syncthreads();
-            if (threadIdx.x == 0) sc->b4 = int(heap_pop(L));
+            if (wave0()) sc->b4 = int(heap_pop(L));
             __syncthreads();
             const int x = find_uid(L, uint32_t(sc->b4));
             if (x < 0) continue;
-            if (threadIdx.x == 0) sc->b5 = zamboni_block(L, P, x);
+            if (wave0()) sc->b5 = zamboni_block(L, P, x);
             __syncthreads();
             if (sc->b5) compact(L);
         }
@@ -755,6 +988,7 @@ struct Eng {
 
     // updateSeqNumbers + setMinSeq, client.ts:877-887 / mergeTree.ts:1025-1044
     static __device__ void update_seq(D& L, const KParams& P, int msn, int seq) {
+        PROF(P_UPDSEQ);
         lptr<Sc> sc = L.sc;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -781,8 +1015,10 @@ struct Eng {
     // ensureIntervalBoundary (mergeTree.ts:1706-1716) on the current scan arrays: split the leaf
     // holding pos at an offset > 0; the two halves' scan entries are set in place.
     static __device__ void split_at(D& L, int pos) {
+        PROF(P_SPLIT);
         lptr<Sc> sc = L.sc;
-        if (threadIdx.x == 0) {
+        if (wave0()) {
+            PROF(P_SPLIT1);
             sc->b0 = -1;
             const int S = sc->nseg;
             const int i = lower_bound_E(L, pos);
@@ -805,14 +1041,16 @@ struct Eng {
         const int j = sc->b0;
         if (j < 0) return;
         shift_right1(L, j + 1);
-        if (threadIdx.x == 0) {  // BaseSegment.splitAt, mergeTreeNodes.ts:481-510
+        if (wave0()) {  // BaseSegment.splitAt, mergeTreeNodes.ts:481-510
             const int off = sc->b1;
             const int r = j + 1;
+            const uint32_t mj = L.meta[j];
             L.len[r] = L.len[j] - off;
             L.len[j] = off;
             L.seq[r] = L.seq[j];
             L.rseq[r] = L.rseq[j];
-            L.meta[r] = set_ns(set_bnd(L.meta[j], 0), NS_UNDEF);
+            L.meta[r] = set_ns(set_bnd(mj, 0), NS_UNDEF);
+            L.meta[j] = (mj & ~M_NL) | M_NLQ;
             L.text[r] = L.text[j] + uint32_t(off);
             L.props[r] = L.props[j];
             L.rm[r] = L.rm[j];
@@ -830,8 +1068,10 @@ struct Eng {
 
     // insertSegments/blockInsert/insertingWalk with onLeaf (mergeTree.ts:1397-1427, 1594-1685),
     // on the current scan arrays
+    // `pre`: lane t holds unit t of the op's text in `pf` (prefetched during the previous op)
     static __device__ void insert_at(D& L, const KParams& P, const View& v, const mtr_op& op, int seq,
-                                     uint32_t client, const mtr_doc_desc& dd) {
+                                     uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf) {
+        PROF(P_INSERT);
         lptr<Sc> sc = L.sc;
         const bool marker = (op.flags & MTR_F_MARKER) != 0;
         const int len = marker ? 1 : int(op.payload2);
@@ -844,11 +1084,18 @@ struct Eng {
                 __syncthreads();
                 return;
             }
-            const gptr<const uint16_t> src = gp(P.btext) + dd.text_base + op.payload;
-            for (int k = threadIdx.x; k < len; k += NT) L.gtext[t0 + k] = src[k];
+            PROF(P_TEXTCOPY);
+            if (pre) {
+                if (lane_id() < len) L.gtext[t0 + lane_id()] = uint16_t(pf);
+            } else {
+                const gptr<const uint16_t> src = gp(P.btext) + dd.text_base + op.payload;
+                for (int k = threadIdx.x; k < len; k += NT) L.gtext[t0 + k] = src[k];
+            }
         }
+        const bool nl = pre && __ballot(lane_id() == len - 1 && pf == u'\n') != 0;
         const int pos = op.pos1;
-        if (threadIdx.x == 0) {
+        if (wave0()) {
+            PROF(P_INS1);
             const int S = sc->nseg;
             int slot = -1, inherit = 0;
             if (S == 0) {
@@ -879,10 +1126,11 @@ struct Eng {
         const int slot = sc->b0;
         if (slot < 0) return;
         shift_right1(L, slot);
-        if (threadIdx.x == 0) {
+        if (wave0()) {
             const int S = sc->nseg;
             uint32_t m = client & M_CLIENT_MASK;
             if (marker) m |= M_MARKER;
+            else m |= pre ? (nl ? M_NL : 0u) : M_NLQ;
             if (op.flags & MTR_F_NOREF) m |= M_NOREF;
             if (S == 0) {
                 sc->height = 1;
@@ -915,8 +1163,9 @@ struct Eng {
     // visible length > 0 inside [start, end), on the current scan arrays.  Lane 0.
     static __device__ void range_walk(D& L, const KParams& P, const View& v, int start, int end, int seq,
                                       uint32_t client, int is_remove, uint32_t pp) {
+        PROF(P_RANGE);
         lptr<Sc> sc = L.sc;
-        if (threadIdx.x == 0 && end != start) {
+        if (wave0() && end != start) {
             const int S = sc->nseg;
             int nmemo = 0;
             for (int j = lower_bound_E(L, start + 1); j < S; j++) {
@@ -1017,6 +1266,9 @@ struct Eng {
             sc->fail_op = h.fail_op; sc->max_heap = h.max_heap; sc->ops_done = 0; sc->texthalf = h.texthalf;
             sc->sum_s = 0;
             sc->sum_l = 0;
+#ifdef MTR_PROF
+            for (int q = 0; q < P_COUNT; q++) sc->prof[q] = 0;
+#endif
             if (P.gen) st_struct(L.gst, ld_struct<mtr_synth_state>(gp(P.gen_state) + d));
         }
         __syncthreads();
@@ -1079,6 +1331,9 @@ struct Eng {
             h.texthalf = sc->texthalf;
             st_struct(hp, h);
             if (P.gen) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
+#ifdef MTR_PROF
+            for (int q = 0; q < P_COUNT; q++) atomicAdd(&g_prof[q], sc->prof[q]);
+#endif
             if (sc->ops_done) {
                 atomicAdd(P.stat_ops, (unsigned long long)sc->ops_done);
                 atomicAdd(P.stat_ops + 1, sc->sum_s);
@@ -1149,9 +1404,43 @@ struct Eng {
         load_doc(L, P, d);
         lptr<Sc> sc = L.sc;
         const gptr<const mtr_op> ops = gp(P.ops) + dd.op_begin + cursor;
+        const gptr<const uint16_t> btext = gp(P.btext) + dd.text_base;
+        const int ln = lane_id();
+        // lane t holds the 8 words of op (chunk + t); the next op's text is prefetched into `pf`
+        uint32_t ow[8];
+        uint32_t pf = 0, npf = 0;
+        bool pre = false, npre = false;
         for (int k = 0; k < n_ops; k++) {
-            if (P.gen) gen_op(L, P, dd, cursor + k);
-            const mtr_op op = ld_struct<mtr_op>(ops + k);
+            PROF(P_OP);
+            mtr_op op;
+            if (P.gen) {
+                gen_op(L, P, dd, cursor + k);
+                op = ld_struct<mtr_op>(ops + k);
+                pre = false;
+            } else {
+                if ((k & 63) == 0) {
+                    const gptr<const uint32_t> w = (gptr<const uint32_t>)(ops + k + ln);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) ow[q] = k + ln < n_ops ? w[q] : 0u;
+                    npre = false;
+                }
+                uint32_t wv[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) wv[q] = rdlane(ow[q], k & 63);
+                __builtin_memcpy(&op, wv, sizeof(op));
+                pre = npre;
+                pf = npf;
+                npre = false;
+                const int t1 = (k + 1) & 63;
+                if (t1 != 0 && k + 1 < n_ops) {  // issue the next insert's text loads now
+                    const uint32_t w0 = rdlane(ow[0], t1), len1 = rdlane(ow[7], t1), off1 = rdlane(ow[6], t1);
+                    const uint32_t ty = w0 & 0xffu, fl = (w0 >> 8) & 0xffu;
+                    if ((ty == MTR_OP_INSERT || ty == MTR_OP_LOCAL_INSERT) && !(fl & MTR_F_MARKER) && len1 <= 64) {
+                        npre = true;
+                        npf = uint32_t(ln) < len1 ? uint32_t(btext[off1 + ln]) : 0u;
+                    }
+                }
+            }
             if (threadIdx.x == 0) {
                 sc->sum_s += (unsigned long long)sc->nseg;
                 if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER))
@@ -1194,7 +1483,7 @@ struct Eng {
                 case MTR_OP_LOCAL_INSERT:
                     prefix(L, v, P.new_length_calc);
                     split_at(L, op.pos1);
-                    insert_at(L, P, v, op, seq, client, dd);
+                    insert_at(L, P, v, op, seq, client, dd, pre, pf);
                     if (sc->collab) zamboni(L, P);
                     break;
                 case MTR_OP_REMOVE:

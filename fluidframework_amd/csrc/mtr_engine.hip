@@ -646,4 +646,25 @@ int mtr_last_timing(mtr_engine* e, double* out, int32_t n) {
     return MTR_OK;
 }
 
+int mtr_profile(mtr_engine* e, uint64_t* out, int32_t n, int32_t reset) {
+    if (!e || !out) return MTR_ERR_BAD_OP;
+    unsigned long long v[32] = {0};
+#ifdef MTR_PROF
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return MTR_ERR_ASSERT;
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(mtr::g_prof), sizeof(v)) != hipSuccess) return MTR_ERR_ASSERT;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mtr::g_prof), z, sizeof(z)) != hipSuccess) return MTR_ERR_ASSERT;
+    }
+#else
+    (void)reset;
+#endif
+    for (int i = 0; i < n && i < 32; i++) out[i] = v[i];
+#ifdef MTR_PROF
+    return MTR_OK;
+#else
+    return MTR_ERR_UNSUPPORTED;
+#endif
+}
+
 }  // extern "C"

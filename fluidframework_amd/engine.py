@@ -36,7 +36,8 @@ def lib():
     """Load libmtr.so (never falls back to anything else)."""
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "libmtr.so")
+        # MTR_LIB=libmtr_prof.so selects the phase-timer build (python -m fluidframework_amd.build --prof)
+        path = os.path.join(_HERE, os.environ.get("MTR_LIB", "libmtr.so"))
         if not os.path.exists(path):
             raise EngineError(f"{path} missing: build it with `python -m fluidframework_amd.build`")
         L = C.CDLL(path)
@@ -65,6 +66,8 @@ def lib():
         L.mtr_last_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.mtr_last_timing.restype = C.c_int
         L.mtr_last_error.restype = C.c_char_p
+        L.mtr_profile.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
+        L.mtr_profile.restype = C.c_int
         L.mtr_generate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mtr_generate.restype = C.c_int
         L.mtr_download_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -198,10 +201,23 @@ class Engine:
                 "sum_leaves_before_op", "text_units_inserted"]
         return dict(zip(keys, (int(x) for x in out)))
 
+    def profile(self, reset=True) -> dict:
+        """Phase timers of a -DMTR_PROF build (empty dict otherwise)."""
+        out = np.zeros(len(PROFILE_KEYS), dtype="<u8")
+        if lib().mtr_profile(self.h, out.ctypes.data, len(PROFILE_KEYS), int(reset)) != 0:
+            return {}
+        return dict(zip(PROFILE_KEYS, (int(x) for x in out)))
+
     def timing(self) -> dict:
         out = np.zeros(3, dtype="<f8")
         lib().mtr_last_timing(self.h, out.ctypes.data, 3)
         return {"apply_ms": float(out[0]), "summary_ms": float(out[1]), "apply_launches": int(out[2])}
+
+
+PROFILE_KEYS = ["op", "prefix", "split", "shift", "insert", "range", "zamboni", "zblock", "compact", "find_uid",
+                "text_gc", "loadstore", "text_copy", "update_seq", "n_zblock", "n_compact", "scour1", "pack", "nlq",
+                "pmatch", "tappend", "heap", "overflow", "n_pack", "n_merge", "n_pmatch", "n_nlq", "split1", "ins1",
+                "fetch", "x1", "x2"]
 
 
 def caps_for(batch, margin=1.25):

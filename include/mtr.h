@@ -110,6 +110,10 @@ int mtr_generate(mtr_engine* e, const struct mtr_synth_cfg* cfg, const mtr_batch
 int mtr_download_batch(mtr_engine* e, uint32_t lo, uint32_t hi, mtr_doc_desc* docs, mtr_op* ops, uint16_t* text,
                        uint64_t text_cap);
 
+/* Apply-kernel phase timers (thread-0 clock cycles summed over documents; see apply.hip.h P_*).
+ * Only a -DMTR_PROF build collects them; otherwise returns MTR_ERR_UNSUPPORTED and zeros. */
+int mtr_profile(mtr_engine* e, uint64_t* out, int32_t n, int32_t reset);
+
 /* Human-readable description of the last engine-level error (static storage). */
 const char* mtr_last_error(void);
 
