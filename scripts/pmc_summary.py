@@ -1,0 +1,50 @@
+"""Summarise a scripts/profile_box.sh run: per-launch averages of the apply kernel's PMC counters
+over the timed launches (the last `--launches` apply_kernel dispatches; the earlier ones are the
+record-mode generation pass), with the gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md, HBM)."""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+ap = argparse.ArgumentParser()
+ap.add_argument("dir")
+ap.add_argument("--launches", type=int, default=16)
+ap.add_argument("--kernel", default="apply_kernel")
+ap.add_argument("--docs", type=int, default=100000)
+ap.add_argument("--ops", type=int, default=1000)
+ap.add_argument("--out", default=None)
+a = ap.parse_args()
+
+per = collections.Counter()
+for f in sorted(glob.glob(os.path.join(a.dir, "*", "*_counter_collection.csv"))):
+    d = collections.defaultdict(dict)
+    for r in csv.DictReader(open(f)):
+        if a.kernel in r["Kernel_Name"]:
+            d[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+    ids = sorted(d)[-a.launches:]
+    for i in ids:
+        for k, v in d[i].items():
+            per[k] += v / len(ids)
+out = {"kernel": a.kernel, "docs": a.docs, "ops": a.ops, "launches_averaged": a.launches}
+out["counters_per_launch"] = dict(per)
+if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+    # FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads
+    # (upper bound of the correction: our reads are 4-B-per-lane, so the raw value is a lower bound)
+    fetch = per["FETCH_SIZE"] * 1024.0
+    write = per["WRITE_SIZE"] * 1024.0
+    out["hbm_read_bytes_per_launch_raw"] = fetch
+    out["hbm_write_bytes_per_launch"] = write
+    out["hbm_bytes_per_launch"] = 2.0 * fetch + write
+    out["note"] = "hbm_bytes = 2*FETCH_SIZE (gfx950 correction) + WRITE_SIZE, KiB->bytes"
+if "SQ_LDS_BANK_CONFLICT" in per and "SQ_LDS_IDX_ACTIVE" in per:
+    out["lds_bank_conflict_rate"] = per["SQ_LDS_BANK_CONFLICT"] / max(1.0, per["SQ_LDS_IDX_ACTIVE"])
+if "SQ_WAVE_CYCLES" in per:
+    wc = per["SQ_WAVE_CYCLES"]
+    out["wait_any_frac"] = per.get("SQ_WAIT_ANY", 0) / wc
+    out["active_inst_frac"] = per.get("SQ_ACTIVE_INST_ANY", 0) / wc
+s = json.dumps(out, indent=1)
+print(s)
+if a.out:
+    open(a.out, "w").write(s + "\n")
