@@ -1,22 +1,26 @@
 // apply.hip.h -- the op-apply kernel of the MI355X merge-tree replay engine.
 //
-// One workgroup (256 threads = 4 wave64) owns one document for the whole launch and applies
-// that document's ops strictly in order (ops never cross documents).  The document's leaves
-// live as flat structure-of-arrays records in tree order -- in LDS when they fit, otherwise in
-// the document's HBM slab (Doc<true>, same code) -- and the reference's B+tree
-// (MaxNodesInBlock = 8, mergeTreeNodes.ts:330) is kept exactly, encoded per leaf as `bnd` =
-// number of tree levels at which the leaf starts a block.
+// One wave64 (the whole workgroup) owns one document for the whole launch and applies that
+// document's ops strictly in order (ops never cross documents).  The document's leaves live as
+// flat structure-of-arrays records in tree order -- in LDS when they fit, otherwise in the
+// document's HBM slab (Doc<true>, same code) -- and the reference's B+tree (MaxNodesInBlock = 8,
+// mergeTreeNodes.ts:330) is kept exactly, encoded per leaf as `bnd` = number of tree levels at
+// which the leaf starts a block.
 //
-// Per op, the O(S) work runs on all lanes: one visibility prefix scan for the op's
-// (refSeq, clientId) view, which replaces PartialSequenceLengths (partialLengths.ts:698) and the
-// length queries of insertingWalk / nodeMap (mergeTree.ts:1740, 2526); the one-slot shift that
-// makes room for a split or an insert (mergeTree.ts:1831-1838); the uid search for popped LRU
-// entries; and the stream compaction after zamboni (zamboni.ts:19-120).  The scan arrays stay
-// valid across the op's splits, so an op scans once.  The sequential control (tie-break, block
-// splits, heap, zamboni scour/pack decisions) runs as uniform code on wave 0, whose 64 lanes turn
-// every walk over leaves (block bounds, binary search, child counts, pack relabelling) into ballots
-// and every HBM access (text copies, property sets) into one coalesced round trip; waves 1-3 wait
-// at the next barrier.
+// Single-wave program:
+//  * the document's scalar state (St: leaf count, tree height, seq window, heap size, arena
+//    cursors, status) is register-resident and wave-uniform (SGPRs); values read from LDS/HBM at
+//    a uniform address are made uniform with readfirstlane;
+//  * there are no workgroup barriers: one wave's LDS and vector-memory operations are performed in
+//    order and are coherent across its lanes (LLVM AMDGPU memory model, wavefront scope), so a
+//    phase boundary is only a compiler ordering point (wsync);
+//  * the O(S) work runs on all lanes: the visibility prefix scan for the op's (refSeq, clientId)
+//    view (replaces PartialSequenceLengths, partialLengths.ts:698, and the length queries of
+//    insertingWalk / nodeMap, mergeTree.ts:1740, 2526), the one-slot shift that makes room for a
+//    split or an insert (mergeTree.ts:1831-1838), the uid search for popped LRU entries, the range
+//    walk of remove/annotate, and the stream compaction after zamboni (zamboni.ts:19-120);
+//  * the sequential control (tie-break, block splits, heap, zamboni scour/pack decisions) is
+//    uniform code whose walks over leaves are ballots over 64 leaves at a time.
 //
 // Memory spaces are explicit: LDS arrays are address_space(3) pointers (ds_read/ds_write),
 // HBM arrays address_space(1) (global_load/store) -- never generic flat accesses.
@@ -29,11 +33,12 @@
 #include "../../include/mtr_synth.h"
 #include "../../include/mtr_types.h"
 
+#define MTR_DI __device__ __forceinline__
+
 namespace mtr {
 
-constexpr int NT = 64;
-constexpr int NWAVES = NT / 64;
-constexpr int32_t RNONE = 0x7fffffff;  // removedSeq of a live leaf
+constexpr int NT = 64;                  // one wave per document
+constexpr int32_t RNONE = 0x7fffffff;   // removedSeq of a live leaf
 constexpr uint32_t NONE32 = 0xffffffffu;
 constexpr int kMaxNodesInBlock = 8;
 constexpr int kGranularity = 256;  // TextSegmentGranularity, textSegment.ts:35
@@ -74,7 +79,7 @@ __device__ inline gptr<T> gp(T* p) {
 // Whole-struct copies through address-space-qualified pointers (C++ copy operations expect
 // generic `this`), done word by word so they stay global_/ds_ accesses.
 template <class T, class Q>
-__device__ inline T ld_struct(Q p) {
+MTR_DI T ld_struct(Q p) {
     static_assert(sizeof(T) % 4 == 0, "word-sized struct");
     typedef typename std::conditional<std::is_same<Q, lptr<T>>::value || std::is_same<Q, lptr<const T>>::value,
                                       lptr<const uint32_t>, gptr<const uint32_t>>::type W;
@@ -86,8 +91,20 @@ __device__ inline T ld_struct(Q p) {
     __builtin_memcpy(&t, v, sizeof(T));
     return t;
 }
+// a struct read at a wave-uniform address, made wave-uniform (SGPRs)
+template <class T>
+MTR_DI T uni_struct(const T& x) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized struct");
+    uint32_t v[sizeof(T) / 4];
+    __builtin_memcpy(v, &x, sizeof(T));
+#pragma unroll
+    for (unsigned i = 0; i < sizeof(T) / 4; i++) v[i] = uint32_t(__builtin_amdgcn_readfirstlane(int(v[i])));
+    T t;
+    __builtin_memcpy(&t, v, sizeof(T));
+    return t;
+}
 template <class T, class Q>
-__device__ inline void st_struct(Q p, const T& t) {
+MTR_DI void st_struct(Q p, const T& t) {
     static_assert(sizeof(T) % 4 == 0, "word-sized struct");
     typedef typename std::conditional<std::is_same<Q, lptr<T>>::value, lptr<uint32_t>, gptr<uint32_t>>::type W;
     const W w = (W)p;
@@ -147,21 +164,22 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
        P_TAPPEND, P_HEAP, P_OVERFLOW, P_NPACK, P_NMERGE, P_NPMATCH, P_NNLQ, P_SPLIT1, P_INS1, P_FETCH, P_X1, P_X2,
        P_COUNT };
 
-// scalar document state, broadcast slots and lane-0 scratch, in LDS
+// LDS-side scratch of one document: per-level block bounds for zamboni, record-mode broadcast
 struct Sc {
-    int nseg, height, minseq, curseq;
-    int collab, local, heapn, uidnext;
-    int textused, propused, rmused, status;
-    int b0, b1, b2, b3;
-    int b4, b5, b6, b7;
-    int red[2 * NWAVES];
-    int fail_op, max_heap, ops_done, texthalf;
-    unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
     int rs[MAXH + 1], re[MAXH + 1], topb[MAXH + 1];
-    uint32_t memo_old[4], memo_new[4];
+    int gen_ref, gen_client;
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];
 #endif
+};
+
+// Register-resident, wave-uniform scalar state of the document being applied.
+struct St {
+    int nseg, height, minseq, curseq;
+    int collab, local, heapn, uidnext;
+    int textused, propused, rmused, status;
+    int fail_op, max_heap, ops_done, texthalf;
+    unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
 
 struct View {
@@ -183,67 +201,38 @@ struct Doc {
     int cap, lhcap;
 };
 
-__device__ inline int bnd_of(uint32_t m) { return int((m & M_BND_MASK) >> M_BND_SHIFT); }
-__device__ inline uint32_t set_bnd(uint32_t m, int b) { return (m & ~M_BND_MASK) | (uint32_t(b) << M_BND_SHIFT); }
-__device__ inline uint32_t ns_of(uint32_t m) { return (m & M_NS_MASK) >> M_NS_SHIFT; }
-__device__ inline uint32_t set_ns(uint32_t m, uint32_t ns) { return (m & ~M_NS_MASK) | (ns << M_NS_SHIFT); }
+MTR_DI int bnd_of(uint32_t m) { return int((m & M_BND_MASK) >> M_BND_SHIFT); }
+MTR_DI uint32_t set_bnd(uint32_t m, int b) { return (m & ~M_BND_MASK) | (uint32_t(b) << M_BND_SHIFT); }
+MTR_DI uint32_t ns_of(uint32_t m) { return (m & M_NS_MASK) >> M_NS_SHIFT; }
+MTR_DI uint32_t set_ns(uint32_t m, uint32_t ns) { return (m & ~M_NS_MASK) | (ns << M_NS_SHIFT); }
 
-// ------------------------------------------------------------------ block primitives
-__device__ inline int wave_incl_scan(int x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        int y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x;
-}
-__device__ inline int lane_id() { return int(threadIdx.x & 63); }
-__device__ inline uint64_t lanes_below() { return (uint64_t(1) << lane_id()) - 1; }
-__device__ inline int first_lane(uint64_t m) { return __ffsll((long long)m) - 1; }
+// ------------------------------------------------------------------ wave primitives
+MTR_DI int lane_id() { return int(threadIdx.x); }  // blockDim.x == 64
+MTR_DI uint64_t lanes_below() { return (uint64_t(1) << lane_id()) - 1; }
+MTR_DI int first_lane(uint64_t m) { return __ffsll((long long)m) - 1; }
+MTR_DI int last_lane(uint64_t m) { return 63 - __clzll((long long)m); }
+MTR_DI int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+MTR_DI uint32_t uniu(uint32_t x) { return uint32_t(__builtin_amdgcn_readfirstlane(int(x))); }
 template <class T>
-__device__ inline T rdlane(T x, int l) {  // v_readlane with a wave-uniform lane index
+MTR_DI T rdlane(T x, int l) {  // v_readlane with a wave-uniform lane index
     return T(__builtin_amdgcn_readlane(int(x), l));
 }
-// order this wave's LDS/HBM writes before its later reads (other lanes' addresses included)
-__device__ inline void wave_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+// Phase boundary inside one wave: orders the compiler's memory operations (the hardware already
+// performs one wave's LDS and vector-memory operations in order; wavefront scope needs no waits).
+MTR_DI void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ inline bool wave0() { return threadIdx.x < 64; }
-__device__ inline int wave_max(int x) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) x = max(x, __shfl_xor(x, d, 64));
+// inclusive add-scan over the 64 lanes: DPP row shifts within rows of 16, then row broadcasts
+MTR_DI int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return x;
-}
-
-// exclusive block scan; also returns the block total in *total
-__device__ inline int block_excl_scan(lptr<Sc> sc, int x, int* total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int inc = wave_incl_scan(x);
-    if (lane == 63) sc->red[w] = inc;
-    __syncthreads();
-    int base = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < NWAVES; k++) {
-        int r = sc->red[k];
-        if (k < w) base += r;
-        tot += r;
-    }
-    __syncthreads();
-    *total = tot;
-    return base + inc - x;
-}
-__device__ inline int block_max(lptr<Sc> sc, int x) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int m = wave_max(x);
-    if (lane == 0) sc->red[w] = m;
-    __syncthreads();
-    int r = sc->red[0];
-#pragma unroll
-    for (int k = 1; k < NWAVES; k++) r = max(r, sc->red[k]);
-    __syncthreads();
-    return r;
 }
 
 // matchProperties (properties.ts:71-105) with values compared by equivalence class
@@ -274,18 +263,18 @@ __host__ __device__ inline size_t lds_bytes(int cap, int lhcap) {
 }
 __host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
 
-// Phase timers (builds with -DMTR_PROF only): thread-0 clock cycles per phase, summed over
+// Phase timers (builds with -DMTR_PROF only): lane-0 clock cycles per phase, summed over
 // documents into g_prof (mtr_profile()).
-
 #ifdef MTR_PROF
 __device__ unsigned long long g_prof[P_COUNT];
 struct ProfScope {
     lptr<Sc> sc;
     int id;
     long long t;
-    __device__ ProfScope(lptr<Sc> s, int i) : sc(s), id(i), t(threadIdx.x == 0 ? clock64() : 0) {}
+    __device__ ProfScope(lptr<Sc> s, int i) : sc(s), id(i), t(clock64()) {}
     __device__ ~ProfScope() {
-        if (threadIdx.x == 0) sc->prof[id] += (unsigned long long)(clock64() - t);
+        const long long d = clock64() - t;
+        if (threadIdx.x == 0) sc->prof[id] += (unsigned long long)d;
     }
 };
 #define PROF(id) ProfScope _prof_scope(L.sc, id)
@@ -303,8 +292,7 @@ struct Eng {
     using A = typename D::template A<T>;
 
     // ------------------------------------------------------------ visibility
-    static __device__ bool in_removers(const D& L, int i, uint32_t c) {
-        const uint32_t m = L.meta[i];
+    static MTR_DI bool in_removers(const D& L, int i, uint32_t m, uint32_t c) {
         if (((m >> M_FREM_SHIFT) & 0xffu) == c) return true;
         if (!(m & M_OVERLAP)) return false;
         uint32_t cell = L.rm[i];
@@ -317,63 +305,61 @@ struct Eng {
     }
 
     // nodeLength for a leaf (mergeTree.ts:916-1004): -1 = undefined
-    static __device__ int vis_len(const D& L, int i, const View& v, int newlen, int minseq) {
+    static MTR_DI int vis_len(const D& L, int i, const View& v, int newlen, int minseq) {
         const int len = L.len[i];
         const int rseq = L.rseq[i];
+        const uint32_t m = L.meta[i];
+        const int seq = L.seq[i];
         const bool removed = rseq != RNONE;
         if (v.local) {  // localNetLength, mergeTree.ts:613-634
             if (removed) return newlen ? 0 : (rseq > minseq ? 0 : -1);
             return len;
         }
-        const uint32_t m = L.meta[i];
         const uint32_t cl = m & M_CLIENT_MASK;
-        const int seq = L.seq[i];
         if (newlen) {  // mergeTree.ts:935-965
             if (removed) {
                 if (rseq <= minseq) return -1;
-                if (rseq <= v.ref || in_removers(L, i, v.client)) return 0;
+                if (rseq <= v.ref || in_removers(L, i, m, v.client)) return 0;
             }
             return (seq <= v.ref || cl == v.client) ? len : 0;
         }
         if (removed && rseq <= v.ref) return -1;  // mergeTree.ts:967-976
         if (cl == v.client || seq <= v.ref) {
-            if (removed) return in_removers(L, i, v.client) ? 0 : len;
+            if (removed) return in_removers(L, i, m, v.client) ? 0 : len;
             return len;
         }
         if (removed) return -1;
         return 0;
     }
 
-    // V[i] = visible length, E[i] = inclusive prefix of max(V,0).  Contiguous chunk per thread.
-    static __device__ void prefix(D& L, const View& v, int newlen) {
+    // V[i] = visible length, E[i] = inclusive prefix of max(V,0); rounds of 64 leaves
+    static MTR_DI void prefix(D& L, const St& s, const View& v, int newlen) {
         PROF(P_PREFIX);
-        const int S = L.sc->nseg;
-        const int minseq = L.sc->minseq;
-        const int per = (S + NT - 1) / NT;
-        const int lo = min(S, int(threadIdx.x) * per), hi = min(S, lo + per);
-        int sum = 0;
-        for (int i = lo; i < hi; i++) {
-            const int x = vis_len(L, i, v, newlen, minseq);
-            L.V[i] = x;
-            sum += max(x, 0);
+        const int S = s.nseg;
+        const int ln = lane_id();
+        int carry = 0;
+        for (int base = 0; base < S; base += 64) {
+            const int i = base + ln;
+            int x = 0;
+            if (i < S) x = vis_len(L, i, v, newlen, s.minseq);
+            const int inc = wave_incl_scan(max(x, 0));
+            if (i < S) {
+                L.V[i] = x;
+                L.E[i] = carry + inc;
+            }
+            carry += rdlane(inc, 63);
         }
-        int tot;
-        int run = block_excl_scan(L.sc, sum, &tot);
-        for (int i = lo; i < hi; i++) {
-            run += max(L.V[i], 0);
-            L.E[i] = run;
-        }
-        __syncthreads();
+        wsync();
     }
 
     // ------------------------------------------------------------ data movement
-    // move leaves [at, S) (with their scan entries) to [at+1, S+1); rounds of NT from the top
-    static __device__ void shift_right1(D& L, int at) {
+    // move leaves [at, S) (with their scan entries) to [at+1, S+1); rounds of 64 from the top
+    static MTR_DI void shift_right1(D& L, const St& s, int at) {
         PROF(P_SHIFT);
-        const int S = L.sc->nseg;
-        for (int hi = S; hi > at; hi -= NT) {
-            const int lo = max(at, hi - NT);
-            const int i = lo + int(threadIdx.x);
+        const int S = s.nseg;
+        for (int hi = S; hi > at; hi -= 64) {
+            const int lo = max(at, hi - 64);
+            const int i = lo + lane_id();
             const bool act = i < hi;
             int a0 = 0, a1 = 0, a2 = 0, a8 = 0, a9 = 0;
             uint32_t a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
@@ -381,24 +367,24 @@ struct Eng {
                 a0 = L.len[i]; a1 = L.seq[i]; a2 = L.rseq[i]; a3 = L.meta[i]; a4 = L.text[i];
                 a5 = L.props[i]; a6 = L.rm[i]; a7 = L.uid[i]; a8 = L.E[i]; a9 = L.V[i];
             }
-            __syncthreads();
+            wsync();
             if (act) {
                 L.len[i + 1] = a0; L.seq[i + 1] = a1; L.rseq[i + 1] = a2; L.meta[i + 1] = a3; L.text[i + 1] = a4;
                 L.props[i + 1] = a5; L.rm[i + 1] = a6; L.uid[i + 1] = a7; L.E[i + 1] = a8; L.V[i + 1] = a9;
             }
-            __syncthreads();
+            wsync();
         }
     }
 
-    // stream compaction of leaves without M_DEL (zamboni unlink / append); rounds of NT from
-    // the bottom; destinations never exceed sources
-    static __device__ void compact(D& L) {
+    // stream compaction of leaves without M_DEL (zamboni unlink / append); rounds of 64 from the
+    // bottom; destinations never exceed sources
+    static MTR_DI void compact(D& L, St& s) {
         PROF(P_COMPACT);
         PROF_COUNT(P_NCOMPACT);
-        const int S = L.sc->nseg;
+        const int S = s.nseg;
         int base = 0;
-        for (int lo = 0; lo < S; lo += NT) {
-            const int i = lo + int(threadIdx.x);
+        for (int lo = 0; lo < S; lo += 64) {
+            const int i = lo + lane_id();
             const bool act = i < S;
             int a0 = 0, a1 = 0, a2 = 0;
             uint32_t a3 = M_DEL, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
@@ -406,85 +392,82 @@ struct Eng {
                 a0 = L.len[i]; a1 = L.seq[i]; a2 = L.rseq[i]; a3 = L.meta[i];
                 a4 = L.text[i]; a5 = L.props[i]; a6 = L.rm[i]; a7 = L.uid[i];
             }
-            const int keep = (act && !(a3 & M_DEL)) ? 1 : 0;
-            int tot;
-            const int off = block_excl_scan(L.sc, keep, &tot);  // its barriers order reads before writes
+            const bool keep = act && !(a3 & M_DEL);
+            const uint64_t km = __ballot(keep);
+            wsync();
             if (keep) {
-                const int d = base + off;
+                const int d = base + __popcll(km & lanes_below());
                 L.len[d] = a0; L.seq[d] = a1; L.rseq[d] = a2; L.meta[d] = a3;
                 L.text[d] = a4; L.props[d] = a5; L.rm[d] = a6; L.uid[d] = a7;
             }
-            base += tot;
-            __syncthreads();
+            base += __popcll(km);
+            wsync();
         }
-        if (threadIdx.x == 0) {
-            L.sc->nseg = base;
-            if (base == 0) L.sc->height = 1;
-        }
-        __syncthreads();
+        s.nseg = base;
+        if (base == 0) s.height = 1;
     }
 
-    // index of the leaf with this uid, -1 if unlinked
-    static __device__ int find_uid(D& L, uint32_t u) {
+    // index of the leaf with this uid, -1 if unlinked (uids are unique)
+    static MTR_DI int find_uid(const D& L, const St& s, uint32_t u) {
         PROF(P_FINDUID);
-        const int S = L.sc->nseg;
-        int found = -1;
-        for (int i = threadIdx.x; i < S; i += NT)
-            if (L.uid[i] == u) found = i;
-        return block_max(L.sc, found);
+        const int S = s.nseg;
+        for (int base = 0; base < S; base += 64) {
+            const int i = base + lane_id();
+            const uint64_t m = __ballot(i < S && L.uid[min(i, S - 1)] == u);
+            if (m) return base + first_lane(m);
+        }
+        return -1;
     }
 
-    // ------------------------------------------------------------ wave-0 helpers
-    // (uniform code on wave 0: every lane holds the same scalars; the searches are ballots)
-
+    // ------------------------------------------------------------ searches (ballots)
     // start of the level-`level` block holding leaf x: last i <= x with i == 0 or bnd >= level
-    static __device__ int block_start(const D& L, int x, int level) {
+    static MTR_DI int block_start(const D& L, int x, int level) {
         for (int base = x;; base -= 64) {
             const int i = base - lane_id();
-            const uint64_t m = __ballot(i <= 0 || bnd_of(L.meta[i]) >= level);
+            const uint64_t m = __ballot(i <= 0 || bnd_of(L.meta[max(i, 0)]) >= level);
             if (m) return max(0, base - first_lane(m));
         }
     }
     // end (exclusive) of the level-`level` block holding leaf x
-    static __device__ int block_end(const D& L, int x, int level) {
-        const int S = L.sc->nseg;
+    static MTR_DI int block_end(const D& L, const St& s, int x, int level) {
+        const int S = s.nseg;
         for (int base = x + 1;; base += 64) {
             const int i = base + lane_id();
-            const uint64_t m = __ballot(i >= S || bnd_of(L.meta[i]) >= level);
+            const uint64_t m = __ballot(i >= S || bnd_of(L.meta[max(min(i, S - 1), 0)]) >= level);
             if (m) return base + first_lane(m);
         }
     }
     // first i with E[i] >= pos (S if none): 64-ary search
-    static __device__ int lower_bound_E(const D& L, int pos) {
-        int lo = 0, hi = L.sc->nseg;  // answer in [lo, hi]
+    static MTR_DI int lower_bound_E(const D& L, const St& s, int pos) {
+        int lo = 0, hi = s.nseg;  // answer in [lo, hi]
         const int ln = lane_id();
         while (hi - lo > 64) {
             const int stride = (hi - lo + 63) >> 6;
             const int idx = lo + (ln + 1) * stride - 1;
-            const uint64_t m = __ballot(idx >= hi || L.E[idx] >= pos);
+            const uint64_t m = __ballot(idx >= hi || L.E[min(idx, hi - 1)] >= pos);
             const int k = first_lane(m);  // lane 63 always qualifies
             const int nlo = lo + k * stride;
             hi = min(hi, lo + (k + 1) * stride - 1);
             lo = nlo;
         }
         const int i = lo + ln;
-        const uint64_t m = __ballot(i < hi && L.E[i] >= pos);
+        const uint64_t m = __ballot(i < hi && L.E[min(i, max(hi - 1, 0))] >= pos);
         return m ? lo + first_lane(m) : hi;
     }
     // number of leaves in [bs, be) with bnd >= minb
-    static __device__ int count_bnd(const D& L, int bs, int be, int minb) {
+    static MTR_DI int count_bnd(const D& L, int bs, int be, int minb) {
         int c = 0;
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
-            c += __popcll(__ballot(i < be && bnd_of(L.meta[i]) >= minb));
+            c += __popcll(__ballot(i < be && bnd_of(L.meta[min(i, be - 1)]) >= minb));
         }
         return c;
     }
     // index of the n-th (0-based) leaf in [bs, be) with bnd >= minb, -1 if none
-    static __device__ int nth_bnd(const D& L, int bs, int be, int minb, int n) {
+    static MTR_DI int nth_bnd(const D& L, int bs, int be, int minb, int n) {
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
-            const bool t = i < be && bnd_of(L.meta[i]) >= minb;
+            const bool t = i < be && bnd_of(L.meta[min(i, be - 1)]) >= minb;
             const uint64_t m = __ballot(t);
             const int pc = __popcll(m);
             if (n < pc) return base + first_lane(__ballot(t && __popcll(m & lanes_below()) == n));
@@ -495,130 +478,141 @@ struct Eng {
 
     // Block overflow after a leaf was added next to x (insertingWalk split + updateRoot,
     // mergeTree.ts:1831-1871, 1268-1277).
-    static __device__ void overflow_fix(D& L, int x) {
+    static MTR_DI void overflow_fix(D& L, St& s, int x) {
         PROF(P_OVERFLOW);
-        lptr<Sc> sc = L.sc;
         int level = 1;
-        int bs = block_start(L, x, 1), be = block_end(L, x, 1);
+        int bs = block_start(L, x, 1), be = block_end(L, s, x, 1);
         int cnt = be - bs;
         while (cnt >= kMaxNodesInBlock) {
             int c5 = bs + kMaxNodesInBlock / 2;
             if (level > 1) c5 = nth_bnd(L, bs, be, level - 1, kMaxNodesInBlock / 2);
-            uint32_t m = set_bnd(L.meta[c5], level);
+            uint32_t m = set_bnd(uniu(L.meta[c5]), level);
             if (level == 1) m = set_ns(m, NS_UNDEF);
             L.meta[c5] = m;
-            if (level == sc->height) {  // root split
-                sc->height++;
-                L.meta[0] = set_bnd(L.meta[0], sc->height);
+            wsync();
+            if (level == s.height) {  // root split
+                s.height++;
+                L.meta[0] = set_bnd(uniu(L.meta[0]), s.height);
+                wsync();
                 break;
             }
             level++;
             bs = block_start(L, bs, level);
-            be = block_end(L, bs, level);
+            be = block_end(L, s, bs, level);
             cnt = count_bnd(L, bs, be, level - 1);
         }
     }
 
-    // ---- LRU heap (collections/heap.ts:11-67), 1-based, lane 0 only
-    static __device__ void heap_push(D& L, uint32_t u, int s) {
-        lptr<Sc> sc = L.sc;
-        if (sc->heapn + 1 >= L.lhcap) {
-            sc->status = MTR_ERR_CAPACITY;
+    // ---- LRU heap (collections/heap.ts:11-67), 1-based, hole-based sifts (same order as swaps)
+    static MTR_DI void heap_push(D& L, St& s, uint32_t u, int sq) {
+        if (s.heapn + 1 >= L.lhcap) {
+            s.status = MTR_ERR_CAPACITY;
             return;
         }
-        int k = ++sc->heapn;
-        L.hseq[k] = s;
-        L.huid[k] = u;
-        while (k > 1 && L.hseq[k >> 1] - L.hseq[k] > 0) {
-            const int ts = L.hseq[k >> 1];
-            const uint32_t tu = L.huid[k >> 1];
-            L.hseq[k >> 1] = L.hseq[k];
-            L.huid[k >> 1] = L.huid[k];
-            L.hseq[k] = ts;
-            L.huid[k] = tu;
+        int k = ++s.heapn;
+        while (k > 1) {
+            const int ps = uni(L.hseq[k >> 1]);
+            if (!(ps - sq > 0)) break;
+            const uint32_t pu = uniu(L.huid[k >> 1]);
+            L.hseq[k] = ps;
+            L.huid[k] = pu;
             k >>= 1;
         }
-        if (sc->heapn > sc->max_heap) sc->max_heap = sc->heapn;
+        L.hseq[k] = sq;
+        L.huid[k] = u;
+        wsync();
+        if (s.heapn > s.max_heap) s.max_heap = s.heapn;
     }
-    static __device__ uint32_t heap_pop(D& L) {
+    static MTR_DI uint32_t heap_pop(D& L, St& s) {
         PROF(P_HEAP);
-        lptr<Sc> sc = L.sc;
-        const uint32_t x = L.huid[1];
-        int n = sc->heapn;
-        L.hseq[1] = L.hseq[n];
-        L.huid[1] = L.huid[n];
+        const uint32_t x = uniu(L.huid[1]);
+        int n = s.heapn;
+        const int ls = uni(L.hseq[n]);
+        const uint32_t lu = uniu(L.huid[n]);
         n--;
-        sc->heapn = n;
+        s.heapn = n;
         int k = 1;
         while ((k << 1) <= n) {
             int j = k << 1;
-            if (j < n && L.hseq[j] - L.hseq[j + 1] > 0) j++;
-            if (L.hseq[k] - L.hseq[j] <= 0) break;
-            const int ts = L.hseq[k];
-            const uint32_t tu = L.huid[k];
-            L.hseq[k] = L.hseq[j];
-            L.huid[k] = L.huid[j];
-            L.hseq[j] = ts;
-            L.huid[j] = tu;
+            int sj = uni(L.hseq[j]);
+            if (j < n) {
+                const int sj1 = uni(L.hseq[j + 1]);
+                if (sj - sj1 > 0) {
+                    j++;
+                    sj = sj1;
+                }
+            }
+            if (ls - sj <= 0) break;
+            L.hseq[k] = sj;
+            L.huid[k] = uniu(L.huid[j]);
             k = j;
         }
+        L.hseq[k] = ls;
+        L.huid[k] = lu;
+        wsync();
         return x;
     }
 
-    // addToLRUSet, mergeTree.ts:741-751
-    static __device__ void add_lru(D& L, int i, int s) {
-        lptr<Sc> sc = L.sc;
-        const int bs = block_start(L, i, 1);
-        const uint32_t m = L.meta[bs];
-        if (ns_of(m) != NS_TRUE && s > sc->curseq) {
+    // addToLRUSet, mergeTree.ts:741-751, for a leaf whose leaf-block starts at bs
+    static MTR_DI void add_lru_block(D& L, St& s, int bs, uint32_t u, int sq) {
+        const uint32_t m = uniu(L.meta[bs]);
+        if (ns_of(m) != NS_TRUE && sq > s.curseq) {
             L.meta[bs] = set_ns(m, NS_TRUE);
-            heap_push(L, L.uid[i], s);
+            wsync();
+            heap_push(L, s, u, sq);
         }
     }
 
     // ---- properties (PropertiesManager.addProperties without combining ops,
     //      segmentPropertiesManager.ts:60-157; JS own-key order).  Entry: [n, k0, v0, k1, v1, ...]
-    static __device__ uint32_t props_apply_serial(D& L, const KParams& P, uint32_t old, uint32_t pp) {
-        lptr<Sc> sc = L.sc;
+    struct PropRes {
+        uint32_t dst;
+        int propused, status;
+    };
+    static MTR_DI PropRes props_apply_serial(gptr<uint32_t> gprop, const KParams& P, int propused,
+                                                              uint32_t old, uint32_t pp) {
+        PropRes r{old, propused, MTR_OK};
         const gptr<const uint32_t> poff = gp(P.propop_off), pkv = gp(P.propop_kv), kix = gp(P.key_index);
-        const uint32_t n_old = old == NONE32 ? 0 : L.gprop[old];
-        const uint32_t lo = poff[pp], hi = poff[pp + 1];
+        const uint32_t n_old = old == NONE32 ? 0 : uniu(gprop[old]);
+        const uint32_t lo = uniu(poff[pp]), hi = uniu(poff[pp + 1]);
         const uint32_t need = 1 + 2 * (n_old + (hi - lo));
-        if (uint32_t(sc->propused) + need > uint32_t(P.pcap)) {
-            sc->status = MTR_ERR_CAPACITY;
-            return old;
+        if (uint32_t(propused) + need > uint32_t(P.pcap)) {
+            r.status = MTR_ERR_CAPACITY;
+            return r;
         }
-        const uint32_t dst = uint32_t(sc->propused);
-        const gptr<uint32_t> e = L.gprop + dst;
+        const uint32_t dst = uint32_t(propused);
+        const gptr<uint32_t> e = gprop + dst;
         uint32_t n = n_old;
-        for (uint32_t k = 0; k < 2 * n_old; k++) e[1 + k] = L.gprop[old + 1 + k];
+        for (uint32_t k = 0; k < 2 * n_old; k++) e[1 + k] = gprop[old + 1 + k];
         for (uint32_t q = lo; q < hi; q++) {
-            const uint32_t key = pkv[2 * q], val = pkv[2 * q + 1];
+            const uint32_t key = uniu(pkv[2 * q]), val = uniu(pkv[2 * q + 1]);
             int at = -1;
             for (uint32_t k = 0; k < n; k++)
-                if (e[1 + 2 * k] == key) {
+                if (uniu(e[1 + 2 * k]) == key) {
                     at = int(k);
                     break;
                 }
             if (val == MTR_NULL_VALUE) {
                 if (at >= 0) {
                     for (uint32_t k = uint32_t(at); k + 1 < n; k++) {
-                        e[1 + 2 * k] = e[1 + 2 * (k + 1)];
-                        e[2 + 2 * k] = e[2 + 2 * (k + 1)];
+                        e[1 + 2 * k] = uniu(e[1 + 2 * (k + 1)]);
+                        e[2 + 2 * k] = uniu(e[2 + 2 * (k + 1)]);
                     }
                     n--;
                 }
             } else if (at >= 0) {
                 e[2 + 2 * at] = val;
             } else {
-                const uint32_t ix = kix[key];
+                const uint32_t ix = uniu(kix[key]);
                 uint32_t pos = n;
                 if (ix != MTR_NOT_INDEX) {
                     pos = 0;
-                    while (pos < n && kix[e[1 + 2 * pos]] != MTR_NOT_INDEX && kix[e[1 + 2 * pos]] < ix) pos++;
+                    while (pos < n && uniu(kix[uniu(e[1 + 2 * pos])]) != MTR_NOT_INDEX &&
+                           uniu(kix[uniu(e[1 + 2 * pos])]) < ix)
+                        pos++;
                     for (uint32_t k = n; k > pos; k--) {
-                        e[1 + 2 * k] = e[1 + 2 * (k - 1)];
-                        e[2 + 2 * k] = e[2 + 2 * (k - 1)];
+                        e[1 + 2 * k] = uniu(e[1 + 2 * (k - 1)]);
+                        e[2 + 2 * k] = uniu(e[2 + 2 * (k - 1)]);
                     }
                 }
                 e[1 + 2 * pos] = key;
@@ -627,21 +621,27 @@ struct Eng {
             }
         }
         e[0] = n;
-        sc->propused += int(1 + 2 * n);
-        return dst;
+        r.propused = propused + int(1 + 2 * n);
+        r.dst = dst;
+        return r;
     }
 
     // Wave version: the old set and the op's keys are fetched once (one lane per entry) and the
     // set is edited in registers (lane t = entry t); falls back to the serial form above 64 keys.
-    static __device__ uint32_t props_apply(D& L, const KParams& P, uint32_t old, uint32_t pp) {
-        lptr<Sc> sc = L.sc;
+    static MTR_DI uint32_t props_apply(D& L, const KParams& P, St& s, uint32_t old, uint32_t pp) {
         const gptr<const uint32_t> poff = gp(P.propop_off), pkv = gp(P.propop_kv), kix = gp(P.key_index);
-        const int n_old = old == NONE32 ? 0 : int(L.gprop[old]);
-        const int lo = int(poff[pp]), nq = int(poff[pp + 1]) - lo;
-        if (n_old + nq > 64) return props_apply_serial(L, P, old, pp);
+        const int n_old = old == NONE32 ? 0 : int(uniu(L.gprop[old]));
+        const int lo = int(uniu(poff[pp])), nq = int(uniu(poff[pp + 1])) - lo;
+        if (n_old + nq > 64) {
+            const PropRes r = props_apply_serial(L.gprop, P, s.propused, old, pp);
+            s.propused = uni(r.propused);
+            if (uni(r.status) != MTR_OK) s.status = uni(r.status);
+            wsync();
+            return uniu(r.dst);
+        }
         const uint32_t need = 1 + 2 * uint32_t(n_old + nq);
-        if (uint32_t(sc->propused) + need > uint32_t(P.pcap)) {
-            sc->status = MTR_ERR_CAPACITY;
+        if (uint32_t(s.propused) + need > uint32_t(P.pcap)) {
+            s.status = MTR_ERR_CAPACITY;
             return old;
         }
         const int ln = lane_id();
@@ -694,26 +694,26 @@ struct Eng {
                 n++;
             }
         }
-        const uint32_t dst = uint32_t(sc->propused);
+        const uint32_t dst = uint32_t(s.propused);
         const gptr<uint32_t> e = L.gprop + dst;
         if (ln < n) {
             e[1 + 2 * ln] = wk;
             e[2 + 2 * ln] = wv;
         }
         e[0] = uint32_t(n);
-        sc->propused += 1 + 2 * n;
-        wave_fence();
+        s.propused += 1 + 2 * n;
+        wsync();
         return dst;
     }
 
-    // matchProperties on wave 0: one lane per key of `a`, `b`'s keys broadcast by readlane
-    static __device__ bool props_match_w(const D& L, const KParams& P, uint32_t a, uint32_t b) {
+    // matchProperties on the wave: one lane per key of `a`, `b`'s keys broadcast by readlane
+    static MTR_DI bool props_match_w(const D& L, const KParams& P, uint32_t a, uint32_t b) {
         if (a == b) return true;
         if (a == NONE32 || b == NONE32) return false;
-        const int na = int(L.gprop[a]), nb = int(L.gprop[b]);
+        const int na = int(uniu(L.gprop[a])), nb = int(uniu(L.gprop[b]));
         if (na != nb) return false;
         const gptr<const uint32_t> veq = gp(P.val_eq);
-        if (na > 64) return props_match(L.gprop, veq, a, b);
+        if (na > 64) return __ballot(!props_match(L.gprop, veq, a, b)) == 0;
         PROF(P_PMATCH);
         PROF_COUNT(P_NPMATCH);
         const int ln = lane_id();
@@ -724,99 +724,101 @@ struct Eng {
             ea = veq[L.gprop[a + 2 + 2 * ln]];
             eb = veq[L.gprop[b + 2 + 2 * ln]];
         }
-        bool ok = ln >= na;
+        bool found = ln >= na, ok = true;
         for (int j = 0; j < nb; j++) {
             const uint32_t kj = rdlane(kb, j), ej = rdlane(eb, j);
-            if (ka == kj && ln < na) ok = ea == ej;
+            if (ka == kj && ln < na) {
+                found = true;
+                ok = ea == ej;
+            }
         }
-        return __ballot(!ok) == 0;
+        return __ballot(!(found && ok)) == 0;
     }
 
     // ---- text
-    static __device__ bool can_append(uint32_t ma, int la, uint32_t mb, int lb) {  // TextSegment.canAppend, textSegment.ts:86-93
+    static MTR_DI bool can_append(uint32_t ma, int la, uint32_t mb, int lb) {  // TextSegment.canAppend, textSegment.ts:86-93
         if ((ma | mb) & M_MARKER) return false;
         if (la > 0 && (ma & M_NL)) return false;
         return la <= kGranularity || lb <= kGranularity;
     }
-    static __device__ void copy_text(const D& L, uint32_t dst, uint32_t src, int n) {  // wave 0
+    static MTR_DI void copy_text(const D& L, uint32_t dst, uint32_t src, int n) {
         for (int k = lane_id(); k < n; k += 64) L.gtext[dst + k] = L.gtext[src + k];
     }
-    static __device__ int text_end(lptr<Sc> sc, const KParams& P) { return (P.tcap / 2) * (sc->texthalf + 1); }
+    static MTR_DI int text_end(const St& s, const KParams& P) { return (P.tcap / 2) * (s.texthalf + 1); }
 
-    // prev.append(seg) (textSegment.ts:99-103): text of b follows text of a
-    // (wave 0; returns false on arena overflow).  Updates L.len/L.text of a; the caller keeps M_NL.
-    static __device__ void text_append(D& L, const KParams& P, int a, int b) {
+    // prev.append(seg) (textSegment.ts:99-103): text of b follows text of a.  Updates L.len/L.text
+    // of a; the caller keeps M_NL.
+    static MTR_DI void text_append(D& L, const KParams& P, St& s, int a, int b) {
         PROF(P_TAPPEND);
         PROF_COUNT(P_NMERGE);
-        lptr<Sc> sc = L.sc;
-        const int tend = text_end(sc, P);
-        const uint32_t oa = L.text[a], ob = L.text[b];
-        const int la = L.len[a], lb = L.len[b];
+        const int tend = text_end(s, P);
+        const uint32_t oa = uniu(L.text[a]), ob = uniu(L.text[b]);
+        const int la = uni(L.len[a]), lb = uni(L.len[b]);
         if (oa + uint32_t(la) == ob) {
             L.len[a] = la + lb;
+            wsync();
             return;
         }
-        if (oa + uint32_t(la) == uint32_t(sc->textused)) {
-            if (sc->textused + lb > tend) {
-                sc->status = MTR_ERR_CAPACITY;
+        if (oa + uint32_t(la) == uint32_t(s.textused)) {
+            if (s.textused + lb > tend) {
+                s.status = MTR_ERR_CAPACITY;
                 return;
             }
-            copy_text(L, uint32_t(sc->textused), ob, lb);
-            sc->textused += lb;
+            copy_text(L, uint32_t(s.textused), ob, lb);
+            s.textused += lb;
             L.len[a] = la + lb;
+            wsync();
             return;
         }
-        if (sc->textused + la + lb > tend) {
-            sc->status = MTR_ERR_CAPACITY;
+        if (s.textused + la + lb > tend) {
+            s.status = MTR_ERR_CAPACITY;
             return;
         }
-        const uint32_t d = uint32_t(sc->textused);
+        const uint32_t d = uint32_t(s.textused);
         copy_text(L, d, oa, la);
         copy_text(L, d + uint32_t(la), ob, lb);
-        sc->textused += la + lb;
+        s.textused += la + lb;
         L.text[a] = d;
         L.len[a] = la + lb;
+        wsync();
     }
 
     // Semi-space compaction of the text arena: copy every leaf's text into the other half in
-    // leaf order (block prefix scan of lengths), then switch halves.
-    static __device__ void text_gc(D& L, const KParams& P) {
+    // leaf order (prefix scan of lengths), then switch halves.
+    static MTR_DI void text_gc(D& L, const KParams& P, St& s) {
         PROF(P_TEXTGC);
-        lptr<Sc> sc = L.sc;
-        const int S = sc->nseg;
-        const int per = (S + NT - 1) / NT;
-        const int lo = min(S, int(threadIdx.x) * per), hi = min(S, lo + per);
-        int sum = 0;
-        for (int i = lo; i < hi; i++)
-            if (!(L.meta[i] & M_MARKER)) sum += L.len[i];
-        int tot;
-        int run = block_excl_scan(sc, sum, &tot);
+        const int S = s.nseg;
         const int half = P.tcap / 2;
-        const int dst0 = sc->texthalf ? 0 : half;
-        for (int i = lo; i < hi; i++) {
-            if (L.meta[i] & M_MARKER) continue;
-            const uint32_t src = L.text[i];
-            const int n = L.len[i];
-            for (int k = 0; k < n; k++) L.gtext[dst0 + run + k] = L.gtext[src + k];
-            L.text[i] = uint32_t(dst0 + run);
-            run += n;
+        const int dst0 = s.texthalf ? 0 : half;
+        int carry = 0;
+        for (int base = 0; base < S; base += 64) {
+            const int i = base + lane_id();
+            int n = 0;
+            uint32_t src = 0;
+            if (i < S && !(L.meta[i] & M_MARKER)) {
+                n = L.len[i];
+                src = L.text[i];
+            }
+            const int inc = wave_incl_scan(n);
+            const int off = dst0 + carry + inc - n;
+            if (i < S && !(L.meta[i] & M_MARKER)) {
+                for (int k = 0; k < n; k++) L.gtext[off + k] = L.gtext[src + k];
+                L.text[i] = uint32_t(off);
+            }
+            carry += rdlane(inc, 63);
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            sc->texthalf ^= 1;
-            sc->textused = dst0 + tot;
-            if (tot > half) sc->status = MTR_ERR_CAPACITY;
-        }
-        __syncthreads();
+        wsync();
+        s.texthalf ^= 1;
+        s.textused = dst0 + carry;
+        if (carry > half) s.status = MTR_ERR_CAPACITY;
     }
 
     // ------------------------------------------------------------ zamboni
     // scourNode (zamboni.ts:122-193) over the child blocks in [cs, ce): a new child block starts at
-    // every leaf with bnd >= 1.  Marks M_DEL; returns #kept (used for a single block).  Wave 0:
-    // the leaves are read 64 at a time into registers and visited in order by readlane.
-    static __device__ int scour_range(D& L, const KParams& P, int cs, int ce) {
-        lptr<Sc> sc = L.sc;
-        const int minseq = sc->minseq;
+    // every leaf with bnd >= 1.  Marks M_DEL; returns #kept (used for a single block).  The leaves
+    // are read 64 at a time into registers and visited in order by readlane.
+    static MTR_DI int scour_range(D& L, const KParams& P, St& s, int cs, int ce) {
+        const int minseq = s.minseq;
         int prev = -1, kept = 0, plen = 0;
         uint32_t pmeta = 0, pprops = 0;
         for (int base = cs; base < ce; base += 64) {
@@ -840,6 +842,7 @@ struct Eng {
                         vm = (vm & ~(M_NLQ | M_NL)) | (u == u'\n' ? M_NL : 0u);
                         L.meta[i] = vm;
                     }
+                    wsync();
                 }
             }
             const int nk = min(64, ce - base);
@@ -850,18 +853,23 @@ struct Eng {
                 if (m & M_DEL) continue;
                 const int rs = rdlane(vr, t);
                 if (rs != RNONE) {
-                    if (rs > minseq) kept++;
-                    else L.meta[k] = m | M_DEL;  // UNLINK
+                    if (rs > minseq) {
+                        kept++;
+                    } else {
+                        L.meta[k] = m | M_DEL;  // UNLINK
+                        wsync();
+                    }
                     prev = -1;
                 } else if (rdlane(vs, t) <= minseq) {
                     const int lk = rdlane(vl, t);
                     const uint32_t pk = rdlane(vp, t);
                     if (prev >= 0 && lk > 0 && can_append(pmeta, plen, m, lk) && props_match_w(L, P, pprops, pk)) {
-                        text_append(L, P, prev, k);
+                        text_append(L, P, s, prev, k);
                         plen += lk;
                         pmeta = (pmeta & ~(M_NL | M_NLQ)) | (m & (M_NL | M_NLQ));
                         L.meta[prev] = pmeta;
                         L.meta[k] = m | M_DEL;
+                        wsync();
                     } else {
                         kept++;
                         if (lk > 0) {
@@ -883,48 +891,56 @@ struct Eng {
     }
 
     // zamboniSegments body for one popped LRU entry whose segment is leaf x
-    // (zamboni.ts:33-58 + packParent zamboni.ts:63-120).  Lane 0.  Returns 1 if leaves were
-    // marked for deletion (the caller compacts).
-    static __device__ int zamboni_block(D& L, const KParams& P, int x) {
+    // (zamboni.ts:33-58 + packParent zamboni.ts:63-120).  Returns 1 if leaves were marked for
+    // deletion (the caller compacts).
+    static MTR_DI int zamboni_block(D& L, const KParams& P, St& s, int x) {
         PROF(P_ZBLOCK);
         PROF_COUNT(P_NZBLOCK);
-        lptr<Sc> sc = L.sc;
-        const int H = sc->height;
-        sc->rs[1] = block_start(L, x, 1);
-        sc->re[1] = block_end(L, x, 1);
-        if (ns_of(L.meta[sc->rs[1]]) == NS_FALSE) return 0;
-        for (int l = 1; l <= H; l++) {
-            if (l > 1) {
-                sc->rs[l] = block_start(L, sc->rs[l - 1], l);
-                sc->re[l] = block_end(L, sc->rs[l - 1], l);
+        const lptr<Sc> sc = L.sc;
+        const int H = s.height;
+        const int rs1 = block_start(L, x, 1), re1 = block_end(L, s, x, 1);
+        if (ns_of(uniu(L.meta[rs1])) == NS_FALSE) return 0;
+        sc->rs[1] = rs1;
+        sc->re[1] = re1;
+        {
+            int ps = rs1;
+            for (int l = 1; l <= H; l++) {
+                if (l > 1) {
+                    const int a = block_start(L, ps, l), b = block_end(L, s, ps, l);
+                    sc->rs[l] = a;
+                    sc->re[l] = b;
+                    ps = a;
+                }
+                sc->topb[l] = bnd_of(uniu(L.meta[ps]));
             }
-            sc->topb[l] = bnd_of(L.meta[sc->rs[l]]);
         }
-        const int rs1 = sc->rs[1], re1 = sc->re[1];
+        wsync();
         const int before = re1 - rs1;
         int kept;
         {
             PROF(P_SCOUR1);
-            kept = scour_range(L, P, rs1, re1);
+            kept = scour_range(L, P, s, rs1, re1);
         }
-        int first = -1;  // block.needsScour = false, kept on the block's first surviving leaf
-        {
+        {  // block.needsScour = false, kept on the block's first surviving leaf
             const int i = rs1 + lane_id();
-            const uint64_t m = __ballot(i < re1 && !(L.meta[i] & M_DEL));
-            if (m) first = rs1 + first_lane(m);
+            const uint64_t m = __ballot(i < re1 && !(L.meta[min(i, re1 - 1)] & M_DEL));
+            if (m) {
+                const int first = rs1 + first_lane(m);
+                L.meta[first] = set_ns(set_bnd(uniu(L.meta[first]), uni(sc->topb[1])), NS_FALSE);
+                wsync();
+            }
         }
-        if (first >= 0) L.meta[first] = set_ns(set_bnd(L.meta[first], sc->topb[1]), NS_FALSE);
         if (kept >= before) return 0;
         if (kept < kMaxNodesInBlock / 2 && H > 1) {
             PROF(P_PACK);
             PROF_COUNT(P_NPACK);
             for (int l = 2; l <= H; l++) {  // packParent chain
-                const int ps = sc->rs[l], pe = sc->re[l];
+                const int ps = uni(sc->rs[l]), pe = uni(sc->re[l]);
                 if (l == 2) {
                     // packParent scours every child of P again -- including the block just
                     // scoured: scourNode is not idempotent (a dropped tombstone no longer resets
                     // the merge candidate), zamboni.ts:68-73,122-193.
-                    scour_range(L, P, ps, pe);
+                    scour_range(L, P, s, ps, pe);
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
                 int T = 0;
@@ -940,7 +956,7 @@ struct Eng {
                     const int base = T / c;
                     const int rem = T % c;
                     const int big = rem * (base + 1);
-                    const int top = sc->topb[l];
+                    const int top = uni(sc->topb[l]);
                     int item0 = 0;
                     for (int wb = ps; wb < pe; wb += 64) {
                         const int i = wb + lane_id();
@@ -957,7 +973,7 @@ struct Eng {
                         }
                         item0 += __popcll(mask);
                     }
-                    wave_fence();
+                    wsync();
                 }
                 if (!(c < kMaxNodesInBlock / 2 && l < H)) break;
             }
@@ -965,258 +981,253 @@ struct Eng {
         return 1;
     }
 
-    // zamboniSegments (zamboni.ts:19-60): all threads
-    static __device__ void zamboni(D& L, const KParams& P) {
+    // zamboniSegments (zamboni.ts:19-60)
+    static MTR_DI void zamboni(D& L, const KParams& P, St& s) {
         PROF(P_ZAMBONI);
-        lptr<Sc> sc = L.sc;
-        if (!sc->collab) return;
+        if (!s.collab) return;
         for (int it = 0; it < 2; it++) {
-            __syncthreads();
-            if (sc->heapn == 0 || sc->status != MTR_OK) return;
-            if (L.hseq[1] > sc->minseq) return;
-            __syncthreads();
-            if (wave0()) sc->b4 = int(heap_pop(L));
-            __syncthreads();
-            const int x = find_uid(L, uint32_t(sc->b4));
+            if (s.heapn == 0 || s.status != MTR_OK) return;
+            if (uni(L.hseq[1]) > s.minseq) return;
+            const uint32_t u = heap_pop(L, s);
+            const int x = find_uid(L, s, u);
             if (x < 0) continue;
-            if (wave0()) sc->b5 = zamboni_block(L, P, x);
-            __syncthreads();
-            if (sc->b5) compact(L);
+            if (zamboni_block(L, P, s, x)) compact(L, s);
         }
-        __syncthreads();
     }
 
-    // updateSeqNumbers + setMinSeq, client.ts:877-887 / mergeTree.ts:1025-1044
-    static __device__ void update_seq(D& L, const KParams& P, int msn, int seq) {
-        PROF(P_UPDSEQ);
-        lptr<Sc> sc = L.sc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int run = 0;
-            if (sc->curseq > seq) {
-                sc->status = MTR_ERR_ASSERT | 0x038;
-            } else {
-                sc->curseq = seq;
-                if (msn > seq) sc->status = MTR_ERR_ASSERT | 0x039;
-                else if (msn > sc->curseq) sc->status = MTR_ERR_ASSERT | 0x04e;
-                else if (sc->minseq > msn) sc->status = MTR_ERR_ASSERT | 0x04f;
-                else if (msn > sc->minseq) {
-                    sc->minseq = msn;
-                    run = 1;
-                }
+    // updateSeqNumbers + setMinSeq, client.ts:877-887 / mergeTree.ts:1025-1044; returns 1 when
+    // minSeq advanced (the caller then runs zamboniSegments)
+    static MTR_DI int update_seq(St& s, int msn, int seq) {
+        int run = 0;
+        if (s.curseq > seq) {
+            s.status = MTR_ERR_ASSERT | 0x038;
+        } else {
+            s.curseq = seq;
+            if (msn > seq) s.status = MTR_ERR_ASSERT | 0x039;
+            else if (msn > s.curseq) s.status = MTR_ERR_ASSERT | 0x04e;
+            else if (s.minseq > msn) s.status = MTR_ERR_ASSERT | 0x04f;
+            else if (msn > s.minseq) {
+                s.minseq = msn;
+                run = 1;
             }
-            sc->b6 = run;
         }
-        __syncthreads();
-        if (sc->b6) zamboni(L, P);
+        return run;
     }
 
     // ------------------------------------------------------------ boundary / insert
     // ensureIntervalBoundary (mergeTree.ts:1706-1716) on the current scan arrays: split the leaf
     // holding pos at an offset > 0; the two halves' scan entries are set in place.
-    static __device__ void split_at(D& L, int pos) {
+    static MTR_DI void split_at(D& L, St& s, int pos) {
         PROF(P_SPLIT);
-        lptr<Sc> sc = L.sc;
-        if (wave0()) {
-            PROF(P_SPLIT1);
-            sc->b0 = -1;
-            const int S = sc->nseg;
-            const int i = lower_bound_E(L, pos);
-            if (i < S) {
-                const int be = block_end(L, i, 1);
-                for (int j = i; j < be; j++) {
-                    if (L.V[j] < 0) continue;
-                    if (pos < L.E[j]) {
-                        const int off = pos - (L.E[j] - L.V[j]);
-                        if (off > 0 && !(L.meta[j] & M_MARKER)) {
-                            sc->b0 = j;
-                            sc->b1 = off;
-                        }
-                        break;
-                    }
-                }
-            }
+        const int S = s.nseg;
+        const int i = lower_bound_E(L, s, pos);
+        if (i >= S) return;
+        const int be = block_end(L, s, i, 1);
+        const int jj = i + lane_id();
+        bool c = false;
+        if (jj < be) {
+            const int vj = L.V[jj];
+            c = vj >= 0 && pos < L.E[jj];
         }
-        __syncthreads();
-        const int j = sc->b0;
-        if (j < 0) return;
-        shift_right1(L, j + 1);
-        if (wave0()) {  // BaseSegment.splitAt, mergeTreeNodes.ts:481-510
-            const int off = sc->b1;
+        const uint64_t cm = __ballot(c);
+        if (!cm) return;
+        const int j = i + first_lane(cm);
+        const int v = uni(L.V[j]), e = uni(L.E[j]);
+        const uint32_t mj = uniu(L.meta[j]);
+        const int off = pos - (e - v);
+        if (!(off > 0 && !(mj & M_MARKER))) return;
+        shift_right1(L, s, j + 1);
+        {  // BaseSegment.splitAt, mergeTreeNodes.ts:481-510
             const int r = j + 1;
-            const uint32_t mj = L.meta[j];
-            L.len[r] = L.len[j] - off;
+            const int lj = uni(L.len[j]);
+            L.len[r] = lj - off;
             L.len[j] = off;
-            L.seq[r] = L.seq[j];
-            L.rseq[r] = L.rseq[j];
+            L.seq[r] = uni(L.seq[j]);
+            L.rseq[r] = uni(L.rseq[j]);
             L.meta[r] = set_ns(set_bnd(mj, 0), NS_UNDEF);
             L.meta[j] = (mj & ~M_NL) | M_NLQ;
-            L.text[r] = L.text[j] + uint32_t(off);
-            L.props[r] = L.props[j];
-            L.rm[r] = L.rm[j];
-            L.uid[r] = uint32_t(sc->uidnext++);
-            const int v = L.V[j], e = L.E[j];  // split leaves are fully visible in this view
+            L.text[r] = uniu(L.text[j]) + uint32_t(off);
+            L.props[r] = uniu(L.props[j]);
+            L.rm[r] = uniu(L.rm[j]);
+            L.uid[r] = uint32_t(s.uidnext++);
+            // split leaves are fully visible in this view
             L.V[j] = off;
             L.E[j] = e - v + off;
             L.V[r] = v - off;
             L.E[r] = e;
-            sc->nseg++;
-            overflow_fix(L, r);
+            wsync();
+            s.nseg++;
+            overflow_fix(L, s, r);
         }
-        __syncthreads();
     }
 
     // insertSegments/blockInsert/insertingWalk with onLeaf (mergeTree.ts:1397-1427, 1594-1685),
-    // on the current scan arrays
-    // `pre`: lane t holds unit t of the op's text in `pf` (prefetched during the previous op)
-    static __device__ void insert_at(D& L, const KParams& P, const View& v, const mtr_op& op, int seq,
-                                     uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf) {
+    // on the current scan arrays.  `pre`: lane t holds unit t of the op's text in `pf`
+    // (prefetched during the previous op).
+    static MTR_DI void insert_at(D& L, const KParams& P, St& s, const View& v, const mtr_op& op, int seq,
+                                 uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf) {
         PROF(P_INSERT);
-        lptr<Sc> sc = L.sc;
         const bool marker = (op.flags & MTR_F_MARKER) != 0;
         const int len = marker ? 1 : int(op.payload2);
         if (len <= 0) return;  // blockInsert skips empty segments
-        const int t0 = sc->textused;
-        if (!marker) {  // copy the op's text into the document arena (all lanes)
-            if (t0 + len > text_end(sc, P)) {
-                __syncthreads();
-                if (threadIdx.x == 0) sc->status = MTR_ERR_CAPACITY;
-                __syncthreads();
+        const int t0 = s.textused;
+        const int ln = lane_id();
+        if (!marker) {  // copy the op's text into the document arena
+            if (t0 + len > text_end(s, P)) {
+                s.status = MTR_ERR_CAPACITY;
                 return;
             }
             PROF(P_TEXTCOPY);
             if (pre) {
-                if (lane_id() < len) L.gtext[t0 + lane_id()] = uint16_t(pf);
+                if (ln < len) L.gtext[t0 + ln] = uint16_t(pf);
             } else {
                 const gptr<const uint16_t> src = gp(P.btext) + dd.text_base + op.payload;
-                for (int k = threadIdx.x; k < len; k += NT) L.gtext[t0 + k] = src[k];
+                for (int k = ln; k < len; k += 64) L.gtext[t0 + k] = src[k];
             }
         }
-        const bool nl = pre && __ballot(lane_id() == len - 1 && pf == u'\n') != 0;
+        const bool nl = pre && __ballot(ln == len - 1 && pf == u'\n') != 0;
         const int pos = op.pos1;
-        if (wave0()) {
+        const int S = s.nseg;
+        int slot = -1, inherit = 0;
+        {
             PROF(P_INS1);
-            const int S = sc->nseg;
-            int slot = -1, inherit = 0;
             if (S == 0) {
                 if (pos == 0) slot = 0;
-                else sc->status = MTR_ERR_INSERT_FAILED;
+                else s.status = MTR_ERR_INSERT_FAILED;
             } else {
-                const int i = lower_bound_E(L, pos);
+                const int i = lower_bound_E(L, s, pos);
                 if (i >= S) {
-                    sc->status = MTR_ERR_INSERT_FAILED;
+                    s.status = MTR_ERR_INSERT_FAILED;
                 } else {
-                    const int bs = block_start(L, i, 1), be = block_end(L, i, 1);
-                    slot = be;
-                    for (int j = i; j < be; j++) {
+                    const int bs = block_start(L, i, 1), be = block_end(L, s, i, 1);
+                    const int j = i + ln;
+                    bool c = false;
+                    if (j < be) {  // breakTie, mergeTree.ts:1719-1738
                         const int vj = L.V[j];
-                        if (vj < 0) continue;
-                        if (L.E[j] > pos || (vj == 0 && seq > L.seq[j])) {  // breakTie, mergeTree.ts:1719-1738
-                            slot = j;
-                            break;
-                        }
+                        c = vj >= 0 && (L.E[j] > pos || (vj == 0 && seq > L.seq[j]));
                     }
+                    const uint64_t cm = __ballot(c);
+                    slot = cm ? i + first_lane(cm) : be;
                     inherit = slot == bs ? 1 : 0;
                 }
             }
-            sc->b0 = slot;
-            sc->b1 = inherit;
         }
-        __syncthreads();
-        const int slot = sc->b0;
         if (slot < 0) return;
-        shift_right1(L, slot);
-        if (wave0()) {
-            const int S = sc->nseg;
-            uint32_t m = client & M_CLIENT_MASK;
-            if (marker) m |= M_MARKER;
-            else m |= pre ? (nl ? M_NL : 0u) : M_NLQ;
-            if (op.flags & MTR_F_NOREF) m |= M_NOREF;
-            if (S == 0) {
-                sc->height = 1;
-                m = set_bnd(m, 1);
-            } else if (sc->b1) {
-                const uint32_t om = L.meta[slot + 1];
-                m = set_ns(set_bnd(m, bnd_of(om)), ns_of(om));
-                L.meta[slot + 1] = set_ns(set_bnd(om, 0), NS_UNDEF);
-            }
-            L.len[slot] = len;
-            L.seq[slot] = seq;
-            L.rseq[slot] = RNONE;
-            L.meta[slot] = m;
-            L.text[slot] = marker ? op.payload : uint32_t(t0);
-            if (!marker) sc->textused = t0 + len;
-            uint32_t pr = NONE32;
-            if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, NONE32, uint32_t(op.pos2));
-            L.props[slot] = pr;
-            L.rm[slot] = NONE32;
-            L.uid[slot] = uint32_t(sc->uidnext++);
-            sc->nseg = S + 1;
-            overflow_fix(L, slot);
-            // saveIfLocal (mergeTree.ts:1618-1637): remote segments above minSeq go to the LRU
-            if (sc->collab && !v.local && seq > sc->minseq) add_lru(L, slot, seq);
+        shift_right1(L, s, slot);
+        uint32_t m = client & M_CLIENT_MASK;
+        if (marker) m |= M_MARKER;
+        else m |= pre ? (nl ? M_NL : 0u) : M_NLQ;
+        if (op.flags & MTR_F_NOREF) m |= M_NOREF;
+        if (S == 0) {
+            s.height = 1;
+            m = set_bnd(m, 1);
+        } else if (inherit) {
+            const uint32_t om = uniu(L.meta[slot + 1]);
+            m = set_ns(set_bnd(m, bnd_of(om)), ns_of(om));
+            L.meta[slot + 1] = set_ns(set_bnd(om, 0), NS_UNDEF);
         }
-        __syncthreads();
+        L.len[slot] = len;
+        L.seq[slot] = seq;
+        L.rseq[slot] = RNONE;
+        L.meta[slot] = m;
+        L.text[slot] = marker ? op.payload : uint32_t(t0);
+        if (!marker) s.textused = t0 + len;
+        uint32_t pr = NONE32;
+        if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
+        L.props[slot] = pr;
+        L.rm[slot] = NONE32;
+        L.uid[slot] = uint32_t(s.uidnext++);
+        wsync();
+        s.nseg = S + 1;
+        overflow_fix(L, s, slot);
+        // saveIfLocal (mergeTree.ts:1618-1637): remote segments above minSeq go to the LRU
+        if (s.collab && !v.local && seq > s.minseq) add_lru_block(L, s, block_start(L, slot, 1), uint32_t(s.uidnext - 1), seq);
     }
 
     // markRangeRemoved / annotateRange walk (mergeTree.ts:1955-2047, 1895-1953): leaves with
-    // visible length > 0 inside [start, end), on the current scan arrays.  Lane 0.
-    static __device__ void range_walk(D& L, const KParams& P, const View& v, int start, int end, int seq,
-                                      uint32_t client, int is_remove, uint32_t pp) {
+    // visible length > 0 inside [start, end), on the current scan arrays, 64 leaves per round.
+    // The walk stops at the first leaf whose view start (E - max(V,0), nondecreasing) is >= end.
+    static MTR_DI void range_walk(D& L, const KParams& P, St& s, const View& v, int start, int end, int seq,
+                                  uint32_t client, int is_remove, uint32_t pp) {
         PROF(P_RANGE);
-        lptr<Sc> sc = L.sc;
-        if (wave0() && end != start) {
-            const int S = sc->nseg;
-            int nmemo = 0;
-            for (int j = lower_bound_E(L, start + 1); j < S; j++) {
-                const int vj = L.V[j];
-                if (L.E[j] - max(vj, 0) >= end) break;
-                if (vj <= 0) continue;
+        if (end == start) return;
+        const int S = s.nseg;
+        const int ln = lane_id();
+        const bool lru = s.collab && !v.local;
+        int last_blk = -1;  // leaf-block start of the last touched leaf
+        for (int base = lower_bound_E(L, s, start + 1); base < S; base += 64) {
+            const int j = base + ln;
+            const bool in = j < S;
+            int vj = 0, ej = 0;
+            uint32_t mj = 0;
+            if (in) {
+                vj = L.V[j];
+                ej = L.E[j];
+                mj = L.meta[j];
+            }
+            const uint64_t stop = __ballot(!in || ej - max(vj, 0) >= end);
+            const int lim = stop ? first_lane(stop) : 64;
+            const bool act = ln < lim && vj > 0;
+            const uint64_t am = __ballot(act);
+            if (am) {
                 if (is_remove) {
-                    if (L.rseq[j] != RNONE) {  // overlapping remove: removedClientIds.push
-                        if (sc->rmused + 1 > P.rcap) {
-                            sc->status = MTR_ERR_CAPACITY;
-                            break;
-                        }
-                        const uint32_t cell = uint32_t(sc->rmused++);
-                        const uint32_t nxt = (L.meta[j] & M_OVERLAP) ? L.rm[j] : 0xffffffu;
+                    const int rs = act ? L.rseq[j] : RNONE;
+                    const bool ov = act && rs != RNONE;  // overlapping remove: removedClientIds.push
+                    const uint64_t om = __ballot(ov);
+                    const int nov = __popcll(om);
+                    if (s.rmused + nov > P.rcap) {
+                        s.status = MTR_ERR_CAPACITY;
+                        return;
+                    }
+                    if (ov) {
+                        const uint32_t cell = uint32_t(s.rmused + __popcll(om & lanes_below()));
+                        const uint32_t nxt = (mj & M_OVERLAP) ? L.rm[j] : 0xffffffu;
                         L.grm[cell] = (client << 24) | (nxt & 0xffffffu);
                         L.rm[j] = cell;
-                        L.meta[j] |= M_OVERLAP;
-                    } else {
+                        mj |= M_OVERLAP;
+                        L.meta[j] = mj;
+                    } else if (act) {
                         L.rseq[j] = seq;
-                        L.meta[j] = (L.meta[j] & ~(0xffu << M_FREM_SHIFT) & ~M_OVERLAP) | (client << M_FREM_SHIFT);
+                        mj = (mj & ~(0xffu << M_FREM_SHIFT) & ~M_OVERLAP) | (client << M_FREM_SHIFT);
+                        L.meta[j] = mj;
                         L.rm[j] = NONE32;
                     }
+                    s.rmused += nov;
                 } else {
-                    const uint32_t old = L.props[j];
-                    uint32_t nw = NONE32;
-                    int hit = -1;
-                    for (int q = 0; q < nmemo; q++)
-                        if (sc->memo_old[q] == old) {
-                            hit = q;
-                            break;
-                        }
-                    if (hit >= 0) {
-                        nw = sc->memo_new[hit];
-                    } else {
-                        nw = props_apply(L, P, old, pp);
-                        const int q = nmemo < 4 ? nmemo++ : 3;
-                        sc->memo_old[q] = old;
-                        sc->memo_new[q] = nw;
+                    // one new property set per distinct old set in the round (memoized addProperties)
+                    const uint32_t old = act ? L.props[j] : 0u;
+                    uint64_t pend = am;
+                    while (pend) {
+                        const uint32_t o = rdlane(old, first_lane(pend));
+                        const uint64_t sel = __ballot(act && old == o);
+                        const uint32_t nw = props_apply(L, P, s, o, pp);
+                        if (act && old == o) L.props[j] = nw;
+                        pend &= ~sel;
                     }
-                    L.props[j] = nw;
                 }
-                if (sc->collab && !v.local) add_lru(L, j, seq);
+                wsync();
+                if (lru) {  // addToLRUSet for every touched leaf, in leaf order (one push per block)
+                    const uint64_t fm = __ballot(in && bnd_of(mj) >= 1);
+                    uint64_t todo = am;
+                    while (todo) {
+                        const int l = first_lane(todo);
+                        todo &= todo - 1;
+                        const uint64_t below = fm & ((uint64_t(2) << l) - 1);
+                        const int b = below ? base + last_lane(below) : block_start(L, base, 1);
+                        if (b != last_blk) {
+                            last_blk = b;
+                            add_lru_block(L, s, b, uniu(L.uid[base + l]), seq);
+                        }
+                    }
+                }
             }
+            if (s.status != MTR_OK || stop) break;
         }
-        __syncthreads();
     }
 
     // ------------------------------------------------------------ record mode
     // draw op `idx` of document d from the synthetic recipe using this engine's exact view length
-    static __device__ void gen_op(D& L, const KParams& P, const mtr_doc_desc& dd, int idx) {
-        lptr<Sc> sc = L.sc;
+    static MTR_DI void gen_op(D& L, const KParams& P, St& s, const mtr_doc_desc& dd, int idx) {
         const gptr<mtr_op> rec = gp(P.gen_ops) + dd.op_begin + idx;
         if (idx == 0) {
             if (threadIdx.x == 0) {
@@ -1224,7 +1235,7 @@ struct Eng {
                 z.type = MTR_OP_START_COLLAB;
                 st_struct(rec, z);
             }
-            __syncthreads();
+            wsync();
             return;
         }
         if (threadIdx.x == 0) {
@@ -1232,77 +1243,79 @@ struct Eng {
             mtr_synth_state st = ld_struct<mtr_synth_state>(L.gst);
             mtr_synth_begin(&P.gen_cfg, &st, idx, &op);
             st_struct(L.gst, st);
-            sc->b2 = op.ref_seq;
-            sc->b3 = op.client;
+            L.sc->gen_ref = op.ref_seq;
+            L.sc->gen_client = op.client;
             st_struct(rec, op);
         }
-        __syncthreads();
+        wsync();
         View v;
-        v.ref = sc->b2;
-        v.client = enc_client(sc->b3);
+        v.ref = uni(L.sc->gen_ref);
+        v.client = enc_client(uni(L.sc->gen_client));
         v.local = 0;
-        prefix(L, v, P.new_length_calc);
+        prefix(L, s, v, P.new_length_calc);
+        const int S = s.nseg;
+        const int len = S > 0 ? uni(L.E[S - 1]) : 0;
         if (threadIdx.x == 0) {
-            const int S = sc->nseg;
-            const int len = S > 0 ? L.E[S - 1] : 0;
             mtr_op op = ld_struct<mtr_op>(rec);
             mtr_synth_state st = ld_struct<mtr_synth_state>(L.gst);
             mtr_synth_finish(&P.gen_cfg, &st, len, &op, P.gen_text + dd.text_base);
             st_struct(L.gst, st);
             st_struct(rec, op);
         }
-        __syncthreads();
+        wsync();
     }
 
     // ------------------------------------------------------------ state load/store
-    static __device__ void load_doc(D& L, const KParams& P, uint32_t d) {
+    static MTR_DI void load_doc(D& L, const KParams& P, St& s, uint32_t d) {
         const gptr<const DocHdr> hp = gp((const DocHdr*)P.hdr) + d;
-        lptr<Sc> sc = L.sc;
+        {
+            const DocHdr h = uni_struct(ld_struct<DocHdr>(hp));
+            s.nseg = h.nseg; s.height = h.height; s.minseq = h.minseq; s.curseq = h.curseq;
+            s.collab = h.collab; s.local = h.local; s.heapn = h.heapn; s.uidnext = h.uidnext;
+            s.textused = h.textused; s.propused = h.propused; s.rmused = h.rmused;
+            s.status = h.status; s.fail_op = h.fail_op; s.max_heap = h.max_heap;
+            s.texthalf = h.texthalf;
+            s.ops_done = 0;
+            s.sum_s = 0;
+            s.sum_l = 0;
+        }
         if (threadIdx.x == 0) {
-            const DocHdr h = ld_struct<DocHdr>(hp);
-            sc->nseg = h.nseg; sc->height = h.height; sc->minseq = h.minseq; sc->curseq = h.curseq;
-            sc->collab = h.collab; sc->local = h.local; sc->heapn = h.heapn; sc->uidnext = h.uidnext;
-            sc->textused = h.textused; sc->propused = h.propused; sc->rmused = h.rmused; sc->status = h.status;
-            sc->fail_op = h.fail_op; sc->max_heap = h.max_heap; sc->ops_done = 0; sc->texthalf = h.texthalf;
-            sc->sum_s = 0;
-            sc->sum_l = 0;
 #ifdef MTR_PROF
-            for (int q = 0; q < P_COUNT; q++) sc->prof[q] = 0;
+            for (int q = 0; q < P_COUNT; q++) L.sc->prof[q] = 0;
 #endif
             if (P.gen) st_struct(L.gst, ld_struct<mtr_synth_state>(gp(P.gen_state) + d));
         }
-        __syncthreads();
-        if (G) return;  // HBM-resident: nothing to stage
-        const int S = sc->nseg;
-        const int cs = P.segcap;
-        const gptr<const uint32_t> g = gp((const uint32_t*)P.seg) + size_t(d) * NF * cs;
-        for (int i = threadIdx.x; i < S; i += NT) {
-            L.len[i] = int(g[F_LEN * cs + i]);
-            L.seq[i] = int(g[F_SEQ * cs + i]);
-            L.rseq[i] = int(g[F_RSEQ * cs + i]);
-            L.meta[i] = g[F_META * cs + i];
-            L.text[i] = g[F_TEXT * cs + i];
-            L.props[i] = g[F_PROPS * cs + i];
-            L.rm[i] = g[F_RM * cs + i];
-            L.uid[i] = g[F_UID * cs + i];
+        if (!G) {  // stage the leaves and the heap into LDS
+            const int S = s.nseg;
+            const int cs = P.segcap;
+            const gptr<const uint32_t> g = gp((const uint32_t*)P.seg) + size_t(d) * NF * cs;
+            for (int i = threadIdx.x; i < S; i += 64) {
+                L.len[i] = int(g[F_LEN * cs + i]);
+                L.seq[i] = int(g[F_SEQ * cs + i]);
+                L.rseq[i] = int(g[F_RSEQ * cs + i]);
+                L.meta[i] = g[F_META * cs + i];
+                L.text[i] = g[F_TEXT * cs + i];
+                L.props[i] = g[F_PROPS * cs + i];
+                L.rm[i] = g[F_RM * cs + i];
+                L.uid[i] = g[F_UID * cs + i];
+            }
+            const int hn = s.heapn;
+            const gptr<const uint32_t> gh = gp((const uint32_t*)P.heap) + size_t(d) * 2 * P.hcap;
+            for (int i = threadIdx.x; i <= hn; i += 64) {
+                L.hseq[i] = int(gh[i]);
+                L.huid[i] = gh[P.hcap + i];
+            }
         }
-        const int hn = sc->heapn;
-        const gptr<const uint32_t> gh = gp((const uint32_t*)P.heap) + size_t(d) * 2 * P.hcap;
-        for (int i = threadIdx.x; i <= hn; i += NT) {
-            L.hseq[i] = int(gh[i]);
-            L.huid[i] = gh[P.hcap + i];
-        }
-        __syncthreads();
+        wsync();
     }
 
-    static __device__ void store_doc(D& L, const KParams& P, uint32_t d) {
-        __syncthreads();
-        lptr<Sc> sc = L.sc;
+    static MTR_DI void store_doc(D& L, const KParams& P, const St& s, uint32_t d) {
+        wsync();
         if (!G) {
-            const int S = sc->nseg;
+            const int S = s.nseg;
             const int cs = P.segcap;
             const gptr<uint32_t> g = gp(P.seg) + size_t(d) * NF * cs;
-            for (int i = threadIdx.x; i < S; i += NT) {
+            for (int i = threadIdx.x; i < S; i += 64) {
                 g[F_LEN * cs + i] = uint32_t(L.len[i]);
                 g[F_SEQ * cs + i] = uint32_t(L.seq[i]);
                 g[F_RSEQ * cs + i] = uint32_t(L.rseq[i]);
@@ -1312,9 +1325,9 @@ struct Eng {
                 g[F_RM * cs + i] = L.rm[i];
                 g[F_UID * cs + i] = L.uid[i];
             }
-            const int hn = sc->heapn;
+            const int hn = s.heapn;
             const gptr<uint32_t> gh = gp(P.heap) + size_t(d) * 2 * P.hcap;
-            for (int i = threadIdx.x; i <= hn; i += NT) {
+            for (int i = threadIdx.x; i <= hn; i += 64) {
                 gh[i] = uint32_t(L.hseq[i]);
                 gh[P.hcap + i] = L.huid[i];
             }
@@ -1322,27 +1335,27 @@ struct Eng {
         if (threadIdx.x == 0) {
             const gptr<DocHdr> hp = gp(P.hdr) + d;
             DocHdr h = ld_struct<DocHdr>(hp);
-            h.nseg = sc->nseg; h.height = sc->height; h.minseq = sc->minseq; h.curseq = sc->curseq;
-            h.collab = sc->collab; h.local = sc->local; h.heapn = sc->heapn; h.uidnext = sc->uidnext;
-            h.textused = sc->textused; h.propused = sc->propused; h.rmused = sc->rmused; h.status = sc->status;
-            h.op_cursor += sc->ops_done;
-            h.fail_op = sc->fail_op;
-            h.max_heap = sc->max_heap;
-            h.texthalf = sc->texthalf;
+            h.nseg = s.nseg; h.height = s.height; h.minseq = s.minseq; h.curseq = s.curseq;
+            h.collab = s.collab; h.local = s.local; h.heapn = s.heapn; h.uidnext = s.uidnext;
+            h.textused = s.textused; h.propused = s.propused; h.rmused = s.rmused; h.status = s.status;
+            h.op_cursor += s.ops_done;
+            h.fail_op = s.fail_op;
+            h.max_heap = s.max_heap;
+            h.texthalf = s.texthalf;
             st_struct(hp, h);
             if (P.gen) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
 #ifdef MTR_PROF
-            for (int q = 0; q < P_COUNT; q++) atomicAdd(&g_prof[q], sc->prof[q]);
+            for (int q = 0; q < P_COUNT; q++) atomicAdd(&g_prof[q], L.sc->prof[q]);
 #endif
-            if (sc->ops_done) {
-                atomicAdd(P.stat_ops, (unsigned long long)sc->ops_done);
-                atomicAdd(P.stat_ops + 1, sc->sum_s);
-                atomicAdd(P.stat_ops + 2, sc->sum_l);
+            if (s.ops_done) {
+                atomicAdd(P.stat_ops, (unsigned long long)s.ops_done);
+                atomicAdd(P.stat_ops + 1, s.sum_s);
+                atomicAdd(P.stat_ops + 2, s.sum_l);
             }
         }
     }
 
-    static __device__ void carve(D& L, char* smem, const KParams& P, uint32_t d) {
+    static MTR_DI void carve(D& L, char* smem, const KParams& P, uint32_t d) {
         if (G) {  // every array lives in the document's HBM slab
             const gptr<uint32_t> g = gp(P.seg) + size_t(d) * NF * P.segcap;
             L.len = (A<int>)(g + F_LEN * P.segcap);
@@ -1394,15 +1407,15 @@ struct Eng {
     }
 
     // ------------------------------------------------------------ per-document driver
-    static __device__ void run(char* smem, const KParams& P, uint32_t d) {
-        const mtr_doc_desc dd = ld_struct<mtr_doc_desc>(gp(P.docs) + d);
-        const int cursor = gp(P.hdr)[d].op_cursor;
+    static MTR_DI void run(char* smem, const KParams& P, uint32_t d) {
+        const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
+        const int cursor = uni(gp(P.hdr)[d].op_cursor);
         const int n_ops = min(int(dd.op_count) - cursor, P.ops_this_launch);
-        if (n_ops <= 0 || gp(P.hdr)[d].status != MTR_OK) return;
+        if (n_ops <= 0 || uni(gp(P.hdr)[d].status) != MTR_OK) return;
         D L;
         carve(L, smem, P, d);
-        load_doc(L, P, d);
-        lptr<Sc> sc = L.sc;
+        St s;
+        load_doc(L, P, s, d);
         const gptr<const mtr_op> ops = gp(P.ops) + dd.op_begin + cursor;
         const gptr<const uint16_t> btext = gp(P.btext) + dd.text_base;
         const int ln = lane_id();
@@ -1414,8 +1427,8 @@ struct Eng {
             PROF(P_OP);
             mtr_op op;
             if (P.gen) {
-                gen_op(L, P, dd, cursor + k);
-                op = ld_struct<mtr_op>(ops + k);
+                gen_op(L, P, s, dd, cursor + k);
+                op = uni_struct(ld_struct<mtr_op>(ops + k));
                 pre = false;
             } else {
                 if ((k & 63) == 0) {
@@ -1441,34 +1454,28 @@ struct Eng {
                     }
                 }
             }
-            if (threadIdx.x == 0) {
-                sc->sum_s += (unsigned long long)sc->nseg;
-                if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER))
-                    sc->sum_l += (unsigned long long)op.payload2;
-            }
+            s.sum_s += (unsigned long long)s.nseg;
+            if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER))
+                s.sum_l += (unsigned long long)op.payload2;
             {  // text arena: keep room for this op's text plus zamboni merge copies
                 const int need =
                     int(op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT ? op.payload2 : 0) + 4096;
-                if (sc->textused + need > text_end(sc, P)) text_gc(L, P);
+                if (s.textused + need > text_end(s, P)) text_gc(L, P, s);
             }
-            if (sc->nseg + 2 >= L.cap) {  // every op adds at most two leaves
-                __syncthreads();
-                if (threadIdx.x == 0) sc->status = MTR_ERR_CAPACITY;
-                __syncthreads();
-            }
-            if (sc->status != MTR_OK) break;
+            if (s.nseg + 2 >= L.cap) s.status = MTR_ERR_CAPACITY;  // every op adds at most two leaves
+            if (s.status != MTR_OK) break;
             const bool local_op = op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE;
+            int zop = 0;
             View v;
             int seq = op.seq;
             uint32_t client = enc_client(op.client);
             if (local_op) {
-                if (sc->collab) {
-                    __syncthreads();
-                    if (threadIdx.x == 0) sc->status = MTR_ERR_UNSUPPORTED;
-                    __syncthreads();
+                if (s.collab) {
+                    s.status = MTR_ERR_UNSUPPORTED;
+                    s.fail_op = cursor + k;
                     break;
                 }
-                v.ref = sc->curseq;
+                v.ref = s.curseq;
                 v.client = CL_LOCAL;
                 v.local = 1;
                 seq = 0;
@@ -1476,58 +1483,62 @@ struct Eng {
             } else {
                 v.ref = op.ref_seq;
                 v.client = client;
-                v.local = (!sc->collab || uint32_t(sc->local) == client) ? 1 : 0;
+                v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
             }
             switch (op.type) {
                 case MTR_OP_INSERT:
                 case MTR_OP_LOCAL_INSERT:
-                    prefix(L, v, P.new_length_calc);
-                    split_at(L, op.pos1);
-                    insert_at(L, P, v, op, seq, client, dd, pre, pf);
-                    if (sc->collab) zamboni(L, P);
+                    prefix(L, s, v, P.new_length_calc);
+                    split_at(L, s, op.pos1);
+                    insert_at(L, P, s, v, op, seq, client, dd, pre, pf);
+                    zop = s.collab;
                     break;
                 case MTR_OP_REMOVE:
                 case MTR_OP_LOCAL_REMOVE:
                 case MTR_OP_ANNOTATE:
                 case MTR_OP_LOCAL_ANNOTATE: {
                     const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
-                    prefix(L, v, P.new_length_calc);
-                    split_at(L, op.pos1);
-                    split_at(L, op.pos2);
-                    range_walk(L, P, v, op.pos1, op.pos2, seq, client, is_remove, op.payload);
-                    if (sc->collab) zamboni(L, P);
+                    prefix(L, s, v, P.new_length_calc);
+                    split_at(L, s, op.pos1);
+                    split_at(L, s, op.pos2);
+                    range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload);
+                    zop = s.collab;
                     break;
                 }
                 case MTR_OP_SEQ:
                     break;
                 case MTR_OP_START_COLLAB:
-                    __syncthreads();
-                    if (threadIdx.x == 0 && !sc->collab) {
-                        sc->collab = 1;
-                        sc->local = 0;
-                        sc->minseq = op.min_seq;
-                        sc->curseq = op.seq;
-                        sc->heapn = 0;
+                    if (!s.collab) {
+                        s.collab = 1;
+                        s.local = 0;
+                        s.minseq = op.min_seq;
+                        s.curseq = op.seq;
+                        s.heapn = 0;
                     }
-                    __syncthreads();
                     break;
                 default:
-                    __syncthreads();
-                    if (threadIdx.x == 0) sc->status = MTR_ERR_BAD_OP;
-                    __syncthreads();
+                    s.status = MTR_ERR_BAD_OP;
                     break;
             }
-            if (!local_op && op.type != MTR_OP_START_COLLAB && (op.flags & MTR_F_LAST) && sc->status == MTR_OK)
-                update_seq(L, P, op.min_seq, op.seq);
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                if (sc->status != MTR_OK) sc->fail_op = cursor + k;
-                else sc->ops_done = k + 1;
+            // zamboniSegments after the op (mergeTree.ts:1420-1426, 1948-1952, 2042-2046), then
+            // updateSeqNumbers, whose minSeq advance runs it again (mergeTree.ts:1037-1042)
+            const bool upd = !local_op && op.type != MTR_OP_START_COLLAB && (op.flags & MTR_F_LAST);
+            for (int phase = 0; phase < 2; phase++) {
+                int zrun = zop;
+                if (phase == 1) {
+                    if (!upd || s.status != MTR_OK) break;
+                    PROF(P_UPDSEQ);
+                    zrun = update_seq(s, op.min_seq, op.seq);
+                }
+                if (zrun) zamboni(L, P, s);
             }
-            __syncthreads();
-            if (sc->status != MTR_OK) break;
+            if (s.status != MTR_OK) {
+                s.fail_op = cursor + k;
+                break;
+            }
+            s.ops_done = k + 1;
         }
-        store_doc(L, P, d);
+        store_doc(L, P, s, d);
     }
 };
 
