@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--ops", type=int, default=1_000, help="sequenced messages per document (C3: 1k)")
     ap.add_argument("--writers", type=int, default=8)
     ap.add_argument("--max-lag", type=int, default=32)
-    ap.add_argument("--ops-per-launch", type=int, default=64)
+    ap.add_argument("--ops-per-launch", type=int, default=16)
     ap.add_argument("--cpu-sample-docs", type=int, default=4000)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -141,6 +141,8 @@ struct KParams {
     int32_t ops_this_launch;
     int32_t new_length_calc;
     uint32_t n_docs;
+    const uint32_t* doc_list;  // documents of this launch (one size class): block b applies doc_list[b]
+    uint32_t n_launch;
     const mtr_op* ops;
     const mtr_doc_desc* docs;
     const uint16_t* btext;
@@ -148,7 +150,7 @@ struct KParams {
     const uint32_t* propop_kv;
     const uint32_t* key_index;
     const uint32_t* val_eq;
-    unsigned long long* stat_ops;  // [0] ops applied, [1] sum of leaves before ops, [2] inserted units
+    unsigned long long* stat_ops;  // [doc][4]: ops applied, sum of leaves before ops, inserted units
     // record mode (synthetic workloads): ops are drawn from include/mtr_synth.h with this
     // engine's own exact view lengths, written to gen_ops/gen_text, then applied
     int32_t gen;
@@ -1347,10 +1349,11 @@ struct Eng {
 #ifdef MTR_PROF
             for (int q = 0; q < P_COUNT; q++) atomicAdd(&g_prof[q], L.sc->prof[q]);
 #endif
-            if (s.ops_done) {
-                atomicAdd(P.stat_ops, (unsigned long long)s.ops_done);
-                atomicAdd(P.stat_ops + 1, s.sum_s);
-                atomicAdd(P.stat_ops + 2, s.sum_l);
+            if (s.ops_done) {  // this document's counters (no cross-document atomics)
+                const gptr<unsigned long long> st = gp(P.stat_ops) + size_t(d) * 4;
+                st[0] += (unsigned long long)s.ops_done;
+                st[1] += s.sum_s;
+                st[2] += s.sum_l;
             }
         }
     }
@@ -1545,8 +1548,8 @@ struct Eng {
 template <bool G>
 __global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint32_t d = blockIdx.x;
-    if (d >= P.n_docs) return;
+    if (blockIdx.x >= P.n_launch) return;
+    const uint32_t d = P.doc_list[blockIdx.x];
     Eng<G>::run(smem, P, d);
 }
 

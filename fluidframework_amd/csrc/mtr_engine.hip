@@ -89,6 +89,9 @@ struct mtr_engine {
     DevBuf<uint8_t> key_bytes, val_bytes, client_bytes;
     DevBuf<unsigned long long> stat;  // [0] ops applied
     DevBuf<int32_t> red;              // small reduction buffer
+    DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
+    DevBuf<uint32_t> dlist;           // [class][n_docs] document lists of one apply round
+    int32_t* h_cls = nullptr;         // pinned host copy of cls
     DevBuf<uint32_t> scratch;         // E/V arrays for HBM-resident (global-mode) launches
     DevBuf<mtr_synth_state> gstate;   // record mode generator state
     mtr_synth_cfg gcfg{};
@@ -132,6 +135,45 @@ __global__ void scan_state_kernel(const DocHdr* h, const mtr_doc_desc* docs, uin
     atomicMax(&out[2], x.heapn);
 }
 
+// Size classes for one apply round: documents with ops left are bucketed by leaf count (64-leaf
+// classes) so that each class launch sizes its LDS by its own largest document.
+// cls layout: [0] max remaining ops, then per class c: cnt[c] at 1+3c, max nseg at 2+3c, max heapn at 3+3c.
+constexpr int kClasses = 64;
+constexpr int kClassLeaves = 64;
+__global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t n,
+                                                      int32_t* cls, uint32_t* list) {
+    // block-local histogram in LDS, then one global atomic per (block, class): the per-document
+    // atomics on a handful of addresses would serialise at the memory side
+    __shared__ int lcnt[kClasses], lmax[kClasses], lheap[kClasses], lbase[kClasses];
+    __shared__ int lrem;
+    const int t = threadIdx.x;
+    if (t < kClasses) lcnt[t] = lmax[t] = lheap[t] = 0;
+    if (t == 0) lrem = 0;
+    __syncthreads();
+    const uint32_t d = blockIdx.x * blockDim.x + t;
+    int c = -1, rank = 0;
+    if (d < n) {
+        const DocHdr x = h[d];
+        const int rem = x.status == MTR_OK ? int(docs[d].op_count) - x.op_cursor : 0;
+        if (rem > 0) {
+            c = min(kClasses - 1, x.nseg / kClassLeaves);
+            rank = atomicAdd(&lcnt[c], 1);
+            atomicMax(&lmax[c], x.nseg);
+            atomicMax(&lheap[c], x.heapn);
+            atomicMax(&lrem, rem);
+        }
+    }
+    __syncthreads();
+    if (t < kClasses && lcnt[t]) {
+        lbase[t] = atomicAdd(&cls[1 + 3 * t], lcnt[t]);
+        atomicMax(&cls[2 + 3 * t], lmax[t]);
+        atomicMax(&cls[3 + 3 * t], lheap[t]);
+    }
+    if (t == 0 && lrem) atomicMax(&cls[0], lrem);
+    __syncthreads();
+    if (c >= 0) list[size_t(c) * n + lbase[c] + rank] = d;
+}
+
 template <class T>
 static int upload(mtr_engine* e, DevBuf<T>& dst, const T* src, size_t n) {
     if (dst.ensure(n)) return -1;
@@ -171,7 +213,7 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
     const size_t D = std::max<uint32_t>(max_docs, 1);
     if (e->hdr.ensure(D) || e->seg.ensure(D * NF * c.max_segments) || e->heap.ensure(D * 2 * c.heap_entries) ||
         e->text.ensure(D * c.text_units) || e->prop.ensure(D * c.prop_words) || e->rm.ensure(D * c.remover_cells) ||
-        e->stat.ensure(4) || e->red.ensure(4)) {
+        e->stat.ensure(D * 4) || e->red.ensure(4)) {
         mtr_engine_destroy(e);
         return nullptr;
     }
@@ -199,6 +241,9 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->client_bytes.release();
     e->stat.release();
     e->red.release();
+    e->cls.release();
+    if (e->h_cls) (void)hipHostFree(e->h_cls);
+    e->dlist.release();
     e->scratch.release();
     e->out_size.release();
     e->out_off.release();
@@ -216,7 +261,7 @@ int mtr_reset(mtr_engine* e) {
     const uint32_t n = std::max<uint32_t>(e->max_docs, 1);
     reset_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, n);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemsetAsync(e->stat.p, 0, 4 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(e->stat.p, 0, e->stat.n * sizeof(unsigned long long), e->stream));
     e->summarized = false;
     return MTR_OK;
 }
@@ -310,45 +355,58 @@ static int run_impl(mtr_engine* e, int gen) {
         (void)hipFuncSetAttribute((const void*)apply_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
     });
+    const size_t ncls = 1 + 3 * kClasses;
+    if (e->cls.ensure(ncls) || e->dlist.ensure(size_t(kClasses) * e->n_docs)) return -1;
+    if (!e->h_cls) HIPCHK(hipHostMalloc((void**)&e->h_cls, (1 + 3 * kClasses) * sizeof(int32_t), hipHostMallocDefault));
+    int32_t* cls = e->h_cls;
     for (;;) {
-        int32_t st[3];
-        if (read_state(e, st)) return -1;
-        const int maxseg = st[0], rem = st[1], maxheap = st[2];
+        HIPCHK(hipMemsetAsync(e->cls.p, 0, ncls * sizeof(int32_t), e->stream));
+        classify_kernel<<<(e->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, e->n_docs, e->cls.p,
+                                                                           e->dlist.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(cls, e->cls.p, ncls * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        const int rem = cls[0];
         if (rem <= 0) break;
         const int k = std::min(K, rem);
-        int cap = round64(maxseg + 2 * k + 8);
-        if (cap > P.segcap) cap = P.segcap;
-        int lhcap = std::min<int>(P.hcap, std::max(cap / 2, round64(maxheap + 2 * k + 8)));
-        size_t lds = lds_bytes(cap, lhcap);
-        int kk = k;
-        P.global_mode = 0;
-        if (lds > size_t(160 * 1024)) {
-            // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
-            if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
-            P.global_mode = 1;
-            P.scratch = e->scratch.p;
-            cap = P.segcap;
-            lhcap = P.hcap;
-            lds = lds_bytes_global_mode();
-            kk = std::max(1, std::min(k, (cap - maxseg - 8) / 2));
-        } else {
-            kk = std::max(1, std::min(k, (cap - maxseg - 8) / 2));
-        }
-        P.cap = cap;
-        P.lhcap = lhcap;
-        P.ops_this_launch = kk;
+        bool stuck = false;
         HIPCHK(hipEventRecord(e->ev[0], e->stream));
-        if (P.global_mode) apply_kernel<true><<<e->n_docs, NT, lds, e->stream>>>(P);
-        else apply_kernel<false><<<e->n_docs, NT, lds, e->stream>>>(P);
-        HIPCHK(hipGetLastError());
+        for (int c = kClasses - 1; c >= 0; c--) {  // one launch per size class, largest documents first
+            const int cnt = cls[1 + 3 * c], maxseg = cls[2 + 3 * c], maxheap = cls[3 + 3 * c];
+            if (cnt <= 0) continue;
+            int cap = round64(maxseg + 2 * k + 8);
+            if (cap > P.segcap) cap = P.segcap;
+            int lhcap = std::min<int>(P.hcap, std::max(cap / 2, round64(maxheap + 2 * k + 8)));
+            size_t lds = lds_bytes(cap, lhcap);
+            P.global_mode = 0;
+            if (lds > size_t(160 * 1024)) {
+                // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
+                if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
+                P.global_mode = 1;
+                P.scratch = e->scratch.p;
+                cap = P.segcap;
+                lhcap = P.hcap;
+                lds = lds_bytes_global_mode();
+            }
+            const int kk = std::max(1, std::min(k, (cap - maxseg - 8) / 2));
+            if (cap - maxseg - 8 < 2) stuck = true;
+            P.cap = cap;
+            P.lhcap = lhcap;
+            P.ops_this_launch = kk;
+            P.doc_list = e->dlist.p + size_t(c) * e->n_docs;
+            P.n_launch = uint32_t(cnt);
+            if (P.global_mode) apply_kernel<true><<<cnt, NT, lds, e->stream>>>(P);
+            else apply_kernel<false><<<cnt, NT, lds, e->stream>>>(P);
+            HIPCHK(hipGetLastError());
+            e->launches++;
+        }
         HIPCHK(hipEventRecord(e->ev[1], e->stream));
         HIPCHK(hipEventSynchronize(e->ev[1]));
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
         e->t_apply += ms;
-        e->launches++;
-        if (kk < 1 || cap - maxseg - 8 < 2) {
-            set_err("document exceeds the LDS leaf capacity");
+        if (stuck) {
+            set_err("document exceeds the leaf capacity");
             break;
         }
     }
@@ -627,7 +685,12 @@ int mtr_stats(mtr_engine* e, int64_t* out, int32_t n) {
     std::vector<DocHdr> h(e->n_docs);
     if (e->n_docs) HIPCHK(hipMemcpy(h.data(), e->hdr.p, e->n_docs * sizeof(DocHdr), hipMemcpyDeviceToHost));
     unsigned long long st[3] = {0, 0, 0};
-    HIPCHK(hipMemcpy(st, e->stat.p, sizeof(st), hipMemcpyDeviceToHost));
+    {  // per-document counters [doc][4]: ops applied, sum of leaves before ops, inserted units
+        std::vector<unsigned long long> sd(size_t(e->n_docs) * 4);
+        if (e->n_docs) HIPCHK(hipMemcpy(sd.data(), e->stat.p, sd.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (uint32_t d = 0; d < e->n_docs; d++)
+            for (int q = 0; q < 3; q++) st[q] += sd[size_t(d) * 4 + q];
+    }
     int64_t v[10] = {int64_t(st[0]), e->n_docs, 0, 0, 0, e->launches, 0, 0, int64_t(st[1]), int64_t(st[2])};
     for (auto& x : h) {
         v[2] = std::max<int64_t>(v[2], x.nseg);
