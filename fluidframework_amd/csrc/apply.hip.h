@@ -57,6 +57,7 @@ constexpr uint32_t M_NOREF = 1u << 24;
 constexpr uint32_t M_DEL = 1u << 25;
 constexpr uint32_t M_NL = 1u << 26;   // text leaf whose last unit is '\n' (TextSegment.canAppend)
 constexpr uint32_t M_NLQ = 1u << 27;  // M_NL not known yet (left half of a split): read lazily by scour
+constexpr uint32_t M_NONL = 1u << 28; // the leaf's text holds no '\n' at all (so neither does any split half)
 constexpr uint32_t NS_UNDEF = 0, NS_FALSE = 1, NS_TRUE = 2;
 
 constexpr uint32_t CL_LOCAL = 0xffu;      // LocalClientId (-1)
@@ -747,6 +748,18 @@ struct Eng {
         for (int k = lane_id(); k < n; k += 64) L.gtext[dst + k] = L.gtext[src + k];
     }
     static MTR_DI int text_end(const St& s, const KParams& P) { return (P.tcap / 2) * (s.texthalf + 1); }
+    // one lane's copy of n units: 8 loads in flight, then 8 stores
+    static MTR_DI void copy_units(const D& L, uint32_t dst, uint32_t src, int n) {
+        for (int u0 = 0; u0 < n; u0 += 8) {
+            uint16_t b[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (u0 + q < n) b[q] = L.gtext[src + u0 + q];
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (u0 + q < n) L.gtext[dst + u0 + q] = b[q];
+        }
+    }
 
     // prev.append(seg) (textSegment.ts:99-103): text of b follows text of a.  Updates L.len/L.text
     // of a; the caller keeps M_NL.
@@ -804,7 +817,7 @@ struct Eng {
             const int inc = wave_incl_scan(n);
             const int off = dst0 + carry + inc - n;
             if (i < S && !(L.meta[i] & M_MARKER)) {
-                for (int k = 0; k < n; k++) L.gtext[off + k] = L.gtext[src + k];
+                copy_units(L, uint32_t(off), src, n);
                 L.text[i] = uint32_t(off);
             }
             carry += rdlane(inc, 63);
@@ -868,7 +881,7 @@ struct Eng {
                     if (prev >= 0 && lk > 0 && can_append(pmeta, plen, m, lk) && props_match_w(L, P, pprops, pk)) {
                         text_append(L, P, s, prev, k);
                         plen += lk;
-                        pmeta = (pmeta & ~(M_NL | M_NLQ)) | (m & (M_NL | M_NLQ));
+                        pmeta = (pmeta & ~(M_NL | M_NLQ | (m & M_NONL ? 0u : M_NONL))) | (m & (M_NL | M_NLQ));
                         L.meta[prev] = pmeta;
                         L.meta[k] = m | M_DEL;
                         wsync();
@@ -889,6 +902,113 @@ struct Eng {
                 }
             }
         }
+        return kept;
+    }
+
+    // scourNode over [cs, ce) with all leaves classified at once (ce - cs <= 64).  For a leaf k
+    // that was not already unlinked, the serial walk's merge candidate `prev` is the nearest
+    // earlier such leaf p when no child-block boundary lies in (p, k] and p is a live leaf below
+    // minSeq with positive length (p is then the chain head or its last merged member; merged
+    // members matched the head, and matchProperties is an equivalence).  Leaf k merges into the
+    // chain iff it is such a leaf too and canAppend/matchProperties hold against p.  The
+    // TextSegmentGranularity clause of canAppend depends on the accumulated chain length, so a
+    // range where a leaf longer than 256 units would link falls back to the serial walk.
+    // Returns #kept, or -1 when the caller must run the serial walk (nothing was modified).
+    static MTR_DI int scour_par(D& L, const KParams& P, St& s, int cs, int ce) {
+        const int minseq = s.minseq;
+        const int ln = lane_id();
+        const int i = cs + ln;
+        const bool in = i < ce;
+        uint32_t vm = M_DEL, vp = 0, vt = 0;
+        int vr = RNONE, vs = 0, vl = 0;
+        if (in) {
+            vm = L.meta[i];
+            vr = L.rseq[i];
+            vs = L.seq[i];
+            vl = L.len[i];
+            vp = L.props[i];
+            vt = L.text[i];
+        }
+        const bool pre = (vm & M_DEL) != 0;
+        const bool removed = vr != RNONE;
+        const bool cand = !pre && !removed && vs <= minseq && vl > 0;
+        {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
+            const bool q = cand && (vm & (M_NLQ | M_MARKER)) == M_NLQ;
+            if (__ballot(q)) {
+                PROF(P_NLQ);
+                PROF_COUNT(P_NNLQ);
+                if (q) {
+                    const uint16_t u = L.gtext[vt + uint32_t(vl) - 1];
+                    vm = (vm & ~(M_NLQ | M_NL)) | (u == u'\n' ? M_NL : 0u);
+                    L.meta[i] = vm;
+                }
+                wsync();
+            }
+        }
+        const uint64_t nd = __ballot(in && !pre);
+        const uint64_t bm = __ballot(in && i > cs && bnd_of(vm) >= 1);
+        const uint64_t below = nd & lanes_below();
+        const int p = below ? last_lane(below) : -1;
+        const int ps = p < 0 ? 0 : p;
+        const int pc = __shfl(int(cand), ps);
+        const uint32_t pm = uint32_t(__shfl(int(vm), ps));
+        const uint32_t pp = uint32_t(__shfl(int(vp), ps));
+        const uint64_t upto = (uint64_t(2) << ln) - 1;  // lanes <= ln
+        const uint64_t after_p = p < 0 ? ~uint64_t(0) : ~((uint64_t(2) << p) - 1);
+        bool link = cand && p >= 0 && pc && !(bm & upto & after_p) && !((vm | pm) & M_MARKER) && !(pm & M_NL);
+        if (link && vp != pp) link = props_match(L.gprop, gp(P.val_eq), pp, vp);
+        if (__ballot(link && vl > kGranularity)) return -1;
+        const bool unlink = !pre && removed && vr <= minseq;
+        const uint64_t lm = __ballot(link);
+        if (unlink || link) L.meta[i] = vm | M_DEL;
+        const int kept = __popcll(__ballot(in && !pre && !unlink && !link));
+        if (lm) {  // concatenate each chain's text behind its head (prev.append, textSegment.ts:99-103)
+            const uint64_t hm = __ballot(in && !pre && !link);  // chain heads and unmerged leaves
+            // lane offsets inside its chain: inclusive scan of lengths restarted at every head
+            const int hd = (hm & upto) ? last_lane(hm & upto) : 0;  // this lane's chain head (chain lanes)
+            const int incl = wave_incl_scan(in && !pre ? vl : 0);
+            const int hbase = __shfl(incl - vl, hd);       // exclusive prefix at the head
+            const int off = incl - vl - hbase;             // offset of this piece inside its chain
+            uint64_t todo = lm;
+            wsync();
+            while (todo) {
+                const int k0 = first_lane(todo);                   // first member of the next chain
+                const int h = last_lane(hm & ((uint64_t(1) << k0) - 1));
+                const uint64_t rest = hm & ~((uint64_t(2) << h) - 1);  // heads after h
+                const uint64_t chain_end = rest ? ((uint64_t(1) << first_lane(rest)) - 1) : ~uint64_t(0);
+                const uint64_t mem = lm & chain_end & ~((uint64_t(2) << h) - 1);
+                todo &= ~mem;
+                const int e = last_lane(mem);
+                const int total = rdlane(incl, e) - rdlane(incl - vl, h);
+                const uint32_t th = rdlane(vt, h);
+                const int lh = rdlane(vl, h);
+                const bool mine = ((mem >> ln) & 1) != 0;
+                const bool inplace = __ballot(mine && vt != th + uint32_t(off)) == 0;
+                uint32_t base = th;
+                if (!inplace) {
+                    const bool tail = th + uint32_t(lh) == uint32_t(s.textused);
+                    base = tail ? th : uint32_t(s.textused);
+                    const int need = int(base + uint32_t(total)) - s.textused;
+                    if (s.textused + need > text_end(s, P)) {
+                        s.status = MTR_ERR_CAPACITY;
+                        return kept;
+                    }
+                    const bool copy = mine || (!tail && ln == h);
+                    if (copy) copy_units(L, base + uint32_t(off), vt, vl);
+                    s.textused = int(base) + total;
+                }
+                const uint32_t me = rdlane(vm, e), mh = rdlane(vm, h);
+                const bool nonl = __ballot(mine && !(vm & M_NONL)) == 0 && (mh & M_NONL);
+                if (ln == 0) {
+                    L.len[cs + h] = total;
+                    L.text[cs + h] = base;
+                    L.meta[cs + h] = (mh & ~(M_NL | M_NLQ | M_NONL)) | (me & (M_NL | M_NLQ)) | (nonl ? M_NONL : 0u);
+                }
+                PROF_COUNT(P_NMERGE);
+                wsync();
+            }
+        }
+        wsync();
         return kept;
     }
 
@@ -921,7 +1041,8 @@ struct Eng {
         int kept;
         {
             PROF(P_SCOUR1);
-            kept = scour_range(L, P, s, rs1, re1);
+            kept = re1 - rs1 <= 64 ? scour_par(L, P, s, rs1, re1) : -1;
+            if (kept < 0) kept = scour_range(L, P, s, rs1, re1);
         }
         {  // block.needsScour = false, kept on the block's first surviving leaf
             const int i = rs1 + lane_id();
@@ -942,7 +1063,7 @@ struct Eng {
                     // packParent scours every child of P again -- including the block just
                     // scoured: scourNode is not idempotent (a dropped tombstone no longer resets
                     // the merge candidate), zamboni.ts:68-73,122-193.
-                    scour_range(L, P, s, ps, pe);
+                    if (pe - ps > 64 || scour_par(L, P, s, ps, pe) < 0) scour_range(L, P, s, ps, pe);
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
                 int T = 0;
@@ -1047,7 +1168,7 @@ struct Eng {
             L.seq[r] = uni(L.seq[j]);
             L.rseq[r] = uni(L.rseq[j]);
             L.meta[r] = set_ns(set_bnd(mj, 0), NS_UNDEF);
-            L.meta[j] = (mj & ~M_NL) | M_NLQ;
+            L.meta[j] = (mj & M_NONL) ? (mj & ~M_NL) : ((mj & ~M_NL) | M_NLQ);
             L.text[r] = uniu(L.text[j]) + uint32_t(off);
             L.props[r] = uniu(L.props[j]);
             L.rm[r] = uniu(L.rm[j]);
@@ -1087,7 +1208,9 @@ struct Eng {
                 for (int k = ln; k < len; k += 64) L.gtext[t0 + k] = src[k];
             }
         }
-        const bool nl = pre && __ballot(ln == len - 1 && pf == u'\n') != 0;
+        const uint64_t nlm = pre ? __ballot(ln < len && pf == u'\n') : 0;
+        const bool nl = pre && ((nlm >> (len - 1)) & 1);
+        const bool nonl = pre && nlm == 0;
         const int pos = op.pos1;
         const int S = s.nseg;
         int slot = -1, inherit = 0;
@@ -1118,7 +1241,7 @@ struct Eng {
         shift_right1(L, s, slot);
         uint32_t m = client & M_CLIENT_MASK;
         if (marker) m |= M_MARKER;
-        else m |= pre ? (nl ? M_NL : 0u) : M_NLQ;
+        else m |= pre ? ((nl ? M_NL : 0u) | (nonl ? M_NONL : 0u)) : M_NLQ;
         if (op.flags & MTR_F_NOREF) m |= M_NOREF;
         if (S == 0) {
             s.height = 1;

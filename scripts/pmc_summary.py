@@ -10,13 +10,17 @@ import os
 
 ap = argparse.ArgumentParser()
 ap.add_argument("dir")
-ap.add_argument("--launches", type=int, default=16)
+ap.add_argument("--launches", type=int, default=0, help="apply launches of the timed step (default: from kt.log)")
 ap.add_argument("--kernel", default="apply_kernel")
 ap.add_argument("--docs", type=int, default=100000)
 ap.add_argument("--ops", type=int, default=1000)
 ap.add_argument("--out", default=None)
 a = ap.parse_args()
 
+if not a.launches:  # the bench line of the kernel-trace run names the launches of one step
+    for line in open(os.path.join(a.dir, "kt.log")):
+        if line.startswith("{"):
+            a.launches = json.loads(line)["roofline"]["launches_per_step"]
 per = collections.Counter()
 for f in sorted(glob.glob(os.path.join(a.dir, "*", "*_counter_collection.csv"))):
     d = collections.defaultdict(dict)
@@ -27,7 +31,8 @@ for f in sorted(glob.glob(os.path.join(a.dir, "*", "*_counter_collection.csv")))
     for i in ids:
         for k, v in d[i].items():
             per[k] += v / len(ids)
-out = {"kernel": a.kernel, "docs": a.docs, "ops": a.ops, "launches_averaged": a.launches}
+out = {"kernel": a.kernel, "docs": a.docs, "ops": a.ops, "launches_averaged": a.launches,
+       "note_launches": "per-launch averages over the last `launches_averaged` apply dispatches (one timed step)"}
 out["counters_per_launch"] = dict(per)
 if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     # FETCH_SIZE/WRITE_SIZE are KiB; gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads
@@ -40,6 +45,9 @@ if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     out["note"] = "hbm_bytes = 2*FETCH_SIZE (gfx950 correction) + WRITE_SIZE, KiB->bytes"
 if "SQ_LDS_BANK_CONFLICT" in per and "SQ_LDS_IDX_ACTIVE" in per:
     out["lds_bank_conflict_rate"] = per["SQ_LDS_BANK_CONFLICT"] / max(1.0, per["SQ_LDS_IDX_ACTIVE"])
+if "SQ_WAVES" in per and "SQ_INSTS_VALU" in per:
+    ops_per_launch = a.docs * a.ops / a.launches
+    out["insts_per_op"] = {k[9:].lower(): per[k] / ops_per_launch for k in per if k.startswith("SQ_INSTS_")}
 if "SQ_WAVE_CYCLES" in per:
     wc = per["SQ_WAVE_CYCLES"]
     out["wait_any_frac"] = per.get("SQ_WAIT_ANY", 0) / wc
