@@ -59,12 +59,14 @@ def main():
         dist_mod.init_process_group("nccl")
         dist = dist_mod
 
+    from fluidframework_amd import shard
     from fluidframework_amd.engine import Engine
     from fluidframework_amd.synth import make_cfg, tables
 
     n, ops = a.docs, a.ops
     tabs = tables(writers=a.writers)
-    cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=rank * n)
+    doc_lo, _ = shard.doc_range(rank, world, n)
+    cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=doc_lo)
     text_units = 2 * int(cfg.text_cap) + 1024
     eng = Engine(n, device=local, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=text_units,
                  prop_words=16384, remover_cells=4096, ops_per_launch=a.ops_per_launch)
@@ -107,21 +109,10 @@ def main():
     st = eng.stats()  # counters of the last step
     hashes = eng.hashes(n)
     messages = n * ops
-    local_vals = np.array([elapsed, float(messages), float(st["bad_docs"])], dtype=np.float64)
-    digest = int(np.bitwise_xor.reduce(hashes.view(np.uint64))) if n else 0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor(local_vals, dtype=torch.float64, device=f"cuda:{local}")
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0].item())
-        total_messages = float(t[1].item())
-        bad = float(t[2].item())
-        d = torch.tensor([digest & 0x7FFFFFFFFFFFFFFF], dtype=torch.int64, device=f"cuda:{local}")
-        dist.all_reduce(d, op=dist.ReduceOp.SUM)  # cross-shard checksum over RCCL/xGMI
-        digest = int(d.item())
+    run_digest = shard.digest(hashes)
+    if dist is not None:  # the only collective: counters + summary digests over RCCL/xGMI
+        r = shard.reduce_run(dist, f"cuda:{local}", elapsed, messages, int(st["bad_docs"]), run_digest)
+        elapsed, total_messages, bad, run_digest = r["elapsed"], float(r["messages"]), float(r["bad_docs"]), r["digest"]
     else:
         total_messages = float(messages)
         bad = float(st["bad_docs"])
@@ -209,7 +200,7 @@ def main():
             "summary_ms_per_step": round(summary_ms / a.steps, 3),
             "summary_bytes": eng.summary_bytes(),
             "bad_docs": int(bad),
-            "digest": digest,
+            "digest": f"{run_digest:016x}",
             "generate_s": round(gen_s, 2),
             "max_leaves": st["max_leaves"],
             "mean_leaves_before_op": st["sum_leaves_before_op"] / max(1, messages),
