@@ -28,7 +28,7 @@ def _stale(target, deps):
 def build_engine(force=False, verbose=False, prof=False):
     out = os.path.join(HERE, "libmtr_prof.so" if prof else "libmtr.so")
     deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", h)
-                                                           for h in ("mtr.h", "mtr_types.h", "mtr_synth.h")]
+                                                           for h in ("mtr.h", "mtr_types.h", "mtr_synth.h", "mtr_digest.h")]
     if force or _stale(out, deps):
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-result"] + (["-DMTR_PROF"] if prof else []) + ["-o", out] + [os.path.join(CSRC, f) for f in ENGINE_SRC]

@@ -97,6 +97,9 @@ struct mtr_engine {
     mtr_synth_cfg gcfg{};
     // summaries
     DevBuf<int64_t> out_size, out_off;
+    DevBuf<uint8_t> s_kind;                       // summary scratch (size pass -> write pass)
+    DevBuf<uint32_t> s_start, s_len, s_bytes;
+    DevBuf<int32_t> s_blob;
     DevBuf<unsigned long long> out_hash;
     DevBuf<uint8_t> out;
     std::vector<int64_t> h_off, h_size;
@@ -246,6 +249,11 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->dlist.release();
     e->scratch.release();
     e->out_size.release();
+    e->s_kind.release();
+    e->s_start.release();
+    e->s_len.release();
+    e->s_bytes.release();
+    e->s_blob.release();
     e->out_off.release();
     e->out_hash.release();
     e->out.release();
@@ -512,6 +520,18 @@ int mtr_summarize(mtr_engine* e) {
     P.out_size = e->out_size.p;
     P.out_off = e->out_off.p;
     P.out_hash = e->out_hash.p;
+    {
+        const size_t sc = size_t(P.segcap);
+        P.maxb = int(std::min<int64_t>(int64_t(sc) + 1, int64_t(P.tcap) / std::max(1, P.chunk_size) + 4));
+        if (e->s_kind.ensure(n * sc) || e->s_start.ensure(n * (sc + 1)) || e->s_len.ensure(n * sc) ||
+            e->s_bytes.ensure(n * sc) || e->s_blob.ensure(n * (4 + 4 * size_t(P.maxb))))
+            return -1;
+        P.s_kind = e->s_kind.p;
+        P.s_start = e->s_start.p;
+        P.s_len = e->s_len.p;
+        P.s_bytes = e->s_bytes.p;
+        P.s_blob = e->s_blob.p;
+    }
     HIPCHK(hipEventRecord(e->ev[2], e->stream));
     summary_size_kernel<<<n, 64, 0, e->stream>>>(P);
     HIPCHK(hipGetLastError());
@@ -521,6 +541,10 @@ int mtr_summarize(mtr_engine* e) {
     HIPCHK(hipStreamSynchronize(e->stream));
     int64_t tot = 0;
     for (uint32_t d = 0; d < n; d++) {
+        if (e->h_size[d] < 0) {
+            set_err("document " + std::to_string(d) + " has more summary chunks than the engine's blob table");
+            return MTR_ERR_CAPACITY;
+        }
         e->h_off[d] = tot;
         tot += e->h_size[d];
     }

@@ -1,11 +1,24 @@
-// summary.hip.h -- Client.summarize on the device (client.ts:966-1000).
+// summary.hip.h -- Client.summarize on the device (client.ts:966-1000) as a gather.
 //
 // SnapshotV1.extractSync/emit (snapshotV1.ts:122-298) and SnapshotLegacy.extractSync/emit
-// (snapshotlegacy.ts:122-255) with the chunk layouts of snapshotChunks.ts:86-149, written as
-// exact JSON.stringify bytes.  One wave per document; a sizing pass and a writing pass share
-// the same code (Writer<false> / Writer<true>).  Output per document:
-//     [u32 nblobs][u32 blob_len x nblobs][blob bytes ...]
+// (snapshotlegacy.ts:122-255) with the chunk layouts of snapshotChunks.ts:86-149, written as exact
+// JSON.stringify bytes.  One wave per document, all lanes working:
+//
+//   size pass  (summary_size_kernel)
+//     A. extract: classify every leaf (skip / coalescable / merge-info), decide for every
+//        coalescable leaf whether it appends to the previous one (canAppend + matchProperties,
+//        textSegment.ts:86-93, properties.ts:71-105) by ballots over 64 leaves with a carried
+//        state, and compact the spec starts into a spec list;
+//     B. one lane per spec: its length in UTF-16 units and its JSON byte size;
+//     C. greedy chunking of the specs into blobs (>= chunk_size chars each) and blob sizes.
+//   host: exclusive scan of the per-document sizes -> output offsets.
+//   write pass (summary_write_kernel)
+//     blob headers/trailers by lane 0, specs by one lane each at scanned offsets, then the
+//     document digest (include/mtr_digest.h) by all lanes.
+//
+// Output per document: [u32 nblobs][u32 blob_len x nblobs][blob bytes ...]
 #pragma once
+#include "../../include/mtr_digest.h"
 #include "apply.hip.h"
 
 namespace mtr {
@@ -27,132 +40,167 @@ struct SParams {
     const uint32_t* val_eq;
     const uint32_t* client_off;
     const uint8_t* client_bytes;
-    int64_t* out_size;        // sizing pass output
-    const int64_t* out_off;   // writing pass input
+    // scratch handed from the size pass to the write pass
+    uint8_t* s_kind;    // [doc][segcap]      leaf kind: 0 skip, 1 coalescable, 2 merge-info (V1)
+    uint32_t* s_start;  // [doc][segcap + 1]  first leaf of every spec (+ sentinel)
+    uint32_t* s_len;    // [doc][segcap]      spec length (UTF-16 units)
+    uint32_t* s_bytes;  // [doc][segcap]      spec JSON bytes
+    int32_t* s_blob;    // [doc][4 + 4 * maxb]: nspec, nblob, totalLength, ok; per blob start, count, length, bytes
+    int32_t maxb;
+    int64_t* out_size;       // size pass output
+    const int64_t* out_off;  // write pass input
     uint8_t* out;
     unsigned long long* out_hash;
 };
 
+// ------------------------------------------------------------------ one lane's JSON writer
 template <bool W>
-struct Writer {
-    uint8_t* p;
-    int64_t n;
-    unsigned long long h;
-    __device__ void put(uint8_t c) {
-        if (W) {
-            p[n] = c;
-            h = (h ^ c) * 1099511628211ull;
-        }
+struct LW {
+    gptr<uint8_t> p;  // document output base (write pass)
+    int64_t n;        // position
+    MTR_DI void put(uint32_t c) {
+        if (W) p[n] = uint8_t(c);
         n++;
     }
-    __device__ void str(const char* s) {
-        while (*s) put(uint8_t(*s++));
+    template <size_t N>
+    MTR_DI void lit(const char (&s)[N]) {
+        if (W) {
+#pragma unroll
+            for (size_t i = 0; i + 1 < N; i++) p[n + int64_t(i)] = uint8_t(s[i]);
+        }
+        n += int64_t(N - 1);
     }
-    __device__ void bytes(const uint8_t* s, uint32_t k) {
-        for (uint32_t i = 0; i < k; i++) put(s[i]);
+    MTR_DI void bytes(gptr<const uint8_t> s, uint32_t k) {
+        if (W)
+            for (uint32_t i = 0; i < k; i++) p[n + i] = s[i];
+        n += k;
     }
-    __device__ void num(int64_t v) {
-        char buf[24];
-        int k = 0;
-        bool neg = v < 0;
+    MTR_DI void num(int64_t v) {
+        const bool neg = v < 0;
         uint64_t u = neg ? uint64_t(-v) : uint64_t(v);
-        do {
-            buf[k++] = char('0' + (u % 10));
-            u /= 10;
-        } while (u);
+        int k = 1;
+        for (uint64_t t = u; t >= 10; t /= 10) k++;
         if (neg) put('-');
-        while (k) put(uint8_t(buf[--k]));
+        if (W)
+            for (int q = k - 1; q >= 0; q--) {
+                p[n + q] = uint8_t('0' + (u % 10));
+                u /= 10;
+            }
+        n += k;
     }
-    __device__ void hex4(uint32_t u) {
-        const char* hx = "0123456789abcdef";
-        put('\\');
-        put('u');
-        put(uint8_t(hx[(u >> 12) & 15]));
-        put(uint8_t(hx[(u >> 8) & 15]));
-        put(uint8_t(hx[(u >> 4) & 15]));
-        put(uint8_t(hx[u & 15]));
+    MTR_DI void hex4(uint32_t u) {
+        if (W) {
+            p[n] = '\\';
+            p[n + 1] = 'u';
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t x = (u >> (12 - 4 * q)) & 15;
+                p[n + 2 + q] = uint8_t(x < 10 ? '0' + x : 'a' + x - 10);
+            }
+        }
+        n += 6;
     }
-    __device__ void utf8(uint32_t cp) {
+    MTR_DI void utf8(uint32_t cp) {
         if (cp < 0x80) {
-            put(uint8_t(cp));
+            put(cp);
         } else if (cp < 0x800) {
-            put(uint8_t(0xC0 | (cp >> 6)));
-            put(uint8_t(0x80 | (cp & 63)));
+            put(0xC0 | (cp >> 6));
+            put(0x80 | (cp & 63));
         } else if (cp < 0x10000) {
-            put(uint8_t(0xE0 | (cp >> 12)));
-            put(uint8_t(0x80 | ((cp >> 6) & 63)));
-            put(uint8_t(0x80 | (cp & 63)));
+            put(0xE0 | (cp >> 12));
+            put(0x80 | ((cp >> 6) & 63));
+            put(0x80 | (cp & 63));
         } else {
-            put(uint8_t(0xF0 | (cp >> 18)));
-            put(uint8_t(0x80 | ((cp >> 12) & 63)));
-            put(uint8_t(0x80 | ((cp >> 6) & 63)));
-            put(uint8_t(0x80 | (cp & 63)));
+            put(0xF0 | (cp >> 18));
+            put(0x80 | ((cp >> 12) & 63));
+            put(0x80 | ((cp >> 6) & 63));
+            put(0x80 | (cp & 63));
         }
     }
-    // JSON string body over a stream of UTF-16 units (ES2019 well-formed JSON.stringify);
-    // `hi` carries a pending high surrogate across pieces of a coalesced segment.
-    __device__ void units(const uint16_t* t, int k, int& hi) {
-        for (int i = 0; i < k; i++) {
-            uint32_t u = t[i];
-            if (hi >= 0) {
-                if (u >= 0xDC00 && u <= 0xDFFF) {
-                    utf8(0x10000 + ((uint32_t(hi) - 0xD800) << 10) + (u - 0xDC00));
-                    hi = -1;
-                    continue;
-                }
-                hex4(uint32_t(hi));
+    // one UTF-16 unit of a JSON string body (ES2019 well-formed JSON.stringify); `hi` carries a
+    // pending high surrogate across units and across the pieces of a coalesced segment
+    MTR_DI void unit(uint32_t u, int& hi) {
+        if (hi >= 0) {
+            if (u >= 0xDC00 && u <= 0xDFFF) {
+                utf8(0x10000 + ((uint32_t(hi) - 0xD800) << 10) + (u - 0xDC00));
                 hi = -1;
+                return;
             }
-            switch (u) {
-                case '"': put('\\'); put('"'); continue;
-                case '\\': put('\\'); put('\\'); continue;
-                case '\b': put('\\'); put('b'); continue;
-                case '\f': put('\\'); put('f'); continue;
-                case '\n': put('\\'); put('n'); continue;
-                case '\r': put('\\'); put('r'); continue;
-                case '\t': put('\\'); put('t'); continue;
-                default: break;
-            }
-            if (u < 0x20) hex4(u);
-            else if (u >= 0xD800 && u <= 0xDBFF) hi = int(u);
-            else if (u >= 0xDC00 && u <= 0xDFFF) hex4(u);
-            else utf8(u);
+            hex4(uint32_t(hi));
+            hi = -1;
         }
+        if (u >= 0x20 && u < 0x80 && u != '"' && u != '\\') {
+            put(u);
+            return;
+        }
+        switch (u) {
+            case '"': put('\\'); put('"'); return;
+            case '\\': put('\\'); put('\\'); return;
+            case '\b': put('\\'); put('b'); return;
+            case '\f': put('\\'); put('f'); return;
+            case '\n': put('\\'); put('n'); return;
+            case '\r': put('\\'); put('r'); return;
+            case '\t': put('\\'); put('t'); return;
+            default: break;
+        }
+        if (u < 0x20) hex4(u);
+        else if (u >= 0xD800 && u <= 0xDBFF) hi = int(u);
+        else if (u >= 0xDC00 && u <= 0xDFFF) hex4(u);
+        else utf8(u);
     }
-    __device__ void flush_hi(int& hi) {
+    MTR_DI void flush_hi(int& hi) {
         if (hi >= 0) hex4(uint32_t(hi));
         hi = -1;
     }
 };
 
-struct DocView {
-    const uint32_t *len, *seq, *rseq, *meta, *text, *props, *rm;
-    const uint16_t* gtext;
-    const uint32_t* gprop;
-    const uint32_t* grm;
+// one document's arrays in HBM
+struct SDoc {
+    gptr<const uint32_t> len, seq, rseq, meta, text, props, rm;
+    gptr<const uint16_t> gtext;
+    gptr<const uint32_t> gprop, grm;
+    gptr<uint8_t> kind;
+    gptr<uint32_t> start, slen, sbytes;
+    gptr<int32_t> blob;
     int S, minseq, curseq, collab, local, newlen;
 };
 
-__device__ inline bool removed(const DocView& D, int k) { return int(D.rseq[k]) != RNONE; }
-
-__device__ inline bool sv_can_append(const DocView& D, int acc_len, uint16_t acc_last, bool acc_marker, int k) {
-    if (acc_marker || (D.meta[k] & M_MARKER)) return false;
-    if (acc_len > 0 && acc_last == u'\n') return false;
-    return acc_len <= kGranularity || int(D.len[k]) <= kGranularity;
+MTR_DI SDoc sdoc(const SParams& P, uint32_t d, const DocHdr& h) {
+    SDoc D;
+    const gptr<const uint32_t> g = gp(P.seg) + size_t(d) * NF * P.segcap;
+    D.len = g + F_LEN * P.segcap;
+    D.seq = g + F_SEQ * P.segcap;
+    D.rseq = g + F_RSEQ * P.segcap;
+    D.meta = g + F_META * P.segcap;
+    D.text = g + F_TEXT * P.segcap;
+    D.props = g + F_PROPS * P.segcap;
+    D.rm = g + F_RM * P.segcap;
+    D.gtext = gp(P.text) + size_t(d) * P.tcap;
+    D.gprop = gp(P.prop) + size_t(d) * P.pcap;
+    D.grm = gp(P.rm) + size_t(d) * P.rcap;
+    D.kind = gp(P.s_kind) + size_t(d) * P.segcap;
+    D.start = gp(P.s_start) + size_t(d) * (P.segcap + 1);
+    D.slen = gp(P.s_len) + size_t(d) * P.segcap;
+    D.sbytes = gp(P.s_bytes) + size_t(d) * P.segcap;
+    D.blob = gp(P.s_blob) + size_t(d) * (4 + 4 * P.maxb);
+    D.S = h.nseg;
+    D.minseq = h.minseq;
+    D.curseq = h.curseq;
+    D.collab = h.collab;
+    D.local = h.collab ? h.local : int(CL_LOCAL);
+    D.newlen = P.new_length_calc;
+    return D;
 }
 
 // visible length in the (minSeq, NonCollabClient) view for SnapshotLegacy's mapRange
-__device__ int legacy_vis(const DocView& D, int k) {
-    int len = int(D.len[k]);
-    int rs = int(D.rseq[k]);
-    bool rem = rs != RNONE;
+MTR_DI int legacy_vis(const SDoc& D, int len, int rs, uint32_t m, int sq) {
+    const bool rem = rs != RNONE;
     if (!D.collab || uint32_t(D.local) == CL_NONCOLLAB) {
         if (rem) return D.newlen ? 0 : (rs > D.minseq ? 0 : -1);
         return len;
     }
-    int ref = D.minseq;
-    uint32_t cl = D.meta[k] & M_CLIENT_MASK;
-    int sq = int(D.seq[k]);
+    const int ref = D.minseq;
+    const uint32_t cl = m & M_CLIENT_MASK;
     if (D.newlen) {
         if (rem) {
             if (rs <= D.minseq) return -1;
@@ -166,177 +214,134 @@ __device__ int legacy_vis(const DocView& D, int k) {
     return 0;
 }
 
-// kind of leaf k for extraction: 0 = skip, 1 = coalescable member, 2 = merge-info (V1 only)
-__device__ int leaf_kind(const DocView& D, int k, int v1) {
-    if (v1) {
-        if (removed(D, k) && int(D.rseq[k]) <= D.minseq) return 0;
-        if (int(D.seq[k]) <= D.minseq && !removed(D, k)) return 1;
+// kind of a leaf for extractSync: 0 = skip, 1 = coalescable, 2 = with merge info (V1 only)
+MTR_DI int leaf_kind(const SDoc& D, int v1, int len, int rs, uint32_t m, int sq) {
+    const bool rem = rs != RNONE;
+    if (v1) {  // snapshotV1.ts:180-298
+        if (rem && rs <= D.minseq) return 0;
+        if (sq <= D.minseq && !rem) return 1;
         return 2;
     }
-    int l = legacy_vis(D, k);
-    if (l <= 0) return 0;
-    if (int(D.seq[k]) <= D.minseq && (!removed(D, k) || int(D.rseq[k]) > D.minseq)) return 1;
+    if (legacy_vis(D, len, rs, m, sq) <= 0) return 0;  // snapshotlegacy.ts:184-255
+    if (sq <= D.minseq && (!rem || rs > D.minseq)) return 1;
     return 0;
 }
 
-struct Spec {
-    int start, end;  // leaves [start, end]; end == start for merge-info specs
-    int kind;        // 1 group, 2 merge-info
-    int length;
-};
-
-// next spec starting at leaf *k (extractSync coalescing loops)
-__device__ bool next_spec(const DocView& D, const SParams& P, int v1, int* k, Spec* sp) {
-    int start = -1, end = -1, acc = 0;
-    uint16_t last = 0;
-    bool accm = false;
-    uint32_t pr = NONE32;
-    while (*k < D.S) {
-        const int i = *k;
-        const int kind = leaf_kind(D, i, v1);
-        if (kind == 0) {
-            (*k)++;
-            continue;
-        }
-        if (kind == 1) {
-            if (start < 0) {
-                start = end = i;
-                acc = int(D.len[i]);
-                accm = (D.meta[i] & M_MARKER) != 0;
-                last = (!accm && acc > 0) ? D.gtext[D.text[i] + acc - 1] : 0;
-                pr = D.props[i];
-                (*k)++;
-                continue;
-            }
-            if (sv_can_append(D, acc, last, accm, i) && props_match(D.gprop, P.val_eq, pr, D.props[i])) {
-                end = i;
-                acc += int(D.len[i]);
-                last = D.gtext[D.text[i] + D.len[i] - 1];
-                (*k)++;
-                continue;
-            }
-            break;
-        }
-        // merge-info
-        if (start >= 0) break;
-        sp->start = sp->end = i;
-        sp->kind = 2;
-        sp->length = int(D.len[i]);
-        (*k)++;
-        return true;
-    }
-    if (start < 0) return false;
-    sp->start = start;
-    sp->end = end;
-    sp->kind = 1;
-    sp->length = acc;
-    return true;
-}
-
 template <bool W>
-__device__ void w_client(Writer<W>& w, const SParams& P, const mtr_doc_desc& dd, uint32_t enc) {
-    int id = dec_client(enc);
+MTR_DI void w_client(LW<W>& w, const SParams& P, const mtr_doc_desc& dd, uint32_t enc) {
+    const int id = dec_client(enc);
     w.put('"');
     if (id < 0 || uint32_t(id) >= dd.n_clients) {
-        w.str("original");
+        w.lit("original");
     } else {
-        uint32_t ix = dd.client_base + uint32_t(id);
-        w.bytes(P.client_bytes + P.client_off[ix], P.client_off[ix + 1] - P.client_off[ix]);
+        const uint32_t ix = dd.client_base + uint32_t(id);
+        const uint32_t a = gp(P.client_off)[ix], b = gp(P.client_off)[ix + 1];
+        w.bytes(gp(P.client_bytes) + a, b - a);
     }
     w.put('"');
 }
 
 template <bool W>
-__device__ void w_props(Writer<W>& w, const DocView& D, const SParams& P, uint32_t pr) {
+MTR_DI void w_props(LW<W>& w, const SDoc& D, const SParams& P, uint32_t pr) {
     w.put('{');
-    uint32_t n = D.gprop[pr];
+    const uint32_t n = D.gprop[pr];
     for (uint32_t i = 0; i < n; i++) {
         if (i) w.put(',');
-        uint32_t k = D.gprop[pr + 1 + 2 * i], v = D.gprop[pr + 2 + 2 * i];
+        const uint32_t k = D.gprop[pr + 1 + 2 * i], v = D.gprop[pr + 2 + 2 * i];
+        const uint32_t ka = gp(P.key_off)[k], kb = gp(P.key_off)[k + 1];
+        const uint32_t va = gp(P.val_off)[v], vb = gp(P.val_off)[v + 1];
         w.put('"');
-        w.bytes(P.key_bytes + P.key_off[k], P.key_off[k + 1] - P.key_off[k]);
+        w.bytes(gp(P.key_bytes) + ka, kb - ka);
         w.put('"');
         w.put(':');
-        w.bytes(P.val_bytes + P.val_off[v], P.val_off[v + 1] - P.val_off[v]);
+        w.bytes(gp(P.val_bytes) + va, vb - va);
     }
     w.put('}');
 }
 
-// toJSONObject of a (possibly coalesced) segment: textSegment.ts:73-77, mergeTreeNodes.ts:577-581
+// the text of one leaf, 8 units per round of loads
 template <bool W>
-__device__ void w_segjson(Writer<W>& w, const DocView& D, const SParams& P, const Spec& s, int v1) {
-    const int f = s.start;
-    const uint32_t m = D.meta[f];
-    const uint32_t pr = D.props[f];
+MTR_DI void w_units(LW<W>& w, const SDoc& D, uint32_t t, int n, int& hi) {
+    for (int u0 = 0; u0 < n; u0 += 8) {
+        uint32_t b[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) b[q] = u0 + q < n ? uint32_t(D.gtext[t + uint32_t(u0 + q)]) : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (u0 + q < n) w.unit(b[q], hi);
+    }
+}
+
+// toJSONObject of the spec [s, e): textSegment.ts:73-77, mergeTreeNodes.ts:577-581; the text of
+// a coalesced group is the concatenation of its kind-1 leaves
+template <bool W>
+MTR_DI void w_segjson(LW<W>& w, const SDoc& D, const SParams& P, int s, int e) {
+    const uint32_t m = D.meta[s];
+    const uint32_t pr = D.props[s];
     if (m & M_MARKER) {
-        w.str("{\"marker\":{");
+        w.lit("{\"marker\":{");
         if (!(m & M_NOREF)) {
-            w.str("\"refType\":");
-            w.num(int64_t(D.text[f]));
+            w.lit("\"refType\":");
+            w.num(int64_t(D.text[s]));
         }
         w.put('}');
         if (pr != NONE32) {
-            w.str(",\"props\":");
+            w.lit(",\"props\":");
             w_props(w, D, P, pr);
         }
         w.put('}');
         return;
     }
-    if (pr != NONE32) w.str("{\"text\":");
+    if (pr != NONE32) w.lit("{\"text\":");
     w.put('"');
     int hi = -1;
-    if (s.kind == 2) {
-        w.units(D.gtext + D.text[f], int(D.len[f]), hi);
-    } else {
-        for (int k = s.start; k <= s.end; k++)
-            if (leaf_kind(D, k, v1) == 1) w.units(D.gtext + D.text[k], int(D.len[k]), hi);
-    }
+    for (int k = s; k < e; k++)
+        if (k == s || D.kind[k] == 1) w_units(w, D, D.text[k], int(D.len[k]), hi);
     w.flush_hi(hi);
     w.put('"');
     if (pr != NONE32) {
-        w.str(",\"props\":");
+        w.lit(",\"props\":");
         w_props(w, D, P, pr);
         w.put('}');
     }
 }
 
-// IJSONSegmentWithMergeInfo (snapshotChunks.ts:64-75) in SnapshotV1 key order (snapshotV1.ts:251-276)
+// one spec: a coalesced group, or IJSONSegmentWithMergeInfo (snapshotChunks.ts:64-75) in
+// SnapshotV1 key order (snapshotV1.ts:251-276)
 template <bool W>
-__device__ void w_spec(Writer<W>& w, const DocView& D, const SParams& P, const mtr_doc_desc& dd, const Spec& s,
-                       int v1) {
-    if (s.kind == 1) {
-        w_segjson(w, D, P, s, v1);
+MTR_DI void w_spec(LW<W>& w, const SDoc& D, const SParams& P, const mtr_doc_desc& dd, int s, int e) {
+    if (D.kind[s] != 2) {
+        w_segjson(w, D, P, s, e);
         return;
     }
-    const int k = s.start;
-    w.str("{\"json\":");
-    w_segjson(w, D, P, s, v1);
-    if (int(D.seq[k]) > D.minseq) {
-        w.str(",\"seq\":");
-        w.num(int(D.seq[k]));
-        w.str(",\"client\":");
-        w_client(w, P, dd, D.meta[k] & M_CLIENT_MASK);
+    w.lit("{\"json\":");
+    w_segjson(w, D, P, s, s + 1);
+    const int sq = int(D.seq[s]);
+    const uint32_t m = D.meta[s];
+    if (sq > D.minseq) {
+        w.lit(",\"seq\":");
+        w.num(sq);
+        w.lit(",\"client\":");
+        w_client(w, P, dd, m & M_CLIENT_MASK);
     }
-    if (removed(D, k)) {
-        w.str(",\"removedSeq\":");
-        w.num(int(D.rseq[k]));
-        const uint32_t first = (D.meta[k] >> M_FREM_SHIFT) & 0xffu;
-        w.str(",\"removedClient\":");
+    const int rs = int(D.rseq[s]);
+    if (rs != RNONE) {
+        w.lit(",\"removedSeq\":");
+        w.num(rs);
+        const uint32_t first = (m >> M_FREM_SHIFT) & 0xffu;
+        w.lit(",\"removedClient\":");
         w_client(w, P, dd, first);
-        w.str(",\"removedClientIds\":[");
+        w.lit(",\"removedClientIds\":[");
         w_client(w, P, dd, first);
-        if (D.meta[k] & M_OVERLAP) {
-            // cons list holds later removers newest-first; emit oldest-first
-            uint32_t cells[64];
+        if (m & M_OVERLAP) {
+            // the cons list holds later removers newest-first: emit oldest-first
             int nc = 0;
-            uint32_t c = D.rm[k];
-            while (c != 0xffffffu && nc < 64) {
-                cells[nc++] = c;
-                c = D.grm[c] & 0xffffffu;
-            }
+            for (uint32_t c = D.rm[s]; c != 0xffffffu; c = D.grm[c] & 0xffffffu) nc++;
             for (int q = nc - 1; q >= 0; q--) {
+                uint32_t c = D.rm[s];
+                for (int t = 0; t < q; t++) c = D.grm[c] & 0xffffffu;
                 w.put(',');
-                w_client(w, P, dd, D.grm[cells[q]] >> 24);
+                w_client(w, P, dd, D.grm[c] >> 24);
             }
         }
         w.put(']');
@@ -344,182 +349,341 @@ __device__ void w_spec(Writer<W>& w, const DocView& D, const SParams& P, const m
     w.put('}');
 }
 
+// blob wrappers.  V1: snapshotV1.ts:122-178 + serializeAsMaxSupportedVersion; legacy:
+// snapshotlegacy.ts:122-182 + serializeAsMinSupportedVersion / buildHeaderMetadataForLegacyChunk.
 template <bool W>
-__device__ void w_blob_len(Writer<W>& w, int64_t at, uint32_t len) {
-    if (W) {
-        w.h = (w.h ^ uint64_t(len)) * 1099511628211ull;  // blob boundary in the hash
-        w.p[at + 0] = uint8_t(len);
-        w.p[at + 1] = uint8_t(len >> 8);
-        w.p[at + 2] = uint8_t(len >> 16);
-        w.p[at + 3] = uint8_t(len >> 24);
+MTR_DI void w_blob_head(LW<W>& w, const SDoc& D, int v1, int start, int count, int length, int total_len, int nspec) {
+    if (v1) {
+        w.lit("{\"version\":\"1\",\"segmentCount\":");
+        w.num(count);
+        w.lit(",\"length\":");
+        w.num(length);
+        w.lit(",\"segments\":[");
+    } else {
+        w.lit("{\"chunkStartSegmentIndex\":");
+        w.num(start);
+        w.lit(",\"chunkSegmentCount\":");
+        w.num(count);
+        w.lit(",\"chunkLengthChars\":");
+        w.num(length);
+        w.lit(",\"totalLengthChars\":");
+        w.num(total_len);
+        w.lit(",\"totalSegmentCount\":");
+        w.num(nspec);
+        w.lit(",\"chunkSequenceNumber\":");
+        w.num(D.minseq);
+        w.lit(",\"segmentTexts\":[");
+    }
+}
+template <bool W>
+MTR_DI void w_blob_tail(LW<W>& w, const SDoc& D, int v1, int c, int nblob, int start, int first_len, int total_len,
+                        int nspec) {
+    if (v1) {
+        w.lit("],\"startIndex\":");
+        w.num(start);
+        if (c == 0) {
+            w.lit(",\"headerMetadata\":{\"minSequenceNumber\":");
+            w.num(D.minseq);
+            w.lit(",\"sequenceNumber\":");
+            w.num(D.curseq);
+            w.lit(",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+            for (int q = 1; q < nblob; q++) {
+                w.lit(",{\"id\":\"body_");
+                w.num(q - 1);
+                w.lit("\"}");
+            }
+            w.lit("],\"totalLength\":");
+            w.num(total_len);
+            w.lit(",\"totalSegmentCount\":");
+            w.num(nspec);
+            w.put('}');
+        }
+        w.put('}');
+    } else {
+        w.put(']');
+        if (c == 0) {
+            w.lit(",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+            if (first_len < total_len) w.lit(",{\"id\":\"body\"}");
+            w.lit("],\"sequenceNumber\":");
+            w.num(D.minseq);
+            w.lit(",\"totalLength\":");
+            w.num(total_len);
+            w.lit(",\"totalSegmentCount\":");
+            w.num(nspec);
+            w.put('}');
+        }
+        w.put('}');
     }
 }
 
-template <bool W>
-__device__ void summarize_doc(const SParams& P, uint32_t d, Writer<W>& w) {
-    const DocHdr h = P.hdr[d];
-    const mtr_doc_desc dd = P.docs[d];
-    DocView D;
-    const uint32_t* g = P.seg + size_t(d) * NF * P.segcap;
-    D.len = g + F_LEN * P.segcap;
-    D.seq = g + F_SEQ * P.segcap;
-    D.rseq = g + F_RSEQ * P.segcap;
-    D.meta = g + F_META * P.segcap;
-    D.text = g + F_TEXT * P.segcap;
-    D.props = g + F_PROPS * P.segcap;
-    D.rm = g + F_RM * P.segcap;
-    D.gtext = P.text + size_t(d) * P.tcap;
-    D.gprop = P.prop + size_t(d) * P.pcap;
-    D.grm = P.rm + size_t(d) * P.rcap;
-    D.S = h.nseg;
-    D.minseq = h.minseq;
-    D.curseq = h.curseq;
-    D.collab = h.collab;
-    D.local = h.collab ? h.local : int(CL_LOCAL);
-    D.newlen = P.new_length_calc;
+// ------------------------------------------------------------------ size pass
+MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
+    const DocHdr h = uni_struct(ld_struct<DocHdr>(gp(P.hdr) + d));
+    const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
+    SDoc D = sdoc(P, d, h);
     const int v1 = P.snapshot_v1;
-    const int chunk = P.chunk_size;
+    const int S = D.S;
+    const int ln = lane_id();
+    const gptr<const uint32_t> veq = gp(P.val_eq);
 
-    // pass A: totals and number of chunks
-    int64_t totalLen = 0, totalCount = 0, nChunks = 0;
-    {
-        int k = 0;
-        Spec sp;
-        int64_t clen = 0, ccnt = 0;
-        bool open = false;
-        while (next_spec(D, P, v1, &k, &sp)) {
-            if (!open) { open = true; clen = 0; ccnt = 0; nChunks++; }
-            clen += sp.length;
-            ccnt++;
-            totalLen += sp.length;
-            totalCount++;
-            if (clen >= chunk) open = false;
+    // A. extract: kinds, appends and spec starts (carry = the last non-skipped leaf so far)
+    bool c_valid = false, c_k1 = false, c_mk = false, c_nl = false;
+    uint32_t c_pr = NONE32;
+    int c_acc = 0;  // chars of the open group (TextSegmentGranularity rule)
+    int nspec = 0;
+    for (int base = 0; base < S; base += 64) {
+        const int i = base + ln;
+        const bool in = i < S;
+        int len = 0, rs = RNONE, sq = 0;
+        uint32_t m = 0, pr = NONE32, tx = 0;
+        if (in) {
+            len = int(D.len[i]);
+            rs = int(D.rseq[i]);
+            sq = int(D.seq[i]);
+            m = D.meta[i];
+            pr = D.props[i];
+            tx = D.text[i];
         }
-        if (nChunks == 0) nChunks = 1;
-    }
-    int nblobs;
-    if (v1) nblobs = int(nChunks);
-    else nblobs = 1;  // legacy: header + optional body, decided below
-    // legacy: chunk1 = first chunk (length >= chunk); body = everything else
-    int64_t c1cnt = 0, c1len = 0;
-    if (!v1) {
-        int k = 0;
-        Spec sp;
-        while (c1len < chunk && next_spec(D, P, v1, &k, &sp)) {
-            c1len += sp.length;
-            c1cnt++;
+        const int kd = in ? leaf_kind(D, v1, len, rs, m, sq) : 0;
+        if (in) D.kind[i] = uint8_t(kd);
+        const bool mk = (m & M_MARKER) != 0;
+        bool nl = false;  // last unit is '\n'
+        if (kd == 1 && !mk && len > 0) nl = (m & M_NLQ) ? D.gtext[tx + uint32_t(len) - 1] == u'\n' : (m & M_NL) != 0;
+        const uint64_t ns = __ballot(kd != 0);
+        const uint64_t below = ns & lanes_below();
+        const int p = below ? last_lane(below) : -1;
+        const int ps = p < 0 ? 0 : p;
+        bool p_k1 = __shfl(int(kd == 1), ps) != 0, p_mk = __shfl(int(mk), ps) != 0, p_nl = __shfl(int(nl), ps) != 0;
+        uint32_t p_pr = uint32_t(__shfl(int(pr), ps));
+        if (p < 0) {
+            p_k1 = c_valid && c_k1;
+            p_mk = c_mk;
+            p_nl = c_nl;
+            p_pr = c_pr;
         }
-        if (c1cnt < totalCount) nblobs = 2;
-    }
-    const int64_t table = 4 + 4 * int64_t(nblobs);
-    const int64_t base = w.n;
-    if (W) w_blob_len(w, base, uint32_t(nblobs));  // hashes nblobs
-    w.n += table;
-    int k = 0;
-    Spec sp;
-    if (v1) {
-        // emit, snapshotV1.ts:122-178
-        int64_t specsBefore = 0;
-        for (int c = 0; c < nblobs; c++) {
-            const int64_t b0 = w.n;
-            // look-ahead: this chunk's count and length
-            int kk = k;
-            int64_t clen = 0, ccnt = 0;
-            Spec t;
-            while (clen < chunk && next_spec(D, P, v1, &kk, &t)) {
-                clen += t.length;
-                ccnt++;
-            }
-            w.str("{\"version\":\"1\",\"segmentCount\":");
-            w.num(ccnt);
-            w.str(",\"length\":");
-            w.num(clen);
-            w.str(",\"segments\":[");
-            int64_t emitted = 0;
-            while (emitted < ccnt && next_spec(D, P, v1, &k, &sp)) {
-                if (emitted) w.put(',');
-                w_spec(w, D, P, dd, sp, v1);
-                emitted++;
-            }
-            w.str("],\"startIndex\":");
-            w.num(specsBefore);
-            specsBefore += ccnt;
-            if (c == 0) {
-                w.str(",\"headerMetadata\":{\"minSequenceNumber\":");
-                w.num(D.minseq);
-                w.str(",\"sequenceNumber\":");
-                w.num(D.curseq);
-                w.str(",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
-                for (int q = 1; q < nblobs; q++) {
-                    w.str(",{\"id\":\"body_");
-                    w.num(q - 1);
-                    w.str("\"}");
+        bool link = kd == 1 && p_k1 && !p_mk && !mk && !p_nl;
+        if (link && pr != p_pr) link = props_match(D.gprop, veq, p_pr, pr);
+        if (__ballot(link && len > kGranularity)) {  // accumulated-length clause, in order
+            uint64_t lm = __ballot(link);
+            int acc = c_valid && c_k1 ? c_acc : 0;
+            for (uint64_t t = ns; t; t &= t - 1) {
+                const int l = first_lane(t);
+                const int lk = rdlane(len, l), kk = rdlane(kd, l);
+                if (kk != 1) {
+                    acc = 0;
+                } else if ((lm >> l) & 1) {
+                    if (acc > kGranularity && lk > kGranularity) {
+                        lm &= ~(uint64_t(1) << l);
+                        acc = lk;
+                    } else {
+                        acc += lk;
+                    }
+                } else {
+                    acc = lk;
                 }
-                w.str("],\"totalLength\":");
-                w.num(totalLen);
-                w.str(",\"totalSegmentCount\":");
-                w.num(totalCount);
-                w.put('}');
             }
-            w.put('}');
-            w_blob_len(w, base + 4 + 4 * c, uint32_t(w.n - b0));
+            link = (lm >> ln) & 1;
         }
-    } else {
-        // emit, snapshotlegacy.ts:122-182 + serializeAsMinSupportedVersion / buildHeaderMetadataForLegacyChunk
-        for (int c = 0; c < nblobs; c++) {
-            const int64_t b0 = w.n;
-            const int64_t cstart = c == 0 ? 0 : c1cnt;
-            const int64_t ccnt = c == 0 ? c1cnt : totalCount - c1cnt;
-            const int64_t clen = c == 0 ? c1len : totalLen - c1len;
-            w.str("{\"chunkStartSegmentIndex\":");
-            w.num(cstart);
-            w.str(",\"chunkSegmentCount\":");
-            w.num(ccnt);
-            w.str(",\"chunkLengthChars\":");
-            w.num(clen);
-            w.str(",\"totalLengthChars\":");
-            w.num(totalLen);
-            w.str(",\"totalSegmentCount\":");
-            w.num(totalCount);
-            w.str(",\"chunkSequenceNumber\":");
-            w.num(D.minseq);
-            w.str(",\"segmentTexts\":[");
-            for (int64_t e = 0; e < ccnt && next_spec(D, P, v1, &k, &sp); e++) {
-                if (e) w.put(',');
-                w_spec(w, D, P, dd, sp, v1);
+        const bool st = kd == 2 || (kd == 1 && !link);
+        const uint64_t sm = __ballot(st);
+        if (st) D.start[nspec + __popcll(sm & lanes_below())] = uint32_t(i);
+        nspec += __popcll(sm);
+        if (ns) {  // carry: the last non-skipped leaf of this round
+            const int q = last_lane(ns);
+            const int incl = wave_incl_scan(kd != 0 ? len : 0);
+            const uint64_t sq_m = sm & ((uint64_t(2) << q) - 1);
+            const bool k1 = rdlane(int(kd == 1), q) != 0;
+            int acc = 0;
+            if (k1) {
+                if (sq_m) {
+                    const int hs = last_lane(sq_m);
+                    acc = rdlane(incl, q) - rdlane(incl, hs) + rdlane(len, hs);
+                } else {
+                    acc = c_acc + rdlane(incl, q);
+                }
             }
-            w.put(']');
-            if (c == 0) {
-                w.str(",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}");
-                if (c1len < totalLen) w.str(",{\"id\":\"body\"}");
-                w.str("],\"sequenceNumber\":");
-                w.num(D.minseq);
-                w.str(",\"totalLength\":");
-                w.num(totalLen);
-                w.str(",\"totalSegmentCount\":");
-                w.num(totalCount);
-                w.put('}');
-            }
-            w.put('}');
-            w_blob_len(w, base + 4 + 4 * c, uint32_t(w.n - b0));
+            c_valid = true;
+            c_k1 = k1;
+            c_mk = rdlane(int(mk), q) != 0;
+            c_nl = rdlane(int(nl), q) != 0;
+            c_pr = rdlane(pr, q);
+            c_acc = acc;
         }
     }
+    if (ln == 0) D.start[nspec] = uint32_t(S);
+    wsync();
+
+    // B. one lane per spec: length and JSON bytes
+    for (int g0 = 0; g0 < nspec; g0 += 64) {
+        const int g = g0 + ln;
+        if (g < nspec) {
+            const int s = int(D.start[g]), e = int(D.start[g + 1]);
+            int length = 0;
+            if (D.kind[s] == 2) {
+                length = int(D.len[s]);
+            } else {
+                for (int k = s; k < e; k++)
+                    if (k == s || D.kind[k] == 1) length += int(D.len[k]);
+            }
+            LW<false> w{(gptr<uint8_t>)nullptr, 0};
+            w_spec(w, D, P, dd, s, e);
+            D.slen[g] = uint32_t(length);
+            D.sbytes[g] = uint32_t(w.n);
+        }
+    }
+    wsync();
+
+    // C. greedy chunking (snapshotV1.ts:70-116 getSeqLengthSegs; legacy: header chunk, then body)
+    int total_len = 0;
+    for (int g0 = 0; g0 < nspec; g0 += 64) {
+        const int g = g0 + ln;
+        total_len += rdlane(wave_incl_scan(g < nspec ? int(D.slen[min(g, nspec - 1)]) : 0), 63);
+    }
+    int nblob = 0, b_start = 0, b_cnt = 0, b_len = 0;
+    int64_t b_bytes = 0, doc_bytes = 0;
+    int first_len = 0;
+    bool ok = true;
+    auto close_blob = [&]() {
+        if (nblob >= P.maxb) {
+            ok = false;
+            return;
+        }
+        if (nblob == 0) first_len = b_len;
+        if (ln == 0) {
+            D.blob[4 + 4 * nblob + 0] = b_start;
+            D.blob[4 + 4 * nblob + 1] = b_cnt;
+            D.blob[4 + 4 * nblob + 2] = b_len;
+        }
+        nblob++;
+        b_start += b_cnt;
+        b_cnt = 0;
+        b_len = 0;
+        b_bytes = 0;
+    };
+    for (int g0 = 0; g0 < nspec; g0 += 64) {
+        const int g = g0 + ln;
+        const uint32_t lv = g < nspec ? D.slen[g] : 0u;
+        const int nk = min(64, nspec - g0);
+        for (int t = 0; t < nk; t++) {
+            b_len += int(rdlane(lv, t));
+            b_cnt++;
+            const bool closes = v1 ? b_len >= P.chunk_size : (nblob == 0 && b_len >= P.chunk_size);
+            if (closes && (v1 || g0 + t + 1 < nspec)) close_blob();
+        }
+    }
+    if (b_cnt > 0 || nblob == 0) close_blob();
+    // blob bytes: wrappers (lane 0) + specs + commas
+    for (int c = 0; c < nblob && ok; c++) {
+        const int bs = uni(D.blob[4 + 4 * c + 0]), bc = uni(D.blob[4 + 4 * c + 1]), bl = uni(D.blob[4 + 4 * c + 2]);
+        int64_t sb = 0;
+        for (int g0 = bs; g0 < bs + bc; g0 += 64) {
+            const int g = g0 + ln;
+            const int x = g < bs + bc ? int(D.sbytes[g]) : 0;
+            sb += rdlane(wave_incl_scan(x), 63);
+        }
+        LW<false> w{(gptr<uint8_t>)nullptr, 0};
+        w_blob_head(w, D, v1, bs, bc, bl, total_len, nspec);
+        w_blob_tail(w, D, v1, c, nblob, bs, first_len, total_len, nspec);
+        const int64_t bytes = w.n + sb + (bc > 0 ? bc - 1 : 0);
+        if (ln == 0) D.blob[4 + 4 * c + 3] = int32_t(bytes);
+        doc_bytes += bytes;
+    }
+    if (ln == 0) {
+        D.blob[0] = nspec;
+        D.blob[1] = nblob;
+        D.blob[2] = total_len;
+        D.blob[3] = ok ? 1 : 0;
+        P.out_size[d] = ok ? 4 + 4 * int64_t(nblob) + doc_bytes : -1;
+    }
+}
+
+// ------------------------------------------------------------------ write pass
+MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
+    const DocHdr h = uni_struct(ld_struct<DocHdr>(gp(P.hdr) + d));
+    const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
+    SDoc D = sdoc(P, d, h);
+    const int v1 = P.snapshot_v1;
+    const int ln = lane_id();
+    const int nspec = uni(D.blob[0]), nblob = uni(D.blob[1]), total_len = uni(D.blob[2]);
+    if (!uni(D.blob[3])) return;
+    const int first_len = uni(D.blob[4 + 2]);
+    const int64_t off0 = gp(P.out_off)[d];
+    const gptr<uint8_t> base = gp(P.out) + uni_struct(off0);
+    if (ln == 0) {
+        base[0] = uint8_t(nblob);
+        base[1] = uint8_t(nblob >> 8);
+        base[2] = uint8_t(nblob >> 16);
+        base[3] = uint8_t(nblob >> 24);
+    }
+    int64_t pos = 4 + 4 * int64_t(nblob);
+    uint64_t hsh = mtr_dg_begin(uint64_t(nblob));
+    for (int c = 0; c < nblob; c++) {
+        const int bs = uni(D.blob[4 + 4 * c + 0]), bc = uni(D.blob[4 + 4 * c + 1]), bl = uni(D.blob[4 + 4 * c + 2]);
+        const int64_t b0 = pos;
+        {
+            LW<true> w{base, pos};
+            if (ln == 0) w_blob_head(w, D, v1, bs, bc, bl, total_len, nspec);
+            pos = uni_struct(w.n);
+        }
+        for (int g0 = bs; g0 < bs + bc; g0 += 64) {
+            const int g = g0 + ln;
+            const bool act = g < bs + bc;
+            const int x = act ? int(D.sbytes[g]) + (g > bs ? 1 : 0) : 0;
+            const int incl = wave_incl_scan(x);
+            if (act) {
+                LW<true> w{base, pos + incl - x};
+                if (g > bs) w.put(',');
+                const int s = int(D.start[g]), e = int(D.start[g + 1]);
+                w_spec(w, D, P, dd, s, e);
+            }
+            pos += rdlane(incl, 63);
+        }
+        {
+            LW<true> w{base, pos};
+            if (ln == 0) w_blob_tail(w, D, v1, c, nblob, bs, first_len, total_len, nspec);
+            pos = uni_struct(w.n);
+        }
+        const int64_t blen = pos - b0;
+        if (ln == 0) {
+            base[4 + 4 * c + 0] = uint8_t(blen);
+            base[4 + 4 * c + 1] = uint8_t(blen >> 8);
+            base[4 + 4 * c + 2] = uint8_t(blen >> 16);
+            base[4 + 4 * c + 3] = uint8_t(blen >> 24);
+        }
+        wsync();
+        // digest of the blob: one 8-byte word per lane per round
+        uint64_t sum = 0;
+        const int64_t nw = (blen + 7) / 8;
+        for (int64_t j0 = 0; j0 < nw; j0 += 64) {
+            const int64_t j = j0 + ln;
+            if (j < nw) {
+                uint64_t wv = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (8 * j + q < blen) wv |= uint64_t(base[b0 + 8 * j + q]) << (8 * q);
+                sum += mtr_dg_word(wv, uint64_t(j));
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t lo = uint32_t(sum), hi = uint32_t(sum >> 32);
+            sum += uint64_t(uint32_t(__shfl_xor(int(lo), o))) | (uint64_t(uint32_t(__shfl_xor(int(hi), o))) << 32);
+        }
+        hsh = mtr_dg_next(hsh, mtr_dg_blob(uni_struct(sum), uint64_t(blen)));
+    }
+    if (ln == 0) P.out_hash[d] = hsh;
 }
 
 __global__ void __launch_bounds__(64) summary_size_kernel(SParams P) {
     const uint32_t d = blockIdx.x;
-    if (d >= P.n_docs || threadIdx.x != 0) return;
-    Writer<false> w{nullptr, 0, 0};
-    summarize_doc<false>(P, d, w);
-    P.out_size[d] = w.n;
+    if (d >= P.n_docs) return;
+    summary_size_doc(P, d);
 }
 
 __global__ void __launch_bounds__(64) summary_write_kernel(SParams P) {
     const uint32_t d = blockIdx.x;
-    if (d >= P.n_docs || threadIdx.x != 0) return;
-    Writer<true> w{P.out + P.out_off[d], 0, 14695981039346656037ull};
-    summarize_doc<true>(P, d, w);
-    P.out_hash[d] = w.h;
+    if (d >= P.n_docs) return;
+    summary_write_doc(P, d);
 }
 
 }  // namespace mtr

@@ -15,6 +15,7 @@
 //    change the observer's text, segment boundaries or summary bytes.
 #include "mtr_oracle.h"
 #include "../include/mtr_synth.h"
+#include "../include/mtr_digest.h"
 
 #include <algorithm>
 #include <climits>
@@ -1279,16 +1280,11 @@ int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_ind
 }
 
 
-// FNV-1a 64 over the summary: nblobs, then per blob its bytes followed by its length
-// (the same digest the engine's summary_write_kernel computes).
+// Summary digest of include/mtr_digest.h over nblobs and every blob (the same value the engine's
+// summary_write_kernel computes).
 static uint64_t summary_hash(const std::vector<std::string>& blobs) {
-    const uint64_t P = 1099511628211ull;
-    uint64_t h = 14695981039346656037ull;
-    h = (h ^ uint64_t(blobs.size())) * P;
-    for (auto& b : blobs) {
-        for (unsigned char c : b) h = (h ^ c) * P;
-        h = (h ^ uint64_t(b.size())) * P;
-    }
+    uint64_t h = mtr_dg_begin(uint64_t(blobs.size()));
+    for (auto& b : blobs) h = mtr_dg_next(h, mtr_dg_blob_bytes((const uint8_t*)b.data(), uint64_t(b.size())));
     return h;
 }
 

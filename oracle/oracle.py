@@ -118,16 +118,23 @@ def replay_batch(batch, lo, hi, threads, opts=None):
     return secs, hashes, status
 
 
-def summary_digest(blobs):
-    """Python restatement of the summary digest (FNV-1a 64)."""
-    P = 1099511628211
+def _mix64(z):
     M = (1 << 64) - 1
-    h = 14695981039346656037
-    h = ((h ^ len(blobs)) * P) & M
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & M
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & M
+    return z ^ (z >> 31)
+
+
+def summary_digest(blobs):
+    """Python restatement of the summary digest (include/mtr_digest.h)."""
+    M = (1 << 64) - 1
+    h = _mix64(len(blobs) ^ 0x6d74723634)
     for b in blobs:
-        for c in b:
-            h = ((h ^ c) * P) & M
-        h = ((h ^ len(b)) * P) & M
+        s = 0
+        for j in range(0, len(b), 8):
+            w = int.from_bytes(b[j:j + 8].ljust(8, b"\0"), "little")
+            s = (s + _mix64(w ^ (((j // 8 + 1) * 0x9e3779b97f4a7c15) & M))) & M
+        h = _mix64(h ^ _mix64(s ^ ((len(b) * 0xd6e8feb86659fd93) & M)))
     return h
 
 
