@@ -23,7 +23,7 @@ from typing import Any, Iterable
 import numpy as np
 
 from . import abi
-from .jsjson import array_index, eq_key, js_key_order, js_string, js_stringify, parse, to_utf8
+from .jsjson import array_index, eq_key, js_key_order, js_string, js_stringify, parse, plain_value, to_utf8
 
 
 class Unsupported(Exception):
@@ -56,6 +56,8 @@ class Interner:
     def value(self, v: Any) -> int:
         if v is None:
             return abi.NULL_VALUE
+        if not plain_value(v):
+            raise Unsupported("property value with a nested null or an empty container")
         s = js_stringify(v)
         i = self.vals.get(s)
         if i is None:
@@ -143,6 +145,10 @@ class DocLog:
             self.short_id(long_id)
             self.collaborating = True
             self.ops.append((abi.OP_START_COLLAB, 0, 0, current_seq, 0, min_seq, 0, 0, 0, 0))
+
+    def seq_update(self, min_seq: int, seq: int) -> None:
+        """Client.updateSeqNumbers(min, seq) outside a message (client.ts:877), e.g. summarize's catch-up."""
+        self.ops.append((abi.OP_SEQ, abi.F_LAST, 0, seq, seq, min_seq, 0, 0, 0, 0))
 
     # -- sequenced messages (Client.applyMsg)
     def message(self, msg: dict, interner: Interner) -> None:

@@ -38,8 +38,30 @@ def build_engine(force=False, verbose=False, prof=False):
     return out
 
 
+NODE_INCLUDE = "/usr/include/node"
+
+
+def build_node_addon(force=False, verbose=False):
+    """The N-API addon (node/mtr_napi.node) a Node host loads; needs the Node headers, links libmtr.so."""
+    src = os.path.join(HERE, "node", "mtr_napi.cc")
+    out = os.path.join(HERE, "node", "mtr_napi.node")
+    if not os.path.exists(os.path.join(NODE_INCLUDE, "node_api.h")):
+        if verbose:
+            print("node headers not found: skipping the N-API addon")
+        return None
+    deps = [src, os.path.join(ROOT, "include", "mtr.h"), os.path.join(HERE, "libmtr.so")]
+    if force or _stale(out, deps):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-DNODE_GYP_MODULE_NAME=mtr_napi",
+               f"-I{NODE_INCLUDE}", "-o", out, src, f"-L{HERE}", "-lmtr", "-Wl,-rpath,$ORIGIN/.."]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return out
+
+
 def build_all(force=False, verbose=False):
     build_engine(force, verbose)
+    build_node_addon(force, verbose)
 
 
 if __name__ == "__main__":

@@ -170,9 +170,22 @@ def parse(text: str) -> Any:
     )
 
 
+def plain_value(v: Any, nested: bool = False) -> bool:
+    """True when matchProperties (properties.ts:71-105) is an equivalence on this value: no nested
+    null and no empty object/array (a top-level null is a delete, not a value)."""
+    if v is None:
+        return not nested
+    if isinstance(v, list):
+        return len(v) > 0 and all(plain_value(x, True) for x in v)
+    if isinstance(v, dict):
+        return len(v) > 0 and all(plain_value(x, True) for x in v.values())
+    return True
+
+
 def eq_key(v: Any) -> str:
     """Canonical form used for matchProperties equivalence (properties.ts:71-105):
-    deep equality that ignores object key order; numbers compared as doubles."""
+    deep equality that ignores object key order; numbers compared as doubles; an array compares
+    like the object of its indices (matchProperties recurses with `for...in`)."""
     if isinstance(v, bool) or v is None:
         return json.dumps(v)
     if isinstance(v, (int, float)):
@@ -183,7 +196,7 @@ def eq_key(v: Any) -> str:
     if isinstance(v, str):
         return "s" + json.dumps(v)
     if isinstance(v, list):
-        return "[" + ",".join(eq_key(x) for x in v) + "]"
+        v = {str(i): x for i, x in enumerate(v)}
     if isinstance(v, dict):
         return "{" + ",".join(json.dumps(k) + ":" + eq_key(v[k]) for k in sorted(v.keys())) + "}"
     raise TypeError(f"unsupported JSON value {type(v)}")

@@ -1,0 +1,55 @@
+/*
+ * TypeScript declarations of the Node host shim (index.js): the observer subset of
+ * @fluidframework/merge-tree's Client (packages/dds/merge-tree/src/client.ts:98) backed by the
+ * MI355X engine through the N-API addon (mtr_napi.node) and the C ABI (include/mtr.h).
+ */
+import type { ISequencedDocumentMessage } from "@fluidframework/protocol-definitions";
+import type { ISummaryTreeWithStats } from "@fluidframework/runtime-definitions";
+
+/** IMergeTreeOptions subset (mergeTree.ts:400-438) plus engine capacities. */
+export interface BatchReplayOptions {
+	newLengthCalc?: 0 | 1; // mergeTreeUseNewLengthCalculations
+	snapshotV1?: 0 | 1; // newMergeTreeSnapshotFormat
+	chunkSize?: number; // mergeTreeSnapshotChunkSize (default 10000)
+	catchUpBlobName?: string; // legacy catch-up blob name (default "catchupOps")
+	device?: number; // HIP device ordinal
+	maxSegments?: number;
+	heapEntries?: number;
+	textUnits?: number;
+	propWords?: number;
+	removerCells?: number;
+	opsPerLaunch?: number;
+}
+
+/** Thrown for inputs outside the observer path: keep this document on the TypeScript Client. */
+export class UnsupportedError extends Error {
+	readonly fallback: true;
+}
+
+/** The observer Clients of many documents on one GPU; messages are applied in batches. */
+export class BatchReplayEngine {
+	constructor(maxDocs: number, options?: BatchReplayOptions);
+	createClient(): BatchReplayClient;
+	/** Apply every queued message of every document (done implicitly before any read). */
+	flush(): void;
+}
+
+/** Drop-in for the observer use of `Client` (client.ts:98). */
+export class BatchReplayClient {
+	startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void; // client.ts:1133
+	applyMsg(msg: ISequencedDocumentMessage, local?: false): void; // client.ts:858
+	updateSeqNumbers(min: number, seq: number): void; // client.ts:877
+	insertTextLocal(pos: number, text: string, props?: Record<string, unknown>): void; // before collaboration only
+	insertMarkerLocal(pos: number, refType: number, props?: Record<string, unknown>): void;
+	removeRangeLocal(start: number, end: number): void;
+	annotateRangeLocal(start: number, end: number, props: Record<string, unknown>): void;
+	getText(): string; // MergeTreeTextHelper.getText, MergeTreeTextHelper.ts:20
+	getLength(): number;
+	getCurrentSeq(): number;
+	summarize(
+		runtime: { deltaManager: { minimumSequenceNumber: number; lastSequenceNumber: number } },
+		handle: unknown,
+		serializer: { stringify(value: unknown, bind: unknown): string } | undefined,
+		catchUpMsgs: ISequencedDocumentMessage[],
+	): ISummaryTreeWithStats; // client.ts:966
+}

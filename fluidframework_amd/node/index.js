@@ -1,0 +1,351 @@
+'use strict';
+/*
+ * Node host side of the MI355X merge-tree replay engine: the observer subset of
+ * @fluidframework/merge-tree's Client (packages/dds/merge-tree/src/client.ts:98) over the N-API
+ * addon (mtr_napi.cc) and the C ABI (include/mtr.h).
+ *
+ *   reference                                          | here
+ *   ---------------------------------------------------+--------------------------------------------
+ *   new Client(specToSegment, logger, options)         | engine.createClient()   (one engine = many docs)
+ *   client.startOrUpdateCollaboration(id, min, cur)    | same name              (client.ts:1133)
+ *   client.applyMsg(msg)                               | same name              (client.ts:858)
+ *   client.updateSeqNumbers(min, seq)                  | same name              (client.ts:877)
+ *   client.insertTextLocal / removeRangeLocal /        | same names, before collaboration only
+ *     annotateRangeLocal (non-collaborating edits)     |   (client.ts:237-285)
+ *   client.summarize(runtime, handle, ser, catchUp)    | same name              (client.ts:966)
+ *   client.getText() / getLength() / getCurrentSeq()   | same names
+ *
+ * Messages are packed on the JS thread exactly as the reference reads them (short client ids in
+ * first-seen order, GROUP ops flattened, JSON.stringify / Object.keys for property values and key
+ * order) and applied on the GPU in batches: applyMsg only queues, and the queue is flushed -- for
+ * every document of the engine at once -- before anything is read back.  Results are identical to
+ * applying each message synchronously because nothing observable happens in between.
+ * Written for Node >= 12 (no optional chaining).
+ */
+const path = require('path');
+
+let addon = null;
+function native() {
+    if (addon === null) addon = require(path.join(__dirname, 'mtr_napi.node'));
+    return addon;
+}
+
+// include/mtr_types.h
+const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
+    START_COLLAB: 12 };
+const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8 };
+const NULL_VALUE = 0xFFFFFFFF;
+const NOT_INDEX = 0xFFFFFFFF;
+const STATUS = { OK: 0, INSERT_FAILED: 1, BAD_OP: 2, CAPACITY: 3, UNSUPPORTED: 4, ASSERT: 0x1000 };
+// protocol-definitions SummaryType
+const SummaryType = { Tree: 1, Blob: 2 };
+
+class UnsupportedError extends Error {
+    constructor(msg) {
+        super(msg);
+        this.name = 'UnsupportedError';
+        this.fallback = true;  // the document must stay on the TypeScript Client
+    }
+}
+
+function arrayIndex(key) {
+    if (/^(0|[1-9][0-9]*)$/.test(key)) {
+        const v = Number(key);
+        if (v < 4294967295) return v;
+    }
+    return null;
+}
+
+/*
+ * matchProperties (properties.ts:71-105) compares values by strict equality and recurses into any
+ * `typeof === "object"` value through `for...in`, so arrays and index-keyed objects compare equal.
+ * That is an equivalence -- and interning equivalence classes is exact -- for values without
+ * nested nulls and empty containers; documents with such values stay on the TypeScript Client.
+ */
+let nanCounter = 0;
+function eqKey(v) {
+    if (typeof v === 'boolean') return v ? 'true' : 'false';
+    if (typeof v === 'number') return Number.isNaN(v) ? 'NaN#' + (nanCounter++) : 'n' + String(v === 0 ? 0 : v);
+    if (typeof v === 'string') return 's' + JSON.stringify(v);
+    return '{' + Object.keys(v).sort().map((k) => JSON.stringify(k) + ':' + eqKey(v[k])).join(',') + '}';
+}
+function plainValue(v, nested) {
+    if (v === null) return !nested;  // a top-level null deletes the key
+    if (typeof v !== 'object') return true;
+    const keys = Object.keys(v);
+    if (keys.length === 0) return false;
+    return keys.every((k) => plainValue(v[k], true));
+}
+
+const utf8 = (s) => Buffer.from(s, 'utf8');
+
+/** Global key / value / prop-op tables (ids stable across batches). */
+class Interner {
+    constructor() {
+        this.keys = new Map(); this.keyBytes = []; this.keyIndex = [];
+        this.vals = new Map(); this.valBytes = []; this.valEq = []; this.eqIds = new Map();
+        this.propops = [];
+    }
+    key(k) {
+        let i = this.keys.get(k);
+        if (i === undefined) {
+            i = this.keyBytes.length;
+            this.keys.set(k, i);
+            this.keyBytes.push(utf8(JSON.stringify(k).slice(1, -1)));
+            const ix = arrayIndex(k);
+            this.keyIndex.push(ix === null ? NOT_INDEX : ix);
+        }
+        return i;
+    }
+    value(v) {
+        if (v === null) return NULL_VALUE;
+        if (!plainValue(v, false)) throw new UnsupportedError('property value with nested null or empty container');
+        const s = JSON.stringify(v);
+        let i = this.vals.get(s);
+        if (i === undefined) {
+            i = this.valBytes.length;
+            this.vals.set(s, i);
+            this.valBytes.push(utf8(s));
+            const ek = eqKey(v);
+            let e = this.eqIds.get(ek);
+            if (e === undefined) { e = this.eqIds.size; this.eqIds.set(ek, e); }
+            this.valEq.push(e);
+        }
+        return i;
+    }
+    propop(props) {  // Object.keys order = JS own-key order
+        this.propops.push(Object.keys(props).map((k) => [this.key(k), this.value(props[k])]));
+        return this.propops.length - 1;
+    }
+}
+
+/** Per-document host state: client registry plus the queued ops/text of the next batch. */
+class DocLog {
+    constructor() {
+        this.observerId = undefined; this.clients = []; this.clientIx = new Map();
+        this.ops = []; this.text = []; this.collaborating = false;
+    }
+    shortId(longId) {  // Client.getOrAddShortClientId, client.ts:673-688
+        let i = this.clientIx.get(longId);
+        if (i === undefined) { i = this.clients.length; this.clientIx.set(longId, i); this.clients.push(longId); }
+        return i;
+    }
+    _text(s) {
+        const off = this.text.length;
+        for (let i = 0; i < s.length; i++) this.text.push(s.charCodeAt(i));
+        return [off, s.length];
+    }
+    _seg(spec, it) {  // specToSegment, sequence/src/sequenceFactory.ts:26-38 -> [flags, payload, payload2, propop]
+        if (typeof spec === 'string') { const t = this._text(spec); return [0, t[0], t[1], -1]; }
+        if (spec && typeof spec === 'object' && 'text' in spec) {
+            const t = this._text(spec.text);
+            if (spec.props !== undefined && spec.props !== null) return [F.PROPS, t[0], t[1], it.propop(spec.props)];
+            return [0, t[0], t[1], -1];
+        }
+        if (spec && typeof spec === 'object' && 'marker' in spec) {
+            const m = spec.marker || {};
+            let flags = F.MARKER, ref = m.refType;
+            if (ref === undefined || ref === null) { flags |= F.NOREF; ref = 0; }
+            let pp = -1;
+            if (spec.props !== undefined && spec.props !== null) { flags |= F.PROPS; pp = it.propop(spec.props); }
+            return [flags, ref >>> 0, 0, pp];
+        }
+        throw new UnsupportedError('unrecognized segment spec');
+    }
+    push(type, flags, client, seq, ref, msn, pos1, pos2, payload, payload2) {
+        this.ops.push([type, flags, client, seq, ref, msn, pos1, pos2, payload, payload2]);
+    }
+    localInsert(pos, spec, it) {
+        const s = this._seg(spec, it);
+        this.push(OP.LOCAL_INSERT, s[0], 0, 0, 0, 0, pos, s[3], s[1], s[2]);
+    }
+    localRemove(start, end) { this.push(OP.LOCAL_REMOVE, 0, 0, 0, 0, 0, start, end, 0, 0); }
+    localAnnotate(start, end, props, it) { this.push(OP.LOCAL_ANNOTATE, 0, 0, 0, 0, 0, start, end, it.propop(props), 0); }
+    startCollab(longId, minSeq, currentSeq) {  // client.ts:1133-1155
+        if (this.observerId === undefined) {
+            this.observerId = longId;
+            this.shortId(longId);
+            this.collaborating = true;
+            this.push(OP.START_COLLAB, 0, 0, currentSeq, 0, minSeq, 0, 0, 0, 0);
+        }
+    }
+    seqUpdate(min, seq) { this.push(OP.SEQ, F.LAST, 0, seq, seq, min, 0, 0, 0, 0); }
+    message(msg, it) {  // Client.applyMsg, client.ts:858-887
+        const cid = msg.clientId === null || msg.clientId === undefined ? 'null' : String(msg.clientId);
+        const short = this.shortId(cid);
+        const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
+        if (msg.type !== 'op') { this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
+        if (cid === this.observerId) throw new UnsupportedError('message authored by the observer (local ack path)');
+        let contents = msg.contents;
+        if (typeof contents === 'string') contents = JSON.parse(contents);
+        const members = contents.type === 3 ? contents.ops : [contents];  // MergeTreeDeltaType.GROUP
+        if (members.length === 0) { this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
+        members.forEach((op, i) => {
+            const last = i === members.length - 1 ? F.LAST : 0;
+            if ('relativePos1' in op || 'relativePos2' in op) throw new UnsupportedError('relative positions');
+            if (op.type === 0) {
+                if (op.seg === undefined || op.seg === null) {  // applyInsertOp returns early
+                    this.push(OP.SEQ, last, short, seq, ref, msn, 0, 0, 0, 0);
+                    return;
+                }
+                const s = this._seg(op.seg, it);
+                this.push(OP.INSERT, s[0] | last, short, seq, ref, msn, op.pos1, s[3], s[1], s[2]);
+            } else if (op.type === 1) {
+                this.push(OP.REMOVE, last, short, seq, ref, msn, op.pos1, op.pos2, 0, 0);
+            } else if (op.type === 2) {
+                if (op.combiningOp !== undefined && op.combiningOp !== null) throw new UnsupportedError('combining ops');
+                this.push(OP.ANNOTATE, last, short, seq, ref, msn, op.pos1, op.pos2, it.propop(op.props), 0);
+            } else {
+                throw new UnsupportedError('op type ' + op.type);
+            }
+        });
+    }
+}
+
+function offsets(chunks) {
+    const off = new Uint32Array(chunks.length + 1);
+    for (let i = 0; i < chunks.length; i++) off[i + 1] = off[i] + chunks[i].length;
+    return [off, Buffer.concat(chunks.concat([Buffer.alloc(1)]))];
+}
+
+/** Pack the queued ops of every DocLog (in order) into the arrays of include/mtr_types.h and clear them. */
+function buildBatch(logs, it) {
+    const nOps = logs.reduce((a, l) => a + l.ops.length, 0);
+    const nText = logs.reduce((a, l) => a + l.text.length, 0);
+    const docs = Buffer.alloc(32 * logs.length);
+    const ops = Buffer.alloc(32 * nOps);
+    const text = new Uint16Array(Math.max(1, nText));
+    const clientChunks = [];
+    let o = 0, t = 0;
+    logs.forEach((log, d) => {
+        const b = 32 * d;
+        docs.writeUInt32LE(o >>> 0, b); docs.writeUInt32LE(Math.floor(o / 4294967296), b + 4);
+        docs.writeUInt32LE(t >>> 0, b + 8); docs.writeUInt32LE(Math.floor(t / 4294967296), b + 12);
+        docs.writeUInt32LE(log.ops.length, b + 16);
+        docs.writeUInt32LE(log.text.length, b + 20);
+        docs.writeUInt32LE(clientChunks.length, b + 24);
+        docs.writeUInt32LE(log.clients.length, b + 28);
+        log.clients.forEach((c) => clientChunks.push(utf8(JSON.stringify(c).slice(1, -1))));
+        for (const r of log.ops) {
+            const q = 32 * o;
+            ops.writeUInt8(r[0], q); ops.writeUInt8(r[1], q + 1); ops.writeUInt16LE(r[2], q + 2);
+            ops.writeInt32LE(r[3], q + 4); ops.writeInt32LE(r[4], q + 8); ops.writeInt32LE(r[5], q + 12);
+            ops.writeInt32LE(r[6], q + 16); ops.writeInt32LE(r[7], q + 20);
+            ops.writeUInt32LE(r[8] >>> 0, q + 24); ops.writeUInt32LE(r[9] >>> 0, q + 28);
+            o++;
+        }
+        text.set(log.text, t);
+        t += log.text.length;
+        log.ops = []; log.text = [];
+    });
+    const po = new Uint32Array(it.propops.length + 1);
+    const kv = [];
+    it.propops.forEach((pairs, i) => { po[i + 1] = po[i] + pairs.length; pairs.forEach((p) => kv.push(p[0], p[1])); });
+    const k = offsets(it.keyBytes), v = offsets(it.valBytes), c = offsets(clientChunks);
+    return {
+        docs, ops, text, propopOff: po, propopKv: Uint32Array.from(kv.length ? kv : [0]),
+        keyOff: k[0], keyBytes: k[1], keyIndex: Uint32Array.from(it.keyIndex.length ? it.keyIndex : [0]),
+        valOff: v[0], valBytes: v[1], valEq: Uint32Array.from(it.valEq.length ? it.valEq : [0]),
+        clientOff: c[0], clientBytes: c[1],
+    };
+}
+
+/** The observer Clients of many documents on one GPU. */
+class BatchReplayEngine {
+    constructor(maxDocs, options) {
+        this.options = Object.assign({ newLengthCalc: 0, snapshotV1: 1, chunkSize: 10000, device: 0 }, options || {});
+        this.maxDocs = maxDocs;
+        this.h = native().createEngine(maxDocs, this.options);
+        this.interner = new Interner();
+        this.logs = [];
+        this.dirty = false;
+        this.summarized = false;
+    }
+    createClient() {
+        if (this.logs.length >= this.maxDocs) throw new Error('engine is full');
+        this.logs.push(new DocLog());
+        return new BatchReplayClient(this, this.logs.length - 1);
+    }
+    flush() {  // apply every queued message of every document
+        if (!this.dirty) return;
+        native().submitRun(this.h, buildBatch(this.logs, this.interner));
+        this.dirty = false;
+        this.summarized = false;
+    }
+}
+
+/** Client (client.ts:98) restricted to the observer path, backed by one engine document. */
+class BatchReplayClient {
+    constructor(engine, doc) {
+        this.engine = engine; this.doc = doc; this.log = engine.logs[doc];
+        this.currentSeq = 0;
+    }
+    _queue(fn) { fn(); this.engine.dirty = true; }
+    _check() {
+        const st = native().docStatus(this.engine.h, this.doc);
+        if (st[0] === STATUS.OK) return;
+        if (st[0] >= STATUS.ASSERT) {  // assert(cond, 0xNNN) throws Error("0xNNN"), common-utils assert.ts:15-21
+            throw new Error('0x' + (st[0] - STATUS.ASSERT).toString(16).padStart(3, '0'));
+        }
+        if (st[0] === STATUS.INSERT_FAILED) throw new Error('MergeTree insert failed');  // mergeTree.ts:1671
+        if (st[0] === STATUS.UNSUPPORTED) throw new UnsupportedError('unsupported op at ' + st[1]);
+        throw new Error('engine status ' + st[0] + ' at op ' + st[1]);
+    }
+    startOrUpdateCollaboration(longClientId, minSeq, currentSeq) {
+        this._queue(() => this.log.startCollab(longClientId, minSeq || 0, currentSeq || 0));
+        this.currentSeq = currentSeq || 0;
+    }
+    applyMsg(msg, local) {
+        if (local) throw new UnsupportedError('local (acked) ops are outside the observer path');
+        this._queue(() => this.log.message(msg, this.engine.interner));
+        this.currentSeq = msg.sequenceNumber;
+    }
+    updateSeqNumbers(min, seq) {
+        this._queue(() => this.log.seqUpdate(min, seq));
+        this.currentSeq = seq;
+    }
+    insertTextLocal(pos, text, props) {
+        this._queue(() => this.log.localInsert(pos, props ? { text, props } : text, this.engine.interner));
+    }
+    insertMarkerLocal(pos, refType, props) {
+        this._queue(() => this.log.localInsert(pos, props ? { marker: { refType }, props } : { marker: { refType } },
+            this.engine.interner));
+    }
+    removeRangeLocal(start, end) { this._queue(() => this.log.localRemove(start, end)); }
+    annotateRangeLocal(start, end, props) { this._queue(() => this.log.localAnnotate(start, end, props, this.engine.interner)); }
+    getCurrentSeq() { return this.currentSeq; }
+    getText() {
+        this.engine.flush();
+        this._check();
+        return native().getText(this.engine.h, this.doc);
+    }
+    getLength() { return this.getText().length; }
+    /** Client.summarize (client.ts:966-1000) -> ISummaryTreeWithStats */
+    summarize(runtime, handle, serializer, catchUpMsgs) {
+        const dm = runtime.deltaManager;
+        this.updateSeqNumbers(dm.minimumSequenceNumber, dm.lastSequenceNumber);
+        const v1 = !!this.engine.options.snapshotV1;
+        if (v1 && catchUpMsgs !== undefined && catchUpMsgs.length > 0) throw new Error('0x03f');
+        this.engine.flush();
+        this._check();
+        if (!this.engine.summarized) { native().summarize(this.engine.h); this.engine.summarized = true; }
+        const blobs = native().getSummary(this.engine.h, this.doc);
+        const names = v1 ? blobs.map((_, i) => (i === 0 ? 'header' : 'body_' + (i - 1))) : ['header', 'body'];
+        const tree = {};
+        let total = 0;
+        blobs.forEach((b, i) => { tree[names[i]] = { type: SummaryType.Blob, content: b.toString('utf8') }; total += b.length; });
+        if (!v1 && catchUpMsgs !== undefined && catchUpMsgs.length > 0) {  // snapshotlegacy.ts:174-179
+            const s = serializer ? serializer.stringify(catchUpMsgs, handle) : JSON.stringify(catchUpMsgs);
+            tree[this.engine.options.catchUpBlobName || 'catchupOps'] = { type: SummaryType.Blob, content: s };
+            total += Buffer.byteLength(s, 'utf8');
+        }
+        return {
+            stats: { treeNodeCount: 1, blobNodeCount: Object.keys(tree).length, handleNodeCount: 0,
+                totalBlobSize: total, unreferencedBlobSize: 0 },
+            summary: { type: SummaryType.Tree, tree },
+        };
+    }
+}
+
+module.exports = { BatchReplayEngine, BatchReplayClient, Interner, DocLog, buildBatch, UnsupportedError, OP, F,
+    SummaryType, native };

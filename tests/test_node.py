@@ -1,0 +1,109 @@
+"""The Node host path (the reference's TypeScript side): the N-API addon over the C ABI and the JS
+packer / BatchReplayClient (fluidframework_amd/node).  CPU: the addon loads, exports its entry points
+and fails loudly without a GPU; the JS packer produces the same batch bytes as the Python packer.
+GPU: the reference replay test through Node, text after every group + summary bytes vs the oracle."""
+import base64
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from fixtures import load_replay, replay_files, replay_log
+from fluidframework_amd.batch import Interner, build_batch
+from oracle.oracle import OracleDoc, options
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE_DIR = os.path.join(ROOT, "fluidframework_amd", "node")
+ADDON = os.path.join(NODE_DIR, "mtr_napi.node")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+pytestmark = pytest.mark.skipif(shutil.which("node") is None, reason="node is not installed")
+
+
+def _addon():
+    if not os.path.exists(ADDON):
+        from fluidframework_amd import build
+        build.build_engine()
+        if build.build_node_addon() is None:
+            pytest.skip("node headers missing")
+    return ADDON
+
+
+def _node(args, timeout=600):
+    r = subprocess.run(["node"] + args, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return r.stdout
+
+
+def test_addon_loads_and_fails_loudly_without_a_gpu():
+    _addon()
+    out = _node(["-e", "const m=require(process.argv[1]);const a=m.native();"
+                 "console.log(JSON.stringify(Object.keys(a).sort()));"
+                 "try{new m.BatchReplayEngine(1,{});console.log('ENGINE')}catch(e){console.log('ERR '+e.message)}",
+                 NODE_DIR])
+    lines = out.strip().splitlines()
+    assert json.loads(lines[0]) == sorted(["createEngine", "submitRun", "summarize", "getSummary", "getText",
+                                           "docStatus", "stats", "reset"])
+    if lines[1] != "ENGINE":  # no HIP device here: construction must throw, never fall back
+        assert lines[1].startswith("ERR mtr_engine_create")
+
+
+def _py_batch(paths):
+    it = Interner()
+    logs = []
+    for p in paths:
+        groups = load_replay(p)
+        log = replay_log(groups, it)
+        for g in groups:
+            for m in g["msgs"]:
+                log.message(m, it)
+        last = groups[-1]["msgs"][-1]
+        log.seq_update(last["minimumSequenceNumber"], last["sequenceNumber"])
+        logs.append(log)
+    return build_batch(logs, it)
+
+
+def test_js_packer_matches_python_packer():
+    paths = replay_files()[:6]
+    _addon()
+    js = json.loads(_node([os.path.join(HERE, "node", "pack_batch.js")] + paths))
+    raw = {k: base64.b64decode(v) for k, v in js.items()}
+    py = _py_batch(paths)
+
+    def arr(name, dtype):
+        return np.frombuffer(raw[name], dtype=dtype)
+
+    assert raw["docs"] == py.docs.tobytes()
+    assert raw["ops"] == py.ops.tobytes()
+    n_text = int(py.docs["text_count"].sum())
+    assert np.array_equal(arr("text", "<u2")[:n_text], py.text[:n_text])
+    assert np.array_equal(arr("propopOff", "<u4"), py.propop_off)
+    n_kv = 2 * int(py.propop_off[-1])
+    assert np.array_equal(arr("propopKv", "<u4")[:n_kv], py.propop_kv[:n_kv])
+    for off, data in (("keyOff", "keyBytes"), ("valOff", "valBytes"), ("clientOff", "clientBytes")):
+        po = {"keyOff": py.key_off, "valOff": py.val_off, "clientOff": py.client_off}[off]
+        pd = {"keyBytes": py.key_bytes, "valBytes": py.val_bytes, "clientBytes": py.client_bytes}[data]
+        assert np.array_equal(arr(off, "<u4"), po)
+        assert raw[data][: int(po[-1])] == pd.tobytes()[: int(po[-1])]
+    n_keys, n_vals = len(py.key_off) - 1, len(py.val_off) - 1
+    assert np.array_equal(arr("keyIndex", "<u4")[:n_keys], py.key_index[:n_keys])
+    assert np.array_equal(arr("valEq", "<u4")[:n_vals], py.val_eq[:n_vals])
+
+
+@pytest.mark.gpu
+def test_replay_logs_through_node_host():
+    paths = replay_files()
+    _addon()
+    res = json.loads(_node([os.path.join(HERE, "node", "replay_engine.js")] + paths, timeout=300))
+    assert res["checks"] == sum(len(load_replay(p)) for p in paths)
+    b = _py_batch(paths)
+    for r in res["result"]:
+        orc = OracleDoc(options())
+        assert orc.apply(b, r["doc"]) == 0
+        exp = orc.summarize(b, r["doc"])
+        got = [base64.b64decode(x) for x in r["blobs"]]
+        assert got == exp, f"doc {r['doc']}: summary bytes differ"
+        assert r["names"] == ["header"] + [f"body_{i}" for i in range(len(got) - 1)]
