@@ -28,21 +28,34 @@ METRIC = "sequenced ops applied/sec (whole node) over 100k docs, bit-exact summa
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: chip-level parameters)
 
 
+# BASELINE.json configs: documents per GPU, messages per document, writers, max lag
+PRESETS = {
+    "C2": dict(docs=10_000, ops=5_000, writers=16, max_lag=64),
+    "C3": dict(docs=100_000, ops=1_000, writers=8, max_lag=32),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=sorted(PRESETS), default="C3",
+                    help="workload preset (C3 = the headline metric's 100k-document run)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--docs", type=int, default=100_000, help="documents per GPU (C3: 100k)")
-    ap.add_argument("--ops", type=int, default=1_000, help="sequenced messages per document (C3: 1k)")
-    ap.add_argument("--writers", type=int, default=8)
-    ap.add_argument("--max-lag", type=int, default=32)
+    ap.add_argument("--docs", type=int, default=None, help="documents per GPU (preset)")
+    ap.add_argument("--ops", type=int, default=None, help="sequenced messages per document (preset)")
+    ap.add_argument("--writers", type=int, default=None)
+    ap.add_argument("--max-lag", type=int, default=None)
     ap.add_argument("--ops-per-launch", type=int, default=16)
-    ap.add_argument("--cpu-sample-docs", type=int, default=4000)
+    ap.add_argument("--cpu-sample-docs", type=int, default=0, help="default: about 4M messages of documents")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in PRESETS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
 def main():
@@ -156,7 +169,7 @@ def main():
     if not a.no_cpu_baseline and world == 1:
         from oracle.oracle import replay_batch
 
-        k = min(a.cpu_sample_docs, n)
+        k = min(a.cpu_sample_docs or max(1, 4_000_000 // ops), n)
         sample = eng.download(0, k)
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
         secs, ohash, ost = replay_batch(sample, 0, k, threads)
@@ -185,7 +198,7 @@ def main():
         "dtype": "int32",
         "data": "synthetic: seeded recipe include/mtr_synth.h recorded on the device (record mode)",
         "config": {
-            "workload": f"C3: {n} docs/GPU x {ops} ops, {a.writers} writers, lag<={a.max_lag}, V1 summaries",
+            "workload": f"{a.config}: {n} docs/GPU x {ops} ops, {a.writers} writers, lag<={a.max_lag}, V1 summaries",
             "docs_per_gpu": n,
             "ops_per_doc": ops,
             "writers": a.writers,

@@ -363,6 +363,11 @@ static int run_impl(mtr_engine* e, int gen) {
         (void)hipFuncSetAttribute((const void*)apply_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
     });
+    // documents whose class needs more LDS than this stay HBM-resident (MTR_LDS_LIMIT, bytes; tuning knob)
+    static const size_t lds_limit = [] {
+        const char* v = std::getenv("MTR_LDS_LIMIT");
+        return v ? std::min<size_t>(size_t(std::atoll(v)), 160 * 1024) : size_t(160 * 1024);
+    }();
     const size_t ncls = 1 + 3 * kClasses;
     if (e->cls.ensure(ncls) || e->dlist.ensure(size_t(kClasses) * e->n_docs)) return -1;
     if (!e->h_cls) HIPCHK(hipHostMalloc((void**)&e->h_cls, (1 + 3 * kClasses) * sizeof(int32_t), hipHostMallocDefault));
@@ -387,7 +392,7 @@ static int run_impl(mtr_engine* e, int gen) {
             int lhcap = std::min<int>(P.hcap, std::max(cap / 2, round64(maxheap + 2 * k + 8)));
             size_t lds = lds_bytes(cap, lhcap);
             P.global_mode = 0;
-            if (lds > size_t(160 * 1024)) {
+            if (lds > lds_limit) {
                 // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
                 if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
                 P.global_mode = 1;
