@@ -13,11 +13,14 @@ OP_LOCAL_INSERT = 8
 OP_LOCAL_REMOVE = 9
 OP_LOCAL_ANNOTATE = 10
 OP_START_COLLAB = 12
+OP_LOAD = 13
+CLIENT_NONCOLLAB = 0xFFFE
 
 F_LAST = 1
 F_MARKER = 2
 F_PROPS = 4
 F_NOREF = 8
+F_APPEND = 16
 
 NULL_VALUE = 0xFFFFFFFF
 NOT_INDEX = 0xFFFFFFFF

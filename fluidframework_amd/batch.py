@@ -142,9 +142,61 @@ class DocLog:
         """Client.startOrUpdateCollaboration (client.ts:1133-1155)."""
         if self.observer_id is None:
             self.observer_id = long_id
-            self.short_id(long_id)
+            me = self.short_id(long_id)
             self.collaborating = True
-            self.ops.append((abi.OP_START_COLLAB, 0, 0, current_seq, 0, min_seq, 0, 0, 0, 0))
+            self.ops.append((abi.OP_START_COLLAB, 0, me, current_seq, 0, min_seq, 0, 0, 0, 0))
+
+    # -- loading a summary (SnapshotLoader, snapshotLoader.ts:41-257)
+    def _snapshot_seg(self, spec: Any, interner: Interner, op_type: int, flags: int) -> None:
+        """specToSegment with merge info (snapshotLoader.ts:88-128) -> one LOAD / APPEND record."""
+        if isinstance(spec, dict) and "json" in spec:  # hasMergeInfo, snapshotChunks.ts:80-84
+            f, p1, p2, pp = self._seg(spec["json"], interner)
+            client = self.short_id(spec["client"]) if spec.get("client") is not None else abi.CLIENT_NONCOLLAB
+            seq = int(spec["seq"]) if spec.get("seq") is not None else 0
+            removers = []
+            if spec.get("removedClient") is not None:
+                removers = [self.short_id(spec["removedClient"])]
+            if spec.get("removedClientIds") is not None:
+                removers = [self.short_id(x) for x in spec["removedClientIds"]]
+            rseq = int(spec["removedSeq"]) if spec.get("removedSeq") is not None else -1
+        else:
+            f, p1, p2, pp = self._seg(spec, interner)
+            client, seq, removers, rseq = abi.CLIENT_NONCOLLAB, 0, [], -1
+        roff = len(self.text)
+        self.text.extend(removers)
+        self.ops.append((op_type, f | flags, client, seq, rseq, len(removers), roff, pp, p1, p2))
+
+    def load_summary(self, blobs: dict, long_id: str, interner: Interner) -> list:
+        """Client.load from the blobs of a merge-tree summary (V1 or legacy): header segments via
+        reloadFromSegments, startOrUpdateCollaboration(long_id, minSeq, seq), body segments appended.
+        Returns the legacy catch-up messages (the caller applies them as ordinary messages)."""
+        header = blobs["header"]
+        chunk = parse(header) if isinstance(header, str) else header
+        if chunk.get("version") == "1":
+            segs, meta = chunk["segments"], chunk["headerMetadata"]
+        else:  # toLatestVersion of a legacy chunk, snapshotChunks.ts:151-200
+            segs = chunk["segmentTexts"]
+            meta = chunk.get("headerMetadata") or {
+                "orderedChunkMetadata": [{"id": "header"}] + (
+                    [{"id": "body"}] if chunk["chunkLengthChars"] < chunk["totalLengthChars"] else []),
+                "minSequenceNumber": chunk.get("chunkMinSequenceNumber"),
+                "sequenceNumber": chunk["chunkSequenceNumber"]}
+        for spec in segs:
+            self._snapshot_seg(spec, interner, abi.OP_LOAD, 0)
+        min_seq = meta.get("minSequenceNumber")
+        seq = int(meta["sequenceNumber"])
+        self.start_collab(long_id, int(min_seq) if min_seq is not None else seq, seq)
+        for md in meta["orderedChunkMetadata"][1:]:
+            body = blobs[md["id"]]
+            body = parse(body) if isinstance(body, str) else body
+            for spec in body.get("segments", body.get("segmentTexts", [])):
+                self._snapshot_seg(spec, interner, abi.OP_INSERT, abi.F_APPEND)
+        names = {"header"} | {md["id"] for md in meta["orderedChunkMetadata"]}
+        extra = [k for k in blobs if k not in names]
+        if extra:
+            cu = blobs[extra[0]]
+            return parse(cu) if isinstance(cu, str) else cu
+        return []
 
     def seq_update(self, min_seq: int, seq: int) -> None:
         """Client.updateSeqNumbers(min, seq) outside a message (client.ts:877), e.g. summarize's catch-up."""

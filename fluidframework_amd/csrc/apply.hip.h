@@ -335,6 +335,18 @@ struct Eng {
         return 0;
     }
 
+    // root.cachedLength: the local view's length (removed leaves count 0), mergeTree.ts:613-634
+    static MTR_DI int local_length(const D& L, const St& s) {
+        int sum = 0;
+        for (int base = 0; base < s.nseg; base += 64) {
+            const int i = base + lane_id();
+            int x = 0;
+            if (i < s.nseg && L.rseq[i] == RNONE) x = L.len[i];
+            sum += rdlane(wave_incl_scan(x), 63);
+        }
+        return sum;
+    }
+
     // V[i] = visible length, E[i] = inclusive prefix of max(V,0); rounds of 64 leaves
     static MTR_DI void prefix(D& L, const St& s, const View& v, int newlen) {
         PROF(P_PREFIX);
@@ -1187,18 +1199,18 @@ struct Eng {
     // insertSegments/blockInsert/insertingWalk with onLeaf (mergeTree.ts:1397-1427, 1594-1685),
     // on the current scan arrays.  `pre`: lane t holds unit t of the op's text in `pf`
     // (prefetched during the previous op).
-    static MTR_DI void insert_at(D& L, const KParams& P, St& s, const View& v, const mtr_op& op, int seq,
-                                 uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf) {
+    static MTR_DI int insert_at(D& L, const KParams& P, St& s, const View& v, const mtr_op& op, int pos, int seq,
+                                uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf) {
         PROF(P_INSERT);
         const bool marker = (op.flags & MTR_F_MARKER) != 0;
         const int len = marker ? 1 : int(op.payload2);
-        if (len <= 0) return;  // blockInsert skips empty segments
+        if (len <= 0) return -1;  // blockInsert skips empty segments
         const int t0 = s.textused;
         const int ln = lane_id();
         if (!marker) {  // copy the op's text into the document arena
             if (t0 + len > text_end(s, P)) {
                 s.status = MTR_ERR_CAPACITY;
-                return;
+                return -1;
             }
             PROF(P_TEXTCOPY);
             if (pre) {
@@ -1211,7 +1223,6 @@ struct Eng {
         const uint64_t nlm = pre ? __ballot(ln < len && pf == u'\n') : 0;
         const bool nl = pre && ((nlm >> (len - 1)) & 1);
         const bool nonl = pre && nlm == 0;
-        const int pos = op.pos1;
         const int S = s.nseg;
         int slot = -1, inherit = 0;
         {
@@ -1237,7 +1248,7 @@ struct Eng {
                 }
             }
         }
-        if (slot < 0) return;
+        if (slot < 0) return -1;
         shift_right1(L, s, slot);
         uint32_t m = client & M_CLIENT_MASK;
         if (marker) m |= M_MARKER;
@@ -1266,7 +1277,99 @@ struct Eng {
         s.nseg = S + 1;
         overflow_fix(L, s, slot);
         // saveIfLocal (mergeTree.ts:1618-1637): remote segments above minSeq go to the LRU
+        if (op.flags & MTR_F_APPEND) set_merge_info(L, P, s, slot, op, dd);
         if (s.collab && !v.local && seq > s.minseq) add_lru_block(L, s, block_start(L, slot, 1), uint32_t(s.uidnext - 1), seq);
+        return slot;
+    }
+
+    // ------------------------------------------------------------ snapshot load
+    // merge info of a snapshot segment on leaf i (SnapshotLoader.specToSegment, snapshotLoader.ts:88-128):
+    // removedSeq, and removedClientIds as first remover + newest-first cons list of the others
+    static MTR_DI void set_merge_info(D& L, const KParams& P, St& s, int i, const mtr_op& op, const mtr_doc_desc& dd) {
+        if (op.ref_seq >= 0) L.rseq[i] = op.ref_seq;
+        const int nrem = op.min_seq;
+        if (nrem > 0) {
+            const gptr<const uint16_t> rl = gp(P.btext) + dd.text_base + uint32_t(op.pos1);
+            uint32_t m = uniu(L.meta[i]);
+            m = (m & ~(0xffu << M_FREM_SHIFT) & ~M_OVERLAP) | (enc_client(int(uniu(rl[0]))) << M_FREM_SHIFT);
+            if (nrem > 1) {
+                if (s.rmused + nrem - 1 > P.rcap) {
+                    s.status = MTR_ERR_CAPACITY;
+                    return;
+                }
+                uint32_t head = 0xffffffu;
+                for (int k = 1; k < nrem; k++) {
+                    const uint32_t cell = uint32_t(s.rmused++);
+                    L.grm[cell] = (enc_client(int(uniu(rl[k]))) << 24) | head;
+                    head = cell;
+                }
+                m |= M_OVERLAP;
+                L.rm[i] = head;
+            }
+            L.meta[i] = m;
+        }
+        wsync();
+    }
+
+    // one header segment appended in order; the block structure is built by finish_load
+    static MTR_DI void load_leaf(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd) {
+        if (s.collab) {  // "Trying to reload from segments while collaborating!"
+            s.status = MTR_ERR_ASSERT | 0x049;
+            return;
+        }
+        if (s.height != 0) {  // reloadFromSegments replaces the whole tree
+            s.nseg = 0;
+            s.height = 0;
+        }
+        const bool marker = (op.flags & MTR_F_MARKER) != 0;
+        const int len = marker ? 1 : int(op.payload2);
+        const int i = s.nseg;
+        const int t0 = s.textused;
+        if (!marker) {
+            if (t0 + len > text_end(s, P)) {
+                s.status = MTR_ERR_CAPACITY;
+                return;
+            }
+            const gptr<const uint16_t> src = gp(P.btext) + dd.text_base + op.payload;
+            for (int k = lane_id(); k < len; k += 64) L.gtext[t0 + k] = src[k];
+            s.textused = t0 + len;
+        }
+        uint32_t m = enc_client(int(int16_t(op.client)));
+        if (marker) m |= M_MARKER;
+        else m |= M_NLQ;
+        if (op.flags & MTR_F_NOREF) m |= M_NOREF;
+        L.len[i] = len;
+        L.seq[i] = op.seq;
+        L.rseq[i] = RNONE;
+        L.meta[i] = m;
+        L.text[i] = marker ? op.payload : uint32_t(t0);
+        uint32_t pr = NONE32;
+        if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
+        L.props[i] = pr;
+        L.rm[i] = NONE32;
+        L.uid[i] = uint32_t(s.uidnext++);
+        wsync();
+        s.nseg = i + 1;
+        set_merge_info(L, P, s, i, op, dd);
+    }
+
+    // MergeTree.reloadFromSegments (mergeTree.ts:678-728): MaxNodesInBlock - 1 = 7 children per block,
+    // built bottom-up, so leaf i starts a level-l block iff 7^l divides i; leaf 0 starts every level
+    static MTR_DI void finish_load(D& L, St& s) {
+        const int S = s.nseg;
+        int H = 1;
+        for (int n = S; n > kMaxNodesInBlock - 1; n = (n + kMaxNodesInBlock - 2) / (kMaxNodesInBlock - 1)) H++;
+        for (int i = lane_id(); i < S; i += 64) {
+            int b = 0;
+            if (i == 0) {
+                b = H;
+            } else {
+                for (int64_t p = kMaxNodesInBlock - 1; b + 1 < H && i % p == 0; p *= kMaxNodesInBlock - 1) b++;
+            }
+            L.meta[i] = set_ns(set_bnd(L.meta[i], b), NS_UNDEF);
+        }
+        wsync();
+        s.height = H;
     }
 
     // markRangeRemoved / annotateRange walk (mergeTree.ts:1955-2047, 1895-1953): leaves with
@@ -1590,11 +1693,21 @@ struct Eng {
             }
             if (s.nseg + 2 >= L.cap) s.status = MTR_ERR_CAPACITY;  // every op adds at most two leaves
             if (s.status != MTR_OK) break;
+            if (op.type == MTR_OP_LOAD) {  // SnapshotLoader.loadHeader segment
+                load_leaf(L, P, s, op, dd);
+                if (s.status != MTR_OK) {
+                    s.fail_op = cursor + k;
+                    break;
+                }
+                s.ops_done = k + 1;
+                continue;
+            }
+            if (s.height == 0) finish_load(L, s);
             const bool local_op = op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE;
             int zop = 0;
             View v;
             int seq = op.seq;
-            uint32_t client = enc_client(op.client);
+            uint32_t client = enc_client(int(int16_t(op.client)));
             if (local_op) {
                 if (s.collab) {
                     s.status = MTR_ERR_UNSUPPORTED;
@@ -1607,18 +1720,22 @@ struct Eng {
                 seq = 0;
                 client = CL_LOCAL;
             } else {
-                v.ref = op.ref_seq;
+                // a snapshot body append walks at (UniversalSequenceNumber, segment client)
+                v.ref = (op.flags & MTR_F_APPEND) ? 0 : op.ref_seq;
                 v.client = client;
                 v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
             }
             switch (op.type) {
                 case MTR_OP_INSERT:
-                case MTR_OP_LOCAL_INSERT:
+                case MTR_OP_LOCAL_INSERT: {
+                    int pos = op.pos1;
+                    if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
                     prefix(L, s, v, P.new_length_calc);
-                    split_at(L, s, op.pos1);
-                    insert_at(L, P, s, v, op, seq, client, dd, pre, pf);
+                    split_at(L, s, pos);
+                    insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf);
                     zop = s.collab;
                     break;
+                }
                 case MTR_OP_REMOVE:
                 case MTR_OP_LOCAL_REMOVE:
                 case MTR_OP_ANNOTATE:
@@ -1636,7 +1753,7 @@ struct Eng {
                 case MTR_OP_START_COLLAB:
                     if (!s.collab) {
                         s.collab = 1;
-                        s.local = 0;
+                        s.local = int(enc_client(int(int16_t(op.client))));
                         s.minseq = op.min_seq;
                         s.curseq = op.seq;
                         s.heapn = 0;
@@ -1664,6 +1781,8 @@ struct Eng {
             }
             s.ops_done = k + 1;
         }
+        // a batch that ends with header segments: build the tree now (queries read it next)
+        if (s.height == 0 && s.status == MTR_OK && cursor + s.ops_done >= int(dd.op_count)) finish_load(L, s);
         store_doc(L, P, s, d);
     }
 };

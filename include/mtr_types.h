@@ -30,7 +30,11 @@ enum {
     MTR_OP_LOCAL_INSERT = 8,    /* non-collaborating local insert (client.ts:237, seq=0, client=-1) */
     MTR_OP_LOCAL_REMOVE = 9,    /* non-collaborating local remove */
     MTR_OP_LOCAL_ANNOTATE = 10, /* non-collaborating local annotate */
-    MTR_OP_START_COLLAB = 12    /* Client.startOrUpdateCollaboration (client.ts:1133): seq/min_seq = currentSeq/minSeq */
+    MTR_OP_START_COLLAB = 12,   /* Client.startOrUpdateCollaboration (client.ts:1133): seq/min_seq = currentSeq/minSeq,
+                                   client = the observer's short id */
+    MTR_OP_LOAD = 13            /* a snapshot header segment (SnapshotLoader.loadHeader, snapshotLoader.ts:130-167):
+                                   consecutive LOAD records are built into the tree bottom-up by
+                                   MergeTree.reloadFromSegments (mergeTree.ts:678-728) before the next record */
 };
 
 /* op.flags */
@@ -38,8 +42,19 @@ enum {
     MTR_F_LAST = 1,    /* last member op of its message: run updateSeqNumbers(min_seq, seq) after it */
     MTR_F_MARKER = 2,  /* insert of a Marker segment (mergeTreeNodes.ts:557); payload = refType */
     MTR_F_PROPS = 4,   /* insert carries initial props: pos2 = prop-op index */
-    MTR_F_NOREF = 8    /* marker has no refType member ({"marker":{}}) */
+    MTR_F_NOREF = 8,   /* marker has no refType member ({"marker":{}}) */
+    MTR_F_APPEND = 16  /* insert at the end of the local view with refSeq = UniversalSequenceNumber
+                          (SnapshotLoader.loadBody append, snapshotLoader.ts:221-256) */
 };
+
+/*
+ * Snapshot segments (MTR_OP_LOAD, and MTR_OP_INSERT with MTR_F_APPEND) carry their merge info
+ * (specToSegment, snapshotLoader.ts:88-128): client = the segment's short id (0xFFFE =
+ * NonCollabClient), seq = its seq (0 = UniversalSequenceNumber), ref_seq = removedSeq or -1,
+ * min_seq = number of removedClientIds, pos1 = offset of those short ids (one UTF-16 unit each) in
+ * the document's text, pos2 = prop-op index or -1, payload/payload2 = text (or marker refType).
+ */
+#define MTR_CLIENT_NONCOLLAB 0xFFFEu
 
 typedef struct mtr_op {
     uint8_t  type;     /* MTR_OP_* */

@@ -761,11 +761,66 @@ class Tree {
         if (collaborating && seq != kUnassignedSeq) zamboniSegments();
     }
 
+    // ------------------------------------------------------------ snapshot load
+    // merge info of a snapshot segment, SnapshotLoader.specToSegment (snapshotLoader.ts:88-128)
+    static int opClient(const mtr_op& op) { return int(int16_t(op.client)); }
+    void setMergeInfo(Seg* s, const mtr_op& op, const mtr_doc_desc& dd) {
+        s->clientId = opClient(op);
+        s->seq = op.seq;
+        if (op.ref_seq >= 0) {
+            s->removed = true;
+            s->removedSeq = op.ref_seq;
+        }
+        s->removedClientIds.clear();
+        for (int k = 0; k < op.min_seq; k++) s->removedClientIds.push_back(int(tabs.b->text[dd.text_base + op.pos1 + k]));
+    }
+
+    // MergeTree.reloadFromSegments (mergeTree.ts:678-728): blocks of MaxNodesInBlock - 1 children,
+    // built bottom-up layer by layer
+    std::vector<Seg*> pendingLoad;
+    void reloadFromSegments() {
+        const int maxChildren = kMaxNodesInBlock - 1;
+        if (pendingLoad.empty()) {
+            root = makeBlock();
+            return;
+        }
+        std::vector<Node*> nodes(pendingLoad.begin(), pendingLoad.end());
+        pendingLoad.clear();
+        for (;;) {
+            const size_t blockCount = (nodes.size() + maxChildren - 1) / maxChildren;
+            std::vector<Node*> blocks;
+            for (size_t ni = 0, bi = 0; bi < blockCount; bi++) {
+                Block* b = makeBlock();
+                for (int ci = 0; ci < maxChildren && ni < nodes.size(); ci++, ni++) assignChild(b, nodes[ni], b->childCount++);
+                blocks.push_back(b);
+            }
+            if (blocks.size() == 1) {
+                root = static_cast<Block*>(blocks[0]);
+                root->parent = nullptr;
+                return;
+            }
+            nodes.swap(blocks);
+        }
+    }
+
     int apply(const mtr_op& op, const mtr_doc_desc& dd) {
         curOpSeq = op.seq;
+        if (op.type == MTR_OP_LOAD) {  // SnapshotLoader.loadHeader segments (snapshotLoader.ts:130-141)
+            if (collaborating) return MTR_ERR_ASSERT | 0x049;  // "Trying to reload from segments while collaborating!"
+            Seg* s = segmentFromSpec(op, dd);
+            setMergeInfo(s, op, dd);
+            pendingLoad.push_back(s);
+            return status;
+        }
+        if (!pendingLoad.empty()) reloadFromSegments();
         switch (op.type) {
             case MTR_OP_INSERT: {
                 Seg* s = segmentFromSpec(op, dd);
+                if (op.flags & MTR_F_APPEND) {  // SnapshotLoader.loadBody append (snapshotLoader.ts:221-256)
+                    setMergeInfo(s, op, dd);
+                    insertSegments(blockLocalLength(root), s, kUniversalSeq, opClient(op), op.seq);
+                    return status;
+                }
                 insertSegments(op.pos1, s, op.ref_seq, op.client, op.seq);
                 break;
             }
@@ -793,7 +848,7 @@ class Tree {
                 return status;
             case MTR_OP_START_COLLAB:  // startOrUpdateCollaboration -> startCollaboration, client.ts:1133, mergeTree.ts:731
                 if (collaborating) return MTR_OK;
-                localClientId = 0;
+                localClientId = opClient(op);
                 minSeq = op.min_seq;
                 currentSeq = op.seq;
                 collaborating = true;
@@ -1001,6 +1056,7 @@ int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint
 }
 
 int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap) {
+    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
     std::u16string s;
     d->tree.gatherText(d->tree.root, s);
     int64_t n = int64_t(s.size());
@@ -1009,10 +1065,12 @@ int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap) {
 }
 
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client) {
+    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
     return d->tree.nodeLength(d->tree.root, ref_seq, client);
 }
 
 void oracle_doc_state(oracle_doc* d, int64_t* out) {
+    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
     Tree& t = d->tree;
     std::vector<Seg*> lv;
     t.leaves(t.root, lv);
@@ -1023,6 +1081,7 @@ void oracle_doc_state(oracle_doc* d, int64_t* out) {
 }
 
 int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap, int32_t* height) {
+    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
     Tree& t = d->tree;
     std::vector<Seg*> lv;
     t.leaves(t.root, lv);
@@ -1064,6 +1123,7 @@ int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap, int32_t* hei
 // SnapshotLegacy (snapshotlegacy.ts:122-255) and the chunk serializers (snapshotChunks.ts:86-149).
 int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint8_t* out, int64_t cap,
                              int64_t* blob_len, int32_t max_blobs) {
+    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
     Tree& t = d->tree;
     t.tabs.b = b;
     Emitter em{b, &b->docs[doc_index]};

@@ -10,7 +10,7 @@ import pytest
 
 from fixtures import (SNAPSHOT_VERSIONS, blob_names, load_replay, load_snapshots, replay_files,
                       replay_log, snapshot_log)
-from fluidframework_amd.batch import Interner, build_batch
+from fluidframework_amd.batch import DocLog, Interner, build_batch
 from oracle.oracle import OracleDoc, options
 
 pytestmark = pytest.mark.gpu
@@ -121,3 +121,78 @@ def test_synthetic_record_mode_matches_oracle(writers, max_lag):
     assert np.array_equal(eng.hashes(n), ohash)
     _, rhash, rst = replay_batch(ob, 0, n, 16)
     assert np.array_equal(rhash, ohash)
+
+
+@pytest.mark.parametrize("v1", [True, False], ids=["v1", "legacy"])
+def test_load_snapshot_fixtures(v1):
+    """Client.load of every reference snapshot fixture on the device (reloadFromSegments + body
+    appends), then summarize: the fixture bytes come back, and the leaf structure equals the oracle's."""
+    keys = sorted(k for k in SNAPS if SNAPSHOT_VERSIONS[k.split("/")[0]] == v1)
+    it = Interner()
+    logs = []
+    for k in keys:
+        log = DocLog()
+        log.load_summary(SNAPS[k], "snapshot", it)
+        logs.append(log)
+    b = build_batch(logs, it)
+    eng = _engine(len(keys), snapshot_v1=v1, max_segments=16384, heap_entries=256)
+    eng.apply(b)
+    eng.summarize()
+    for d, k in enumerate(keys):
+        st, op = eng.status(d)
+        assert st == 0, f"{k}: status {st:#x} at op {op}"
+        orc = OracleDoc(options(snapshot_v1=v1))
+        assert orc.apply(b, d) == 0
+        _compare_export(eng, d, orc)
+        blobs = eng.summary(d)
+        got = dict(zip(blob_names(len(blobs), v1), blobs))
+        assert got == {n: v.encode("utf-8") for n, v in SNAPS[k].items()}, k
+
+
+def test_summarize_load_continue_on_device():
+    """Summarize the replay logs mid-collaboration on the device, load those summaries into new
+    documents, keep applying the remaining messages to both: text after every group equals
+    resultText, and the loaded documents match the oracle leaf-for-leaf and byte-for-byte."""
+    files = [p for p in replay_files() if "clients_8" in p]
+    all_groups = [load_replay(p) for p in files]
+    it = Interner()
+    logs = [replay_log(g, it) for g in all_groups]
+    cut = 32
+    for log, groups in zip(logs, all_groups):
+        for g in groups[:cut]:
+            for m in g["msgs"]:
+                log.message(m, it)
+        last = groups[cut - 1]["msgs"][-1]
+        log.seq_update(last["minimumSequenceNumber"], last["sequenceNumber"])
+    n = len(files)
+    eng = _engine(2 * n, ops_per_launch=64)
+    b = build_batch(logs + [DocLog() for _ in range(n)], it)
+    eng.apply(b)
+    eng.summarize()
+    loaded = []
+    for d in range(n):
+        blobs = eng.summary(d)
+        log = DocLog()
+        log.load_summary(dict(zip(blob_names(len(blobs), True), [x.decode() for x in blobs])), "snapshot", it)
+        loaded.append(log)
+    orcs = [OracleDoc(options()) for _ in range(n)]
+    b = build_batch([DocLog() for _ in range(n)] + loaded, it)
+    eng.apply(b)
+    for d in range(n):
+        assert orcs[d].apply(b, n + d) == 0
+        assert eng.text(n + d) == all_groups[d][cut - 1]["resultText"]
+    for gi in range(cut, 64):
+        for d, groups in enumerate(all_groups):
+            for m in groups[gi]["msgs"]:
+                logs[d].message(m, it)
+                loaded[d].message(m, it)
+        b = build_batch(logs + loaded, it)
+        eng.apply(b)
+        for d, groups in enumerate(all_groups):
+            assert orcs[d].apply(b, n + d) == 0
+            assert eng.status(n + d)[0] == 0
+            assert eng.text(d) == eng.text(n + d) == groups[gi]["resultText"], f"doc {d} group {gi}"
+    eng.summarize()
+    for d in range(n):
+        _compare_export(eng, n + d, orcs[d])
+        assert eng.summary(n + d) == orcs[d].summarize(b, n + d)
