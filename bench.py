@@ -106,7 +106,7 @@ def main():
 
     barrier()
     eng.sync()
-    apply_ms = summary_ms = 0.0
+    apply_ms = summary_ms = kernel_ms = 0.0
     launches = 0
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -115,6 +115,7 @@ def main():
         apply_ms += tm["apply_ms"]
         summary_ms += tm["summary_ms"]
         launches += tm["apply_launches"]
+        kernel_ms += tm["apply_kernel_ms"]
     eng.sync()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -159,8 +160,12 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
         "algorithmic_bytes_per_launch": b_step / launches_per_step,
-        "avg_launch_ms": apply_ms / max(1, launches),
+        "avg_launch_ms": kernel_ms / max(1, launches),
         "launches_per_step": launches_per_step,
+        "apply_wall_ms_per_step": apply_ms / a.steps,
+        "note": "achieved = algorithmic bytes of a step / apply wall time of the step; a round's size-class "
+                "launches overlap on 4 streams, so avg_launch_ms (each launch's own HIP-event duration, "
+                "comparable to rocprof) x launches exceeds the wall time",
         "model": "B_op = 16*S_d(t) + 32 + 2*L_ins (SURVEY.md 8d)",
     }
 

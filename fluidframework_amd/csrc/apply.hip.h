@@ -393,12 +393,12 @@ struct Eng {
 
     // stream compaction of leaves without M_DEL (zamboni unlink / append); rounds of 64 from the
     // bottom; destinations never exceed sources
-    static MTR_DI void compact(D& L, St& s) {
+    static MTR_DI void compact(D& L, St& s, int from) {
         PROF(P_COMPACT);
         PROF_COUNT(P_NCOMPACT);
         const int S = s.nseg;
-        int base = 0;
-        for (int lo = 0; lo < S; lo += 64) {
+        int base = from;
+        for (int lo = from; lo < S; lo += 64) {
             const int i = lo + lane_id();
             const bool act = i < S;
             int a0 = 0, a1 = 0, a2 = 0;
@@ -1025,15 +1025,15 @@ struct Eng {
     }
 
     // zamboniSegments body for one popped LRU entry whose segment is leaf x
-    // (zamboni.ts:33-58 + packParent zamboni.ts:63-120).  Returns 1 if leaves were marked for
-    // deletion (the caller compacts).
+    // (zamboni.ts:33-58 + packParent zamboni.ts:63-120).  Returns the first leaf index at or
+    // after which leaves may be marked for deletion (the caller compacts from there), or -1.
     static MTR_DI int zamboni_block(D& L, const KParams& P, St& s, int x) {
         PROF(P_ZBLOCK);
         PROF_COUNT(P_NZBLOCK);
         const lptr<Sc> sc = L.sc;
         const int H = s.height;
         const int rs1 = block_start(L, x, 1), re1 = block_end(L, s, x, 1);
-        if (ns_of(uniu(L.meta[rs1])) == NS_FALSE) return 0;
+        if (ns_of(uniu(L.meta[rs1])) == NS_FALSE) return -1;
         sc->rs[1] = rs1;
         sc->re[1] = re1;
         {
@@ -1065,13 +1065,15 @@ struct Eng {
                 wsync();
             }
         }
-        if (kept >= before) return 0;
+        if (kept >= before) return -1;
+        int from = rs1;
         if (kept < kMaxNodesInBlock / 2 && H > 1) {
             PROF(P_PACK);
             PROF_COUNT(P_NPACK);
             for (int l = 2; l <= H; l++) {  // packParent chain
                 const int ps = uni(sc->rs[l]), pe = uni(sc->re[l]);
                 if (l == 2) {
+                    from = ps;
                     // packParent scours every child of P again -- including the block just
                     // scoured: scourNode is not idempotent (a dropped tombstone no longer resets
                     // the merge candidate), zamboni.ts:68-73,122-193.
@@ -1113,7 +1115,7 @@ struct Eng {
                 if (!(c < kMaxNodesInBlock / 2 && l < H)) break;
             }
         }
-        return 1;
+        return from;
     }
 
     // zamboniSegments (zamboni.ts:19-60)
@@ -1126,7 +1128,8 @@ struct Eng {
             const uint32_t u = heap_pop(L, s);
             const int x = find_uid(L, s, u);
             if (x < 0) continue;
-            if (zamboni_block(L, P, s, x)) compact(L, s);
+            const int from = zamboni_block(L, P, s, x);
+            if (from >= 0) compact(L, s, from);
         }
     }
 
@@ -1213,16 +1216,32 @@ struct Eng {
                 return -1;
             }
             PROF(P_TEXTCOPY);
+        }
+        // the trailing-newline bit (TextSegment.canAppend) and "no newline at all" are known
+        // here for every text insert, so scour never has to read them back from the arena
+        bool nl = false, nonl = false;
+        if (!marker) {
+            bool any = false, last = false;
             if (pre) {
-                if (ln < len) L.gtext[t0 + ln] = uint16_t(pf);
+                if (ln < len) {
+                    L.gtext[t0 + ln] = uint16_t(pf);
+                    any = pf == u'\n';
+                    last = any && ln == len - 1;
+                }
             } else {
                 const gptr<const uint16_t> src = gp(P.btext) + dd.text_base + op.payload;
-                for (int k = ln; k < len; k += 64) L.gtext[t0 + k] = src[k];
+                for (int k = ln; k < len; k += 64) {
+                    const uint16_t u = src[k];
+                    L.gtext[t0 + k] = u;
+                    if (u == u'\n') {
+                        any = true;
+                        last = last || k == len - 1;
+                    }
+                }
             }
+            nonl = __ballot(any) == 0;
+            nl = __ballot(last) != 0;
         }
-        const uint64_t nlm = pre ? __ballot(ln < len && pf == u'\n') : 0;
-        const bool nl = pre && ((nlm >> (len - 1)) & 1);
-        const bool nonl = pre && nlm == 0;
         const int S = s.nseg;
         int slot = -1, inherit = 0;
         {
@@ -1252,7 +1271,7 @@ struct Eng {
         shift_right1(L, s, slot);
         uint32_t m = client & M_CLIENT_MASK;
         if (marker) m |= M_MARKER;
-        else m |= pre ? ((nl ? M_NL : 0u) | (nonl ? M_NONL : 0u)) : M_NLQ;
+        else m |= (nl ? M_NL : 0u) | (nonl ? M_NONL : 0u);
         if (op.flags & MTR_F_NOREF) m |= M_NOREF;
         if (S == 0) {
             s.height = 1;

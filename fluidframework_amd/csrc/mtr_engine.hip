@@ -75,6 +75,12 @@ struct mtr_engine {
     uint32_t max_docs = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {};
+    // size-class launches of one apply round run concurrently: class i on lane[i % kLanes]
+    // (lane 0 = `stream`), joined back into `stream` before the next round
+    static constexpr int kLanes = 4;
+    hipStream_t aux[kLanes - 1] = {};
+    hipEvent_t lane_done[kLanes] = {};
+    std::vector<hipEvent_t> kev;  // per-launch start/stop events (kernel durations)
     // persistent document state
     DevBuf<DocHdr> hdr;
     DevBuf<uint32_t> seg, heap, prop, rm;
@@ -108,6 +114,7 @@ struct mtr_engine {
     bool summarized = false;
     // timing
     double t_apply = 0, t_summary = 0;
+    double t_kernels = 0;  // sum of the apply launches' own durations (they overlap across lanes)
     int launches = 0;
 };
 
@@ -213,6 +220,8 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
         return nullptr;
     }
     for (auto& x : e->ev) (void)hipEventCreate(&x);
+    for (auto& x : e->aux) (void)hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+    for (auto& x : e->lane_done) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
     const size_t D = std::max<uint32_t>(max_docs, 1);
     if (e->hdr.ensure(D) || e->seg.ensure(D * NF * c.max_segments) || e->heap.ensure(D * 2 * c.heap_entries) ||
         e->text.ensure(D * c.text_units) || e->prop.ensure(D * c.prop_words) || e->rm.ensure(D * c.remover_cells) ||
@@ -259,6 +268,15 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->out.release();
     for (auto& x : e->ev)
         if (x) (void)hipEventDestroy(x);
+    for (auto& x : e->kev)
+        if (x) (void)hipEventDestroy(x);
+    for (auto& x : e->lane_done)
+        if (x) (void)hipEventDestroy(x);
+    for (auto& x : e->aux)
+        if (x) {
+            (void)hipStreamSynchronize(x);
+            (void)hipStreamDestroy(x);
+        }
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return 0;
@@ -325,6 +343,7 @@ static int run_impl(mtr_engine* e, int gen) {
     const int K = int(e->caps.ops_per_launch ? e->caps.ops_per_launch : 0x7fffffff);
     e->launches = 0;
     e->t_apply = 0;
+    e->t_kernels = 0;
     KParams P{};
     P.hdr = e->hdr.p;
     P.seg = e->seg.p;
@@ -384,6 +403,7 @@ static int run_impl(mtr_engine* e, int gen) {
         const int k = std::min(K, rem);
         bool stuck = false;
         HIPCHK(hipEventRecord(e->ev[0], e->stream));
+        int nl = 0;  // launches of this round
         for (int c = kClasses - 1; c >= 0; c--) {  // one launch per size class, largest documents first
             const int cnt = cls[1 + 3 * c], maxseg = cls[2 + 3 * c], maxheap = cls[3 + 3 * c];
             if (cnt <= 0) continue;
@@ -408,16 +428,36 @@ static int run_impl(mtr_engine* e, int gen) {
             P.ops_this_launch = kk;
             P.doc_list = e->dlist.p + size_t(c) * e->n_docs;
             P.n_launch = uint32_t(cnt);
-            if (P.global_mode) apply_kernel<true><<<cnt, NT, lds, e->stream>>>(P);
-            else apply_kernel<false><<<cnt, NT, lds, e->stream>>>(P);
+            const int lane = nl % mtr_engine::kLanes;
+            hipStream_t st = lane == 0 ? e->stream : e->aux[lane - 1];
+            if (lane != 0 && nl < mtr_engine::kLanes) HIPCHK(hipStreamWaitEvent(st, e->ev[0], 0));
+            while (e->kev.size() < size_t(2 * (nl + 1))) {
+                hipEvent_t x;
+                HIPCHK(hipEventCreate(&x));
+                e->kev.push_back(x);
+            }
+            HIPCHK(hipEventRecord(e->kev[2 * nl], st));
+            if (P.global_mode) apply_kernel<true><<<cnt, NT, lds, st>>>(P);
+            else apply_kernel<false><<<cnt, NT, lds, st>>>(P);
             HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(e->kev[2 * nl + 1], st));
             e->launches++;
+            nl++;
+        }
+        for (int l = 1; l < std::min(nl, int(mtr_engine::kLanes)); l++) {  // join the lanes
+            HIPCHK(hipEventRecord(e->lane_done[l], e->aux[l - 1]));
+            HIPCHK(hipStreamWaitEvent(e->stream, e->lane_done[l], 0));
         }
         HIPCHK(hipEventRecord(e->ev[1], e->stream));
         HIPCHK(hipEventSynchronize(e->ev[1]));
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
         e->t_apply += ms;
+        for (int q = 0; q < nl; q++) {
+            float kms = 0;
+            HIPCHK(hipEventElapsedTime(&kms, e->kev[2 * q], e->kev[2 * q + 1]));
+            e->t_kernels += kms;
+        }
         if (stuck) {
             set_err("document exceeds the leaf capacity");
             break;
@@ -733,8 +773,8 @@ int mtr_stats(mtr_engine* e, int64_t* out, int32_t n) {
 }
 
 int mtr_last_timing(mtr_engine* e, double* out, int32_t n) {
-    double v[3] = {e->t_apply, e->t_summary, double(e->launches)};
-    for (int i = 0; i < n && i < 3; i++) out[i] = v[i];
+    double v[4] = {e->t_apply, e->t_summary, double(e->launches), e->t_kernels};
+    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
     return MTR_OK;
 }
 

@@ -209,9 +209,10 @@ class Engine:
         return dict(zip(PROFILE_KEYS, (int(x) for x in out)))
 
     def timing(self) -> dict:
-        out = np.zeros(3, dtype="<f8")
-        lib().mtr_last_timing(self.h, out.ctypes.data, 3)
-        return {"apply_ms": float(out[0]), "summary_ms": float(out[1]), "apply_launches": int(out[2])}
+        out = np.zeros(4, dtype="<f8")
+        lib().mtr_last_timing(self.h, out.ctypes.data, 4)
+        return {"apply_ms": float(out[0]), "summary_ms": float(out[1]), "apply_launches": int(out[2]),
+                "apply_kernel_ms": float(out[3])}
 
 
 PROFILE_KEYS = ["op", "prefix", "split", "shift", "insert", "range", "zamboni", "zblock", "compact", "find_uid",

@@ -95,8 +95,9 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap_leaves
  * before the op, out[9]=UTF-16 units inserted.  Counters accumulate from mtr_reset. */
 int mtr_stats(mtr_engine* e, int64_t* out, int32_t n);
 
-/* Device time (ms) of the last mtr_run / mtr_summarize measured with HIP events on the
- * engine stream: out[0]=apply, out[1]=summarize, out[2]=apply kernel launches. */
+/* Device time (ms) of the last mtr_run / mtr_summarize measured with HIP events: out[0]=apply
+ * (wall, engine stream), out[1]=summarize, out[2]=apply kernel launches, out[3]=sum of the apply
+ * launches' own durations (a round's size-class launches overlap on up to 4 streams). */
 int mtr_last_timing(mtr_engine* e, double* out, int32_t n);
 
 /* Record mode (synthetic workloads, include/mtr_synth.h): draw cfg->n_docs documents' op logs
