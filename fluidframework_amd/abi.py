@@ -14,6 +14,8 @@ OP_LOCAL_REMOVE = 9
 OP_LOCAL_ANNOTATE = 10
 OP_START_COLLAB = 12
 OP_LOAD = 13
+OP_SETCELL = 14
+HANDLE_UNALLOCATED = -0x80000000
 CLIENT_NONCOLLAB = 0xFFFE
 
 F_LAST = 1
@@ -21,6 +23,7 @@ F_MARKER = 2
 F_PROPS = 4
 F_NOREF = 8
 F_APPEND = 16
+F_COLS = 32
 
 NULL_VALUE = 0xFFFFFFFF
 NOT_INDEX = 0xFFFFFFFF

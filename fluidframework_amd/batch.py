@@ -250,6 +250,79 @@ class DocLog:
                 raise Unsupported(f"op type {t}")
 
 
+@dataclass
+class MatrixLog(DocLog):
+    """Host state of one SharedMatrix (SharedMatrix.processCore, matrix.ts:636-693, remote branch):
+    vector ops (``contents.target`` "rows" / "cols") are merge-tree ops on that PermutationVector,
+    whose segment specs are ``[length, start]`` (PermutationSegment.fromJSONObject,
+    permutationvector.ts:45-48; the remote ``start`` is discarded by ``reset()`` on INSERT); a set-cell
+    message becomes one MTR_OP_SETCELL record.  Both vectors share this log's client table (short ids
+    are only compared for equality and mapped back to long ids in summaries)."""
+
+    def start_collab(self, long_id: str, min_seq: int = 0, current_seq: int = 0) -> None:
+        """startOrUpdateCollaboration on both vectors (SharedMatrix.onConnect, matrix.ts:523-532)."""
+        super().start_collab(long_id, min_seq, current_seq)
+
+    def message(self, msg: dict, interner: Interner) -> None:
+        cid = msg.get("clientId")
+        cid = "null" if cid is None else str(cid)
+        if msg.get("type") != "op":
+            return  # SharedMatrix has no MSN handler: only its vectors' own messages move their windows
+        if cid == self.observer_id:
+            raise Unsupported("message authored by the observer (local ack path)")
+        short = self.short_id(cid)
+        seq = int(msg["sequenceNumber"])
+        ref = int(msg["referenceSequenceNumber"])
+        msn = int(msg["minimumSequenceNumber"])
+        contents = msg["contents"]
+        if isinstance(contents, str):
+            contents = parse(contents)
+        target = contents.get("target")
+        if target is None:  # MatrixOp.set (matrix/src/ops.ts:8-12)
+            if contents.get("type") != 2:
+                raise Unsupported("matrix message without a target")
+            self.ops.append((abi.OP_SETCELL, 0, short, seq, ref, msn, int(contents["row"]), int(contents["col"]), 0, 0))
+            return
+        if target not in ("rows", "cols"):
+            raise Unsupported(f"matrix target {target!r}")
+        tf = abi.F_COLS if target == "cols" else 0
+        members = contents["ops"] if contents.get("type") == 3 else [contents]
+        if not members:
+            self.ops.append((abi.OP_SEQ, abi.F_LAST | tf, short, seq, ref, msn, 0, 0, 0, 0))
+            return
+        for i, op in enumerate(members):
+            last = (abi.F_LAST if i == len(members) - 1 else 0) | tf
+            t = op.get("type")
+            if "relativePos1" in op or "relativePos2" in op:
+                raise Unsupported("relative positions")
+            if t == 0:
+                seg = op.get("seg")
+                if seg is None:
+                    self.ops.append((abi.OP_SEQ, last, short, seq, ref, msn, 0, 0, 0, 0))
+                    continue
+                if not (isinstance(seg, list) and len(seg) == 2):
+                    raise Unsupported("PermutationSegment spec")
+                self.ops.append((abi.OP_INSERT, last, short, seq, ref, msn, int(op["pos1"]), -1, 0, int(seg[0])))
+            elif t == 1:
+                self.ops.append((abi.OP_REMOVE, last, short, seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0))
+            else:
+                raise Unsupported(f"vector op type {t}")
+
+    def cols_log(self) -> DocLog:
+        """The cols vector's engine document: no ops of its own, the same client table."""
+        return DocLog(observer_id=self.observer_id, clients=list(self.clients), client_ix=dict(self.client_ix))
+
+
+def matrix_logs(logs: list[MatrixLog]) -> list[DocLog]:
+    """Engine document order for matrices: [rows 0, cols 0, rows 1, cols 1, ...]
+    (declare each pair with Engine.set_matrix(2 m, 2 m + 1))."""
+    out: list[DocLog] = []
+    for m in logs:
+        out.append(m)
+        out.append(m.cols_log())
+    return out
+
+
 class Batch:
     """Numpy-backed arrays + the ctypes MtrBatch view of them (keeps the arrays alive)."""
 

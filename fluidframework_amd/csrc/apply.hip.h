@@ -152,6 +152,10 @@ struct KParams {
     const uint32_t* key_index;
     const uint32_t* val_eq;
     unsigned long long* stat_ops;  // [doc][4]: ops applied, sum of leaves before ops, inserted units
+    // SharedMatrix pairs (mtr_set_matrix): dkind[doc] 0 = SharedString, 1 = rows PermutationVector
+    // (drives the pair; dpart[doc] = its cols document), 2 = cols PermutationVector
+    const uint32_t* dkind;
+    const uint32_t* dpart;
     // record mode (synthetic workloads): ops are drawn from include/mtr_synth.h with this
     // engine's own exact view lengths, written to gen_ops/gen_text, then applied
     int32_t gen;
@@ -180,7 +184,7 @@ struct Sc {
 struct St {
     int nseg, height, minseq, curseq;
     int collab, local, heapn, uidnext;
-    int textused, propused, rmused, status;
+    int textused, propused, rmused, status;  // textused: handle-table length for permutation vectors
     int fail_op, max_heap, ops_done, texthalf;
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
@@ -288,7 +292,10 @@ struct ProfScope {
 #define PROF_COUNT(id)
 #endif
 
-template <bool G>
+// G: leaves in HBM (documents larger than LDS); PM: PermutationVector documents (SharedMatrix
+// rows/cols, permutationvector.ts) -- a separate instantiation so the SharedString kernel carries
+// no permutation code
+template <bool G, bool PM = false>
 struct Eng {
     using D = Doc<G>;
     template <class T>
@@ -840,6 +847,52 @@ struct Eng {
         if (carry > half) s.status = MTR_ERR_CAPACITY;
     }
 
+    // ------------------------------------------------------------ HandleTable (matrix/src/handletable.ts)
+    // A permutation vector keeps its HandleTable in its (otherwise unused) text arena as int32
+    // words; handles[0] is the head of the free list, s.textused the array length.
+    static MTR_DI gptr<int32_t> handles(const D& L) { return (gptr<int32_t>)L.gtext; }
+    static MTR_DI int handle_cap(const KParams& P) { return P.tcap / 2; }
+    // HandleTable.allocate, handletable.ts:37-42
+    static MTR_DI int alloc_handle(D& L, const KParams& P, St& s) {
+        const gptr<int32_t> h = handles(L);
+        const int fr = uni(h[0]);
+        const int hlen = s.textused;
+        int nx;
+        if (fr < hlen) {
+            nx = uni(h[fr]);
+        } else {  // handles[free] === undefined: the array grows by one
+            if (hlen + 1 > handle_cap(P)) {
+                s.status = MTR_ERR_CAPACITY;
+                return MTR_HANDLE_UNALLOCATED;
+            }
+            nx = fr + 1;
+            s.textused = hlen + 1;
+        }
+        if (lane_id() == 0) {
+            h[fr] = 0;
+            h[0] = nx;
+        }
+        wsync();
+        return fr;
+    }
+    // HandleTable.free of handles a, a+1, ..., a+n-1 in that order (onMaintenance UNLINK frees a
+    // segment's handles in ascending order, permutationvector.ts:418-443): handles[a] = old head,
+    // handles[a+q] = a+q-1, head = a+n-1
+    static MTR_DI void free_handles(D& L, int a, int n) {
+        const gptr<int32_t> h = handles(L);
+        const int head = uni(h[0]);
+        for (int q = lane_id(); q < n; q += 64) h[a + q] = q == 0 ? head : a + q - 1;
+        wsync();
+        if (lane_id() == 0) h[0] = a + n - 1;
+        wsync();
+    }
+    // PermutationSegment.canAppend (permutationvector.ts:131-137) of a chain whose head starts at
+    // handle pt with accumulated length pl, and a segment starting at handle t
+    static MTR_DI bool perm_contig(uint32_t pt, int pl, uint32_t t) {
+        return pt == uint32_t(MTR_HANDLE_UNALLOCATED) ? t == uint32_t(MTR_HANDLE_UNALLOCATED)
+                                                      : t == pt + uint32_t(pl);
+    }
+
     // ------------------------------------------------------------ zamboni
     // scourNode (zamboni.ts:122-193) over the child blocks in [cs, ce): a new child block starts at
     // every leaf with bnd >= 1.  Marks M_DEL; returns #kept (used for a single block).  The leaves
@@ -847,10 +900,10 @@ struct Eng {
     static MTR_DI int scour_range(D& L, const KParams& P, St& s, int cs, int ce) {
         const int minseq = s.minseq;
         int prev = -1, kept = 0, plen = 0;
-        uint32_t pmeta = 0, pprops = 0;
+        uint32_t pmeta = 0, pprops = 0, ptext = 0;
         for (int base = cs; base < ce; base += 64) {
             const int i = base + lane_id();
-            uint32_t vm = M_DEL, vp = 0;
+            uint32_t vm = M_DEL, vp = 0, vt = 0;
             int vr = 0, vs = 0, vl = 0;
             if (i < ce) {
                 vm = L.meta[i];
@@ -858,9 +911,11 @@ struct Eng {
                 vs = L.seq[i];
                 vl = L.len[i];
                 vp = L.props[i];
+                vt = L.text[i];
             }
             {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
-                const bool q = (vm & (M_NLQ | M_DEL | M_MARKER)) == M_NLQ && vl > 0 && vr == RNONE && vs <= minseq;
+                const bool q = !PM && (vm & (M_NLQ | M_DEL | M_MARKER)) == M_NLQ && vl > 0 && vr == RNONE &&
+                               vs <= minseq;
                 if (__ballot(q)) {
                     PROF(P_NLQ);
                     PROF_COUNT(P_NNLQ);
@@ -885,13 +940,22 @@ struct Eng {
                     } else {
                         L.meta[k] = m | M_DEL;  // UNLINK
                         wsync();
+                        const uint32_t tk = rdlane(vt, t);
+                        if (PM && tk != uint32_t(MTR_HANDLE_UNALLOCATED)) free_handles(L, int(tk), rdlane(vl, t));
                     }
                     prev = -1;
                 } else if (rdlane(vs, t) <= minseq) {
                     const int lk = rdlane(vl, t);
                     const uint32_t pk = rdlane(vp, t);
-                    if (prev >= 0 && lk > 0 && can_append(pmeta, plen, m, lk) && props_match_w(L, P, pprops, pk)) {
-                        text_append(L, P, s, prev, k);
+                    const uint32_t tk = rdlane(vt, t);
+                    const bool ca = PM ? perm_contig(ptext, plen, tk) : can_append(pmeta, plen, m, lk);
+                    if (prev >= 0 && lk > 0 && ca && props_match_w(L, P, pprops, pk)) {
+                        if (PM) {
+                            L.len[prev] = plen + lk;
+                            wsync();
+                        } else {
+                            text_append(L, P, s, prev, k);
+                        }
                         plen += lk;
                         pmeta = (pmeta & ~(M_NL | M_NLQ | (m & M_NONL ? 0u : M_NONL))) | (m & (M_NL | M_NLQ));
                         L.meta[prev] = pmeta;
@@ -904,6 +968,7 @@ struct Eng {
                             pmeta = m;
                             plen = lk;
                             pprops = pk;
+                            ptext = tk;
                         } else {
                             prev = -1;
                         }
@@ -945,7 +1010,7 @@ struct Eng {
         const bool removed = vr != RNONE;
         const bool cand = !pre && !removed && vs <= minseq && vl > 0;
         {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
-            const bool q = cand && (vm & (M_NLQ | M_MARKER)) == M_NLQ;
+            const bool q = cand && !PM && (vm & (M_NLQ | M_MARKER)) == M_NLQ;
             if (__ballot(q)) {
                 PROF(P_NLQ);
                 PROF_COUNT(P_NNLQ);
@@ -967,12 +1032,25 @@ struct Eng {
         const uint32_t pp = uint32_t(__shfl(int(vp), ps));
         const uint64_t upto = (uint64_t(2) << ln) - 1;  // lanes <= ln
         const uint64_t after_p = p < 0 ? ~uint64_t(0) : ~((uint64_t(2) << p) - 1);
-        bool link = cand && p >= 0 && pc && !(bm & upto & after_p) && !((vm | pm) & M_MARKER) && !(pm & M_NL);
+        bool link = cand && p >= 0 && pc && !(bm & upto & after_p);
+        if (PM) {  // handle contiguity with the previous chain member (permutationvector.ts:131-137)
+            const uint32_t pt = uint32_t(__shfl(int(vt), ps));
+            const int pl = __shfl(vl, ps);
+            link = link && perm_contig(pt, pl, vt);
+        } else {
+            link = link && !((vm | pm) & M_MARKER) && !(pm & M_NL);
+        }
         if (link && vp != pp) link = props_match(L.gprop, gp(P.val_eq), pp, vp);
-        if (__ballot(link && vl > kGranularity)) return -1;
+        if (!PM && __ballot(link && vl > kGranularity)) return -1;
         const bool unlink = !pre && removed && vr <= minseq;
         const uint64_t lm = __ballot(link);
         if (unlink || link) L.meta[i] = vm | M_DEL;
+        if (PM) {  // UNLINK frees the segment's handles, in leaf order
+            for (uint64_t um = __ballot(unlink && vt != uint32_t(MTR_HANDLE_UNALLOCATED)); um; um &= um - 1) {
+                const int l = first_lane(um);
+                free_handles(L, int(rdlane(vt, l)), rdlane(vl, l));
+            }
+        }
         const int kept = __popcll(__ballot(in && !pre && !unlink && !link));
         if (lm) {  // concatenate each chain's text behind its head (prev.append, textSegment.ts:99-103)
             const uint64_t hm = __ballot(in && !pre && !link);  // chain heads and unmerged leaves
@@ -992,6 +1070,12 @@ struct Eng {
                 todo &= ~mem;
                 const int e = last_lane(mem);
                 const int total = rdlane(incl, e) - rdlane(incl - vl, h);
+                if (PM) {  // BaseSegment.append: lengths only
+                    if (ln == 0) L.len[cs + h] = total;
+                    PROF_COUNT(P_NMERGE);
+                    wsync();
+                    continue;
+                }
                 const uint32_t th = rdlane(vt, h);
                 const int lh = rdlane(vl, h);
                 const bool mine = ((mem >> ln) & 1) != 0;
@@ -1184,7 +1268,10 @@ struct Eng {
             L.rseq[r] = uni(L.rseq[j]);
             L.meta[r] = set_ns(set_bnd(mj, 0), NS_UNDEF);
             L.meta[j] = (mj & M_NONL) ? (mj & ~M_NL) : ((mj & ~M_NL) | M_NLQ);
-            L.text[r] = uniu(L.text[j]) + uint32_t(off);
+            {  // TextSegment: text offset; PermutationSegment: start + pos unless unallocated
+                const uint32_t tj = uniu(L.text[j]);
+                L.text[r] = tj == uint32_t(MTR_HANDLE_UNALLOCATED) ? tj : tj + uint32_t(off);
+            }
             L.props[r] = uniu(L.props[j]);
             L.rm[r] = uniu(L.rm[j]);
             L.uid[r] = uint32_t(s.uidnext++);
@@ -1210,7 +1297,7 @@ struct Eng {
         if (len <= 0) return -1;  // blockInsert skips empty segments
         const int t0 = s.textused;
         const int ln = lane_id();
-        if (!marker) {  // copy the op's text into the document arena
+        if (!marker && !PM) {  // copy the op's text into the document arena
             if (t0 + len > text_end(s, P)) {
                 s.status = MTR_ERR_CAPACITY;
                 return -1;
@@ -1220,7 +1307,7 @@ struct Eng {
         // the trailing-newline bit (TextSegment.canAppend) and "no newline at all" are known
         // here for every text insert, so scour never has to read them back from the arena
         bool nl = false, nonl = false;
-        if (!marker) {
+        if (!marker && !PM) {
             bool any = false, last = false;
             if (pre) {
                 if (ln < len) {
@@ -1285,8 +1372,9 @@ struct Eng {
         L.seq[slot] = seq;
         L.rseq[slot] = RNONE;
         L.meta[slot] = m;
-        L.text[slot] = marker ? op.payload : uint32_t(t0);
-        if (!marker) s.textused = t0 + len;
+        // PermutationSegment: start reset to unallocated on INSERT (permutationvector.ts:354-361)
+        L.text[slot] = marker ? op.payload : (PM ? uint32_t(MTR_HANDLE_UNALLOCATED) : uint32_t(t0));
+        if (!marker && !PM) s.textused = t0 + len;
         uint32_t pr = NONE32;
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[slot] = pr;
@@ -1526,6 +1614,10 @@ struct Eng {
             s.sum_s = 0;
             s.sum_l = 0;
         }
+        if (PM && s.textused == 0) {  // new HandleTable: handles = [1] (handletable.ts:24)
+            if (threadIdx.x == 0) handles(L)[0] = 1;
+            s.textused = 1;
+        }
         if (threadIdx.x == 0) {
 #ifdef MTR_PROF
             for (int q = 0; q < P_COUNT; q++) L.sc->prof[q] = 0;
@@ -1654,12 +1746,125 @@ struct Eng {
         L.grm = gp(P.rm) + size_t(d) * P.rcap;
     }
 
+    // ------------------------------------------------------------ one op
+    // Client.applyMsg for one member op (client.ts:858-887): dispatch, zamboni after the op, then
+    // updateSeqNumbers on the message's last member op.  Returns false when the document stops
+    // (s.status != MTR_OK; s.fail_op = gidx).
+    static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
+                                uint32_t pf, int gidx) {
+        s.sum_s += (unsigned long long)s.nseg;
+        if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER) && !PM)
+            s.sum_l += (unsigned long long)op.payload2;
+        if (!PM) {  // text arena: keep room for this op's text plus zamboni merge copies
+            const int need = int(op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT ? op.payload2 : 0) + 4096;
+            if (s.textused + need > text_end(s, P)) text_gc(L, P, s);
+        }
+        if (s.nseg + 2 >= L.cap) s.status = MTR_ERR_CAPACITY;  // every op adds at most two leaves
+        if (s.status != MTR_OK) {
+            s.fail_op = gidx;
+            return false;
+        }
+        if (op.type == MTR_OP_LOAD) {  // SnapshotLoader.loadHeader segment
+            load_leaf(L, P, s, op, dd);
+            if (s.status != MTR_OK) {
+                s.fail_op = gidx;
+                return false;
+            }
+            return true;
+        }
+        if (s.height == 0) finish_load(L, s);
+        const bool local_op = op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE;
+        int zop = 0;
+        View v;
+        int seq = op.seq;
+        uint32_t client = enc_client(int(int16_t(op.client)));
+        if (local_op) {
+            if (s.collab) {
+                s.status = MTR_ERR_UNSUPPORTED;
+                s.fail_op = gidx;
+                return false;
+            }
+            v.ref = s.curseq;
+            v.client = CL_LOCAL;
+            v.local = 1;
+            seq = 0;
+            client = CL_LOCAL;
+        } else {
+            // a snapshot body append walks at (UniversalSequenceNumber, segment client)
+            v.ref = (op.flags & MTR_F_APPEND) ? 0 : op.ref_seq;
+            v.client = client;
+            v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
+        }
+        switch (op.type) {
+            case MTR_OP_INSERT:
+            case MTR_OP_LOCAL_INSERT: {
+                int pos = op.pos1;
+                if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
+                prefix(L, s, v, P.new_length_calc);
+                split_at(L, s, pos);
+                insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf);
+                zop = s.collab;
+                break;
+            }
+            case MTR_OP_REMOVE:
+            case MTR_OP_LOCAL_REMOVE:
+            case MTR_OP_ANNOTATE:
+            case MTR_OP_LOCAL_ANNOTATE: {
+                const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
+                prefix(L, s, v, P.new_length_calc);
+                split_at(L, s, op.pos1);
+                split_at(L, s, op.pos2);
+                range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload);
+                zop = s.collab;
+                break;
+            }
+            case MTR_OP_SEQ:
+                break;
+            case MTR_OP_START_COLLAB:
+                if (!s.collab) {
+                    s.collab = 1;
+                    s.local = int(enc_client(int(int16_t(op.client))));
+                    s.minseq = op.min_seq;
+                    s.curseq = op.seq;
+                    s.heapn = 0;
+                }
+                break;
+            default:
+                s.status = MTR_ERR_BAD_OP;
+                break;
+        }
+        // zamboniSegments after the op (mergeTree.ts:1420-1426, 1948-1952, 2042-2046), then
+        // updateSeqNumbers, whose minSeq advance runs it again (mergeTree.ts:1037-1042)
+        const bool upd = !local_op && op.type != MTR_OP_START_COLLAB && (op.flags & MTR_F_LAST);
+        for (int phase = 0; phase < 2; phase++) {
+            int zrun = zop;
+            if (phase == 1) {
+                if (!upd || s.status != MTR_OK) break;
+                PROF(P_UPDSEQ);
+                zrun = update_seq(s, op.min_seq, op.seq);
+            }
+            if (zrun) zamboni(L, P, s);
+        }
+        if (s.status != MTR_OK) {
+            s.fail_op = gidx;
+            return false;
+        }
+        return true;
+    }
+
     // ------------------------------------------------------------ per-document driver
     static MTR_DI void run(char* smem, const KParams& P, uint32_t d) {
         const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
         const int cursor = uni(gp(P.hdr)[d].op_cursor);
         const int n_ops = min(int(dd.op_count) - cursor, P.ops_this_launch);
         if (n_ops <= 0 || uni(gp(P.hdr)[d].status) != MTR_OK) return;
+        if (P.dkind && uniu(gp(P.dkind)[d]) != 0) {  // a cols vector has no op list of its own
+            if (lane_id() == 0) {
+                gp(P.hdr)[d].status = MTR_ERR_BAD_OP;
+                gp(P.hdr)[d].fail_op = cursor;
+            }
+            return;
+        }
         D L;
         carve(L, smem, P, d);
         St s;
@@ -1702,107 +1907,111 @@ struct Eng {
                     }
                 }
             }
-            s.sum_s += (unsigned long long)s.nseg;
-            if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER))
-                s.sum_l += (unsigned long long)op.payload2;
-            {  // text arena: keep room for this op's text plus zamboni merge copies
-                const int need =
-                    int(op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT ? op.payload2 : 0) + 4096;
-                if (s.textused + need > text_end(s, P)) text_gc(L, P, s);
-            }
-            if (s.nseg + 2 >= L.cap) s.status = MTR_ERR_CAPACITY;  // every op adds at most two leaves
-            if (s.status != MTR_OK) break;
-            if (op.type == MTR_OP_LOAD) {  // SnapshotLoader.loadHeader segment
-                load_leaf(L, P, s, op, dd);
-                if (s.status != MTR_OK) {
-                    s.fail_op = cursor + k;
-                    break;
-                }
-                s.ops_done = k + 1;
-                continue;
-            }
-            if (s.height == 0) finish_load(L, s);
-            const bool local_op = op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE;
-            int zop = 0;
-            View v;
-            int seq = op.seq;
-            uint32_t client = enc_client(int(int16_t(op.client)));
-            if (local_op) {
-                if (s.collab) {
-                    s.status = MTR_ERR_UNSUPPORTED;
-                    s.fail_op = cursor + k;
-                    break;
-                }
-                v.ref = s.curseq;
-                v.client = CL_LOCAL;
-                v.local = 1;
-                seq = 0;
-                client = CL_LOCAL;
-            } else {
-                // a snapshot body append walks at (UniversalSequenceNumber, segment client)
-                v.ref = (op.flags & MTR_F_APPEND) ? 0 : op.ref_seq;
-                v.client = client;
-                v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
-            }
-            switch (op.type) {
-                case MTR_OP_INSERT:
-                case MTR_OP_LOCAL_INSERT: {
-                    int pos = op.pos1;
-                    if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
-                    prefix(L, s, v, P.new_length_calc);
-                    split_at(L, s, pos);
-                    insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf);
-                    zop = s.collab;
-                    break;
-                }
-                case MTR_OP_REMOVE:
-                case MTR_OP_LOCAL_REMOVE:
-                case MTR_OP_ANNOTATE:
-                case MTR_OP_LOCAL_ANNOTATE: {
-                    const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
-                    prefix(L, s, v, P.new_length_calc);
-                    split_at(L, s, op.pos1);
-                    split_at(L, s, op.pos2);
-                    range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload);
-                    zop = s.collab;
-                    break;
-                }
-                case MTR_OP_SEQ:
-                    break;
-                case MTR_OP_START_COLLAB:
-                    if (!s.collab) {
-                        s.collab = 1;
-                        s.local = int(enc_client(int(int16_t(op.client))));
-                        s.minseq = op.min_seq;
-                        s.curseq = op.seq;
-                        s.heapn = 0;
-                    }
-                    break;
-                default:
-                    s.status = MTR_ERR_BAD_OP;
-                    break;
-            }
-            // zamboniSegments after the op (mergeTree.ts:1420-1426, 1948-1952, 2042-2046), then
-            // updateSeqNumbers, whose minSeq advance runs it again (mergeTree.ts:1037-1042)
-            const bool upd = !local_op && op.type != MTR_OP_START_COLLAB && (op.flags & MTR_F_LAST);
-            for (int phase = 0; phase < 2; phase++) {
-                int zrun = zop;
-                if (phase == 1) {
-                    if (!upd || s.status != MTR_OK) break;
-                    PROF(P_UPDSEQ);
-                    zrun = update_seq(s, op.min_seq, op.seq);
-                }
-                if (zrun) zamboni(L, P, s);
-            }
-            if (s.status != MTR_OK) {
-                s.fail_op = cursor + k;
-                break;
-            }
+            if (!apply_op(L, P, s, op, dd, pre, pf, cursor + k)) break;
             s.ops_done = k + 1;
         }
         // a batch that ends with header segments: build the tree now (queries read it next)
         if (s.height == 0 && s.status == MTR_OK && cursor + s.ops_done >= int(dd.op_count)) finish_load(L, s);
         store_doc(L, P, s, d);
+    }
+
+    // ------------------------------------------------------------ SharedMatrix
+    // PermutationVector.adjustPosition (permutationvector.ts:232-247): getContainingSegment at the
+    // op's (refSeq, clientId) view (mergeTree.ts:795-813), undefined for a removed segment, else
+    // its local-view position (getPosition, mergeTree.ts:768-785) plus the offset.  -1 = undefined.
+    static MTR_DI int adjust_position(D& L, const KParams& P, St& s, int pos, const View& v) {
+        prefix(L, s, v, P.new_length_calc);
+        const int S = s.nseg;
+        const int i = lower_bound_E(L, s, pos + 1);  // the leaf whose view range [E - V, E) holds pos
+        if (i >= S) return -1;
+        if (uni(L.rseq[i]) != RNONE) return -1;
+        const int off = pos - (uni(L.E[i]) - uni(L.V[i]));
+        int before = 0;  // local-view length of the leaves before i (removed leaves count 0)
+        for (int base = 0; base < i; base += 64) {
+            const int j = base + lane_id();
+            const int x = j < i && L.rseq[min(j, S - 1)] == RNONE ? int(L.len[min(j, S - 1)]) : 0;
+            before += rdlane(wave_incl_scan(x), 63);
+        }
+        return before + off;
+    }
+    // PermutationVector.getAllocatedHandle (permutationvector.ts:209-230) at the local view: a
+    // segment without a handle is split to [pos, pos + 1) (walkSegments with splitRange ->
+    // MergeTree.mapRange, mergeTree.ts:2451-2469: `if (start)` skips the split at 0) and that
+    // one-position segment gets the next handle (HandleTable.allocate)
+    static MTR_DI void allocated_handle(D& L, const KParams& P, St& s, int pos) {
+        View v;
+        v.ref = s.curseq;
+        v.client = uint32_t(s.local);
+        v.local = 1;
+        prefix(L, s, v, P.new_length_calc);
+        {
+            const int i = lower_bound_E(L, s, pos + 1);
+            if (i >= s.nseg) {  // "Trying to get handle of out-of-bounds position!"
+                s.status = MTR_ERR_ASSERT | 0x027;
+                return;
+            }
+            if (uniu(L.text[i]) != uint32_t(MTR_HANDLE_UNALLOCATED)) return;  // already has a handle
+        }
+        if (pos) split_at(L, s, pos);
+        split_at(L, s, pos + 1);
+        const int i = lower_bound_E(L, s, pos + 1);
+        const int h = alloc_handle(L, P, s);
+        if (s.status != MTR_OK) return;
+        L.text[i] = uint32_t(h);
+        wsync();
+    }
+
+    // A matrix pair: the rows vector's op list drives the rows (L0, s0) and cols (L1, s1)
+    // PermutationVectors (SharedMatrix.processCore, matrix.ts:636-693, remote branch).
+    static MTR_DI void run_pair(char* smem, size_t region, const KParams& P, uint32_t d) {
+        const uint32_t d1 = uniu(gp(P.dpart)[d]);
+        const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
+        const int cursor = uni(gp(P.hdr)[d].op_cursor);
+        const int n_ops = min(int(dd.op_count) - cursor, P.ops_this_launch);
+        if (n_ops <= 0 || uni(gp(P.hdr)[d].status) != MTR_OK || uni(gp(P.hdr)[d1].status) != MTR_OK) return;
+        D L0, L1;
+        carve(L0, smem, P, d);
+        carve(L1, smem + region, P, d1);
+        St s0, s1;
+        load_doc(L0, P, s0, d);
+        load_doc(L1, P, s1, d1);
+        s1.ops_done = 0;
+        const gptr<const mtr_op> ops = gp(P.ops) + dd.op_begin + cursor;
+        for (int k = 0; k < n_ops; k++) {
+            const mtr_op op = uni_struct(ld_struct<mtr_op>(ops + k));
+            bool ok = true;
+            if (op.type == MTR_OP_START_COLLAB) {  // didAttach / onConnect start both vectors (matrix.ts:514-532)
+                ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k) && apply_op(L1, P, s1, op, dd, false, 0, cursor + k);
+            } else if (op.type == MTR_OP_SETCELL) {
+                View v;
+                v.ref = op.ref_seq;
+                v.client = enc_client(int(int16_t(op.client)));
+                v.local = 0;
+                View v1 = v;
+                v.local = (!s0.collab || uint32_t(s0.local) == v.client) ? 1 : 0;
+                v1.local = (!s1.collab || uint32_t(s1.local) == v1.client) ? 1 : 0;
+                const int r = adjust_position(L0, P, s0, op.pos1, v);
+                if (r >= 0) {
+                    const int c = adjust_position(L1, P, s1, op.pos2, v1);
+                    if (c >= 0) {
+                        allocated_handle(L0, P, s0, r);
+                        allocated_handle(L1, P, s1, c);
+                    }
+                }
+                if (s0.status != MTR_OK) s0.fail_op = cursor + k;
+                if (s1.status != MTR_OK) s1.fail_op = cursor + k;
+                ok = s0.status == MTR_OK && s1.status == MTR_OK;
+            } else if (op.flags & MTR_F_COLS) {
+                ok = apply_op(L1, P, s1, op, dd, false, 0, cursor + k);
+            } else {
+                ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k);
+            }
+            if (!ok) break;
+            s0.ops_done = k + 1;
+        }
+        store_doc(L0, P, s0, d);
+        s1.ops_done = 0;  // the cols vector's op cursor stays at 0 (it has no op list of its own)
+        store_doc(L1, P, s1, d1);
     }
 };
 
@@ -1812,6 +2021,16 @@ __global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
     Eng<G>::run(smem, P, d);
+}
+
+// SharedMatrix pairs: one wave applies a matrix's op list to its two PermutationVectors, each with
+// its own LDS region of `pair_region` bytes (HBM-resident arrays in global mode)
+template <bool G>
+__global__ void __launch_bounds__(NT) apply_pair_kernel(KParams P, uint32_t pair_region) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (blockIdx.x >= P.n_launch) return;
+    const uint32_t d = P.doc_list[blockIdx.x];
+    Eng<G, true>::run_pair(smem, pair_region, P, d);
 }
 
 }  // namespace mtr

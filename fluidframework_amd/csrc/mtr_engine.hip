@@ -100,6 +100,10 @@ struct mtr_engine {
     int32_t* h_cls = nullptr;         // pinned host copy of cls
     DevBuf<uint32_t> scratch;         // E/V arrays for HBM-resident (global-mode) launches
     DevBuf<mtr_synth_state> gstate;   // record mode generator state
+    // SharedMatrix pairs (mtr_set_matrix): per document kind (0 SharedString, 1 rows vector, 2 cols
+    // vector) and partner; they survive mtr_reset
+    DevBuf<uint32_t> dkind, dpart;
+    std::vector<uint32_t> h_kind, h_part;
     mtr_synth_cfg gcfg{};
     // summaries
     DevBuf<int64_t> out_size, out_off;
@@ -148,16 +152,20 @@ __global__ void scan_state_kernel(const DocHdr* h, const mtr_doc_desc* docs, uin
 // Size classes for one apply round: documents with ops left are bucketed by leaf count (64-leaf
 // classes) so that each class launch sizes its LDS by its own largest document.
 // cls layout: [0] max remaining ops, then per class c: cnt[c] at 1+3c, max nseg at 2+3c, max heapn at 3+3c.
+// Classes [kClasses, 2 kClasses) hold matrix pairs (rows vector documents), classed by the larger
+// of the two vectors; they launch apply_pair_kernel with two LDS regions.
 constexpr int kClasses = 64;
 constexpr int kClassLeaves = 64;
+constexpr int kAllClasses = 2 * kClasses;
 __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t n,
-                                                      int32_t* cls, uint32_t* list) {
+                                                      const uint32_t* dkind, const uint32_t* dpart, int32_t* cls,
+                                                      uint32_t* list) {
     // block-local histogram in LDS, then one global atomic per (block, class): the per-document
     // atomics on a handful of addresses would serialise at the memory side
-    __shared__ int lcnt[kClasses], lmax[kClasses], lheap[kClasses], lbase[kClasses];
+    __shared__ int lcnt[kAllClasses], lmax[kAllClasses], lheap[kAllClasses], lbase[kAllClasses];
     __shared__ int lrem;
     const int t = threadIdx.x;
-    if (t < kClasses) lcnt[t] = lmax[t] = lheap[t] = 0;
+    if (t < kAllClasses) lcnt[t] = lmax[t] = lheap[t] = 0;
     if (t == 0) lrem = 0;
     __syncthreads();
     const uint32_t d = blockIdx.x * blockDim.x + t;
@@ -166,15 +174,22 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
         const DocHdr x = h[d];
         const int rem = x.status == MTR_OK ? int(docs[d].op_count) - x.op_cursor : 0;
         if (rem > 0) {
-            c = min(kClasses - 1, x.nseg / kClassLeaves);
+            int nseg = x.nseg, heapn = x.heapn, base = 0;
+            if (dkind[d] == 1) {
+                const DocHdr y = h[dpart[d]];
+                nseg = max(nseg, y.nseg);
+                heapn = max(heapn, y.heapn);
+                base = kClasses;
+            }
+            c = base + min(kClasses - 1, nseg / kClassLeaves);
             rank = atomicAdd(&lcnt[c], 1);
-            atomicMax(&lmax[c], x.nseg);
-            atomicMax(&lheap[c], x.heapn);
+            atomicMax(&lmax[c], nseg);
+            atomicMax(&lheap[c], heapn);
             atomicMax(&lrem, rem);
         }
     }
     __syncthreads();
-    if (t < kClasses && lcnt[t]) {
+    if (t < kAllClasses && lcnt[t]) {
         lbase[t] = atomicAdd(&cls[1 + 3 * t], lcnt[t]);
         atomicMax(&cls[2 + 3 * t], lmax[t]);
         atomicMax(&cls[3 + 3 * t], lheap[t]);
@@ -223,6 +238,14 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
     for (auto& x : e->aux) (void)hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
     for (auto& x : e->lane_done) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
     const size_t D = std::max<uint32_t>(max_docs, 1);
+    e->h_kind.assign(D, 0);
+    e->h_part.assign(D, 0);
+    if (e->dkind.ensure(D) || e->dpart.ensure(D) ||
+        hipMemset(e->dkind.p, 0, D * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(e->dpart.p, 0, D * sizeof(uint32_t)) != hipSuccess) {
+        mtr_engine_destroy(e);
+        return nullptr;
+    }
     if (e->hdr.ensure(D) || e->seg.ensure(D * NF * c.max_segments) || e->heap.ensure(D * 2 * c.heap_entries) ||
         e->text.ensure(D * c.text_units) || e->prop.ensure(D * c.prop_words) || e->rm.ensure(D * c.remover_cells) ||
         e->stat.ensure(D * 4) || e->red.ensure(4)) {
@@ -256,6 +279,8 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->cls.release();
     if (e->h_cls) (void)hipHostFree(e->h_cls);
     e->dlist.release();
+    e->dkind.release();
+    e->dpart.release();
     e->scratch.release();
     e->out_size.release();
     e->s_kind.release();
@@ -337,6 +362,25 @@ static int run_impl(mtr_engine* e, int gen);
 
 int mtr_run(mtr_engine* e) { return run_impl(e, 0); }
 
+int mtr_set_matrix(mtr_engine* e, uint32_t rows_doc, uint32_t cols_doc) {
+    HIPCHK(hipSetDevice(e->device));
+    if (rows_doc >= e->h_kind.size() || cols_doc >= e->h_kind.size() || rows_doc == cols_doc ||
+        e->h_kind[rows_doc] || e->h_kind[cols_doc]) {
+        set_err("mtr_set_matrix: bad or already paired documents");
+        return MTR_ERR_BAD_OP;
+    }
+    e->h_kind[rows_doc] = 1;
+    e->h_kind[cols_doc] = 2;
+    e->h_part[rows_doc] = cols_doc;
+    e->h_part[cols_doc] = rows_doc;
+    HIPCHK(hipMemcpyAsync(e->dkind.p, e->h_kind.data(), e->h_kind.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          e->stream));
+    HIPCHK(hipMemcpyAsync(e->dpart.p, e->h_part.data(), e->h_part.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return MTR_OK;
+}
+
 static int run_impl(mtr_engine* e, int gen) {
     HIPCHK(hipSetDevice(e->device));
     if (e->n_docs == 0) return MTR_OK;
@@ -366,6 +410,8 @@ static int run_impl(mtr_engine* e, int gen) {
     P.key_index = e->key_index.p;
     P.val_eq = e->val_eq.p;
     P.stat_ops = e->stat.p;
+    P.dkind = e->dkind.p;
+    P.dpart = e->dpart.p;
     P.gen = gen;
     if (gen) {
         P.gen_cfg = e->gcfg;
@@ -381,20 +427,24 @@ static int run_impl(mtr_engine* e, int gen) {
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
     });
     // documents whose class needs more LDS than this stay HBM-resident (MTR_LDS_LIMIT, bytes; tuning knob)
     static const size_t lds_limit = [] {
         const char* v = std::getenv("MTR_LDS_LIMIT");
         return v ? std::min<size_t>(size_t(std::atoll(v)), 160 * 1024) : size_t(160 * 1024);
     }();
-    const size_t ncls = 1 + 3 * kClasses;
-    if (e->cls.ensure(ncls) || e->dlist.ensure(size_t(kClasses) * e->n_docs)) return -1;
-    if (!e->h_cls) HIPCHK(hipHostMalloc((void**)&e->h_cls, (1 + 3 * kClasses) * sizeof(int32_t), hipHostMallocDefault));
+    const size_t ncls = 1 + 3 * kAllClasses;
+    if (e->cls.ensure(ncls) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
+    if (!e->h_cls) HIPCHK(hipHostMalloc((void**)&e->h_cls, ncls * sizeof(int32_t), hipHostMallocDefault));
     int32_t* cls = e->h_cls;
     for (;;) {
         HIPCHK(hipMemsetAsync(e->cls.p, 0, ncls * sizeof(int32_t), e->stream));
-        classify_kernel<<<(e->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, e->n_docs, e->cls.p,
-                                                                           e->dlist.p);
+        classify_kernel<<<(e->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, e->n_docs, e->dkind.p,
+                                                                           e->dpart.p, e->cls.p, e->dlist.p);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(cls, e->cls.p, ncls * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
@@ -404,13 +454,15 @@ static int run_impl(mtr_engine* e, int gen) {
         bool stuck = false;
         HIPCHK(hipEventRecord(e->ev[0], e->stream));
         int nl = 0;  // launches of this round
-        for (int c = kClasses - 1; c >= 0; c--) {  // one launch per size class, largest documents first
+        for (int c = kAllClasses - 1; c >= 0; c--) {  // one launch per size class: matrix pairs, then the
+            const bool pair = c >= kClasses;              // SharedString classes, largest documents first
             const int cnt = cls[1 + 3 * c], maxseg = cls[2 + 3 * c], maxheap = cls[3 + 3 * c];
             if (cnt <= 0) continue;
             int cap = round64(maxseg + 2 * k + 8);
             if (cap > P.segcap) cap = P.segcap;
             int lhcap = std::min<int>(P.hcap, std::max(cap / 2, round64(maxheap + 2 * k + 8)));
             size_t lds = lds_bytes(cap, lhcap);
+            if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             P.global_mode = 0;
             if (lds > lds_limit) {
                 // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
@@ -420,6 +472,7 @@ static int run_impl(mtr_engine* e, int gen) {
                 cap = P.segcap;
                 lhcap = P.hcap;
                 lds = lds_bytes_global_mode();
+                if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             }
             const int kk = std::max(1, std::min(k, (cap - maxseg - 8) / 2));
             if (cap - maxseg - 8 < 2) stuck = true;
@@ -437,8 +490,19 @@ static int run_impl(mtr_engine* e, int gen) {
                 e->kev.push_back(x);
             }
             HIPCHK(hipEventRecord(e->kev[2 * nl], st));
-            if (P.global_mode) apply_kernel<true><<<cnt, NT, lds, st>>>(P);
-            else apply_kernel<false><<<cnt, NT, lds, st>>>(P);
+            if (pair) {
+                if (P.gen) {
+                    set_err("record mode does not generate matrix documents");
+                    return MTR_ERR_UNSUPPORTED;
+                }
+                const uint32_t region = uint32_t(lds / 2);
+                if (P.global_mode) apply_pair_kernel<true><<<cnt, NT, lds, st>>>(P, region);
+                else apply_pair_kernel<false><<<cnt, NT, lds, st>>>(P, region);
+            } else if (P.global_mode) {
+                apply_kernel<true><<<cnt, NT, lds, st>>>(P);
+            } else {
+                apply_kernel<false><<<cnt, NT, lds, st>>>(P);
+            }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e->kev[2 * nl + 1], st));
             e->launches++;
@@ -562,12 +626,13 @@ int mtr_summarize(mtr_engine* e) {
     P.val_eq = e->val_eq.p;
     P.client_off = e->client_off.p;
     P.client_bytes = e->client_bytes.p;
+    P.dkind = e->dkind.p;
     P.out_size = e->out_size.p;
     P.out_off = e->out_off.p;
     P.out_hash = e->out_hash.p;
     {
         const size_t sc = size_t(P.segcap);
-        P.maxb = int(std::min<int64_t>(int64_t(sc) + 1, int64_t(P.tcap) / std::max(1, P.chunk_size) + 4));
+        P.maxb = int(std::min<int64_t>(int64_t(sc) + 1, std::max<int64_t>(int64_t(P.tcap) / std::max(1, P.chunk_size) + 4, 64)));
         if (e->s_kind.ensure(n * sc) || e->s_start.ensure(n * (sc + 1)) || e->s_len.ensure(n * sc) ||
             e->s_bytes.ensure(n * sc) || e->s_blob.ensure(n * (4 + 4 * size_t(P.maxb))))
             return -1;
@@ -742,7 +807,8 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
         r[3] = rs == RNONE ? INT32_MIN : rs;
         r[4] = nrem;
         r[5] = int32_t((m & M_BND_MASK) >> M_BND_SHIFT);
-        r[6] = (m & M_MARKER) ? 1 : 0;
+        // PermutationSegment: its start handle (the oracle export does the same)
+        r[6] = e->h_kind[doc] ? int32_t(hd.seg[F_TEXT * sc + i]) : ((m & M_MARKER) ? 1 : 0);
         r[7] = int32_t(h);
     }
     return hd.h.nseg;

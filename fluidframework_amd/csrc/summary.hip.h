@@ -40,6 +40,7 @@ struct SParams {
     const uint32_t* val_eq;
     const uint32_t* client_off;
     const uint8_t* client_bytes;
+    const uint32_t* dkind;  // non-zero: a PermutationVector of a SharedMatrix (mtr_set_matrix)
     // scratch handed from the size pass to the write pass
     uint8_t* s_kind;    // [doc][segcap]      leaf kind: 0 skip, 1 coalescable, 2 merge-info (V1)
     uint32_t* s_start;  // [doc][segcap + 1]  first leaf of every spec (+ sentinel)
@@ -163,6 +164,7 @@ struct SDoc {
     gptr<uint32_t> start, slen, sbytes;
     gptr<int32_t> blob;
     int S, minseq, curseq, collab, local, newlen;
+    int perm, hlen;  // PermutationVector: [length, start] specs, HandleTable of hlen words in the arena
 };
 
 MTR_DI SDoc sdoc(const SParams& P, uint32_t d, const DocHdr& h) {
@@ -189,6 +191,8 @@ MTR_DI SDoc sdoc(const SParams& P, uint32_t d, const DocHdr& h) {
     D.collab = h.collab;
     D.local = h.collab ? h.local : int(CL_LOCAL);
     D.newlen = P.new_length_calc;
+    D.perm = P.dkind ? int(uniu(gp(P.dkind)[d]) != 0) : 0;
+    D.hlen = h.textused;
     return D;
 }
 
@@ -276,6 +280,17 @@ MTR_DI void w_units(LW<W>& w, const SDoc& D, uint32_t t, int n, int& hi) {
 // a coalesced group is the concatenation of its kind-1 leaves
 template <bool W>
 MTR_DI void w_segjson(LW<W>& w, const SDoc& D, const SParams& P, int s, int e) {
+    if (D.perm) {  // PermutationSegment.toJSONObject (permutationvector.ts:118-120) of the coalesced group
+        int length = 0;
+        for (int k = s; k < e; k++)
+            if (k == s || D.kind[k] == 1) length += int(D.len[k]);
+        w.put('[');
+        w.num(length);
+        w.put(',');
+        w.num(int64_t(int32_t(D.text[s])));
+        w.put(']');
+        return;
+    }
     const uint32_t m = D.meta[s];
     const uint32_t pr = D.props[s];
     if (m & M_MARKER) {
@@ -421,15 +436,16 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
     const DocHdr h = uni_struct(ld_struct<DocHdr>(gp(P.hdr) + d));
     const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
     SDoc D = sdoc(P, d, h);
-    const int v1 = P.snapshot_v1;
+    const int v1 = D.perm ? 1 : P.snapshot_v1;  // PermutationVector forces newMergeTreeSnapshotFormat
     const int S = D.S;
     const int ln = lane_id();
     const gptr<const uint32_t> veq = gp(P.val_eq);
 
     // A. extract: kinds, appends and spec starts (carry = the last non-skipped leaf so far)
     bool c_valid = false, c_k1 = false, c_mk = false, c_nl = false;
-    uint32_t c_pr = NONE32;
+    uint32_t c_pr = NONE32, c_tx = 0;
     int c_acc = 0;  // chars of the open group (TextSegmentGranularity rule)
+    int c_len = 0;  // length of the last non-skipped leaf (PermutationSegment contiguity)
     int nspec = 0;
     for (int base = 0; base < S; base += 64) {
         const int i = base + ln;
@@ -448,22 +464,29 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
         if (in) D.kind[i] = uint8_t(kd);
         const bool mk = (m & M_MARKER) != 0;
         bool nl = false;  // last unit is '\n'
-        if (kd == 1 && !mk && len > 0) nl = (m & M_NLQ) ? D.gtext[tx + uint32_t(len) - 1] == u'\n' : (m & M_NL) != 0;
+        if (kd == 1 && !mk && len > 0 && !D.perm)
+            nl = (m & M_NLQ) ? D.gtext[tx + uint32_t(len) - 1] == u'\n' : (m & M_NL) != 0;
         const uint64_t ns = __ballot(kd != 0);
         const uint64_t below = ns & lanes_below();
         const int p = below ? last_lane(below) : -1;
         const int ps = p < 0 ? 0 : p;
         bool p_k1 = __shfl(int(kd == 1), ps) != 0, p_mk = __shfl(int(mk), ps) != 0, p_nl = __shfl(int(nl), ps) != 0;
-        uint32_t p_pr = uint32_t(__shfl(int(pr), ps));
+        uint32_t p_pr = uint32_t(__shfl(int(pr), ps)), p_tx = uint32_t(__shfl(int(tx), ps));
+        int p_len = __shfl(len, ps);
         if (p < 0) {
             p_k1 = c_valid && c_k1;
             p_mk = c_mk;
             p_nl = c_nl;
             p_pr = c_pr;
+            p_tx = c_tx;
+            p_len = c_len;
         }
         bool link = kd == 1 && p_k1 && !p_mk && !mk && !p_nl;
+        if (D.perm)  // PermutationSegment.canAppend: contiguous handles (permutationvector.ts:131-137)
+            link = link && (p_tx == uint32_t(MTR_HANDLE_UNALLOCATED) ? tx == uint32_t(MTR_HANDLE_UNALLOCATED)
+                                                                     : tx == p_tx + uint32_t(p_len));
         if (link && pr != p_pr) link = props_match(D.gprop, veq, p_pr, pr);
-        if (__ballot(link && len > kGranularity)) {  // accumulated-length clause, in order
+        if (!D.perm && __ballot(link && len > kGranularity)) {  // accumulated-length clause, in order
             uint64_t lm = __ballot(link);
             int acc = c_valid && c_k1 ? c_acc : 0;
             for (uint64_t t = ns; t; t &= t - 1) {
@@ -507,6 +530,8 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
             c_mk = rdlane(int(mk), q) != 0;
             c_nl = rdlane(int(nl), q) != 0;
             c_pr = rdlane(pr, q);
+            c_tx = rdlane(tx, q);
+            c_len = rdlane(len, q);
             c_acc = acc;
         }
     }
@@ -588,13 +613,52 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
         if (ln == 0) D.blob[4 + 4 * c + 3] = int32_t(bytes);
         doc_bytes += bytes;
     }
+    int hbytes = 0;  // PermutationVector: the handleTable blob, JSON.stringify(handles)
+    if (D.perm) {
+        const gptr<const int32_t> ht = (gptr<const int32_t>)D.gtext;
+        int digits = 0;
+        for (int g0 = 0; g0 < D.hlen; g0 += 64) {
+            const int g = g0 + ln;
+            int x = 0;
+            if (g < D.hlen) {
+                LW<false> w{(gptr<uint8_t>)nullptr, 0};
+                w.num(ht[g]);
+                x = int(w.n);
+            }
+            digits += rdlane(wave_incl_scan(x), 63);
+        }
+        hbytes = 2 + digits + max(D.hlen - 1, 0);
+    }
     if (ln == 0) {
         D.blob[0] = nspec;
         D.blob[1] = nblob;
         D.blob[2] = total_len;
         D.blob[3] = ok ? 1 : 0;
-        P.out_size[d] = ok ? 4 + 4 * int64_t(nblob) + doc_bytes : -1;
+        P.out_size[d] = ok ? 4 + 4 * int64_t(nblob + D.perm) + doc_bytes + hbytes : -1;
     }
+}
+
+// digest of one written blob (include/mtr_digest.h): one 8-byte word per lane per round
+MTR_DI uint64_t blob_digest(gptr<uint8_t> base, int64_t b0, int64_t blen) {
+    const int ln = lane_id();
+    uint64_t sum = 0;
+    const int64_t nw = (blen + 7) / 8;
+    for (int64_t j0 = 0; j0 < nw; j0 += 64) {
+        const int64_t j = j0 + ln;
+        if (j < nw) {
+            uint64_t wv = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (8 * j + q < blen) wv |= uint64_t(base[b0 + 8 * j + q]) << (8 * q);
+            sum += mtr_dg_word(wv, uint64_t(j));
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = uint32_t(sum), hi = uint32_t(sum >> 32);
+        sum += uint64_t(uint32_t(__shfl_xor(int(lo), o))) | (uint64_t(uint32_t(__shfl_xor(int(hi), o))) << 32);
+    }
+    return mtr_dg_blob(uni_struct(sum), uint64_t(blen));
 }
 
 // ------------------------------------------------------------------ write pass
@@ -602,21 +666,22 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
     const DocHdr h = uni_struct(ld_struct<DocHdr>(gp(P.hdr) + d));
     const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
     SDoc D = sdoc(P, d, h);
-    const int v1 = P.snapshot_v1;
+    const int v1 = D.perm ? 1 : P.snapshot_v1;
     const int ln = lane_id();
     const int nspec = uni(D.blob[0]), nblob = uni(D.blob[1]), total_len = uni(D.blob[2]);
     if (!uni(D.blob[3])) return;
     const int first_len = uni(D.blob[4 + 2]);
     const int64_t off0 = gp(P.out_off)[d];
     const gptr<uint8_t> base = gp(P.out) + uni_struct(off0);
+    const int nall = nblob + D.perm;  // + the handleTable blob of a PermutationVector
     if (ln == 0) {
-        base[0] = uint8_t(nblob);
-        base[1] = uint8_t(nblob >> 8);
-        base[2] = uint8_t(nblob >> 16);
-        base[3] = uint8_t(nblob >> 24);
+        base[0] = uint8_t(nall);
+        base[1] = uint8_t(nall >> 8);
+        base[2] = uint8_t(nall >> 16);
+        base[3] = uint8_t(nall >> 24);
     }
-    int64_t pos = 4 + 4 * int64_t(nblob);
-    uint64_t hsh = mtr_dg_begin(uint64_t(nblob));
+    int64_t pos = 4 + 4 * int64_t(nall);
+    uint64_t hsh = mtr_dg_begin(uint64_t(nall));
     for (int c = 0; c < nblob; c++) {
         const int bs = uni(D.blob[4 + 4 * c + 0]), bc = uni(D.blob[4 + 4 * c + 1]), bl = uni(D.blob[4 + 4 * c + 2]);
         const int64_t b0 = pos;
@@ -651,25 +716,43 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
             base[4 + 4 * c + 3] = uint8_t(blen >> 24);
         }
         wsync();
-        // digest of the blob: one 8-byte word per lane per round
-        uint64_t sum = 0;
-        const int64_t nw = (blen + 7) / 8;
-        for (int64_t j0 = 0; j0 < nw; j0 += 64) {
-            const int64_t j = j0 + ln;
-            if (j < nw) {
-                uint64_t wv = 0;
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (8 * j + q < blen) wv |= uint64_t(base[b0 + 8 * j + q]) << (8 * q);
-                sum += mtr_dg_word(wv, uint64_t(j));
+        hsh = mtr_dg_next(hsh, blob_digest(base, b0, blen));
+    }
+    if (D.perm) {  // handleTable blob: "[h0,h1,...]" (HandleTable.getSummaryContent, handletable.ts:84)
+        const gptr<const int32_t> ht = (gptr<const int32_t>)D.gtext;
+        const int64_t b0 = pos;
+        if (ln == 0) base[pos] = '[';
+        pos++;
+        for (int g0 = 0; g0 < D.hlen; g0 += 64) {
+            const int g = g0 + ln;
+            const bool act = g < D.hlen;
+            int x = 0;
+            int32_t v = 0;
+            if (act) {
+                v = ht[g];
+                LW<false> w{(gptr<uint8_t>)nullptr, 0};
+                w.num(v);
+                x = int(w.n) + (g > 0 ? 1 : 0);
             }
+            const int incl = wave_incl_scan(x);
+            if (act) {
+                LW<true> w{base, pos + incl - x};
+                if (g > 0) w.put(',');
+                w.num(v);
+            }
+            pos += rdlane(incl, 63);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint32_t lo = uint32_t(sum), hi = uint32_t(sum >> 32);
-            sum += uint64_t(uint32_t(__shfl_xor(int(lo), o))) | (uint64_t(uint32_t(__shfl_xor(int(hi), o))) << 32);
+        if (ln == 0) base[pos] = ']';
+        pos++;
+        const int64_t blen = pos - b0;
+        if (ln == 0) {
+            base[4 + 4 * nblob + 0] = uint8_t(blen);
+            base[4 + 4 * nblob + 1] = uint8_t(blen >> 8);
+            base[4 + 4 * nblob + 2] = uint8_t(blen >> 16);
+            base[4 + 4 * nblob + 3] = uint8_t(blen >> 24);
         }
-        hsh = mtr_dg_next(hsh, mtr_dg_blob(uni_struct(sum), uint64_t(blen)));
+        wsync();
+        hsh = mtr_dg_next(hsh, blob_digest(base, b0, blen));
     }
     if (ln == 0) P.out_hash[d] = hsh;
 }

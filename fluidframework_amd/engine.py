@@ -63,6 +63,8 @@ def lib():
         L.mtr_export.restype = C.c_int64
         L.mtr_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.mtr_stats.restype = C.c_int
+        L.mtr_set_matrix.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.mtr_set_matrix.restype = C.c_int
         L.mtr_last_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.mtr_last_timing.restype = C.c_int
         L.mtr_last_error.restype = C.c_char_p
@@ -115,6 +117,11 @@ class Engine:
 
     def run(self):
         self._check(lib().mtr_run(self.h), "mtr_run")
+
+    def set_matrix(self, rows_doc, cols_doc):
+        """Documents rows_doc / cols_doc are the rows / cols PermutationVectors of one SharedMatrix
+        (the rows document's op list drives both; see include/mtr.h mtr_set_matrix)."""
+        self._check(lib().mtr_set_matrix(self.h, int(rows_doc), int(cols_doc)), "mtr_set_matrix")
 
     def summarize(self):
         self._check(lib().mtr_summarize(self.h), "mtr_summarize")

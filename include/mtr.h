@@ -59,6 +59,13 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b);
 /* Apply the submitted ops (Client.applyMsg for each message, in order, per document). Async. */
 int mtr_run(mtr_engine* e);
 
+/* Declare documents rows_doc and cols_doc to be the rows and cols PermutationVectors of one
+ * SharedMatrix (replaces `new PermutationVector(...)` x2 in the SharedMatrix constructor,
+ * matrix.ts:106-121).  The rows document's op list drives both (see MTR_OP_SETCELL / MTR_F_COLS in
+ * mtr_types.h); each vector's summary is its SnapshotV1 blobs followed by its handleTable blob
+ * (PermutationVector.summarize, permutationvector.ts:310-325).  Persistent across mtr_reset. */
+int mtr_set_matrix(mtr_engine* e, uint32_t rows_doc, uint32_t cols_doc);
+
 /* Build every document's summary blobs on the device (Client.summarize). Async except for
  * one small size read-back between the sizing and writing passes. */
 int mtr_summarize(mtr_engine* e);

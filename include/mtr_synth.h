@@ -150,6 +150,44 @@ MTR_HD static inline void mtr_synth_finish(const mtr_synth_cfg* cfg, mtr_synth_s
     }
 }
 
+/* SharedMatrix recipe: after mtr_synth_begin, given the writer's view lengths of
+ * the rows and cols vectors, choose a row/col splice (insertRows/removeRows/insertCols/removeCols,
+ * matrix.ts:363-372) with weights w_insert / w_remove, or a setCell (weight w_annotate) at a row and
+ * col inside the writer's view.  Splices insert 1..max_text positions and remove 1..max_range. */
+MTR_HD static inline void mtr_synth_matrix_finish(const mtr_synth_cfg* cfg, mtr_synth_state* st, int32_t Lr,
+                                                  int32_t Lc, mtr_op* op) {
+    const uint32_t tot = cfg->w_insert + cfg->w_remove + cfg->w_annotate;
+    const uint32_t pick = mtr_rng_below(&st->rng, tot);
+    int kind = pick < cfg->w_insert ? 0 : (pick < cfg->w_insert + cfg->w_remove ? 1 : 2);
+    const int cols = (int)mtr_rng_below(&st->rng, 2u);
+    if (kind == 2 && (Lr <= 0 || Lc <= 0)) kind = 0;
+    const int32_t L = cols ? Lc : Lr;
+    if (kind == 1 && L <= 0) kind = 0;
+    op->payload = 0;
+    op->payload2 = 0;
+    if (kind == 2) {
+        op->type = MTR_OP_SETCELL;
+        op->flags = 0;
+        op->pos1 = (int32_t)mtr_rng_below(&st->rng, (uint32_t)Lr);
+        op->pos2 = (int32_t)mtr_rng_below(&st->rng, (uint32_t)Lc);
+        return;
+    }
+    op->flags = (uint8_t)(MTR_F_LAST | (cols ? MTR_F_COLS : 0));
+    if (kind == 0) {
+        op->type = MTR_OP_INSERT;
+        op->pos1 = (int32_t)mtr_rng_below(&st->rng, (uint32_t)L + 1u);
+        op->pos2 = -1;
+        op->payload2 = 1u + mtr_rng_below(&st->rng, cfg->max_text);
+    } else {
+        const int32_t start = (int32_t)mtr_rng_below(&st->rng, (uint32_t)L);
+        uint32_t room = (uint32_t)(L - start);
+        if (room > cfg->max_range) room = cfg->max_range;
+        op->type = MTR_OP_REMOVE;
+        op->pos1 = start;
+        op->pos2 = start + 1 + (int32_t)mtr_rng_below(&st->rng, room);
+    }
+}
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,9 +32,14 @@ enum {
     MTR_OP_LOCAL_ANNOTATE = 10, /* non-collaborating local annotate */
     MTR_OP_START_COLLAB = 12,   /* Client.startOrUpdateCollaboration (client.ts:1133): seq/min_seq = currentSeq/minSeq,
                                    client = the observer's short id */
-    MTR_OP_LOAD = 13            /* a snapshot header segment (SnapshotLoader.loadHeader, snapshotLoader.ts:130-167):
+    MTR_OP_LOAD = 13,           /* a snapshot header segment (SnapshotLoader.loadHeader, snapshotLoader.ts:130-167):
                                    consecutive LOAD records are built into the tree bottom-up by
                                    MergeTree.reloadFromSegments (mergeTree.ts:678-728) before the next record */
+    MTR_OP_SETCELL = 14         /* SharedMatrix set-cell message (matrix.ts:636-693, remote branch): pos1 = row,
+                                   pos2 = col at (ref_seq, client); resolves both positions
+                                   (PermutationVector.adjustPosition, permutationvector.ts:232-247) and, when both
+                                   are live, allocates row and col handles (getAllocatedHandle, :209-230).
+                                   No updateSeqNumbers on either vector. */
 };
 
 /* op.flags */
@@ -43,9 +48,22 @@ enum {
     MTR_F_MARKER = 2,  /* insert of a Marker segment (mergeTreeNodes.ts:557); payload = refType */
     MTR_F_PROPS = 4,   /* insert carries initial props: pos2 = prop-op index */
     MTR_F_NOREF = 8,   /* marker has no refType member ({"marker":{}}) */
-    MTR_F_APPEND = 16  /* insert at the end of the local view with refSeq = UniversalSequenceNumber
+    MTR_F_APPEND = 16, /* insert at the end of the local view with refSeq = UniversalSequenceNumber
                           (SnapshotLoader.loadBody append, snapshotLoader.ts:221-256) */
+    MTR_F_COLS = 32    /* matrix documents: the vector op targets the cols PermutationVector (contents.target
+                          "cols", matrix.ts:645-651); without it, the rows vector */
 };
+
+/*
+ * SharedMatrix documents: a matrix is a pair of engine documents, the rows
+ * and the cols PermutationVector (permutationvector.ts:150), declared with mtr_set_matrix().  The rows
+ * document's op list drives both (vector ops carry MTR_F_COLS for the cols vector; MTR_OP_SETCELL
+ * touches both; MTR_OP_START_COLLAB starts both); the cols document has no ops of its own.
+ * Permutation segments are [length, start] (PermutationSegment.toJSONObject, permutationvector.ts:118):
+ * an insert carries its length in payload2; start is always reset to MTR_HANDLE_UNALLOCATED on
+ * insert (onDelta INSERT, permutationvector.ts:354-361).
+ */
+#define MTR_HANDLE_UNALLOCATED ((int32_t)0x80000000) /* Handle.unallocated, handletable.ts:11 */
 
 /*
  * Snapshot segments (MTR_OP_LOAD, and MTR_OP_INSERT with MTR_F_APPEND) carry their merge info

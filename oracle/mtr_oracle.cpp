@@ -63,6 +63,8 @@ struct Node {
 
 struct Seg : Node {
     bool marker = false;
+    bool perm = false;                      // PermutationSegment (matrix/src/permutationvector.ts:41)
+    int start = MTR_HANDLE_UNALLOCATED;     // PermutationSegment._start
     bool noRef = false;
     int refType = 0;
     std::u16string text;
@@ -286,8 +288,12 @@ class Tree {
     }
 
     // ------------------------------------------------------------ segments
-    // TextSegment.canAppend, textSegment.ts:86-93; Marker.canAppend -> false
+    // TextSegment.canAppend, textSegment.ts:86-93; Marker.canAppend -> false;
+    // PermutationSegment.canAppend, permutationvector.ts:131-137 (handle ranges stay contiguous)
     static bool canAppend(const Seg* a, const Seg* b) {
+        if (a->perm)
+            return a->start == MTR_HANDLE_UNALLOCATED ? b->start == MTR_HANDLE_UNALLOCATED
+                                                      : int64_t(b->start) == int64_t(a->start) + a->len;
         if (a->marker || b->marker) return false;
         if (!a->text.empty() && a->text.back() == u'\n') return false;
         return a->len <= kTextSegmentGranularity || b->len <= kTextSegmentGranularity;
@@ -297,10 +303,17 @@ class Tree {
     Seg* splitAt(Seg* s, int pos) {
         if (pos <= 0 || s->marker) return nullptr;
         Seg* r = makeSeg();
-        r->text = s->text.substr(pos);
-        s->text.resize(pos);
-        s->len = int(s->text.size());
-        r->len = int(r->text.size());
+        if (s->perm) {  // PermutationSegment.createSplitSegmentAt, permutationvector.ts:139-154
+            r->perm = true;
+            r->start = s->start == MTR_HANDLE_UNALLOCATED ? MTR_HANDLE_UNALLOCATED : s->start + pos;
+            r->len = s->len - pos;
+            s->len = pos;
+        } else {
+            r->text = s->text.substr(pos);
+            s->text.resize(pos);
+            s->len = int(s->text.size());
+            r->len = int(r->text.size());
+        }
         if (s->hasPropMgr && s->hasProps) {  // copyPropertiesTo, mergeTreeNodes.ts:512-522
             r->hasPropMgr = true;
             r->hasProps = true;
@@ -529,7 +542,11 @@ class Tree {
                     if (s->removedSeq > minSeq) {
                         hold.push_back(s);
                     } else {
-                        s->parent = nullptr;  // UNLINK
+                        // UNLINK; a PermutationVector frees the segment's handles in order
+                        // (onMaintenance, permutationvector.ts:418-443)
+                        if (s->perm && s->start >= 1)
+                            for (int h = 0; h < s->len; h++) freeHandle(s->start + h);
+                        s->parent = nullptr;
                     }
                     prev = nullptr;
                 } else {
@@ -537,7 +554,7 @@ class Tree {
                         int ln = localNetLength(s);
                         bool ok = prev && canAppend(prev, s) && matchProperties(prev, s, tabs.b) && (ln > 0);
                         if (ok) {
-                            prev->text += s->text;  // TextSegment.append textSegment.ts:99-103
+                            prev->text += s->text;  // TextSegment.append textSegment.ts:99-103 (BaseSegment.append for perm)
                             prev->len += s->len;
                             s->parent = nullptr;
                         } else {
@@ -685,6 +702,12 @@ class Tree {
 
     Seg* segmentFromSpec(const mtr_op& op, const mtr_doc_desc& dd) {  // sequenceFactory.ts:26-38
         Seg* s = makeSeg();
+        if (permMode) {  // PermutationSegment.fromJSONObject + reset() on INSERT (permutationvector.ts:45-48, 354-361)
+            s->perm = true;
+            s->len = int(op.payload2);
+            s->start = MTR_HANDLE_UNALLOCATED;
+            return s;
+        }
         if (op.flags & MTR_F_MARKER) {
             s->marker = true;
             s->refType = int(op.payload);
@@ -861,6 +884,78 @@ class Tree {
         return status;
     }
 
+    // ------------------------------------------------------------ PermutationVector (matrix)
+    bool permMode = false;
+    // HandleTable (matrix/src/handletable.ts:19-91): handles[0] = head of the free list
+    std::vector<int64_t> handles{1};
+    int allocateHandle() {  // handletable.ts:37-42
+        const int64_t fr = handles[0];
+        handles[0] = size_t(fr) < handles.size() ? handles[size_t(fr)] : fr + 1;
+        if (size_t(fr) == handles.size()) handles.push_back(0);
+        else handles[size_t(fr)] = 0;
+        return int(fr);
+    }
+    void freeHandle(int h) {  // handletable.ts:57-60
+        if (size_t(h) >= handles.size()) handles.resize(size_t(h) + 1, 0);
+        handles[size_t(h)] = handles[0];
+        handles[0] = h;
+    }
+    // getContainingSegment, mergeTree.ts:795-813: the leaf holding pos at (refSeq, clientId)
+    Seg* containingSegment(int pos, int refSeq, int clientId, int& offset) {
+        Seg* found = nullptr;
+        offset = 0;
+        int p = 0;
+        bool exit = false;
+        std::vector<Seg*> visit;
+        walkMap(root, refSeq, clientId, pos, pos + 1, p, exit, visit);
+        if (!visit.empty()) {
+            found = visit[0];
+            // position of the leaf in this view: sum of the lengths of the leaves before it
+            int before = 0;
+            std::vector<Seg*> lv;
+            leaves(root, lv);
+            for (Seg* x : lv) {
+                if (x == found) break;
+                const int l = nodeLength(x, refSeq, clientId);
+                if (l > 0) before += l;
+            }
+            offset = pos - before;
+        }
+        return found;
+    }
+    // getPosition at the local view, mergeTree.ts:768-785
+    int localPosition(Seg* seg) {
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        int before = 0;
+        for (Seg* x : lv) {
+            if (x == seg) break;
+            const int l = localNetLength(x);
+            if (l > 0) before += l;
+        }
+        return before;
+    }
+    // PermutationVector.adjustPosition, permutationvector.ts:232-247 (-1 = undefined)
+    int adjustPosition(int pos, int refSeq, int clientId) {
+        int off = 0;
+        Seg* s = containingSegment(pos, refSeq, clientId, off);
+        if (!s || s->removed) return -1;
+        return localPosition(s) + off;
+    }
+    // PermutationVector.getAllocatedHandle, permutationvector.ts:209-230: a miss splits out the
+    // one-position segment (Client.walkSegments with splitRange -> MergeTree.mapRange,
+    // mergeTree.ts:2451-2469, whose `if (start)` skips the split at 0) and allocates its handle
+    int getAllocatedHandle(int pos) {
+        int off = 0;
+        Seg* s = containingSegment(pos, currentSeq, localClientId, off);
+        if (s && s->start >= 1) return s->start + off;
+        if (pos) ensureIntervalBoundary(pos, currentSeq, localClientId);
+        ensureIntervalBoundary(pos + 1, currentSeq, localClientId);
+        int h = MTR_HANDLE_UNALLOCATED;
+        nodeMap(currentSeq, localClientId, [&](Seg* x) { x->start = h = allocateHandle(); }, pos, pos + 1);
+        return h;
+    }
+
     // ------------------------------------------------------------ text
     void gatherText(Block* b, std::u16string& out) {
         for (int i = 0; i < b->childCount; i++) {
@@ -990,6 +1085,14 @@ struct Emitter {
     }
     // toJSONObject: textSegment.ts:73-77, mergeTreeNodes.ts:577-581
     void segJson(Out& o, const Seg* s) const {
+        if (s->perm) {  // PermutationSegment.toJSONObject, permutationvector.ts:118-120
+            o.raw("[");
+            o.num(s->len);
+            o.raw(",");
+            o.num(s->start);
+            o.raw("]");
+            return;
+        }
         if (s->marker) {
             o.raw("{\"marker\":{");
             if (!s->noRef) {
@@ -1021,9 +1124,36 @@ struct SpecOut {
 
 }  // namespace
 
+// A SharedString document is one Tree.  A SharedMatrix document holds its two PermutationVectors
+// (matrix.ts:106-121): rows in `tree`, cols in `cols`; queries read the selected one.
 struct oracle_doc {
     Tree tree;
-    explicit oracle_doc(const mtr_options& o) : tree(o) {}
+    Tree cols;
+    bool matrix = false;
+    int sel = 0;
+    explicit oracle_doc(const mtr_options& o) : tree(o), cols(o) {}
+    Tree& view() { return sel ? cols : tree; }
+    // SharedMatrix.processCore, remote branch (matrix.ts:636-693)
+    int applyMatrix(const mtr_op& op, const mtr_doc_desc& dd) {
+        if (op.type == MTR_OP_START_COLLAB) {  // didAttach/onConnect start both vectors, matrix.ts:514-532
+            int st = tree.apply(op, dd);
+            return st != MTR_OK ? st : cols.apply(op, dd);
+        }
+        if (op.type == MTR_OP_SETCELL) {
+            if (!tree.pendingLoad.empty()) tree.reloadFromSegments();
+            if (!cols.pendingLoad.empty()) cols.reloadFromSegments();
+            const int client = int(int16_t(op.client));
+            const int r = tree.adjustPosition(op.pos1, op.ref_seq, client);
+            if (r < 0) return MTR_OK;
+            const int c = cols.adjustPosition(op.pos2, op.ref_seq, client);
+            if (c < 0) return MTR_OK;
+            const int rh = tree.getAllocatedHandle(r);
+            const int ch = cols.getAllocatedHandle(c);
+            if (rh < 1 || ch < 1) return MTR_ERR_ASSERT | 0x022;  // "row and/or col handles are invalid"
+            return tree.status != MTR_OK ? tree.status : cols.status;
+        }
+        return (op.flags & MTR_F_COLS) ? cols.apply(op, dd) : tree.apply(op, dd);
+    }
 };
 
 extern "C" {
@@ -1043,35 +1173,47 @@ oracle_doc* oracle_doc_new(const mtr_options* opt) {
 
 void oracle_doc_free(oracle_doc* d) { delete d; }
 
+oracle_doc* oracle_doc_new_matrix(const mtr_options* opt) {
+    oracle_doc* d = oracle_doc_new(opt);
+    d->matrix = true;
+    d->tree.permMode = true;
+    d->cols.permMode = true;
+    return d;
+}
+
+void oracle_doc_select(oracle_doc* d, int32_t which) { d->sel = d->matrix && which ? 1 : 0; }
+
 int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint32_t op_lo, uint32_t op_hi) {
     Tree& t = d->tree;
     t.tabs.b = b;
+    d->cols.tabs.b = b;
     const mtr_doc_desc& dd = b->docs[doc_index];
     if (op_hi > dd.op_count) op_hi = dd.op_count;
     for (uint32_t i = op_lo; i < op_hi; i++) {
-        int st = t.apply(b->ops[dd.op_begin + i], dd);
+        const mtr_op& op = b->ops[dd.op_begin + i];
+        int st = d->matrix ? d->applyMatrix(op, dd) : t.apply(op, dd);
         if (st != MTR_OK) return st;
     }
-    return t.status;
+    return d->matrix ? (t.status != MTR_OK ? t.status : d->cols.status) : t.status;
 }
 
 int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap) {
-    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
+    if (!d->view().pendingLoad.empty()) d->view().reloadFromSegments();
     std::u16string s;
-    d->tree.gatherText(d->tree.root, s);
+    d->view().gatherText(d->view().root, s);
     int64_t n = int64_t(s.size());
     if (out) std::memcpy(out, s.data(), size_t(std::min(n, cap)) * 2);
     return n;
 }
 
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client) {
-    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
-    return d->tree.nodeLength(d->tree.root, ref_seq, client);
+    if (!d->view().pendingLoad.empty()) d->view().reloadFromSegments();
+    return d->view().nodeLength(d->view().root, ref_seq, client);
 }
 
 void oracle_doc_state(oracle_doc* d, int64_t* out) {
-    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
-    Tree& t = d->tree;
+    if (!d->view().pendingLoad.empty()) d->view().reloadFromSegments();
+    Tree& t = d->view();
     std::vector<Seg*> lv;
     t.leaves(t.root, lv);
     out[0] = t.minSeq;
@@ -1081,8 +1223,8 @@ void oracle_doc_state(oracle_doc* d, int64_t* out) {
 }
 
 int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap, int32_t* height) {
-    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
-    Tree& t = d->tree;
+    if (!d->view().pendingLoad.empty()) d->view().reloadFromSegments();
+    Tree& t = d->view();
     std::vector<Seg*> lv;
     t.leaves(t.root, lv);
     if (height) *height = t.height();
@@ -1113,7 +1255,7 @@ int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap, int32_t* hei
         r[3] = s->removed ? s->removedSeq : INT32_MIN;
         r[4] = int32_t(s->removedClientIds.size());
         r[5] = bnd;
-        r[6] = s->marker ? 1 : 0;
+        r[6] = s->perm ? s->start : (s->marker ? 1 : 0);  // PermutationSegment: its start handle
         r[7] = int32_t(s->hasProps ? h : 0);
     }
     return int64_t(lv.size());
@@ -1123,8 +1265,8 @@ int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap, int32_t* hei
 // SnapshotLegacy (snapshotlegacy.ts:122-255) and the chunk serializers (snapshotChunks.ts:86-149).
 int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint8_t* out, int64_t cap,
                              int64_t* blob_len, int32_t max_blobs) {
-    if (!d->tree.pendingLoad.empty()) d->tree.reloadFromSegments();
-    Tree& t = d->tree;
+    if (!d->view().pendingLoad.empty()) d->view().reloadFromSegments();
+    Tree& t = d->view();
     t.tabs.b = b;
     Emitter em{b, &b->docs[doc_index]};
     const int minSeq = t.minSeq;
@@ -1327,6 +1469,16 @@ int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_ind
             blobs.push_back(o.s);
         }
     }
+    if (d->matrix) {  // PermutationVector.summarize, permutationvector.ts:310-325: + the handleTable blob
+        Out o;
+        o.raw("[");
+        for (size_t k = 0; k < t.handles.size(); k++) {
+            if (k) o.raw(",");
+            o.num(t.handles[k]);
+        }
+        o.raw("]");
+        blobs.push_back(o.s);
+    }
     int64_t need = 0;
     for (auto& s : blobs) need += int64_t(s.size());
     if (need > cap || int32_t(blobs.size()) > max_blobs) return -need;
@@ -1388,6 +1540,73 @@ double oracle_replay_batch(const mtr_batch* b, const mtr_options* opt, uint32_t 
 
 
 // Synthetic op logs (include/mtr_synth.h) with the oracle as the exact simulator.
+// SharedMatrix op logs from the matrix recipe (mtr_synth_matrix_finish), one document per task;
+// per document: ops_per_doc + 1 records (START_COLLAB first); no text.  Digests are over the rows
+// vector's blobs followed by the cols vector's.
+int oracle_generate_matrix(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
+                           uint32_t hi, int nthreads, mtr_op* ops_out, uint64_t* hashes, int32_t* status) {
+    std::atomic<uint32_t> next{lo};
+    const uint32_t per = cfg->ops_per_doc + 1;
+    auto work = [&]() {
+        std::vector<uint8_t> out(1 << 16);
+        std::vector<int64_t> lens(4096);
+        uint16_t dummy_text[1] = {0};
+        for (;;) {
+            const uint32_t d = next.fetch_add(1);
+            if (d >= hi) break;
+            const uint32_t r = d - lo;
+            mtr_op* ops = ops_out + size_t(r) * per;
+            mtr_batch b = *tables;
+            mtr_doc_desc dd{};
+            dd.op_count = per;
+            dd.n_clients = cfg->writers + 1;
+            b.n_docs = 1;
+            b.docs = &dd;
+            b.ops = ops;
+            b.text = dummy_text;
+            oracle_doc* doc = oracle_doc_new_matrix(opt);
+            doc->tree.tabs.b = &b;
+            doc->cols.tabs.b = &b;
+            mtr_synth_state st;
+            mtr_synth_init(cfg, d, &st);
+            std::memset(ops, 0, sizeof(mtr_op) * per);
+            ops[0].type = MTR_OP_START_COLLAB;
+            int rc = doc->applyMatrix(ops[0], dd);
+            for (uint32_t k = 1; k < per && rc == MTR_OK; k++) {
+                mtr_op& op = ops[k];
+                mtr_synth_begin(cfg, &st, int32_t(k), &op);
+                const int Lr = std::max(0, doc->tree.nodeLength(doc->tree.root, op.ref_seq, op.client));
+                const int Lc = std::max(0, doc->cols.nodeLength(doc->cols.root, op.ref_seq, op.client));
+                mtr_synth_matrix_finish(cfg, &st, Lr, Lc, &op);
+                rc = doc->applyMatrix(op, dd);
+            }
+            uint64_t h = 0;
+            if (rc == MTR_OK && hashes) {
+                std::vector<std::string> blobs;
+                for (int w = 0; w < 2; w++) {
+                    oracle_doc_select(doc, w);
+                    int64_t nb;
+                    while ((nb = oracle_doc_summarize(doc, &b, 0, out.data(), int64_t(out.size()), lens.data(), 4096)) < 0)
+                        out.resize(size_t(-nb) + 16);
+                    int64_t off = 0;
+                    for (int64_t k = 0; k < nb; k++) {
+                        blobs.emplace_back(reinterpret_cast<const char*>(out.data() + off), size_t(lens[k]));
+                        off += lens[k];
+                    }
+                }
+                h = summary_hash(blobs);
+            }
+            if (hashes) hashes[r] = h;
+            if (status) status[r] = rc;
+            oracle_doc_free(doc);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
+    for (auto& x : th) x.join();
+    return MTR_OK;
+}
+
 int oracle_generate(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
                     uint32_t hi, int nthreads, mtr_op* ops_out, uint16_t* text_out, uint32_t* text_counts,
                     uint64_t* hashes, int32_t* status) {

@@ -21,6 +21,11 @@ extern "C" {
 typedef struct oracle_doc oracle_doc;
 
 oracle_doc* oracle_doc_new(const mtr_options* opt);
+/* A SharedMatrix document: rows and cols PermutationVectors driven by one op list (MTR_F_COLS,
+ * MTR_OP_SETCELL); text/length/state/export/summarize read the vector chosen by oracle_doc_select
+ * (0 = rows, 1 = cols); a vector's summary ends with its handleTable blob. */
+oracle_doc* oracle_doc_new_matrix(const mtr_options* opt);
+void oracle_doc_select(oracle_doc* d, int32_t which);
 void oracle_doc_free(oracle_doc* d);
 
 /* Apply ops [op_lo, op_hi) of document doc_index of batch b. Returns MTR_OK or an error code. */
@@ -37,7 +42,7 @@ int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_ind
                              uint8_t* out, int64_t cap, int64_t* blob_len, int32_t max_blobs);
 
 /* Export the leaf sequence for structural parity checks.  Per leaf 8 int32:
- * [len, seq, client, removed_seq (INT32_MIN if not removed), n_removers, bnd, is_marker, props_hash]
+ * [len, seq, client, removed_seq (INT32_MIN if not removed), n_removers, bnd, is_marker (permutation segment: start handle), props_hash]
  * bnd = number of tree levels at which the leaf starts a block (1 = starts its leaf block).
  * Returns number of leaves (or -(needed) if cap too small); *height = tree height. */
 int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap_leaves, int32_t* height);
@@ -57,6 +62,11 @@ struct mtr_synth_cfg;
 int oracle_generate(const struct mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
                     uint32_t hi, int nthreads, mtr_op* ops_out, uint16_t* text_out, uint32_t* text_counts,
                     uint64_t* hashes, int32_t* status);
+
+/* SharedMatrix op logs from mtr_synth_matrix_finish: (hi-lo) * (ops_per_doc+1) records; digest =
+ * rows blobs then cols blobs. */
+int oracle_generate_matrix(const struct mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt,
+                           uint32_t lo, uint32_t hi, int nthreads, mtr_op* ops_out, uint64_t* hashes, int32_t* status);
 
 /* Debug: print zamboni decisions to stdout */
 void oracle_set_trace(int on);

@@ -26,6 +26,9 @@ def lib():
         L.oracle_doc_new.restype = C.c_void_p
         L.oracle_doc_new.argtypes = [C.POINTER(abi.MtrOptions)]
         L.oracle_doc_free.argtypes = [C.c_void_p]
+        L.oracle_doc_new_matrix.restype = C.c_void_p
+        L.oracle_doc_new_matrix.argtypes = [C.POINTER(abi.MtrOptions)]
+        L.oracle_doc_select.argtypes = [C.c_void_p, C.c_int32]
         L.oracle_doc_apply.restype = C.c_int
         L.oracle_doc_apply.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]
         L.oracle_doc_text.restype = C.c_int64
@@ -40,6 +43,9 @@ def lib():
         L.oracle_generate.restype = C.c_int
         L.oracle_generate.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32,
                                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_generate_matrix.restype = C.c_int
+        L.oracle_generate_matrix.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32,
+                                             C.c_uint32, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_replay_batch.restype = C.c_double
         L.oracle_replay_batch.argtypes = [C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32, C.c_int,
                                           C.c_void_p, C.c_void_p]
@@ -54,9 +60,15 @@ def options(new_length_calc=False, snapshot_v1=True, chunk_size=10000):
 
 
 class OracleDoc:
-    def __init__(self, opts=None):
+    def __init__(self, opts=None, matrix=False):
         self.opts = opts or options()
-        self.h = lib().oracle_doc_new(C.byref(self.opts))
+        self.matrix = matrix
+        self.h = (lib().oracle_doc_new_matrix if matrix else lib().oracle_doc_new)(C.byref(self.opts))
+
+    def select(self, which: int) -> "OracleDoc":
+        """Matrix documents: direct queries at the rows (0) or cols (1) PermutationVector."""
+        lib().oracle_doc_select(self.h, which)
+        return self
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -166,3 +178,22 @@ def generate(cfg, tabs, lo, hi, threads=8, opts=None):
     packed = np.concatenate([text[i * int(cfg.text_cap): i * int(cfg.text_cap) + int(counts[i])] for i in range(n)]) \
         if n else np.zeros(0, "<u2")
     return with_docs(tabs, docs, ops, packed), hashes, status
+
+
+def generate_matrix(cfg, tabs, lo, hi, threads=8, opts=None):
+    """SharedMatrix op logs (mtr_synth_matrix_finish) of matrices [lo, hi) recorded with the oracle
+    -> (Batch with one document per matrix (the rows vector's op list), digests, statuses)."""
+    from fluidframework_amd.synth import with_docs
+    opts = opts or options()
+    n = hi - lo
+    per = cfg.ops_per_doc + 1
+    ops = np.zeros(n * per, dtype=abi.OP_DTYPE)
+    hashes = np.zeros(n, dtype="<u8")
+    status = np.zeros(n, dtype="<i4")
+    lib().oracle_generate_matrix(C.byref(cfg), C.addressof(tabs.c), C.byref(opts), lo, hi, threads,
+                                 ops.ctypes.data, hashes.ctypes.data, status.ctypes.data)
+    docs = np.zeros(n, dtype=abi.DOC_DTYPE)
+    docs["op_begin"] = np.arange(n, dtype=np.uint64) * per
+    docs["op_count"] = per
+    docs["n_clients"] = cfg.writers + 1
+    return with_docs(tabs, docs, ops, np.zeros(0, "<u2")), hashes, status

@@ -1,0 +1,188 @@
+"""SharedMatrix row/col PermutationVectors.
+
+CPU tests pin the oracle's restatement with hand-derived known answers from the reference code
+(matrix/src/matrix.ts:636-693 processCore, permutationvector.ts:209-247 getAllocatedHandle /
+adjustPosition, :418-443 handle recycling on UNLINK, handletable.ts:35-60 allocate/free) and check
+invariants on seeded synthetic logs.  The reference has no committed matrix summary fixtures, so
+parity for matrix summaries is unpinned by the reference (oracle restatement + engine agreement);
+GPU tests compare the HIP engine with the oracle vector by vector, leaf by leaf and byte by byte.
+"""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import abi
+from fluidframework_amd.batch import Interner, MatrixLog, build_batch, matrix_logs
+from fluidframework_amd.synth import make_cfg, tables, with_docs
+from oracle.oracle import OracleDoc, generate_matrix, options
+
+U = abi.HANDLE_UNALLOCATED
+
+
+def _msg(seq, ref, client, contents, msn=0):
+    return {"type": "op", "sequenceNumber": seq, "referenceSequenceNumber": ref, "minimumSequenceNumber": msn,
+            "clientId": client, "contents": contents}
+
+
+def _kat_log():
+    it = Interner()
+    log = MatrixLog()
+    log.start_collab("observer")
+    log.message(_msg(1, 0, "A", {"target": "rows", "type": 0, "pos1": 0, "seg": [3, 7]}), it)   # insertRows(0, 3)
+    log.message(_msg(2, 1, "A", {"target": "cols", "type": 0, "pos1": 0, "seg": [2, 9]}), it)   # insertCols(0, 2)
+    log.message(_msg(3, 2, "B", {"type": 2, "row": 1, "col": 1, "value": "x"}), it)             # setCell(1, 1)
+    log.message(_msg(4, 2, "B", {"type": 2, "row": 1, "col": 0, "value": "y"}), it)             # setCell(1, 0)
+    return log, it
+
+
+def _oracle(batch, doc=0):
+    o = OracleDoc(options(), matrix=True)
+    assert o.apply(batch, doc) == 0
+    return o
+
+
+def test_known_answer_handle_allocation():
+    """Inserted segments start unallocated (the remote start 7/9 is reset, permutationvector.ts:354-361);
+    setCell(1, 1) splits row 1 and col 1 out and gives each handle 1; setCell(1, 0) reuses row handle 1
+    (cache hit) and allocates col handle 2 for col 0 (no split at position 0: `if (start)`,
+    mergeTree.ts:2461)."""
+    log, it = _kat_log()
+    b = build_batch([log], it)
+    o = _oracle(b)
+    rows = o.select(0).summarize(b, 0)
+    cols = o.select(1).summarize(b, 0)
+    seg = lambda j: {"json": j, "seq": 1, "client": "A"}  # noqa: E731
+    assert json.loads(rows[0]) == {
+        "version": "1", "segmentCount": 3, "length": 3,
+        "segments": [seg([1, U]), seg([1, 1]), seg([1, U])], "startIndex": 0,
+        "headerMetadata": {"minSequenceNumber": 0, "sequenceNumber": 1, "orderedChunkMetadata": [{"id": "header"}],
+                           "totalLength": 3, "totalSegmentCount": 3}}
+    assert rows[1] == b"[2,0]"
+    seg2 = lambda j: {"json": j, "seq": 2, "client": "A"}  # noqa: E731
+    assert json.loads(cols[0])["segments"] == [seg2([1, 2]), seg2([1, 1])]
+    assert json.loads(cols[0])["headerMetadata"]["sequenceNumber"] == 2
+    assert cols[1] == b"[3,0,0]"
+
+
+def test_known_answer_recycling_and_coalescing():
+    """Removing an allocated row and moving the MSN past the removal unlinks it and frees its handle
+    (free list head = that handle, handles[h] = old head); below-MSN segments with contiguous handles
+    coalesce in the summary ([1,1] + [1,2] -> [2,1], PermutationSegment.canAppend)."""
+    it = Interner()
+    log = MatrixLog()
+    log.start_collab("observer")
+    log.message(_msg(1, 0, "A", {"target": "rows", "type": 0, "pos1": 0, "seg": [4, -1]}), it)
+    log.message(_msg(2, 1, "A", {"target": "cols", "type": 0, "pos1": 0, "seg": [1, -1]}), it)
+    for s, r in ((3, 0), (4, 1), (5, 2)):  # rows 0, 1, 2 get handles 1, 2, 3
+        log.message(_msg(s, 2, "A", {"type": 2, "row": r, "col": 0, "value": s}), it)
+    log.message(_msg(6, 5, "A", {"target": "rows", "type": 1, "pos1": 2, "pos2": 3}, msn=5), it)  # removeRows(2, 1)
+    log.message(_msg(7, 6, "A", {"target": "rows", "type": 0, "pos1": 3, "seg": [1, -1]}, msn=6), it)
+    b = build_batch([log], it)
+    o = _oracle(b)
+    rows = o.select(0).summarize(b, 0)
+    head = json.loads(rows[0])
+    # the removal found its block already queued for scouring (needsScour, mergeTree.ts:741-751), so
+    # the scour at MSN 5 kept it (removedSeq 6 > 5); nothing has unlinked it yet
+    assert head["headerMetadata"]["minSequenceNumber"] == 6
+    assert head["segments"] == [[2, 1], [1, U], {"json": [1, U], "seq": 7, "client": "A"}]
+    assert rows[1] == b"[4,0,0,0]"
+    # MSN 7 pops the block queued by seq 7: the removed row is unlinked and handle 3 freed
+    # (head -> 3 -> 4), the two unallocated rows below the MSN coalesce
+    log.message(_msg(8, 7, "A", {"target": "rows", "type": 0, "pos1": 0, "seg": [1, -1]}, msn=7), it)
+    b = build_batch([log], it)
+    assert o.apply(b, 0) == 0
+    rows = o.select(0).summarize(b, 0)
+    assert json.loads(rows[0])["segments"] == [{"json": [1, U], "seq": 8, "client": "A"}, [2, 1], [2, U]]
+    assert rows[1] == b"[3,0,0,4]"
+
+
+def test_packer_matrix_messages():
+    log, it = _kat_log()
+    ops = build_batch(matrix_logs([log]), it).ops
+    assert list(ops["type"]) == [abi.OP_START_COLLAB, abi.OP_INSERT, abi.OP_INSERT, abi.OP_SETCELL, abi.OP_SETCELL]
+    assert list(ops["flags"]) == [0, abi.F_LAST, abi.F_LAST | abi.F_COLS, 0, 0]
+    assert list(ops["payload2"][1:3]) == [3, 2]
+    assert list(ops["pos1"][3:]) == [1, 1] and list(ops["pos2"][3:]) == [1, 0]
+
+
+def matrix_cfg(n, ops, writers=8, max_lag=16, seed=0xfeedbed):
+    # C4 mix: 20 % row/col splices (insert 12 : remove 8), 80 % setCell
+    return make_cfg(n, ops, writers=writers, max_lag=max_lag, weights=(12, 8, 80), max_text=4, max_range=3,
+                    seed=seed)
+
+
+def handle_invariants(o, batch, doc):
+    """Every live handle is covered by exactly one segment range, the free list is acyclic and holds
+    exactly the handles no segment owns."""
+    ex, _ = o.export()
+    table = json.loads(o.summarize(batch, doc)[-1])
+    owned = set()
+    for r in ex:
+        if r[6] >= 1:
+            for h in range(int(r[6]), int(r[6]) + int(r[0])):
+                assert h not in owned
+                owned.add(h)
+    free, h, seen = set(), table[0], 0
+    while h < len(table):
+        assert h not in free
+        free.add(h)
+        h = table[h]
+        seen += 1
+        assert seen <= len(table)
+    assert owned.isdisjoint(free)
+    assert owned | free == set(range(1, len(table)))
+
+
+@pytest.mark.parametrize("writers,lag", [(8, 16), (3, 0), (16, 64)])
+def test_synthetic_matrix_oracle_invariants(writers, lag):
+    cfg = matrix_cfg(8, 1500, writers=writers, max_lag=lag)
+    tabs = tables(writers=writers)
+    b, hashes, status = generate_matrix(cfg, tabs, 0, 8, threads=4)
+    assert (status == 0).all()
+    for d in range(8):
+        o = _oracle(b, d)
+        for w in (0, 1):
+            handle_invariants(o.select(w), b, d)
+
+
+def expand_pairs(batch, tabs):
+    """One generated document per matrix -> engine order [rows 0, cols 0, rows 1, ...]."""
+    n = batch.n_docs
+    docs = np.zeros(2 * n, dtype=abi.DOC_DTYPE)
+    docs[0::2] = batch.docs
+    docs[1::2]["op_begin"] = batch.docs["op_begin"]
+    docs[1::2]["n_clients"] = batch.docs["n_clients"]
+    return with_docs(tabs, docs, batch.ops, batch.text)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("writers,lag,ops", [(8, 16, 2000), (16, 64, 1500), (3, 0, 1000)])
+def test_matrix_engine_matches_oracle(writers, lag, ops):
+    from fluidframework_amd.engine import Engine
+
+    n = 48
+    cfg = matrix_cfg(n, ops, writers=writers, max_lag=lag)
+    tabs = tables(writers=writers)
+    gb, _, status = generate_matrix(cfg, tabs, 0, n, threads=8)
+    assert (status == 0).all()
+    b = expand_pairs(gb, tabs)
+    eng = Engine(2 * n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=1 << 15,
+                 prop_words=1024, remover_cells=4096, ops_per_launch=64)
+    for m in range(n):
+        eng.set_matrix(2 * m, 2 * m + 1)
+    eng.apply(b)
+    eng.summarize()
+    for m in range(n):
+        o = _oracle(gb, m)
+        for w in (0, 1):
+            d = 2 * m + w
+            st, op = eng.status(d)
+            assert st == 0, f"matrix {m} vector {w}: status {st:#x} at op {op}"
+            o.select(w)
+            ge, gh = eng.export(d)
+            oe, oh = o.export()
+            assert gh == oh and np.array_equal(ge, oe), f"matrix {m} vector {w}: leaves differ"
+            assert eng.summary(d) == o.summarize(gb, m), f"matrix {m} vector {w}: summary bytes differ"
