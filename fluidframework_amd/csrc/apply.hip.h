@@ -461,10 +461,11 @@ struct Eng {
     }
     // first i with E[i] >= pos (S if none): 64-ary search
     static MTR_DI int lower_bound_E(const D& L, const St& s, int pos) {
-        int lo = 0, hi = s.nseg;  // answer in [lo, hi]
+        int lo = 0, hi = s.nseg;  // answer in [lo, hi]; hi qualifies (or is S)
         const int ln = lane_id();
         while (hi - lo > 64) {
-            const int stride = (hi - lo + 63) >> 6;
+            // the hi - lo + 1 candidates in 64 strides: lane 63's probe reaches hi, which qualifies
+            const int stride = (hi - lo + 64) >> 6;
             const int idx = lo + (ln + 1) * stride - 1;
             const uint64_t m = __ballot(idx >= hi || L.E[min(idx, hi - 1)] >= pos);
             const int k = first_lane(m);  // lane 63 always qualifies

@@ -814,6 +814,17 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
     return hd.h.nseg;
 }
 
+// debug: the scan arrays (E, V) an HBM-resident document's last op left in the scratch slab
+int64_t mtr_debug_scan(mtr_engine* e, uint32_t doc, int32_t* out, int64_t n) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const size_t sc = e->caps.max_segments;
+    if (!e->scratch.p || doc >= e->n_docs || n > int64_t(sc)) return -1;
+    HIPCHK(hipMemcpy(out, e->scratch.p + size_t(doc) * 2 * sc, size_t(n) * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out + n, e->scratch.p + size_t(doc) * 2 * sc + sc, size_t(n) * 4, hipMemcpyDeviceToHost));
+    return n;
+}
+
 int mtr_stats(mtr_engine* e, int64_t* out, int32_t n) {
     HIPCHK(hipSetDevice(e->device));
     HIPCHK(hipStreamSynchronize(e->stream));

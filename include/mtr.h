@@ -122,6 +122,10 @@ int mtr_download_batch(mtr_engine* e, uint32_t lo, uint32_t hi, mtr_doc_desc* do
  * Only a -DMTR_PROF build collects them; otherwise returns MTR_ERR_UNSUPPORTED and zeros. */
 int mtr_profile(mtr_engine* e, uint64_t* out, int32_t n, int32_t reset);
 
+/* Debug: copy the scan arrays (E = inclusive visible-length prefix, V = visible length per leaf) that
+ * the last op of HBM-resident document `doc` computed: out[0..n) = E, out[n..2n) = V.  Returns n or -1. */
+int64_t mtr_debug_scan(mtr_engine* e, uint32_t doc, int32_t* out, int64_t n);
+
 /* Human-readable description of the last engine-level error (static storage). */
 const char* mtr_last_error(void);
 

@@ -1607,11 +1607,15 @@ int oracle_generate_matrix(const mtr_synth_cfg* cfg, const mtr_batch* tables, co
     return MTR_OK;
 }
 
-int oracle_generate(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
-                    uint32_t hi, int nthreads, mtr_op* ops_out, uint16_t* text_out, uint32_t* text_counts,
-                    uint64_t* hashes, int32_t* status) {
+// The recipe of include/mtr_synth.h driven by this oracle.  With grow > 0 every document first
+// loads `grow` two-unit segments as a summary header (MTR_OP_LOAD, reloadFromSegments) before
+// collaboration starts: the pre-grown documents of config C5.  Per document:
+// grow + 1 + ops_per_doc records; text capacity cfg->text_cap units (>= 2 * grow + inserts).
+static int generate_impl(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
+                         uint32_t hi, int nthreads, uint32_t grow, mtr_op* ops_out, uint16_t* text_out,
+                         uint32_t* text_counts, uint64_t* hashes, int32_t* status) {
     std::atomic<uint32_t> next{lo};
-    const uint32_t per = cfg->ops_per_doc + 1;
+    const uint32_t per = grow + cfg->ops_per_doc + 1;
     auto work = [&]() {
         std::vector<uint8_t> out(1 << 16);
         std::vector<int64_t> lens(4096);
@@ -1637,10 +1641,24 @@ int oracle_generate(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr
             mtr_synth_state st;
             mtr_synth_init(cfg, d, &st);
             std::memset(ops, 0, sizeof(mtr_op) * per);
-            ops[0].type = MTR_OP_START_COLLAB;
-            int rc = doc->tree.apply(ops[0], dd);
-            for (uint32_t k = 1; k < per && rc == MTR_OK; k++) {
+            int rc = MTR_OK;
+            for (uint32_t k = 0; k < grow && rc == MTR_OK; k++) {  // snapshot header segments
                 mtr_op& op = ops[k];
+                op.type = MTR_OP_LOAD;
+                op.client = uint16_t(MTR_CLIENT_NONCOLLAB);
+                op.ref_seq = -1;
+                op.pos2 = -1;
+                op.payload = 2 * k;
+                op.payload2 = 2;
+                text[2 * k] = uint16_t('a' + k % 26);
+                text[2 * k + 1] = uint16_t('A' + (k / 26) % 26);
+                rc = doc->tree.apply(op, dd);
+            }
+            st.text_used = 2 * grow;
+            ops[grow].type = MTR_OP_START_COLLAB;
+            if (rc == MTR_OK) rc = doc->tree.apply(ops[grow], dd);
+            for (uint32_t k = 1; k <= cfg->ops_per_doc && rc == MTR_OK; k++) {
+                mtr_op& op = ops[grow + k];
                 mtr_synth_begin(cfg, &st, int32_t(k), &op);
                 const int L = std::max(0, doc->tree.nodeLength(doc->tree.root, op.ref_seq, op.client));
                 mtr_synth_finish(cfg, &st, L, &op, text);
@@ -1670,6 +1688,18 @@ int oracle_generate(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr
     for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
     for (auto& t : th) t.join();
     return 0;
+}
+
+int oracle_generate(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
+                    uint32_t hi, int nthreads, mtr_op* ops_out, uint16_t* text_out, uint32_t* text_counts,
+                    uint64_t* hashes, int32_t* status) {
+    return generate_impl(cfg, tables, opt, lo, hi, nthreads, 0, ops_out, text_out, text_counts, hashes, status);
+}
+
+int oracle_generate_grown(const mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt, uint32_t lo,
+                          uint32_t hi, int nthreads, uint32_t grow, mtr_op* ops_out, uint16_t* text_out,
+                          uint32_t* text_counts, uint64_t* hashes, int32_t* status) {
+    return generate_impl(cfg, tables, opt, lo, hi, nthreads, grow, ops_out, text_out, text_counts, hashes, status);
 }
 
 }  // extern "C"

@@ -63,6 +63,12 @@ int oracle_generate(const struct mtr_synth_cfg* cfg, const mtr_batch* tables, co
                     uint32_t hi, int nthreads, mtr_op* ops_out, uint16_t* text_out, uint32_t* text_counts,
                     uint64_t* hashes, int32_t* status);
 
+/* As oracle_generate, after `grow` pre-loaded two-unit header segments per document (config C5):
+ * (hi-lo) * (grow + 1 + ops_per_doc) records; cfg->text_cap must hold 2 * grow + the inserts. */
+int oracle_generate_grown(const struct mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt,
+                          uint32_t lo, uint32_t hi, int nthreads, uint32_t grow, mtr_op* ops_out, uint16_t* text_out,
+                          uint32_t* text_counts, uint64_t* hashes, int32_t* status);
+
 /* SharedMatrix op logs from mtr_synth_matrix_finish: (hi-lo) * (ops_per_doc+1) records; digest =
  * rows blobs then cols blobs. */
 int oracle_generate_matrix(const struct mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt,

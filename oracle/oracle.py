@@ -43,6 +43,10 @@ def lib():
         L.oracle_generate.restype = C.c_int
         L.oracle_generate.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32,
                                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_generate_grown.restype = C.c_int
+        L.oracle_generate_grown.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32,
+                                            C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_void_p]
         L.oracle_generate_matrix.restype = C.c_int
         L.oracle_generate_matrix.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32,
                                              C.c_uint32, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -150,20 +154,22 @@ def summary_digest(blobs):
     return h
 
 
-def generate(cfg, tabs, lo, hi, threads=8, opts=None):
+def generate(cfg, tabs, lo, hi, threads=8, opts=None, grow=0):
     """Synthetic op logs of documents [lo, hi) recorded with the oracle as the exact simulator
-    -> (Batch, summary digests, statuses)."""
+    -> (Batch, summary digests, statuses).  grow > 0: every document first loads `grow` two-unit
+    header segments (config C5's pre-grown documents); cfg.text_cap must cover 2 * grow more units."""
     from fluidframework_amd.synth import with_docs
     opts = opts or options()
     n = hi - lo
-    per = cfg.ops_per_doc + 1
+    per = grow + cfg.ops_per_doc + 1
     ops = np.zeros(n * per, dtype=abi.OP_DTYPE)
     text = np.zeros(n * int(cfg.text_cap), dtype="<u2")
     counts = np.zeros(n, dtype="<u4")
     hashes = np.zeros(n, dtype="<u8")
     status = np.zeros(n, dtype="<i4")
-    lib().oracle_generate(C.byref(cfg), C.addressof(tabs.c), C.byref(opts), lo, hi, threads, ops.ctypes.data,
-                          text.ctypes.data, counts.ctypes.data, hashes.ctypes.data, status.ctypes.data)
+    lib().oracle_generate_grown(C.byref(cfg), C.addressof(tabs.c), C.byref(opts), lo, hi, threads, grow,
+                                ops.ctypes.data, text.ctypes.data, counts.ctypes.data, hashes.ctypes.data,
+                                status.ctypes.data)
     docs = np.zeros(n, dtype=abi.DOC_DTYPE)
     docs["op_begin"] = np.arange(n, dtype=np.uint64) * per
     docs["op_count"] = per

@@ -196,3 +196,33 @@ def test_summarize_load_continue_on_device():
     for d in range(n):
         _compare_export(eng, n + d, orcs[d])
         assert eng.summary(n + d) == orcs[d].summarize(b, n + d)
+
+
+def test_c5_shaped_hbm_resident():
+    """Config C5's shape at test scale: documents pre-grown through a summary load
+    (20k header segments, reloadFromSegments), then 64 writers with lags up to 4096 keeping the MSN
+    far behind (deep collaboration window).  The documents exceed LDS, so the engine runs them
+    HBM-resident (apply_kernel<true>); leaves, tree shape and summary bytes equal the oracle's."""
+    import time
+
+    from fluidframework_amd.synth import make_cfg, tables
+    from oracle.oracle import generate
+
+    n, grow, ops = 8, 20000, 2000
+    cfg = make_cfg(n, ops, writers=64, max_lag=4096, text_cap=2 * grow + ops * 18 + 16)
+    tabs = tables(writers=64)
+    b, _, status = generate(cfg, tabs, 0, n, threads=8, grow=grow)
+    assert (status == 0).all()
+    eng = _engine(n, max_segments=grow + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
+                  text_units=2 * (int(cfg.text_cap) + 8192), ops_per_launch=256)
+    t0 = time.time()
+    eng.apply(b)
+    eng.summarize()
+    print(f"C5-shaped: {n} docs x ({grow} loaded + {ops} ops) in {time.time() - t0:.2f} s", eng.timing())
+    for d in range(n):
+        st, op = eng.status(d)
+        assert st == 0, f"doc {d}: status {st:#x} at op {op}"
+        orc = OracleDoc(options())
+        assert orc.apply(b, d) == 0
+        _compare_export(eng, d, orc)
+        assert eng.summary(d) == orc.summarize(b, d)
