@@ -294,8 +294,10 @@ struct ProfScope {
 
 // G: leaves in HBM (documents larger than LDS); PM: PermutationVector documents (SharedMatrix
 // rows/cols, permutationvector.ts) -- a separate instantiation so the SharedString kernel carries
-// no permutation code
-template <bool G, bool PM = false>
+// no permutation code; CAP: the launch's LDS leaf capacity as a compile-time constant (0 = runtime),
+// which puts every leaf array at a constant LDS offset (ds_read/ds_write immediate offsets from one
+// per-lane address instead of a base register and an address add per array)
+template <bool G, bool PM = false, int CAP = 0>
 struct Eng {
     using D = Doc<G>;
     template <class T>
@@ -1718,7 +1720,7 @@ struct Eng {
             L.sc = (lptr<Sc>)(smem);
             L.gst = (lptr<mtr_synth_state>)(smem + ((sizeof(Sc) + 15) & ~size_t(15)));
         } else {
-            const int cap = P.cap, lhcap = P.lhcap;
+            const int cap = CAP ? CAP : P.cap, lhcap = P.lhcap;
             char* p = smem;
             auto take = [&](size_t n) {
                 char* r = p;
@@ -2016,13 +2018,17 @@ struct Eng {
     }
 };
 
-template <bool G>
+template <bool G, int CAP = 0>
 __global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
-    Eng<G>::run(smem, P, d);
+    Eng<G, false, CAP>::run(smem, P, d);
 }
+
+// leaf capacities with a compile-time LDS layout (apply_kernel<false, CAP>); other capacities use
+// the runtime layout (CAP = 0)
+#define MTR_FIXED_CAPS(X) X(128) X(192) X(256) X(320) X(384) X(448) X(512) X(640) X(768)
 
 // SharedMatrix pairs: one wave applies a matrix's op list to its two PermutationVectors, each with
 // its own LDS region of `pair_region` bytes (HBM-resident arrays in global mode)

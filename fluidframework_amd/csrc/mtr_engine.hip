@@ -429,6 +429,11 @@ static int run_impl(mtr_engine* e, int gen) {
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
+#define MTR_CAP_ATTR(C)                                                                                   \
+    (void)hipFuncSetAttribute((const void*)apply_kernel<false, C>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              160 * 1024);
+        MTR_FIXED_CAPS(MTR_CAP_ATTR)
+#undef MTR_CAP_ATTR
         (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
     });
@@ -501,7 +506,16 @@ static int run_impl(mtr_engine* e, int gen) {
             } else if (P.global_mode) {
                 apply_kernel<true><<<cnt, NT, lds, st>>>(P);
             } else {
-                apply_kernel<false><<<cnt, NT, lds, st>>>(P);
+                switch (cap) {
+#define MTR_CAP_CASE(C)                                     \
+    case C:                                                 \
+        apply_kernel<false, C><<<cnt, NT, lds, st>>>(P);    \
+        break;
+                    MTR_FIXED_CAPS(MTR_CAP_CASE)
+#undef MTR_CAP_CASE
+                    default:
+                        apply_kernel<false><<<cnt, NT, lds, st>>>(P);
+                }
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e->kev[2 * nl + 1], st));
