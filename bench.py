@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--ops", type=int, default=None, help="sequenced messages per document (preset)")
     ap.add_argument("--writers", type=int, default=None)
     ap.add_argument("--max-lag", type=int, default=None)
-    ap.add_argument("--ops-per-launch", type=int, default=16)
+    ap.add_argument("--ops-per-launch", type=int, default=24)
     ap.add_argument("--cpu-sample-docs", type=int, default=0, help="default: about 4M messages of documents")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
