@@ -186,6 +186,7 @@ struct St {
     int collab, local, heapn, uidnext;
     int textused, propused, rmused, status;  // textused: handle-table length for permutation vectors
     int fail_op, max_heap, ops_done, texthalf;
+    int htop;  // seq of the LRU heap's top entry (valid while heapn > 0)
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
 
@@ -501,12 +502,27 @@ struct Eng {
         return -1;
     }
 
+    // [bs, be) = the leaf block holding leaf x, from one ballot over leaves x-31 .. x+32 (leaf
+    // blocks hold at most 7 leaves); the loops above take over only if a bound lies outside
+    static MTR_DI void block_bounds1(const D& L, const St& s, int x, int& bs, int& be) {
+        const int S = s.nseg;
+        const int ln = lane_id();
+        const int i = x - 31 + ln;
+        const bool in = i >= 0 && i < S;
+        const bool b = in && bnd_of(L.meta[in ? i : 0]) >= 1;
+        const uint64_t sm = __ballot(ln <= 31 && (i <= 0 || b));
+        const uint64_t em = __ballot(ln > 31 && (i >= S || b));
+        bs = sm ? max(0, x - 31 + last_lane(sm)) : block_start(L, x - 32, 1);
+        be = em ? x - 31 + first_lane(em) : block_end(L, s, x + 32, 1);
+    }
+
     // Block overflow after a leaf was added next to x (insertingWalk split + updateRoot,
     // mergeTree.ts:1831-1871, 1268-1277).
     static MTR_DI void overflow_fix(D& L, St& s, int x) {
         PROF(P_OVERFLOW);
         int level = 1;
-        int bs = block_start(L, x, 1), be = block_end(L, s, x, 1);
+        int bs, be;
+        block_bounds1(L, s, x, bs, be);
         int cnt = be - bs;
         while (cnt >= kMaxNodesInBlock) {
             int c5 = bs + kMaxNodesInBlock / 2;
@@ -546,6 +562,7 @@ struct Eng {
         L.hseq[k] = sq;
         L.huid[k] = u;
         wsync();
+        if (k == 1) s.htop = sq;
         if (s.heapn > s.max_heap) s.max_heap = s.heapn;
     }
     static MTR_DI uint32_t heap_pop(D& L, St& s) {
@@ -557,6 +574,7 @@ struct Eng {
         n--;
         s.heapn = n;
         int k = 1;
+        s.htop = ls;
         while ((k << 1) <= n) {
             int j = k << 1;
             int sj = uni(L.hseq[j]);
@@ -568,6 +586,7 @@ struct Eng {
                 }
             }
             if (ls - sj <= 0) break;
+            if (k == 1) s.htop = sj;
             L.hseq[k] = sj;
             L.huid[k] = uniu(L.huid[j]);
             k = j;
@@ -1119,23 +1138,11 @@ struct Eng {
         PROF_COUNT(P_NZBLOCK);
         const lptr<Sc> sc = L.sc;
         const int H = s.height;
-        const int rs1 = block_start(L, x, 1), re1 = block_end(L, s, x, 1);
-        if (ns_of(uniu(L.meta[rs1])) == NS_FALSE) return -1;
-        sc->rs[1] = rs1;
-        sc->re[1] = re1;
-        {
-            int ps = rs1;
-            for (int l = 1; l <= H; l++) {
-                if (l > 1) {
-                    const int a = block_start(L, ps, l), b = block_end(L, s, ps, l);
-                    sc->rs[l] = a;
-                    sc->re[l] = b;
-                    ps = a;
-                }
-                sc->topb[l] = bnd_of(uniu(L.meta[ps]));
-            }
-        }
-        wsync();
+        int rs1, re1;
+        block_bounds1(L, s, x, rs1, re1);
+        const uint32_t m1 = uniu(L.meta[rs1]);
+        if (ns_of(m1) == NS_FALSE) return -1;
+        const int topb1 = bnd_of(m1);
         const int before = re1 - rs1;
         int kept;
         {
@@ -1143,18 +1150,30 @@ struct Eng {
             kept = re1 - rs1 <= 64 ? scour_par(L, P, s, rs1, re1) : -1;
             if (kept < 0) kept = scour_range(L, P, s, rs1, re1);
         }
+        const bool pack = kept < before && kept < kMaxNodesInBlock / 2 && H > 1;
+        if (pack) {  // the enclosing blocks, read before any bnd value moves (scour keeps them)
+            int ps = rs1;
+            for (int l = 2; l <= H; l++) {
+                const int a = block_start(L, ps, l), b = block_end(L, s, ps, l);
+                sc->rs[l] = a;
+                sc->re[l] = b;
+                sc->topb[l] = bnd_of(uniu(L.meta[a]));
+                ps = a;
+            }
+            wsync();
+        }
         {  // block.needsScour = false, kept on the block's first surviving leaf
             const int i = rs1 + lane_id();
             const uint64_t m = __ballot(i < re1 && !(L.meta[min(i, re1 - 1)] & M_DEL));
             if (m) {
                 const int first = rs1 + first_lane(m);
-                L.meta[first] = set_ns(set_bnd(uniu(L.meta[first]), uni(sc->topb[1])), NS_FALSE);
+                L.meta[first] = set_ns(set_bnd(uniu(L.meta[first]), topb1), NS_FALSE);
                 wsync();
             }
         }
         if (kept >= before) return -1;
         int from = rs1;
-        if (kept < kMaxNodesInBlock / 2 && H > 1) {
+        if (pack) {
             PROF(P_PACK);
             PROF_COUNT(P_NPACK);
             for (int l = 2; l <= H; l++) {  // packParent chain
@@ -1211,7 +1230,7 @@ struct Eng {
         if (!s.collab) return;
         for (int it = 0; it < 2; it++) {
             if (s.heapn == 0 || s.status != MTR_OK) return;
-            if (uni(L.hseq[1]) > s.minseq) return;
+            if (s.htop > s.minseq) return;
             const uint32_t u = heap_pop(L, s);
             const int x = find_uid(L, s, u);
             if (x < 0) continue;
@@ -1649,6 +1668,7 @@ struct Eng {
             }
         }
         wsync();
+        s.htop = s.heapn > 0 ? uni(L.hseq[1]) : 0;
     }
 
     static MTR_DI void store_doc(D& L, const KParams& P, const St& s, uint32_t d) {
