@@ -1266,36 +1266,42 @@ struct Eng {
         const int S = s.nseg;
         const int i = lower_bound_E(L, s, pos);
         if (i >= S) return;
-        const int be = block_end(L, s, i, 1);
-        const int jj = i + lane_id();
-        bool c = false;
-        if (jj < be) {
-            const int vj = L.V[jj];
-            c = vj >= 0 && pos < L.E[jj];
+        // one batch of loads for leaves i .. i+63: the leaf block's end, the leaf to split and
+        // every field the split copies (a leaf block holds at most 7 leaves)
+        const int ln = lane_id();
+        const int jj = i + ln;
+        const bool in = jj < S;
+        int vj = 0, ej = 0, lj = 0, sqj = 0, rsj = 0;
+        uint32_t mj = 0, tj = 0, pj = 0, rmj = 0;
+        if (in) {
+            vj = L.V[jj]; ej = L.E[jj]; mj = L.meta[jj]; lj = L.len[jj]; sqj = L.seq[jj];
+            rsj = L.rseq[jj]; tj = L.text[jj]; pj = L.props[jj]; rmj = L.rm[jj];
         }
-        const uint64_t cm = __ballot(c);
+        const uint64_t em = __ballot(!in || (ln > 0 && bnd_of(mj) >= 1));
+        const int be = em ? i + first_lane(em) : block_end(L, s, i + 63, 1);
+        const uint64_t cm = __ballot(jj < be && vj >= 0 && pos < ej);
         if (!cm) return;
-        const int j = i + first_lane(cm);
-        const int v = uni(L.V[j]), e = uni(L.E[j]);
-        const uint32_t mj = uniu(L.meta[j]);
+        const int jl = first_lane(cm);
+        const int j = i + jl;
+        const int v = rdlane(vj, jl), e = rdlane(ej, jl);
+        const uint32_t m0 = rdlane(mj, jl);
         const int off = pos - (e - v);
-        if (!(off > 0 && !(mj & M_MARKER))) return;
+        if (!(off > 0 && !(m0 & M_MARKER))) return;
         shift_right1(L, s, j + 1);
         {  // BaseSegment.splitAt, mergeTreeNodes.ts:481-510
             const int r = j + 1;
-            const int lj = uni(L.len[j]);
-            L.len[r] = lj - off;
+            L.len[r] = rdlane(lj, jl) - off;
             L.len[j] = off;
-            L.seq[r] = uni(L.seq[j]);
-            L.rseq[r] = uni(L.rseq[j]);
-            L.meta[r] = set_ns(set_bnd(mj, 0), NS_UNDEF);
-            L.meta[j] = (mj & M_NONL) ? (mj & ~M_NL) : ((mj & ~M_NL) | M_NLQ);
+            L.seq[r] = rdlane(sqj, jl);
+            L.rseq[r] = rdlane(rsj, jl);
+            L.meta[r] = set_ns(set_bnd(m0, 0), NS_UNDEF);
+            L.meta[j] = (m0 & M_NONL) ? (m0 & ~M_NL) : ((m0 & ~M_NL) | M_NLQ);
             {  // TextSegment: text offset; PermutationSegment: start + pos unless unallocated
-                const uint32_t tj = uniu(L.text[j]);
-                L.text[r] = tj == uint32_t(MTR_HANDLE_UNALLOCATED) ? tj : tj + uint32_t(off);
+                const uint32_t t0 = rdlane(tj, jl);
+                L.text[r] = t0 == uint32_t(MTR_HANDLE_UNALLOCATED) ? t0 : t0 + uint32_t(off);
             }
-            L.props[r] = uniu(L.props[j]);
-            L.rm[r] = uniu(L.rm[j]);
+            L.props[r] = rdlane(pj, jl);
+            L.rm[r] = rdlane(rmj, jl);
             L.uid[r] = uint32_t(s.uidnext++);
             // split leaves are fully visible in this view
             L.V[j] = off;
@@ -1353,6 +1359,8 @@ struct Eng {
         }
         const int S = s.nseg;
         int slot = -1, inherit = 0;
+        uint32_t om = 0;  // meta of the leaf that starts the block when the new leaf takes its place
+        bool om_known = false;
         {
             PROF(P_INS1);
             if (S == 0) {
@@ -1363,16 +1371,41 @@ struct Eng {
                 if (i >= S) {
                     s.status = MTR_ERR_INSERT_FAILED;
                 } else {
-                    const int bs = block_start(L, i, 1), be = block_end(L, s, i, 1);
-                    const int j = i + ln;
-                    bool c = false;
-                    if (j < be) {  // breakTie, mergeTree.ts:1719-1738
-                        const int vj = L.V[j];
-                        c = vj >= 0 && (L.E[j] > pos || (vj == 0 && seq > L.seq[j]));
+                    // one batch of loads over leaves i-31 .. i+32: the leaf block's bounds and the
+                    // breakTie candidates (mergeTree.ts:1719-1738) in [i, be)
+                    const int w = i - 31 + ln;
+                    const bool inw = w >= 0 && w < S;
+                    int vw = 0, ew = 0, sw = 0;
+                    uint32_t mw = 0;
+                    if (inw) {
+                        vw = L.V[w]; ew = L.E[w]; sw = L.seq[w]; mw = L.meta[w];
                     }
-                    const uint64_t cm = __ballot(c);
-                    slot = cm ? i + first_lane(cm) : be;
-                    inherit = slot == bs ? 1 : 0;
+                    const bool bw = inw && bnd_of(mw) >= 1;
+                    const uint64_t sm = __ballot(ln <= 31 && (w <= 0 || bw));
+                    const uint64_t em = __ballot(ln > 31 && (w >= S || bw));
+                    if (sm && em) {
+                        const int bs = max(0, i - 31 + last_lane(sm));
+                        const int be = i - 31 + first_lane(em);
+                        const uint64_t cm =
+                            __ballot(ln >= 31 && w < be && vw >= 0 && (ew > pos || (vw == 0 && seq > sw)));
+                        slot = cm ? i - 31 + first_lane(cm) : be;
+                        inherit = slot == bs ? 1 : 0;
+                        if (inherit) {
+                            om = uint32_t(rdlane(int(mw), bs - i + 31));
+                            om_known = true;
+                        }
+                    } else {  // a bound outside the window
+                        const int bs = block_start(L, i, 1), be = block_end(L, s, i, 1);
+                        const int j = i + ln;
+                        bool c = false;
+                        if (j < be) {
+                            const int vj = L.V[j];
+                            c = vj >= 0 && (L.E[j] > pos || (vj == 0 && seq > L.seq[j]));
+                        }
+                        const uint64_t cm = __ballot(c);
+                        slot = cm ? i + first_lane(cm) : be;
+                        inherit = slot == bs ? 1 : 0;
+                    }
                 }
             }
         }
@@ -1386,7 +1419,7 @@ struct Eng {
             s.height = 1;
             m = set_bnd(m, 1);
         } else if (inherit) {
-            const uint32_t om = uniu(L.meta[slot + 1]);
+            if (!om_known) om = uniu(L.meta[slot + 1]);
             m = set_ns(set_bnd(m, bnd_of(om)), ns_of(om));
             L.meta[slot + 1] = set_ns(set_bnd(om, 0), NS_UNDEF);
         }
@@ -1515,12 +1548,13 @@ struct Eng {
         for (int base = lower_bound_E(L, s, start + 1); base < S; base += 64) {
             const int j = base + ln;
             const bool in = j < S;
-            int vj = 0, ej = 0;
+            int vj = 0, ej = 0, rj = RNONE;
             uint32_t mj = 0;
             if (in) {
                 vj = L.V[j];
                 ej = L.E[j];
                 mj = L.meta[j];
+                if (is_remove) rj = L.rseq[j];
             }
             const uint64_t stop = __ballot(!in || ej - max(vj, 0) >= end);
             const int lim = stop ? first_lane(stop) : 64;
@@ -1528,7 +1562,7 @@ struct Eng {
             const uint64_t am = __ballot(act);
             if (am) {
                 if (is_remove) {
-                    const int rs = act ? L.rseq[j] : RNONE;
+                    const int rs = act ? rj : RNONE;
                     const bool ov = act && rs != RNONE;  // overlapping remove: removedClientIds.push
                     const uint64_t om = __ballot(ov);
                     const int nov = __popcll(om);
