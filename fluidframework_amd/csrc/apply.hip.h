@@ -517,15 +517,18 @@ struct Eng {
     }
 
     // Block overflow after a leaf was added next to x (insertingWalk split + updateRoot,
-    // mergeTree.ts:1831-1871, 1268-1277).
-    static MTR_DI void overflow_fix(D& L, St& s, int x) {
+    // mergeTree.ts:1831-1871, 1268-1277).  [hbs, hbe) = x's leaf block when the caller knows it.
+    // Returns the start of x's leaf block afterwards.
+    static MTR_DI int overflow_fix(D& L, St& s, int x, int hbs = -1, int hbe = -1) {
         PROF(P_OVERFLOW);
         int level = 1;
-        int bs, be;
-        block_bounds1(L, s, x, bs, be);
+        int bs = hbs, be = hbe;
+        if (bs < 0) block_bounds1(L, s, x, bs, be);
         int cnt = be - bs;
+        int xbs = bs;
         while (cnt >= kMaxNodesInBlock) {
             int c5 = bs + kMaxNodesInBlock / 2;
+            if (level == 1 && x >= c5) xbs = c5;
             if (level > 1) c5 = nth_bnd(L, bs, be, level - 1, kMaxNodesInBlock / 2);
             uint32_t m = set_bnd(uniu(L.meta[c5]), level);
             if (level == 1) m = set_ns(m, NS_UNDEF);
@@ -542,6 +545,7 @@ struct Eng {
             be = block_end(L, s, bs, level);
             cnt = count_bnd(L, bs, be, level - 1);
         }
+        return xbs;
     }
 
     // ---- LRU heap (collections/heap.ts:11-67), 1-based, hole-based sifts (same order as swaps)
@@ -1136,7 +1140,6 @@ struct Eng {
     static MTR_DI int zamboni_block(D& L, const KParams& P, St& s, int x) {
         PROF(P_ZBLOCK);
         PROF_COUNT(P_NZBLOCK);
-        const lptr<Sc> sc = L.sc;
         const int H = s.height;
         int rs1, re1;
         block_bounds1(L, s, x, rs1, re1);
@@ -1150,18 +1153,6 @@ struct Eng {
             kept = re1 - rs1 <= 64 ? scour_par(L, P, s, rs1, re1) : -1;
             if (kept < 0) kept = scour_range(L, P, s, rs1, re1);
         }
-        const bool pack = kept < before && kept < kMaxNodesInBlock / 2 && H > 1;
-        if (pack) {  // the enclosing blocks, read before any bnd value moves (scour keeps them)
-            int ps = rs1;
-            for (int l = 2; l <= H; l++) {
-                const int a = block_start(L, ps, l), b = block_end(L, s, ps, l);
-                sc->rs[l] = a;
-                sc->re[l] = b;
-                sc->topb[l] = bnd_of(uniu(L.meta[a]));
-                ps = a;
-            }
-            wsync();
-        }
         {  // block.needsScour = false, kept on the block's first surviving leaf
             const int i = rs1 + lane_id();
             const uint64_t m = __ballot(i < re1 && !(L.meta[min(i, re1 - 1)] & M_DEL));
@@ -1173,11 +1164,19 @@ struct Eng {
         }
         if (kept >= before) return -1;
         int from = rs1;
-        if (pack) {
+        if (kept < kMaxNodesInBlock / 2 && H > 1) {
             PROF(P_PACK);
             PROF_COUNT(P_NPACK);
+            // The level-l block around the level-(l-1) block [cs, ce): its start is found scanning
+            // back from cs and its end scanning on from ce -- leaves whose bnd the scour and the
+            // rebalancing below never change (they touch [cs, ce) only, where the first
+            // surviving leaf may now repeat its block's start marker).
+            int cs = rs1, ce = re1;
             for (int l = 2; l <= H; l++) {  // packParent chain
-                const int ps = uni(sc->rs[l]), pe = uni(sc->re[l]);
+                const int ps = block_start(L, cs, l), pe = block_end(L, s, ce - 1, l);
+                const int top = bnd_of(uniu(L.meta[ps]));
+                cs = ps;
+                ce = pe;
                 if (l == 2) {
                     from = ps;
                     // packParent scours every child of P again -- including the block just
@@ -1187,9 +1186,11 @@ struct Eng {
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
                 int T = 0;
+                uint32_t m1r = M_DEL;  // a one-round range keeps its meta words in registers
                 for (int wb = ps; wb < pe; wb += 64) {
                     const int i = wb + lane_id();
                     const uint32_t m = i < pe ? L.meta[i] : M_DEL;
+                    if (wb == ps) m1r = m;
                     T += __popcll(__ballot(!(m & M_DEL) && (l == 2 || bnd_of(m) >= l - 2)));
                 }
                 int c = 0;
@@ -1199,11 +1200,10 @@ struct Eng {
                     const int base = T / c;
                     const int rem = T % c;
                     const int big = rem * (base + 1);
-                    const int top = uni(sc->topb[l]);
                     int item0 = 0;
                     for (int wb = ps; wb < pe; wb += 64) {
                         const int i = wb + lane_id();
-                        uint32_t m = i < pe ? L.meta[i] : M_DEL;
+                        uint32_t m = pe - ps <= 64 ? m1r : (i < pe ? L.meta[i] : M_DEL);
                         const bool it = !(m & M_DEL) && (l == 2 || bnd_of(m) >= l - 2);
                         const uint64_t mask = __ballot(it);
                         if (it) {
@@ -1361,6 +1361,7 @@ struct Eng {
         int slot = -1, inherit = 0;
         uint32_t om = 0;  // meta of the leaf that starts the block when the new leaf takes its place
         bool om_known = false;
+        int wbs = -1, wbe = -1;  // the leaf block around the slot, when the window saw both ends
         {
             PROF(P_INS1);
             if (S == 0) {
@@ -1390,6 +1391,8 @@ struct Eng {
                             __ballot(ln >= 31 && w < be && vw >= 0 && (ew > pos || (vw == 0 && seq > sw)));
                         slot = cm ? i - 31 + first_lane(cm) : be;
                         inherit = slot == bs ? 1 : 0;
+                        wbs = bs;
+                        wbe = be + 1;  // the block after the insert
                         if (inherit) {
                             om = uint32_t(rdlane(int(mw), bs - i + 31));
                             om_known = true;
@@ -1437,10 +1440,10 @@ struct Eng {
         L.uid[slot] = uint32_t(s.uidnext++);
         wsync();
         s.nseg = S + 1;
-        overflow_fix(L, s, slot);
+        const int xbs = S == 0 ? 0 : overflow_fix(L, s, slot, wbs, wbe);
         // saveIfLocal (mergeTree.ts:1618-1637): remote segments above minSeq go to the LRU
         if (op.flags & MTR_F_APPEND) set_merge_info(L, P, s, slot, op, dd);
-        if (s.collab && !v.local && seq > s.minseq) add_lru_block(L, s, block_start(L, slot, 1), uint32_t(s.uidnext - 1), seq);
+        if (s.collab && !v.local && seq > s.minseq) add_lru_block(L, s, xbs, uint32_t(s.uidnext - 1), seq);
         return slot;
     }
 
