@@ -200,7 +200,7 @@ template <bool G>
 struct Doc {
     template <class T>
     using A = typename std::conditional<G, gptr<T>, lptr<T>>::type;
-    A<int> len, seq, rseq, E, V, hseq;
+    A<int> len, seq, rseq, E, hseq;  // E: scan array (see Eng::prefix)
     A<uint32_t> meta, text, props, rm, uid, huid;
     lptr<Sc> sc;
     lptr<mtr_synth_state> gst;
@@ -265,9 +265,9 @@ __device__ bool props_match(PA gprop, PB val_eq, uint32_t a, uint32_t b) {
 }
 
 constexpr size_t kScBytes = ((sizeof(Sc) + 15) & ~size_t(15)) + ((sizeof(mtr_synth_state) + 15) & ~size_t(15));
-// LDS bytes of a launch with leaf capacity cap and heap capacity lhcap (10 leaf arrays + heap)
+// LDS bytes of a launch with leaf capacity cap and heap capacity lhcap (9 leaf arrays + heap)
 __host__ __device__ inline size_t lds_bytes(int cap, int lhcap) {
-    return size_t(cap) * 4 * 10 + size_t(lhcap) * 4 * 2 + kScBytes;
+    return size_t(cap) * 4 * 9 + size_t(lhcap) * 4 * 2 + kScBytes;
 }
 __host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
 
@@ -357,7 +357,11 @@ struct Eng {
         return sum;
     }
 
-    // V[i] = visible length, E[i] = inclusive prefix of max(V,0); rounds of 64 leaves
+    // The scan array: E[i] = inclusive prefix of the leaves' visible lengths in the op's view, with
+    // bit 31 set when leaf i's length is undefined (nodeLength === undefined).  A leaf's visible
+    // length is E[i] - E[i-1] (masked), -1 if flagged.  Rounds of 64 leaves.
+    static constexpr int EMASK = 0x7fffffff;
+    static MTR_DI int ev(int e, int eprev) { return e < 0 ? -1 : e - (eprev & EMASK); }
     static MTR_DI void prefix(D& L, const St& s, const View& v, int newlen) {
         PROF(P_PREFIX);
         const int S = s.nseg;
@@ -368,10 +372,7 @@ struct Eng {
             int x = 0;
             if (i < S) x = vis_len(L, i, v, newlen, s.minseq);
             const int inc = wave_incl_scan(max(x, 0));
-            if (i < S) {
-                L.V[i] = x;
-                L.E[i] = carry + inc;
-            }
+            if (i < S) L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
             carry += rdlane(inc, 63);
         }
         wsync();
@@ -386,16 +387,16 @@ struct Eng {
             const int lo = max(at, hi - 64);
             const int i = lo + lane_id();
             const bool act = i < hi;
-            int a0 = 0, a1 = 0, a2 = 0, a8 = 0, a9 = 0;
+            int a0 = 0, a1 = 0, a2 = 0, a8 = 0;
             uint32_t a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
             if (act) {
                 a0 = L.len[i]; a1 = L.seq[i]; a2 = L.rseq[i]; a3 = L.meta[i]; a4 = L.text[i];
-                a5 = L.props[i]; a6 = L.rm[i]; a7 = L.uid[i]; a8 = L.E[i]; a9 = L.V[i];
+                a5 = L.props[i]; a6 = L.rm[i]; a7 = L.uid[i]; a8 = L.E[i];
             }
             wsync();
             if (act) {
                 L.len[i + 1] = a0; L.seq[i + 1] = a1; L.rseq[i + 1] = a2; L.meta[i + 1] = a3; L.text[i + 1] = a4;
-                L.props[i + 1] = a5; L.rm[i + 1] = a6; L.uid[i + 1] = a7; L.E[i + 1] = a8; L.V[i + 1] = a9;
+                L.props[i + 1] = a5; L.rm[i + 1] = a6; L.uid[i + 1] = a7; L.E[i + 1] = a8;
             }
             wsync();
         }
@@ -470,14 +471,14 @@ struct Eng {
             // the hi - lo + 1 candidates in 64 strides: lane 63's probe reaches hi, which qualifies
             const int stride = (hi - lo + 64) >> 6;
             const int idx = lo + (ln + 1) * stride - 1;
-            const uint64_t m = __ballot(idx >= hi || L.E[min(idx, hi - 1)] >= pos);
+            const uint64_t m = __ballot(idx >= hi || (L.E[min(idx, hi - 1)] & EMASK) >= pos);
             const int k = first_lane(m);  // lane 63 always qualifies
             const int nlo = lo + k * stride;
             hi = min(hi, lo + (k + 1) * stride - 1);
             lo = nlo;
         }
         const int i = lo + ln;
-        const uint64_t m = __ballot(i < hi && L.E[min(i, max(hi - 1, 0))] >= pos);
+        const uint64_t m = __ballot(i < hi && (L.E[min(i, max(hi - 1, 0))] & EMASK) >= pos);
         return m ? lo + first_lane(m) : hi;
     }
     // number of leaves in [bs, be) with bnd >= minb
@@ -1274,8 +1275,10 @@ struct Eng {
         int vj = 0, ej = 0, lj = 0, sqj = 0, rsj = 0;
         uint32_t mj = 0, tj = 0, pj = 0, rmj = 0;
         if (in) {
-            vj = L.V[jj]; ej = L.E[jj]; mj = L.meta[jj]; lj = L.len[jj]; sqj = L.seq[jj];
+            ej = L.E[jj]; mj = L.meta[jj]; lj = L.len[jj]; sqj = L.seq[jj];
             rsj = L.rseq[jj]; tj = L.text[jj]; pj = L.props[jj]; rmj = L.rm[jj];
+            vj = ev(ej, jj > 0 ? L.E[jj - 1] : 0);
+            ej &= EMASK;
         }
         const uint64_t em = __ballot(!in || (ln > 0 && bnd_of(mj) >= 1));
         const int be = em ? i + first_lane(em) : block_end(L, s, i + 63, 1);
@@ -1304,9 +1307,7 @@ struct Eng {
             L.rm[r] = rdlane(rmj, jl);
             L.uid[r] = uint32_t(s.uidnext++);
             // split leaves are fully visible in this view
-            L.V[j] = off;
             L.E[j] = e - v + off;
-            L.V[r] = v - off;
             L.E[r] = e;
             wsync();
             s.nseg++;
@@ -1379,7 +1380,9 @@ struct Eng {
                     int vw = 0, ew = 0, sw = 0;
                     uint32_t mw = 0;
                     if (inw) {
-                        vw = L.V[w]; ew = L.E[w]; sw = L.seq[w]; mw = L.meta[w];
+                        ew = L.E[w]; sw = L.seq[w]; mw = L.meta[w];
+                        vw = ev(ew, w > 0 ? L.E[w - 1] : 0);
+                        ew &= EMASK;
                     }
                     const bool bw = inw && bnd_of(mw) >= 1;
                     const uint64_t sm = __ballot(ln <= 31 && (w <= 0 || bw));
@@ -1402,8 +1405,9 @@ struct Eng {
                         const int j = i + ln;
                         bool c = false;
                         if (j < be) {
-                            const int vj = L.V[j];
-                            c = vj >= 0 && (L.E[j] > pos || (vj == 0 && seq > L.seq[j]));
+                            const int ej = L.E[j];
+                            const int vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
+                            c = vj >= 0 && ((ej & EMASK) > pos || (vj == 0 && seq > L.seq[j]));
                         }
                         const uint64_t cm = __ballot(c);
                         slot = cm ? i + first_lane(cm) : be;
@@ -1554,8 +1558,9 @@ struct Eng {
             int vj = 0, ej = 0, rj = RNONE;
             uint32_t mj = 0;
             if (in) {
-                vj = L.V[j];
                 ej = L.E[j];
+                vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
+                ej &= EMASK;
                 mj = L.meta[j];
                 if (is_remove) rj = L.rseq[j];
             }
@@ -1648,7 +1653,7 @@ struct Eng {
         v.local = 0;
         prefix(L, s, v, P.new_length_calc);
         const int S = s.nseg;
-        const int len = S > 0 ? uni(L.E[S - 1]) : 0;
+        const int len = S > 0 ? (uni(L.E[S - 1]) & EMASK) : 0;
         if (threadIdx.x == 0) {
             mtr_op op = ld_struct<mtr_op>(rec);
             mtr_synth_state st = ld_struct<mtr_synth_state>(L.gst);
@@ -1768,7 +1773,6 @@ struct Eng {
             L.uid = (A<uint32_t>)(g + F_UID * P.segcap);
             const gptr<uint32_t> sx = gp(P.scratch) + size_t(d) * 2 * P.segcap;
             L.E = (A<int>)(sx);
-            L.V = (A<int>)(sx + P.segcap);
             const gptr<uint32_t> gh = gp(P.heap) + size_t(d) * 2 * P.hcap;
             L.hseq = (A<int>)(gh);
             L.huid = (A<uint32_t>)(gh + P.hcap);
@@ -1793,7 +1797,6 @@ struct Eng {
             L.rm = (A<uint32_t>)(take(4 * size_t(cap)));
             L.uid = (A<uint32_t>)(take(4 * size_t(cap)));
             L.E = (A<int>)(take(4 * size_t(cap)));
-            L.V = (A<int>)(take(4 * size_t(cap)));
             L.hseq = (A<int>)(take(4 * size_t(lhcap)));
             L.huid = (A<uint32_t>)(take(4 * size_t(lhcap)));
             L.sc = (lptr<Sc>)(take(sizeof(Sc)));
@@ -1985,7 +1988,7 @@ struct Eng {
         const int i = lower_bound_E(L, s, pos + 1);  // the leaf whose view range [E - V, E) holds pos
         if (i >= S) return -1;
         if (uni(L.rseq[i]) != RNONE) return -1;
-        const int off = pos - (uni(L.E[i]) - uni(L.V[i]));
+        const int off = pos - (i > 0 ? (uni(L.E[i - 1]) & EMASK) : 0);
         int before = 0;  // local-view length of the leaves before i (removed leaves count 0)
         for (int base = 0; base < i; base += 64) {
             const int j = base + lane_id();

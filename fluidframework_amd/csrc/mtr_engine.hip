@@ -835,7 +835,11 @@ int64_t mtr_debug_scan(mtr_engine* e, uint32_t doc, int32_t* out, int64_t n) {
     const size_t sc = e->caps.max_segments;
     if (!e->scratch.p || doc >= e->n_docs || n > int64_t(sc)) return -1;
     HIPCHK(hipMemcpy(out, e->scratch.p + size_t(doc) * 2 * sc, size_t(n) * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(out + n, e->scratch.p + size_t(doc) * 2 * sc + sc, size_t(n) * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++) {  // the scan array keeps the undefined flag in bit 31
+        const int32_t ei = out[i], ep = i ? (out[i - 1] & 0x7fffffff) : 0;
+        out[n + i] = ei < 0 ? -1 : ei - ep;
+    }
+    for (int64_t i = 0; i < n; i++) out[i] &= 0x7fffffff;
     return n;
 }
 
