@@ -121,6 +121,8 @@ struct DocHdr {
     int32_t collab, local, heapn, uidnext;
     int32_t textused, propused, rmused, status;
     int32_t op_cursor, fail_op, max_heap, texthalf;  // texthalf: active half of the text arena
+    int32_t heap_need;  // LRU heap capacity the next launch must give this document (0 = none)
+    int32_t pad[3];
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -187,6 +189,7 @@ struct St {
     int textused, propused, rmused, status;  // textused: handle-table length for permutation vectors
     int fail_op, max_heap, ops_done, texthalf;
     int htop;  // seq of the LRU heap's top entry (valid while heapn > 0)
+    int heap_need;
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
 
@@ -264,10 +267,12 @@ __device__ bool props_match(PA gprop, PB val_eq, uint32_t a, uint32_t b) {
     return true;
 }
 
-constexpr size_t kScBytes = ((sizeof(Sc) + 15) & ~size_t(15)) + ((sizeof(mtr_synth_state) + 15) & ~size_t(15));
+// LDS scratch: Sc, plus the generator state in record-mode launches only
+constexpr size_t kScOnly = (sizeof(Sc) + 15) & ~size_t(15);
+constexpr size_t kScBytes = kScOnly + ((sizeof(mtr_synth_state) + 15) & ~size_t(15));
 // LDS bytes of a launch with leaf capacity cap and heap capacity lhcap (9 leaf arrays + heap)
-__host__ __device__ inline size_t lds_bytes(int cap, int lhcap) {
-    return size_t(cap) * 4 * 9 + size_t(lhcap) * 4 * 2 + kScBytes;
+__host__ __device__ inline size_t lds_bytes(int cap, int lhcap, bool gen = true) {
+    return size_t(cap) * 4 * 9 + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
 }
 __host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
 
@@ -1674,6 +1679,7 @@ struct Eng {
             s.textused = h.textused; s.propused = h.propused; s.rmused = h.rmused;
             s.status = h.status; s.fail_op = h.fail_op; s.max_heap = h.max_heap;
             s.texthalf = h.texthalf;
+            s.heap_need = 0;
             s.ops_done = 0;
             s.sum_s = 0;
             s.sum_l = 0;
@@ -1746,6 +1752,7 @@ struct Eng {
             h.fail_op = s.fail_op;
             h.max_heap = s.max_heap;
             h.texthalf = s.texthalf;
+            h.heap_need = s.heap_need;
             st_struct(hp, h);
             if (P.gen) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
 #ifdef MTR_PROF
@@ -1800,7 +1807,7 @@ struct Eng {
             L.hseq = (A<int>)(take(4 * size_t(lhcap)));
             L.huid = (A<uint32_t>)(take(4 * size_t(lhcap)));
             L.sc = (lptr<Sc>)(take(sizeof(Sc)));
-            L.gst = (lptr<mtr_synth_state>)(take(sizeof(mtr_synth_state)));
+            L.gst = (lptr<mtr_synth_state>)(P.gen ? take(sizeof(mtr_synth_state)) : p);
             L.cap = cap;
             L.lhcap = lhcap;
         }
@@ -1815,6 +1822,17 @@ struct Eng {
     // (s.status != MTR_OK; s.fail_op = gidx).
     static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
                                 uint32_t pf, int gidx) {
+        if (!G && s.collab && L.lhcap < P.hcap) {
+            // LRU pushes this op can make (one per touched leaf block): if the launch's LDS heap
+            // could overflow, stop before the op and ask the next launch for a larger heap
+            int need = 0;
+            if (op.type == MTR_OP_INSERT) need = 1;
+            else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) need = min(max(op.pos2 - op.pos1, 0), s.nseg + 2);
+            if (need && s.heapn + need + 1 >= L.lhcap) {
+                s.heap_need = s.heapn + need + 2;
+                return false;
+            }
+        }
         s.sum_s += (unsigned long long)s.nseg;
         if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER) && !PM)
             s.sum_l += (unsigned long long)op.payload2;

@@ -174,11 +174,11 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
         const DocHdr x = h[d];
         const int rem = x.status == MTR_OK ? int(docs[d].op_count) - x.op_cursor : 0;
         if (rem > 0) {
-            int nseg = x.nseg, heapn = x.heapn, base = 0;
+            int nseg = x.nseg, heapn = max(x.heapn, x.heap_need), base = 0;
             if (dkind[d] == 1) {
                 const DocHdr y = h[dpart[d]];
                 nseg = max(nseg, y.nseg);
-                heapn = max(heapn, y.heapn);
+                heapn = max(heapn, max(y.heapn, y.heap_need));
                 base = kClasses;
             }
             c = base + min(kClasses - 1, nseg / kClassLeaves);
@@ -465,8 +465,10 @@ static int run_impl(mtr_engine* e, int gen) {
             if (cnt <= 0) continue;
             int cap = round64(maxseg + 2 * k + 8);
             if (cap > P.segcap) cap = P.segcap;
-            int lhcap = std::min<int>(P.hcap, std::max(cap / 2, round64(maxheap + 2 * k + 8)));
-            size_t lds = lds_bytes(cap, lhcap);
+            // LRU heap: what the class holds now plus room for this launch's pushes; a document that
+            // could overflow it stops before the op and asks for more (DocHdr.heap_need)
+            int lhcap = std::min<int>(P.hcap, std::max(cap / 4, round64(maxheap + 2 * k + 8)));
+            size_t lds = lds_bytes(cap, lhcap, P.gen != 0);
             if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             P.global_mode = 0;
             if (lds > lds_limit) {
