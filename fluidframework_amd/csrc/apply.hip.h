@@ -1822,7 +1822,7 @@ struct Eng {
     // (s.status != MTR_OK; s.fail_op = gidx).
     static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
                                 uint32_t pf, int gidx) {
-        if (!G && s.collab && L.lhcap < P.hcap) {
+        if (!G && !P.gen && s.collab && L.lhcap < P.hcap) {  // (record mode never yields: ops are drawn once)
             // LRU pushes this op can make (one per touched leaf block): if the launch's LDS heap
             // could overflow, stop before the op and ask the next launch for a larger heap
             int need = 0;

@@ -226,3 +226,25 @@ def test_c5_shaped_hbm_resident():
         assert orc.apply(b, d) == 0
         _compare_export(eng, d, orc)
         assert eng.summary(d) == orc.summarize(b, d)
+
+
+def test_long_ranges_grow_the_lds_heap():
+    """Removes/annotates over up to 120 units touch many leaf blocks, each an LRU push: documents
+    whose LDS heap could overflow yield before the op and are relaunched with a larger heap
+    (DocHdr.heap_need).  Summaries equal the oracle's."""
+    from fluidframework_amd.synth import make_cfg, tables
+    from oracle.oracle import generate, replay_batch
+
+    n, ops = 256, 1200
+    tabs = tables(writers=8)
+    cfg = make_cfg(n, ops, writers=8, max_lag=32, max_range=120, weights=(60, 30, 10), seed=0xa11)
+    b, ohash, ost = generate(cfg, tabs, 0, n, threads=16)
+    assert (ost == 0).all()
+    eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 8192,
+                  prop_words=1 << 16, remover_cells=1 << 14, ops_per_launch=16)
+    eng.apply(b)
+    eng.summarize()
+    for d in range(n):
+        st, op = eng.status(d)
+        assert st == 0, f"doc {d}: status {st:#x} at op {op}"
+    assert np.array_equal(eng.hashes(n), ohash)
