@@ -322,32 +322,41 @@ struct Eng {
         return false;
     }
 
-    // nodeLength for a leaf (mergeTree.ts:916-1004): -1 = undefined
-    static MTR_DI int vis_len(const D& L, int i, const View& v, int newlen, int minseq) {
+    // nodeLength for a leaf (mergeTree.ts:916-1004): -1 = undefined.  Every lane evaluates the
+    // same select chain (no divergent branches); only lanes whose answer depends on a later
+    // remover in the overlap list walk it, behind one ballot.
+    static MTR_DI int vis_len(const D& L, int i, const View& v, int newlen, int minseq, bool valid = true) {
         const int len = L.len[i];
         const int rseq = L.rseq[i];
         const uint32_t m = L.meta[i];
         const int seq = L.seq[i];
         const bool removed = rseq != RNONE;
         if (v.local) {  // localNetLength, mergeTree.ts:613-634
-            if (removed) return newlen ? 0 : (rseq > minseq ? 0 : -1);
-            return len;
+            return removed ? (newlen ? 0 : (rseq > minseq ? 0 : -1)) : len;
         }
-        const uint32_t cl = m & M_CLIENT_MASK;
-        if (newlen) {  // mergeTree.ts:935-965
-            if (removed) {
-                if (rseq <= minseq) return -1;
-                if (rseq <= v.ref || in_removers(L, i, m, v.client)) return 0;
+        const bool vis = (m & M_CLIENT_MASK) == v.client || seq <= v.ref;
+        bool inr = removed && ((m >> M_FREM_SHIFT) & 0xffu) == v.client;
+        // lanes whose result still depends on removedClientIds[1..] (mergeTree.ts:935-1003)
+        const bool walk =
+            valid && removed && !inr && (m & M_OVERLAP) && rseq > v.ref && (newlen ? rseq > minseq : vis);
+        if (__ballot(walk)) {
+            if (walk) {
+                uint32_t cell = L.rm[i];
+                while (cell != 0xffffffu) {
+                    const uint32_t w = L.grm[cell];
+                    if ((w >> 24) == v.client) {
+                        inr = true;
+                        break;
+                    }
+                    cell = w & 0xffffffu;
+                }
             }
-            return (seq <= v.ref || cl == v.client) ? len : 0;
         }
-        if (removed && rseq <= v.ref) return -1;  // mergeTree.ts:967-976
-        if (cl == v.client || seq <= v.ref) {
-            if (removed) return in_removers(L, i, m, v.client) ? 0 : len;
-            return len;
-        }
-        if (removed) return -1;
-        return 0;
+        if (newlen)  // mergeTree.ts:935-965
+            return removed ? (rseq <= minseq ? -1 : ((rseq <= v.ref || inr) ? 0 : (vis ? len : 0))) : (vis ? len : 0);
+        // mergeTree.ts:967-1003
+        if (removed && rseq <= v.ref) return -1;
+        return vis ? ((removed && inr) ? 0 : len) : (removed ? -1 : 0);
     }
 
     // root.cachedLength: the local view's length (removed leaves count 0), mergeTree.ts:613-634
@@ -373,11 +382,13 @@ struct Eng {
         const int ln = lane_id();
         int carry = 0;
         for (int base = 0; base < S; base += 64) {
+            // leaf slots up to the next multiple of 64 exist (capacities are multiples of 64):
+            // every lane evaluates, lanes past the last leaf contribute 0 and store harmlessly
             const int i = base + ln;
-            int x = 0;
-            if (i < S) x = vis_len(L, i, v, newlen, s.minseq);
+            const int x0 = vis_len(L, i, v, newlen, s.minseq, i < S);
+            const int x = i < S ? x0 : 0;
             const int inc = wave_incl_scan(max(x, 0));
-            if (i < S) L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
+            L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
             carry += rdlane(inc, 63);
         }
         wsync();
