@@ -248,3 +248,39 @@ def test_long_ranges_grow_the_lds_heap():
         st, op = eng.status(d)
         assert st == 0, f"doc {d}: status {st:#x} at op {op}"
     assert np.array_equal(eng.hashes(n), ohash)
+
+
+@pytest.mark.parametrize("newlen,v1,chunk", [(True, True, 10000), (False, True, 64), (False, False, 10000),
+                                             (True, False, 256)],
+                         ids=["newlen", "v1-chunk64", "legacy", "newlen-legacy-chunk256"])
+def test_options_synthetic(newlen, v1, chunk):
+    """IMergeTreeOptions the engine honours (mergeTree.ts:400-438): mergeTreeUseNewLengthCalculations
+    (the other nodeLength branch, mergeTree.ts:935-965), SnapshotLegacy vs SnapshotV1 mid-collaboration,
+    and small mergeTreeSnapshotChunkSize (many body chunks).  The oracle generates the logs under the
+    same options; summaries must agree byte for byte."""
+    from fluidframework_amd.synth import make_cfg, tables
+    from oracle.oracle import generate
+
+    n, ops = 192, 1000
+    opts = options(new_length_calc=newlen, snapshot_v1=v1, chunk_size=chunk)
+    tabs = tables(writers=8)
+    cfg = make_cfg(n, ops, writers=8, max_lag=32, seed=0xc0ffee + chunk)
+    b, ohash, ost = generate(cfg, tabs, 0, n, threads=16, opts=opts)
+    assert (ost == 0).all()
+    eng = _engine(n, new_length_calc=newlen, snapshot_v1=v1, chunk_size=chunk, max_segments=2 * ops + 128,
+                  heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 8192, prop_words=1 << 16,
+                  remover_cells=4096, ops_per_launch=32)
+    eng.apply(b)
+    eng.summarize()
+    for d in range(n):
+        st, op = eng.status(d)
+        assert st == 0, f"doc {d}: status {st:#x} at op {op}"
+    ghash = eng.hashes(n)
+    bad = np.nonzero(ghash != ohash)[0]
+    if bad.size:
+        d = int(bad[0])
+        orc = OracleDoc(opts)
+        assert orc.apply(b, d) == 0
+        _compare_export(eng, d, orc)
+        assert eng.summary(d) == orc.summarize(b, d)
+    assert bad.size == 0
