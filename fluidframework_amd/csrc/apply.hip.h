@@ -126,8 +126,14 @@ struct DocHdr {
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
-constexpr int NF = 8;
-enum { F_LEN = 0, F_SEQ, F_RSEQ, F_META, F_TEXT, F_PROPS, F_RM, F_UID };
+constexpr int NF = 7;
+enum { F_LEN = 0, F_SEQ, F_RSEQ, F_META, F_TEXT, F_PROPS, F_UID };
+
+// Remover lists (removedClientIds[1..]) are cons cells in the document's remover arena; the head
+// of a leaf's list is found by its uid in an open-addressing table after the cells (key = uid + 1,
+// 0 = empty; cleared by mtr_reset), so leaves carry no per-slot list field: only leaves with
+// M_OVERLAP have an entry.  rm slab per document: [rcap cells][2 * rtab words].
+__host__ __device__ inline uint32_t rtab_hash(uint32_t uid) { return uid * 2654435761u; }
 
 struct KParams {
     DocHdr* hdr;
@@ -135,8 +141,9 @@ struct KParams {
     uint32_t* heap;  // [doc][2][hcap]   (seq, uid), 1-based
     uint16_t* text;  // [doc][tcap]
     uint32_t* prop;  // [doc][pcap]
-    uint32_t* rm;    // [doc][rcap]
+    uint32_t* rm;    // [doc][rcap + 2 * rtab]: remover cells, then the uid -> list head table
     int32_t segcap, hcap, tcap, pcap, rcap;
+    int32_t rtab;         // remover-head table entries (power of two)
     int32_t cap;          // leaf capacity of this launch (LDS mode)
     int32_t lhcap;        // heap capacity of this launch (LDS mode)
     int32_t global_mode;  // 1: leaves/heap stay in HBM (documents larger than LDS)
@@ -204,12 +211,12 @@ struct Doc {
     template <class T>
     using A = typename std::conditional<G, gptr<T>, lptr<T>>::type;
     A<int> len, seq, rseq, E, hseq;  // E: scan array (see Eng::prefix)
-    A<uint32_t> meta, text, props, rm, uid, huid;
+    A<uint32_t> meta, text, props, uid, huid;
     lptr<Sc> sc;
     lptr<mtr_synth_state> gst;
     gptr<uint16_t> gtext;
-    gptr<uint32_t> gprop, grm;
-    int cap, lhcap;
+    gptr<uint32_t> gprop, grm, grt;  // grt: remover-head table (2 words per entry)
+    int cap, lhcap, rtmask;
 };
 
 MTR_DI int bnd_of(uint32_t m) { return int((m & M_BND_MASK) >> M_BND_SHIFT); }
@@ -270,9 +277,9 @@ __device__ bool props_match(PA gprop, PB val_eq, uint32_t a, uint32_t b) {
 // LDS scratch: Sc, plus the generator state in record-mode launches only
 constexpr size_t kScOnly = (sizeof(Sc) + 15) & ~size_t(15);
 constexpr size_t kScBytes = kScOnly + ((sizeof(mtr_synth_state) + 15) & ~size_t(15));
-// LDS bytes of a launch with leaf capacity cap and heap capacity lhcap (9 leaf arrays + heap)
+// LDS bytes of a launch with leaf capacity cap and heap capacity lhcap (8 leaf arrays + heap)
 __host__ __device__ inline size_t lds_bytes(int cap, int lhcap, bool gen = true) {
-    return size_t(cap) * 4 * 9 + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
+    return size_t(cap) * 4 * 8 + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
 }
 __host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
 
@@ -310,10 +317,36 @@ struct Eng {
     using A = typename D::template A<T>;
 
     // ------------------------------------------------------------ visibility
+    // ---- remover-list heads by uid (per-lane probes; only M_OVERLAP leaves have entries)
+    static MTR_DI uint32_t rm_get(const D& L, uint32_t uid) {
+        uint32_t h = rtab_hash(uid) & uint32_t(L.rtmask);
+        for (int n = 0; n <= L.rtmask; n++) {
+            const uint32_t k = L.grt[2 * h];
+            if (k == uid + 1) return L.grt[2 * h + 1];
+            if (k == 0) break;
+            h = (h + 1) & uint32_t(L.rtmask);
+        }
+        return 0xffffffu;
+    }
+    // set uid's head (lanes may insert concurrently: empty keys are claimed with a CAS); false = full
+    static MTR_DI bool rm_set(const D& L, uint32_t uid, uint32_t head) {
+        uint32_t h = rtab_hash(uid) & uint32_t(L.rtmask);
+        for (int n = 0; n <= L.rtmask; n++) {
+            uint32_t k = L.grt[2 * h];
+            if (k == 0) k = atomicCAS((uint32_t*)&L.grt[2 * h], 0u, uid + 1);
+            if (k == 0 || k == uid + 1) {
+                L.grt[2 * h + 1] = head;
+                return true;
+            }
+            h = (h + 1) & uint32_t(L.rtmask);
+        }
+        return false;
+    }
+
     static MTR_DI bool in_removers(const D& L, int i, uint32_t m, uint32_t c) {
         if (((m >> M_FREM_SHIFT) & 0xffu) == c) return true;
         if (!(m & M_OVERLAP)) return false;
-        uint32_t cell = L.rm[i];
+        uint32_t cell = rm_get(L, L.uid[i]);
         while (cell != 0xffffffu) {
             const uint32_t v = L.grm[cell];
             if ((v >> 24) == c) return true;
@@ -341,7 +374,7 @@ struct Eng {
             valid && removed && !inr && (m & M_OVERLAP) && rseq > v.ref && (newlen ? rseq > minseq : vis);
         if (__ballot(walk)) {
             if (walk) {
-                uint32_t cell = L.rm[i];
+                uint32_t cell = rm_get(L, L.uid[i]);
                 while (cell != 0xffffffu) {
                     const uint32_t w = L.grm[cell];
                     if ((w >> 24) == v.client) {
@@ -404,15 +437,15 @@ struct Eng {
             const int i = lo + lane_id();
             const bool act = i < hi;
             int a0 = 0, a1 = 0, a2 = 0, a8 = 0;
-            uint32_t a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+            uint32_t a3 = 0, a4 = 0, a5 = 0, a7 = 0;
             if (act) {
                 a0 = L.len[i]; a1 = L.seq[i]; a2 = L.rseq[i]; a3 = L.meta[i]; a4 = L.text[i];
-                a5 = L.props[i]; a6 = L.rm[i]; a7 = L.uid[i]; a8 = L.E[i];
+                a5 = L.props[i]; a7 = L.uid[i]; a8 = L.E[i];
             }
             wsync();
             if (act) {
                 L.len[i + 1] = a0; L.seq[i + 1] = a1; L.rseq[i + 1] = a2; L.meta[i + 1] = a3; L.text[i + 1] = a4;
-                L.props[i + 1] = a5; L.rm[i + 1] = a6; L.uid[i + 1] = a7; L.E[i + 1] = a8;
+                L.props[i + 1] = a5; L.uid[i + 1] = a7; L.E[i + 1] = a8;
             }
             wsync();
         }
@@ -429,10 +462,10 @@ struct Eng {
             const int i = lo + lane_id();
             const bool act = i < S;
             int a0 = 0, a1 = 0, a2 = 0;
-            uint32_t a3 = M_DEL, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+            uint32_t a3 = M_DEL, a4 = 0, a5 = 0, a7 = 0;
             if (act) {
                 a0 = L.len[i]; a1 = L.seq[i]; a2 = L.rseq[i]; a3 = L.meta[i];
-                a4 = L.text[i]; a5 = L.props[i]; a6 = L.rm[i]; a7 = L.uid[i];
+                a4 = L.text[i]; a5 = L.props[i]; a7 = L.uid[i];
             }
             const bool keep = act && !(a3 & M_DEL);
             const uint64_t km = __ballot(keep);
@@ -440,7 +473,7 @@ struct Eng {
             if (keep) {
                 const int d = base + __popcll(km & lanes_below());
                 L.len[d] = a0; L.seq[d] = a1; L.rseq[d] = a2; L.meta[d] = a3;
-                L.text[d] = a4; L.props[d] = a5; L.rm[d] = a6; L.uid[d] = a7;
+                L.text[d] = a4; L.props[d] = a5; L.uid[d] = a7;
             }
             base += __popcll(km);
             wsync();
@@ -1289,10 +1322,10 @@ struct Eng {
         const int jj = i + ln;
         const bool in = jj < S;
         int vj = 0, ej = 0, lj = 0, sqj = 0, rsj = 0;
-        uint32_t mj = 0, tj = 0, pj = 0, rmj = 0;
+        uint32_t mj = 0, tj = 0, pj = 0, uj = 0;
         if (in) {
             ej = L.E[jj]; mj = L.meta[jj]; lj = L.len[jj]; sqj = L.seq[jj];
-            rsj = L.rseq[jj]; tj = L.text[jj]; pj = L.props[jj]; rmj = L.rm[jj];
+            rsj = L.rseq[jj]; tj = L.text[jj]; pj = L.props[jj]; uj = L.uid[jj];
             vj = ev(ej, jj > 0 ? L.E[jj - 1] : 0);
             ej &= EMASK;
         }
@@ -1320,8 +1353,12 @@ struct Eng {
                 L.text[r] = t0 == uint32_t(MTR_HANDLE_UNALLOCATED) ? t0 : t0 + uint32_t(off);
             }
             L.props[r] = rdlane(pj, jl);
-            L.rm[r] = rdlane(rmj, jl);
-            L.uid[r] = uint32_t(s.uidnext++);
+            const uint32_t ur = uint32_t(s.uidnext++);
+            L.uid[r] = ur;
+            if (m0 & M_OVERLAP) {  // the right half shares the remover list
+                if (lane_id() == 0 && !rm_set(L, ur, rm_get(L, rdlane(uj, jl)))) s.status = MTR_ERR_CAPACITY;
+                s.status = uni(s.status);
+            }
             // split leaves are fully visible in this view
             L.E[j] = e - v + off;
             L.E[r] = e;
@@ -1456,7 +1493,6 @@ struct Eng {
         uint32_t pr = NONE32;
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[slot] = pr;
-        L.rm[slot] = NONE32;
         L.uid[slot] = uint32_t(s.uidnext++);
         wsync();
         s.nseg = S + 1;
@@ -1489,7 +1525,8 @@ struct Eng {
                     head = cell;
                 }
                 m |= M_OVERLAP;
-                L.rm[i] = head;
+                if (lane_id() == 0 && !rm_set(L, uniu(L.uid[i]), head)) s.status = MTR_ERR_CAPACITY;
+                s.status = uni(s.status);
             }
             L.meta[i] = m;
         }
@@ -1531,7 +1568,6 @@ struct Eng {
         uint32_t pr = NONE32;
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[i] = pr;
-        L.rm[i] = NONE32;
         L.uid[i] = uint32_t(s.uidnext++);
         wsync();
         s.nseg = i + 1;
@@ -1594,19 +1630,21 @@ struct Eng {
                         s.status = MTR_ERR_CAPACITY;
                         return;
                     }
+                    bool full = false;
                     if (ov) {
                         const uint32_t cell = uint32_t(s.rmused + __popcll(om & lanes_below()));
-                        const uint32_t nxt = (mj & M_OVERLAP) ? L.rm[j] : 0xffffffu;
+                        const uint32_t uj = L.uid[j];
+                        const uint32_t nxt = (mj & M_OVERLAP) ? rm_get(L, uj) : 0xffffffu;
                         L.grm[cell] = (client << 24) | (nxt & 0xffffffu);
-                        L.rm[j] = cell;
+                        full = !rm_set(L, uj, cell);
                         mj |= M_OVERLAP;
                         L.meta[j] = mj;
                     } else if (act) {
                         L.rseq[j] = seq;
                         mj = (mj & ~(0xffu << M_FREM_SHIFT) & ~M_OVERLAP) | (client << M_FREM_SHIFT);
                         L.meta[j] = mj;
-                        L.rm[j] = NONE32;
                     }
+                    if (__ballot(full)) s.status = MTR_ERR_CAPACITY;
                     s.rmused += nov;
                 } else {
                     // one new property set per distinct old set in the round (memoized addProperties)
@@ -1716,7 +1754,6 @@ struct Eng {
                 L.meta[i] = g[F_META * cs + i];
                 L.text[i] = g[F_TEXT * cs + i];
                 L.props[i] = g[F_PROPS * cs + i];
-                L.rm[i] = g[F_RM * cs + i];
                 L.uid[i] = g[F_UID * cs + i];
             }
             const int hn = s.heapn;
@@ -1743,7 +1780,6 @@ struct Eng {
                 g[F_META * cs + i] = L.meta[i];
                 g[F_TEXT * cs + i] = L.text[i];
                 g[F_PROPS * cs + i] = L.props[i];
-                g[F_RM * cs + i] = L.rm[i];
                 g[F_UID * cs + i] = L.uid[i];
             }
             const int hn = s.heapn;
@@ -1787,7 +1823,6 @@ struct Eng {
             L.meta = (A<uint32_t>)(g + F_META * P.segcap);
             L.text = (A<uint32_t>)(g + F_TEXT * P.segcap);
             L.props = (A<uint32_t>)(g + F_PROPS * P.segcap);
-            L.rm = (A<uint32_t>)(g + F_RM * P.segcap);
             L.uid = (A<uint32_t>)(g + F_UID * P.segcap);
             const gptr<uint32_t> sx = gp(P.scratch) + size_t(d) * 2 * P.segcap;
             L.E = (A<int>)(sx);
@@ -1812,7 +1847,6 @@ struct Eng {
             L.meta = (A<uint32_t>)(take(4 * size_t(cap)));
             L.text = (A<uint32_t>)(take(4 * size_t(cap)));
             L.props = (A<uint32_t>)(take(4 * size_t(cap)));
-            L.rm = (A<uint32_t>)(take(4 * size_t(cap)));
             L.uid = (A<uint32_t>)(take(4 * size_t(cap)));
             L.E = (A<int>)(take(4 * size_t(cap)));
             L.hseq = (A<int>)(take(4 * size_t(lhcap)));
@@ -1824,7 +1858,9 @@ struct Eng {
         }
         L.gtext = gp(P.text) + size_t(d) * P.tcap;
         L.gprop = gp(P.prop) + size_t(d) * P.pcap;
-        L.grm = gp(P.rm) + size_t(d) * P.rcap;
+        L.grm = gp(P.rm) + size_t(d) * (size_t(P.rcap) + 2 * size_t(P.rtab));
+        L.grt = L.grm + P.rcap;
+        L.rtmask = P.rtab - 1;
     }
 
     // ------------------------------------------------------------ one op

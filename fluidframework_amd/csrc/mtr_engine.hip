@@ -3,11 +3,12 @@
 //
 // Memory layout in HBM (one slab per document, sized by mtr_caps):
 //   DocHdr                      64 B                  (collaboration window + arena cursors)
-//   leaves  [NF][segcap] u32    len seq rseq meta text props rm uid   (SoA, tree order)
+//   leaves  [NF][segcap] u32    len seq rseq meta text props uid   (SoA, tree order)
 //   heap    [2][hcap]    u32    zamboni LRU heap (seq, uid), 1-based
 //   text    [tcap]       u16    UTF-16 text arena (segments hold offsets)
 //   props   [pcap]       u32    immutable property-set entries [n, k0, v0, ...]
-//   removers[rcap]       u32    cons cells of overlapping removers (client<<24 | next)
+//   removers[rcap]       u32    cons cells of overlapping removers (client<<24 | next), then the
+//           [2*rtab]     u32    uid -> list head table (open addressing, key uid+1)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -71,6 +72,7 @@ int round64(int x) { return std::max(64, (x + 63) & ~63); }
 struct mtr_engine {
     mtr_options opt{};
     mtr_caps caps{};
+    int32_t rtab = 64;  // remover-head table entries per document (power of two >= 2 * remover_cells)
     int device = 0;
     uint32_t max_docs = 0;
     hipStream_t stream = nullptr;
@@ -227,6 +229,7 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
     c.heap_entries = (c.heap_entries + 63) & ~63u;
     if (c.remover_cells > 0xfffffe) c.remover_cells = 0xfffffe;
     e->caps = c;
+    while (e->rtab < 2 * int32_t(c.remover_cells)) e->rtab *= 2;
     e->device = device;
     e->max_docs = max_docs;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -247,7 +250,7 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
         return nullptr;
     }
     if (e->hdr.ensure(D) || e->seg.ensure(D * NF * c.max_segments) || e->heap.ensure(D * 2 * c.heap_entries) ||
-        e->text.ensure(D * c.text_units) || e->prop.ensure(D * c.prop_words) || e->rm.ensure(D * c.remover_cells) ||
+        e->text.ensure(D * c.text_units) || e->prop.ensure(D * c.prop_words) || e->rm.ensure(D * (c.remover_cells + 2 * size_t(e->rtab))) ||
         e->stat.ensure(D * 4) || e->red.ensure(4)) {
         mtr_engine_destroy(e);
         return nullptr;
@@ -311,6 +314,8 @@ int mtr_reset(mtr_engine* e) {
     HIPCHK(hipSetDevice(e->device));
     const uint32_t n = std::max<uint32_t>(e->max_docs, 1);
     reset_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, n);
+    // remover-head tables start empty (their keys are uids, which restart at 0)
+    HIPCHK(hipMemsetAsync(e->rm.p, 0, e->rm.n * sizeof(uint32_t), e->stream));
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(e->stat.p, 0, e->stat.n * sizeof(unsigned long long), e->stream));
     e->summarized = false;
@@ -400,6 +405,7 @@ static int run_impl(mtr_engine* e, int gen) {
     P.tcap = int(e->caps.text_units);
     P.pcap = int(e->caps.prop_words);
     P.rcap = int(e->caps.remover_cells);
+    P.rtab = e->rtab;
     P.new_length_calc = e->opt.new_length_calc;
     P.n_docs = e->n_docs;
     P.ops = e->ops.p;
@@ -630,6 +636,7 @@ int mtr_summarize(mtr_engine* e) {
     P.tcap = int(e->caps.text_units);
     P.pcap = int(e->caps.prop_words);
     P.rcap = int(e->caps.remover_cells);
+    P.rtab = e->rtab;
     P.snapshot_v1 = e->opt.snapshot_v1;
     P.chunk_size = e->opt.chunk_size;
     P.new_length_calc = e->opt.new_length_calc;
@@ -735,7 +742,18 @@ struct HostDoc {
     DocHdr h;
     std::vector<uint32_t> seg;
     std::vector<uint16_t> text;
-    std::vector<uint32_t> prop, rm;
+    std::vector<uint32_t> prop, rm, rt;
+    // head of leaf i's later-removers list (the device's uid table)
+    uint32_t rm_head(uint32_t uid) const {
+        const uint32_t mask = uint32_t(rt.size() / 2 - 1);
+        uint32_t h = rtab_hash(uid) & mask;
+        for (size_t n = 0; n <= mask; n++) {
+            if (rt[2 * h] == uid + 1) return rt[2 * h + 1];
+            if (rt[2 * h] == 0) break;
+            h = (h + 1) & mask;
+        }
+        return 0xffffffu;
+    }
 };
 
 static int fetch_doc(mtr_engine* e, uint32_t doc, HostDoc& hd) {
@@ -751,8 +769,11 @@ static int fetch_doc(mtr_engine* e, uint32_t doc, HostDoc& hd) {
     hd.prop.resize(std::max(hd.h.propused, 1));
     HIPCHK(hipMemcpy(hd.prop.data(), e->prop.p + size_t(doc) * e->caps.prop_words, hd.prop.size() * 4,
                      hipMemcpyDeviceToHost));
+    const size_t rs = e->caps.remover_cells + 2 * size_t(e->rtab);
     hd.rm.resize(std::max(hd.h.rmused, 1));
-    HIPCHK(hipMemcpy(hd.rm.data(), e->rm.p + size_t(doc) * e->caps.remover_cells, hd.rm.size() * 4,
+    HIPCHK(hipMemcpy(hd.rm.data(), e->rm.p + size_t(doc) * rs, hd.rm.size() * 4, hipMemcpyDeviceToHost));
+    hd.rt.resize(2 * size_t(e->rtab));
+    HIPCHK(hipMemcpy(hd.rt.data(), e->rm.p + size_t(doc) * rs + e->caps.remover_cells, hd.rt.size() * 4,
                      hipMemcpyDeviceToHost));
     return 0;
 }
@@ -799,7 +820,7 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
         if (rs != RNONE) {
             nrem = 1;
             if (m & M_OVERLAP) {
-                uint32_t c = hd.seg[F_RM * sc + i];
+                uint32_t c = hd.rm_head(hd.seg[F_UID * sc + i]);
                 while (c != 0xffffffu) {
                     nrem++;
                     c = hd.rm[c] & 0xffffffu;

@@ -29,7 +29,7 @@ struct SParams {
     const uint16_t* text;
     const uint32_t* prop;
     const uint32_t* rm;
-    int32_t segcap, tcap, pcap, rcap;
+    int32_t segcap, tcap, pcap, rcap, rtab;
     int32_t snapshot_v1, chunk_size, new_length_calc;
     uint32_t n_docs;
     const mtr_doc_desc* docs;
@@ -157,9 +157,10 @@ struct LW {
 
 // one document's arrays in HBM
 struct SDoc {
-    gptr<const uint32_t> len, seq, rseq, meta, text, props, rm;
+    gptr<const uint32_t> len, seq, rseq, meta, text, props, uid;
     gptr<const uint16_t> gtext;
-    gptr<const uint32_t> gprop, grm;
+    gptr<const uint32_t> gprop, grm, grt;
+    int rtmask;
     gptr<uint8_t> kind;
     gptr<uint32_t> start, slen, sbytes;
     gptr<int32_t> blob;
@@ -176,10 +177,12 @@ MTR_DI SDoc sdoc(const SParams& P, uint32_t d, const DocHdr& h) {
     D.meta = g + F_META * P.segcap;
     D.text = g + F_TEXT * P.segcap;
     D.props = g + F_PROPS * P.segcap;
-    D.rm = g + F_RM * P.segcap;
+    D.uid = g + F_UID * P.segcap;
     D.gtext = gp(P.text) + size_t(d) * P.tcap;
     D.gprop = gp(P.prop) + size_t(d) * P.pcap;
-    D.grm = gp(P.rm) + size_t(d) * P.rcap;
+    D.grm = gp(P.rm) + size_t(d) * (size_t(P.rcap) + 2 * size_t(P.rtab));
+    D.grt = D.grm + P.rcap;
+    D.rtmask = P.rtab - 1;
     D.kind = gp(P.s_kind) + size_t(d) * P.segcap;
     D.start = gp(P.s_start) + size_t(d) * (P.segcap + 1);
     D.slen = gp(P.s_len) + size_t(d) * P.segcap;
@@ -194,6 +197,19 @@ MTR_DI SDoc sdoc(const SParams& P, uint32_t d, const DocHdr& h) {
     D.perm = P.dkind ? int(uniu(gp(P.dkind)[d]) != 0) : 0;
     D.hlen = h.textused;
     return D;
+}
+
+// head of leaf s's later-removers list (the uid table of apply.hip.h)
+MTR_DI uint32_t rm_head(const SDoc& D, int s) {
+    const uint32_t uid = D.uid[s];
+    uint32_t h = rtab_hash(uid) & uint32_t(D.rtmask);
+    for (int n = 0; n <= D.rtmask; n++) {
+        const uint32_t k = D.grt[2 * h];
+        if (k == uid + 1) return D.grt[2 * h + 1];
+        if (k == 0) break;
+        h = (h + 1) & uint32_t(D.rtmask);
+    }
+    return 0xffffffu;
 }
 
 // visible length in the (minSeq, NonCollabClient) view for SnapshotLegacy's mapRange
@@ -351,9 +367,10 @@ MTR_DI void w_spec(LW<W>& w, const SDoc& D, const SParams& P, const mtr_doc_desc
         if (m & M_OVERLAP) {
             // the cons list holds later removers newest-first: emit oldest-first
             int nc = 0;
-            for (uint32_t c = D.rm[s]; c != 0xffffffu; c = D.grm[c] & 0xffffffu) nc++;
+            const uint32_t head = rm_head(D, s);
+            for (uint32_t c = head; c != 0xffffffu; c = D.grm[c] & 0xffffffu) nc++;
             for (int q = nc - 1; q >= 0; q--) {
-                uint32_t c = D.rm[s];
+                uint32_t c = head;
                 for (int t = 0; t < q; t++) c = D.grm[c] & 0xffffffu;
                 w.put(',');
                 w_client(w, P, dd, D.grm[c] >> 24);
