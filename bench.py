@@ -221,6 +221,7 @@ def main():
             "digest": f"{run_digest:016x}",
             "generate_s": round(gen_s, 2),
             "max_leaves": st["max_leaves"],
+            "max_heap": st["max_heap"],
             "mean_leaves_before_op": st["sum_leaves_before_op"] / max(1, messages),
         },
     }

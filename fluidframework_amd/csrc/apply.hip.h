@@ -180,9 +180,8 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
        P_TAPPEND, P_HEAP, P_OVERFLOW, P_NPACK, P_NMERGE, P_NPMATCH, P_NNLQ, P_SPLIT1, P_INS1, P_FETCH, P_X1, P_X2,
        P_COUNT };
 
-// LDS-side scratch of one document: per-level block bounds for zamboni, record-mode broadcast
+// LDS-side scratch of one document: record-mode broadcast, phase timers
 struct Sc {
-    int rs[MAXH + 1], re[MAXH + 1], topb[MAXH + 1];
     int gen_ref, gen_client;
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];

@@ -473,7 +473,7 @@ static int run_impl(mtr_engine* e, int gen) {
             if (cap > P.segcap) cap = P.segcap;
             // LRU heap: what the class holds now plus room for this launch's pushes; a document that
             // could overflow it stops before the op and asks for more (DocHdr.heap_need)
-            int lhcap = std::min<int>(P.hcap, std::max(cap / 4, round64(maxheap + 2 * k + 8)));
+            int lhcap = std::min<int>(P.hcap, std::max(cap / 8, round64(maxheap + 2 * k + 8)));
             size_t lds = lds_bytes(cap, lhcap, P.gen != 0);
             if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             P.global_mode = 0;
