@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--writers", type=int, default=None)
     ap.add_argument("--max-lag", type=int, default=None)
     ap.add_argument("--ops-per-launch", type=int, default=24)
-    ap.add_argument("--cpu-sample-docs", type=int, default=0, help="default: about 4M messages of documents")
+    ap.add_argument("--cpu-sample-docs", type=int, default=0,
+                    help="default: about 60M messages of documents (~8 s on 16 host threads)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
@@ -174,7 +175,7 @@ def main():
     if not a.no_cpu_baseline and world == 1:
         from oracle.oracle import replay_batch
 
-        k = min(a.cpu_sample_docs or max(1, 4_000_000 // ops), n)
+        k = min(a.cpu_sample_docs or max(1, 60_000_000 // ops), n)
         sample = eng.download(0, k)
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
         secs, ohash, ost = replay_batch(sample, 0, k, threads)
