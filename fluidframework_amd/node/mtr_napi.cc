@@ -267,13 +267,28 @@ napi_value Reset(napi_env env, napi_callback_info info) {
     return r;
 }
 
+// setMatrix(h, rowsDoc, colsDoc): the two PermutationVectors of one SharedMatrix (mtr_set_matrix)
+napi_value SetMatrix(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t rows = 0, cols = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &rows));
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &cols));
+    if (mtr_set_matrix(e, rows, cols) != MTR_OK) return throw_engine(env, "mtr_set_matrix");
+    napi_value r;
+    NAPI_CALL(env, napi_get_undefined(env, &r));
+    return r;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     const struct {
         const char* name;
         napi_callback cb;
     } fns[] = {{"createEngine", CreateEngine}, {"submitRun", SubmitRun}, {"summarize", Summarize},
                {"getSummary", GetSummary},     {"getText", GetText},     {"docStatus", DocStatus},
-               {"stats", Stats},               {"reset", Reset}};
+               {"stats", Stats},               {"reset", Reset},         {"setMatrix", SetMatrix}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||
