@@ -24,6 +24,7 @@ F_PROPS = 4
 F_NOREF = 8
 F_APPEND = 16
 F_COLS = 32
+F_DELTA = 64
 
 NULL_VALUE = 0xFFFFFFFF
 NOT_INDEX = 0xFFFFFFFF
@@ -50,6 +51,8 @@ OP_DTYPE = np.dtype(
     ]
 )
 assert OP_DTYPE.itemsize == 32
+
+DELTA_DTYPE = np.dtype([("op", "<u4"), ("pos", "<i4"), ("len", "<i4"), ("kind", "<u4")])  # mtr_delta
 
 DOC_DTYPE = np.dtype(
     [

@@ -58,6 +58,7 @@ constexpr uint32_t M_DEL = 1u << 25;
 constexpr uint32_t M_NL = 1u << 26;   // text leaf whose last unit is '\n' (TextSegment.canAppend)
 constexpr uint32_t M_NLQ = 1u << 27;  // M_NL not known yet (left half of a split): read lazily by scour
 constexpr uint32_t M_NONL = 1u << 28; // the leaf's text holds no '\n' at all (so neither does any split half)
+constexpr uint32_t M_TOUCH = 1u << 29;  // transient: a delta segment of the current MTR_F_DELTA op
 constexpr uint32_t NS_UNDEF = 0, NS_FALSE = 1, NS_TRUE = 2;
 
 constexpr uint32_t CL_LOCAL = 0xffu;      // LocalClientId (-1)
@@ -122,7 +123,8 @@ struct DocHdr {
     int32_t textused, propused, rmused, status;
     int32_t op_cursor, fail_op, max_heap, texthalf;  // texthalf: active half of the text arena
     int32_t heap_need;  // LRU heap capacity the next launch must give this document (0 = none)
-    int32_t pad[3];
+    int32_t dused;      // delta ranges recorded for the current batch
+    int32_t pad[2];
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -161,6 +163,8 @@ struct KParams {
     const uint32_t* key_index;
     const uint32_t* val_eq;
     unsigned long long* stat_ops;  // [doc][4]: ops applied, sum of leaves before ops, inserted units
+    uint32_t* delta;               // delta ranges of MTR_F_DELTA ops (mtr_delta records)
+    const uint64_t* doff;          // [doc + 1]: document d's records are [doff[d], doff[d+1])
     // SharedMatrix pairs (mtr_set_matrix): dkind[doc] 0 = SharedString, 1 = rows PermutationVector
     // (drives the pair; dpart[doc] = its cols document), 2 = cols PermutationVector
     const uint32_t* dkind;
@@ -196,6 +200,7 @@ struct St {
     int fail_op, max_heap, ops_done, texthalf;
     int htop;  // seq of the LRU heap's top entry (valid while heapn > 0)
     int heap_need;
+    int dused;
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
 
@@ -215,6 +220,8 @@ struct Doc {
     lptr<mtr_synth_state> gst;
     gptr<uint16_t> gtext;
     gptr<uint32_t> gprop, grm, grt;  // grt: remover-head table (2 words per entry)
+    gptr<uint32_t> gdelta;           // this document's delta ranges (mtr_delta records)
+    int dcap;                        // ... and their capacity in this batch
     int cap, lhcap, rtmask;
 };
 
@@ -1474,6 +1481,7 @@ struct Eng {
         if (marker) m |= M_MARKER;
         else m |= (nl ? M_NL : 0u) | (nonl ? M_NONL : 0u);
         if (op.flags & MTR_F_NOREF) m |= M_NOREF;
+        if (op.flags & MTR_F_DELTA) m |= M_TOUCH;
         if (S == 0) {
             s.height = 1;
             m = set_bnd(m, 1);
@@ -1596,7 +1604,7 @@ struct Eng {
     // visible length > 0 inside [start, end), on the current scan arrays, 64 leaves per round.
     // The walk stops at the first leaf whose view start (E - max(V,0), nondecreasing) is >= end.
     static MTR_DI void range_walk(D& L, const KParams& P, St& s, const View& v, int start, int end, int seq,
-                                  uint32_t client, int is_remove, uint32_t pp) {
+                                  uint32_t client, int is_remove, uint32_t pp, bool dl) {
         PROF(P_RANGE);
         if (end == start) return;
         const int S = s.nseg;
@@ -1641,6 +1649,7 @@ struct Eng {
                     } else if (act) {
                         L.rseq[j] = seq;
                         mj = (mj & ~(0xffu << M_FREM_SHIFT) & ~M_OVERLAP) | (client << M_FREM_SHIFT);
+                        if (dl) mj |= M_TOUCH;  // removedSegments: first removals only (mergeTree.ts:1975-2000)
                         L.meta[j] = mj;
                     }
                     if (__ballot(full)) s.status = MTR_ERR_CAPACITY;
@@ -1655,6 +1664,10 @@ struct Eng {
                         const uint32_t nw = props_apply(L, P, s, o, pp);
                         if (act && old == o) L.props[j] = nw;
                         pend &= ~sel;
+                    }
+                    if (dl && act) {  // every annotated segment is a delta segment
+                        mj |= M_TOUCH;
+                        L.meta[j] = mj;
                     }
                 }
                 wsync();
@@ -1728,6 +1741,7 @@ struct Eng {
             s.status = h.status; s.fail_op = h.fail_op; s.max_heap = h.max_heap;
             s.texthalf = h.texthalf;
             s.heap_need = 0;
+            s.dused = h.dused;
             s.ops_done = 0;
             s.sum_s = 0;
             s.sum_l = 0;
@@ -1799,6 +1813,7 @@ struct Eng {
             h.max_heap = s.max_heap;
             h.texthalf = s.texthalf;
             h.heap_need = s.heap_need;
+            h.dused = s.dused;
             st_struct(hp, h);
             if (P.gen) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
 #ifdef MTR_PROF
@@ -1860,6 +1875,57 @@ struct Eng {
         L.grm = gp(P.rm) + size_t(d) * (size_t(P.rcap) + 2 * size_t(P.rtab));
         L.grt = L.grm + P.rcap;
         L.rtmask = P.rtab - 1;
+        if (P.doff) {
+            const uint64_t o = gp(P.doff)[d];
+            L.gdelta = gp(P.delta) + o * 4;
+            L.dcap = int(gp(P.doff)[d + 1] - o);
+        } else {
+            L.gdelta = gp(P.delta);
+            L.dcap = 0;
+        }
+    }
+
+    // ------------------------------------------------------------ delta ranges
+    // The ranges of a SequenceDeltaEvent (sequenceDeltaEvent.ts): every M_TOUCH leaf in tree order
+    // with its position in the local view (Client.getPosition: removed segments count 0) and its
+    // cachedLength; clears the marks.
+    static MTR_DI void emit_deltas(D& L, const KParams& P, St& s, int gidx, uint32_t kind) {
+        const int S = s.nseg;
+        const int ln = lane_id();
+        int carry = 0;
+        for (int base = 0; base < S; base += 64) {
+            const int i = base + ln;
+            const bool in = i < S;
+            uint32_t m = 0;
+            int len = 0, rs = RNONE;
+            if (in) {
+                m = L.meta[i];
+                len = L.len[i];
+                rs = L.rseq[i];
+            }
+            const int loc = in && rs == RNONE ? len : 0;
+            const int inc = wave_incl_scan(loc);
+            const bool t = in && (m & M_TOUCH);
+            const uint64_t tm = __ballot(t);
+            if (tm) {
+                const int n = __popcll(tm);
+                if (s.dused + n > L.dcap) {
+                    s.status = MTR_ERR_CAPACITY;
+                    return;
+                }
+                if (t) {
+                    const gptr<uint32_t> r = L.gdelta + 4 * size_t(s.dused + __popcll(tm & lanes_below()));
+                    r[0] = uint32_t(gidx);
+                    r[1] = uint32_t(carry + inc - loc);
+                    r[2] = uint32_t(len);
+                    r[3] = kind;
+                    L.meta[i] = m & ~M_TOUCH;
+                }
+                s.dused += n;
+            }
+            carry += rdlane(inc, 63);
+        }
+        wsync();
     }
 
     // ------------------------------------------------------------ one op
@@ -1941,7 +2007,8 @@ struct Eng {
                 prefix(L, s, v, P.new_length_calc);
                 split_at(L, s, op.pos1);
                 split_at(L, s, op.pos2);
-                range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload);
+                range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload,
+                           (op.flags & MTR_F_DELTA) != 0);
                 zop = s.collab;
                 break;
             }
@@ -1960,6 +2027,10 @@ struct Eng {
                 s.status = MTR_ERR_BAD_OP;
                 break;
         }
+        // mergeTreeDeltaCallback (mergeTree.ts:1414, 1943, 2028) fires before zamboni
+        if ((op.flags & MTR_F_DELTA) && s.status == MTR_OK &&
+            (op.type == MTR_OP_INSERT || op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE))
+            emit_deltas(L, P, s, gidx, op.type);
         // zamboniSegments after the op (mergeTree.ts:1420-1426, 1948-1952, 2042-2046), then
         // updateSeqNumbers, whose minSeq advance runs it again (mergeTree.ts:1037-1042)
         const bool upd = !local_op && op.type != MTR_OP_START_COLLAB && (op.flags & MTR_F_LAST);

@@ -96,6 +96,10 @@ struct mtr_engine {
     DevBuf<uint32_t> propop_off, propop_kv, key_off, key_index, val_off, val_eq, client_off;
     DevBuf<uint8_t> key_bytes, val_bytes, client_bytes;
     DevBuf<unsigned long long> stat;  // [0] ops applied
+    DevBuf<uint32_t> delta;           // delta ranges of the MTR_F_DELTA ops of the current batch
+    DevBuf<uint64_t> doff;            // [doc + 1] record offsets into delta (exact per-batch bound)
+    std::vector<uint64_t> h_doff;
+    bool has_delta = false;
     DevBuf<int32_t> red;              // small reduction buffer
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
     DevBuf<uint32_t> dlist;           // [class][n_docs] document lists of one apply round
@@ -137,7 +141,10 @@ __global__ void reset_kernel(DocHdr* h, uint32_t n) {
 
 __global__ void cursor_reset_kernel(DocHdr* h, uint32_t n) {
     uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d < n) h[d].op_cursor = 0;
+    if (d < n) {
+        h[d].op_cursor = 0;
+        h[d].dused = 0;  // delta ranges are per batch
+    }
 }
 
 // out[0] = max nseg, out[1] = max remaining ops, out[2] = max heapn
@@ -278,6 +285,8 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->val_bytes.release();
     e->client_bytes.release();
     e->stat.release();
+    e->delta.release();
+    e->doff.release();
     e->red.release();
     e->cls.release();
     if (e->h_cls) (void)hipHostFree(e->h_cls);
@@ -348,6 +357,34 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
         upload(e, e->client_bytes, b->client_bytes, size_t(b->client_off[ncl - 1])))
         return -1;
     e->h_val_eq.assign(b->val_eq, b->val_eq + b->n_vals);
+    // delta ranges (MTR_F_DELTA): per-document slices sized by an exact bound of this batch's ranges
+    // (an insert reports its one segment; a remove / annotate at most one range per unit of its range
+    // and per segment)
+    e->has_delta = false;
+    e->h_doff.assign(size_t(b->n_docs) + 1, 0);
+    bool any = false;
+    for (uint64_t i = 0; i < b->n_ops && !any; i++) any = (b->ops[i].flags & MTR_F_DELTA) != 0;
+    for (uint32_t d = 0; any && d < b->n_docs; d++) {
+        const mtr_doc_desc& dd = b->docs[d];
+        uint64_t need = 0;
+        // (record mode submits op lists that are only written on the device: n_ops bounds the scan)
+        const uint64_t end = std::min<uint64_t>(dd.op_begin + dd.op_count, b->n_ops);
+        for (uint64_t i = dd.op_begin; i < end; i++) {
+            const mtr_op& op = b->ops[i];
+            if (!(op.flags & MTR_F_DELTA)) continue;
+            if (op.type == MTR_OP_INSERT) need += 1;
+            else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE)
+                need += uint64_t(std::min<int64_t>(std::max<int64_t>(int64_t(op.pos2) - op.pos1, 0),
+                                                   int64_t(e->caps.max_segments)));
+        }
+        e->h_doff[d + 1] = e->h_doff[d] + need;
+    }
+    if (e->h_doff[b->n_docs]) {
+        e->has_delta = true;
+        if (e->delta.ensure(size_t(e->h_doff[b->n_docs]) * 4) || e->doff.ensure(size_t(b->n_docs) + 1)) return -1;
+        HIPCHK(hipMemcpyAsync(e->doff.p, e->h_doff.data(), (size_t(b->n_docs) + 1) * sizeof(uint64_t),
+                              hipMemcpyHostToDevice, e->stream));
+    }
     cursor_reset_kernel<<<(b->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, b->n_docs);
     HIPCHK(hipGetLastError());
     e->summarized = false;
@@ -366,6 +403,23 @@ static int read_state(mtr_engine* e, int32_t out[3]) {
 static int run_impl(mtr_engine* e, int gen);
 
 int mtr_run(mtr_engine* e) { return run_impl(e, 0); }
+
+int64_t mtr_get_deltas(mtr_engine* e, uint32_t doc, mtr_delta* out, int64_t cap) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (doc >= e->max_docs) {
+        set_err("mtr_get_deltas: bad document");
+        return -1;
+    }
+    DocHdr h;
+    HIPCHK(hipMemcpy(&h, e->hdr.p + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
+    const int64_t n = h.dused;
+    if (n > cap) return -n;
+    if (n && e->has_delta && doc < e->n_docs)
+        HIPCHK(hipMemcpy(out, e->delta.p + e->h_doff[doc] * 4, size_t(n) * sizeof(mtr_delta),
+                         hipMemcpyDeviceToHost));
+    return n;
+}
 
 int mtr_set_matrix(mtr_engine* e, uint32_t rows_doc, uint32_t cols_doc) {
     HIPCHK(hipSetDevice(e->device));
@@ -416,6 +470,8 @@ static int run_impl(mtr_engine* e, int gen) {
     P.key_index = e->key_index.p;
     P.val_eq = e->val_eq.p;
     P.stat_ops = e->stat.p;
+    P.delta = e->delta.p;
+    P.doff = e->has_delta ? e->doff.p : nullptr;
     P.dkind = e->dkind.p;
     P.dpart = e->dpart.p;
     P.gen = gen;

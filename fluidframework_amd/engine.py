@@ -65,6 +65,8 @@ def lib():
         L.mtr_stats.restype = C.c_int
         L.mtr_set_matrix.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         L.mtr_set_matrix.restype = C.c_int
+        L.mtr_get_deltas.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
+        L.mtr_get_deltas.restype = C.c_int64
         L.mtr_last_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.mtr_last_timing.restype = C.c_int
         L.mtr_last_error.restype = C.c_char_p
@@ -187,6 +189,19 @@ class Engine:
         buf = np.zeros(max(n, 1), dtype="<u2")
         lib().mtr_get_text(self.h, doc, buf.ctypes.data, n)
         return buf[:n].tobytes().decode("utf-16-le", "surrogatepass")
+
+    def deltas(self, doc) -> np.ndarray:
+        """The delta ranges (abi.DELTA_DTYPE) of the MTR_F_DELTA ops of the last batch for one document."""
+        cap = 1024  # cap >= 1, so -1 can only mean an error
+        while True:
+            out = np.zeros(cap, dtype=abi.DELTA_DTYPE)
+            n = lib().mtr_get_deltas(self.h, doc, out.ctypes.data, cap)
+            if n == -1:
+                raise EngineError(_err())
+            if n >= 0:
+                break
+            cap = -n
+        return out[:n]
 
     def status(self, doc):
         op = C.c_int32(-1)

@@ -50,9 +50,24 @@ enum {
     MTR_F_NOREF = 8,   /* marker has no refType member ({"marker":{}}) */
     MTR_F_APPEND = 16, /* insert at the end of the local view with refSeq = UniversalSequenceNumber
                           (SnapshotLoader.loadBody append, snapshotLoader.ts:221-256) */
-    MTR_F_COLS = 32    /* matrix documents: the vector op targets the cols PermutationVector (contents.target
+    MTR_F_COLS = 32,   /* matrix documents: the vector op targets the cols PermutationVector (contents.target
                           "cols", matrix.ts:645-651); without it, the rows vector */
+    MTR_F_DELTA = 64   /* report this op's delta ranges (mtr_get_deltas): the SequenceDeltaEvent ranges
+                          SharedSegmentSequence.processMergeTreeMsg turns into catch-up ops for lagging
+                          messages in the legacy format (sequence.ts:120-173, 697-736) */
 };
+
+/* One delta range of an MTR_F_DELTA op (ISequenceDeltaRange, sequenceDeltaEvent.ts): the op's
+ * index in its document's op list, the segment's position in the local view right after the op
+ * (Client.getPosition) and its cachedLength; ranges come in tree order (SortedSegmentSet by ordinal).
+ * kind: MTR_OP_INSERT (the inserted segment), MTR_OP_REMOVE (segments this op removed first),
+ * MTR_OP_ANNOTATE (every annotated segment). */
+typedef struct mtr_delta {
+    uint32_t op;
+    int32_t  pos;
+    int32_t  len;
+    uint32_t kind;
+} mtr_delta;
 
 /*
  * SharedMatrix documents: a matrix is a pair of engine documents, the rows

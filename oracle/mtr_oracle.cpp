@@ -722,6 +722,16 @@ class Tree {
         return s;
     }
 
+    // SequenceDeltaEvent ranges of MTR_F_DELTA ops (sequenceDeltaEvent.ts: position = getPosition
+    // at the local view when the delta callback fires, before zamboni; tree order)
+    bool deltaOn = false;
+    uint32_t curOpIndex = 0;
+    std::vector<mtr_delta> deltas;
+    void recordDeltas(const std::vector<Seg*>& segs, uint32_t kind) {
+        if (!deltaOn) return;
+        for (Seg* x : segs) deltas.push_back({curOpIndex, localPosition(x), x->len, kind});
+    }
+
     // insertSegments + blockInsert, mergeTree.ts:1397-1427,1594-1685
     void insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq) {
         ensureIntervalBoundary(pos, refSeq, clientId);
@@ -735,6 +745,7 @@ class Tree {
                 return;
             }
             updateRoot(splitNode);
+            recordDeltas({seg}, MTR_OP_INSERT);  // mergeTree.ts:1414-1418
             if (collaborating) {  // saveIfLocal, mergeTree.ts:1618-1637
                 if (!(seg->seq == kUnassignedSeq && clientId == localClientId) && seg->seq > minSeq)
                     addToLRUSet(seg, seg->seq);
@@ -747,6 +758,7 @@ class Tree {
     void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq) {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
+        std::vector<Seg*> fresh;  // removedSegments (mergeTree.ts:1975-2000)
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
@@ -761,12 +773,14 @@ class Tree {
                     s->removed = true;
                     s->removedClientIds.assign(1, clientId);
                     s->removedSeq = seq;
+                    fresh.push_back(s);
                 }
                 if (collaborating) {
                     if (!(s->removedSeq == kUnassignedSeq && clientId == localClientId)) addToLRUSet(s, seq);
                 }
             },
             start, end);
+        recordDeltas(fresh, MTR_OP_REMOVE);  // mergeTree.ts:2026-2031
         if (collaborating && seq != kUnassignedSeq) zamboniSegments();
     }
 
@@ -774,13 +788,16 @@ class Tree {
     void annotateRange(int start, int end, uint32_t propop, int refSeq, int clientId, int seq) {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
+        std::vector<Seg*> touched;
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
                 addProperties(s, propop);
+                touched.push_back(s);
                 if (collaborating && seq != kUnassignedSeq) addToLRUSet(s, seq);
             },
             start, end);
+        recordDeltas(touched, MTR_OP_ANNOTATE);  // mergeTree.ts:1941-1946
         if (collaborating && seq != kUnassignedSeq) zamboniSegments();
     }
 
@@ -1191,10 +1208,22 @@ int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint
     if (op_hi > dd.op_count) op_hi = dd.op_count;
     for (uint32_t i = op_lo; i < op_hi; i++) {
         const mtr_op& op = b->ops[dd.op_begin + i];
+        t.curOpIndex = i;
+        t.deltaOn = (op.flags & MTR_F_DELTA) != 0;
         int st = d->matrix ? d->applyMatrix(op, dd) : t.apply(op, dd);
+        t.deltaOn = false;
         if (st != MTR_OK) return st;
     }
     return d->matrix ? (t.status != MTR_OK ? t.status : d->cols.status) : t.status;
+}
+
+int64_t oracle_doc_deltas(oracle_doc* d, mtr_delta* out, int64_t cap) {
+    std::vector<mtr_delta>& v = d->tree.deltas;
+    const int64_t n = int64_t(v.size());
+    if (n > cap) return -n;
+    if (n) std::memcpy(out, v.data(), size_t(n) * sizeof(mtr_delta));
+    v.clear();
+    return n;
 }
 
 int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap) {

@@ -38,6 +38,8 @@ def lib():
                                            C.c_void_p, C.c_int32]
         L.oracle_doc_export.restype = C.c_int64
         L.oracle_doc_export.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
+        L.oracle_doc_deltas.restype = C.c_int64
+        L.oracle_doc_deltas.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.oracle_doc_state.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_set_trace.argtypes = [C.c_int]
         L.oracle_generate.restype = C.c_int
@@ -113,6 +115,14 @@ class OracleDoc:
         out = np.zeros((max(n, 1), 8), dtype="<i4")
         lib().oracle_doc_export(self.h, out.ctypes.data, n, C.byref(h))
         return out[:n], h.value
+
+    def deltas(self) -> np.ndarray:
+        """Delta ranges (abi.DELTA_DTYPE) of the MTR_F_DELTA ops applied since the last call."""
+        n = lib().oracle_doc_deltas(self.h, None, 0)
+        n = -n if n < 0 else n
+        out = np.zeros(max(n, 1), dtype=abi.DELTA_DTYPE)
+        lib().oracle_doc_deltas(self.h, out.ctypes.data, n)
+        return out[:n]
 
     def state(self):
         out = np.zeros(4, dtype="<i8")
