@@ -316,7 +316,7 @@ struct ProfScope {
 // no permutation code; CAP: the launch's LDS leaf capacity as a compile-time constant (0 = runtime),
 // which puts every leaf array at a constant LDS offset (ds_read/ds_write immediate offsets from one
 // per-lane address instead of a base register and an address add per array)
-template <bool G, bool PM = false, int CAP = 0>
+template <bool G, bool PM = false, int CAP = 0, bool DL = false>
 struct Eng {
     using D = Doc<G>;
     template <class T>
@@ -1481,7 +1481,7 @@ struct Eng {
         if (marker) m |= M_MARKER;
         else m |= (nl ? M_NL : 0u) | (nonl ? M_NONL : 0u);
         if (op.flags & MTR_F_NOREF) m |= M_NOREF;
-        if (op.flags & MTR_F_DELTA) m |= M_TOUCH;
+        if (DL && (op.flags & MTR_F_DELTA)) m |= M_TOUCH;
         if (S == 0) {
             s.height = 1;
             m = set_bnd(m, 1);
@@ -2008,7 +2008,7 @@ struct Eng {
                 split_at(L, s, op.pos1);
                 split_at(L, s, op.pos2);
                 range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload,
-                           (op.flags & MTR_F_DELTA) != 0);
+                           DL && (op.flags & MTR_F_DELTA) != 0);
                 zop = s.collab;
                 break;
             }
@@ -2028,7 +2028,7 @@ struct Eng {
                 break;
         }
         // mergeTreeDeltaCallback (mergeTree.ts:1414, 1943, 2028) fires before zamboni
-        if ((op.flags & MTR_F_DELTA) && s.status == MTR_OK &&
+        if (DL && (op.flags & MTR_F_DELTA) && s.status == MTR_OK &&
             (op.type == MTR_OP_INSERT || op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE))
             emit_deltas(L, P, s, gidx, op.type);
         // zamboniSegments after the op (mergeTree.ts:1420-1426, 1948-1952, 2042-2046), then
@@ -2213,12 +2213,12 @@ struct Eng {
     }
 };
 
-template <bool G, int CAP = 0>
+template <bool G, int CAP = 0, bool DL = false>
 __global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
-    Eng<G, false, CAP>::run(smem, P, d);
+    Eng<G, false, CAP, DL>::run(smem, P, d);
 }
 
 // leaf capacities with a compile-time LDS layout (apply_kernel<false, CAP>); other capacities use

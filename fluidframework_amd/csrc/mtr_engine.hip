@@ -491,6 +491,10 @@ static int run_impl(mtr_engine* e, int gen) {
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_kernel<false, 0, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_kernel<true, 0, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 #define MTR_CAP_ATTR(C)                                                                                   \
     (void)hipFuncSetAttribute((const void*)apply_kernel<false, C>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                               160 * 1024);
@@ -567,6 +571,9 @@ static int run_impl(mtr_engine* e, int gen) {
                 const uint32_t region = uint32_t(lds / 2);
                 if (P.global_mode) apply_pair_kernel<true><<<cnt, NT, lds, st>>>(P, region);
                 else apply_pair_kernel<false><<<cnt, NT, lds, st>>>(P, region);
+            } else if (P.doff) {  // a batch with MTR_F_DELTA ops: the delta-reporting instantiation
+                if (P.global_mode) apply_kernel<true, 0, true><<<cnt, NT, lds, st>>>(P);
+                else apply_kernel<false, 0, true><<<cnt, NT, lds, st>>>(P);
             } else if (P.global_mode) {
                 apply_kernel<true><<<cnt, NT, lds, st>>>(P);
             } else {
