@@ -33,7 +33,7 @@ function native() {
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
     START_COLLAB: 12 };
-const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8 };
+const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, DELTA: 64 };
 const NULL_VALUE = 0xFFFFFFFF;
 const NOT_INDEX = 0xFFFFFFFF;
 const STATUS = { OK: 0, INSERT_FAILED: 1, BAD_OP: 2, CAPACITY: 3, UNSUPPORTED: 4, ASSERT: 0x1000 };
@@ -250,6 +250,106 @@ function buildBatch(logs, it) {
     };
 }
 
+/*
+ * Legacy-format catch-up messages (SURVEY.md §8 row f2).  SharedSegmentSequence keeps the messages
+ * since the MSN and rewrites each lagging one (refSeq != seq - 1) from the sequenceDelta events its
+ * application raised (createOpsFromDelta / processMergeTreeMsg, sequence.ts:120-173, 697-736).  The
+ * engine applies messages in batches and raises no events, so the shim keeps that list itself: the
+ * lagging message's ops are flagged F.DELTA, the engine reports each delta range (op, position in the
+ * local view, cachedLength, kind; mtr_get_deltas) and the ops are rebuilt here after the batch.
+ */
+function sameProps(a, b) {  // matchProperties, properties.ts:71-105 (JS semantics, written out)
+    if (!a) return !b;
+    if (!b) return false;
+    for (const k in a) {
+        const y = b[k];
+        if (y === undefined) return false;
+        if (typeof y === 'object' ? !sameProps(a[k], y) : y !== a[k]) return false;
+    }
+    for (const k in b) if (a[k] === undefined) return false;
+    return true;
+}
+function insertedSegmentJson(spec) {  // segment.clone().toJSONObject() of the segment an insert creates
+    const kept = (p) => { const o = {}; Object.keys(p).forEach((k) => { if (p[k] !== null) o[k] = p[k]; }); return o; };
+    if (typeof spec === 'string') return spec;
+    const hasProps = spec.props !== undefined && spec.props !== null;
+    if ('text' in spec) return hasProps ? { text: spec.text, props: kept(spec.props) } : spec.text;
+    const m = spec.marker || {};
+    const out = { marker: m.refType === undefined || m.refType === null ? {} : { refType: m.refType } };
+    if (hasProps) out.props = kept(spec.props);
+    return out;
+}
+function opsFromDeltas(members, opIndex, byOp) {
+    const ops = [];
+    members.forEach((member, i) => {
+        for (const r of byOp.get(opIndex[i]) || []) {
+            const pos = r[1], len = r[2], last = ops.length ? ops[ops.length - 1] : undefined;
+            if (r[3] === OP.ANNOTATE) {  // an observer's propertyDeltas hold every key of the op
+                const props = {};
+                Object.keys(member.props).forEach((k) => { props[k] = member.props[k]; });
+                if (last && last.pos2 === pos && sameProps(last.props, props)) last.pos2 += len;
+                else ops.push({ pos1: pos, pos2: pos + len, props, type: 2 });
+            } else if (r[3] === OP.INSERT) {
+                ops.push({ pos1: pos, seg: insertedSegmentJson(member.seg), type: 0 });
+            } else if (r[3] === OP.REMOVE) {
+                if (last && last.pos1 === pos) {
+                    if (last.pos2 === undefined) throw new Error('0x3ff');  // sequence.ts:155-158
+                    last.pos2 += len;
+                } else {
+                    ops.push({ pos1: pos, pos2: pos + len, type: 1 });
+                }
+            }
+        }
+    });
+    return ops;
+}
+class CatchUpLog {
+    constructor() { this.stash = []; this.pending = []; }
+    /** After log.message(msg) queued the message's records from op index `lo` on. */
+    add(msg, log, lo) {
+        const copy = JSON.parse(JSON.stringify(msg));  // parseHandles (sequence.ts:698)
+        if (typeof copy.contents === 'string') copy.contents = JSON.parse(copy.contents);
+        if (copy.referenceSequenceNumber !== copy.sequenceNumber - 1) {
+            const members = copy.contents.type === 3 ? copy.contents.ops : [copy.contents];
+            const opIndex = members.map((_, i) => {
+                const r = log.ops[lo + i];
+                if (r[0] !== OP.INSERT && r[0] !== OP.REMOVE && r[0] !== OP.ANNOTATE) return -1;
+                r[1] |= F.DELTA;
+                return lo + i;
+            });
+            copy.referenceSequenceNumber = copy.sequenceNumber - 1;
+            this.pending.push({ msg: copy, members, opIndex });
+        }
+        this.stash.push(copy);
+        if (this.stash.length > 20 && this.stash[20].sequenceNumber < msg.minimumSequenceNumber) {
+            this.trim(msg.minimumSequenceNumber);  // sequence.ts:728-734
+        }
+    }
+    resolve(deltas) {  // Int32Array of [op, pos, len, kind] records of the batch just applied
+        const byOp = new Map();
+        for (let i = 0; i < deltas.length; i += 4) {
+            const r = [deltas[i], deltas[i + 1], deltas[i + 2], deltas[i + 3]];
+            if (!byOp.has(r[0])) byOp.set(r[0], []);
+            byOp.get(r[0]).push(r);
+        }
+        for (const p of this.pending) {
+            const ops = opsFromDeltas(p.members, p.opIndex, byOp);
+            p.msg.contents = ops.length === 1 ? ops[0] : { ops, type: 3 };  // createGroupOp
+        }
+        this.pending = [];
+    }
+    trim(minSeq) {  // processMinSequenceNumberChanged, sequence.ts:738-748
+        let i = 0;
+        while (i < this.stash.length && this.stash[i].sequenceNumber <= minSeq) i++;
+        if (i) this.stash = this.stash.slice(i);
+    }
+    forSummary(minSeq) {  // summarizeMergeTree, sequence.ts:675-695
+        this.trim(minSeq);
+        this.stash.forEach((m) => { m.minimumSequenceNumber = minSeq; });
+        return this.stash;
+    }
+}
+
 /** The observer Clients of many documents on one GPU. */
 class BatchReplayEngine {
     constructor(maxDocs, options) {
@@ -258,17 +358,20 @@ class BatchReplayEngine {
         this.h = native().createEngine(maxDocs, this.options);
         this.interner = new Interner();
         this.logs = [];
+        this.catchUps = [];
         this.dirty = false;
         this.summarized = false;
     }
     createClient() {
         if (this.logs.length >= this.maxDocs) throw new Error('engine is full');
         this.logs.push(new DocLog());
+        this.catchUps.push(new CatchUpLog());
         return new BatchReplayClient(this, this.logs.length - 1);
     }
     flush() {  // apply every queued message of every document
         if (!this.dirty) return;
         native().submitRun(this.h, buildBatch(this.logs, this.interner));
+        this.catchUps.forEach((c, d) => { if (c.pending.length) c.resolve(native().getDeltas(this.h, d)); });
         this.dirty = false;
         this.summarized = false;
     }
@@ -297,7 +400,11 @@ class BatchReplayClient {
     }
     applyMsg(msg, local) {
         if (local) throw new UnsupportedError('local (acked) ops are outside the observer path');
-        this._queue(() => this.log.message(msg, this.engine.interner));
+        this._queue(() => {
+            const lo = this.log.ops.length;
+            this.log.message(msg, this.engine.interner);
+            if (!this.engine.options.snapshotV1 && msg.type === 'op') this.engine.catchUps[this.doc].add(msg, this.log, lo);
+        });
         this.currentSeq = msg.sequenceNumber;
     }
     updateSeqNumbers(min, seq) {
@@ -320,7 +427,11 @@ class BatchReplayClient {
         return native().getText(this.engine.h, this.doc);
     }
     getLength() { return this.getText().length; }
-    /** Client.summarize (client.ts:966-1000) -> ISummaryTreeWithStats */
+    /**
+     * Client.summarize (client.ts:966-1000) -> ISummaryTreeWithStats.  In the legacy format the
+     * catch-up messages are the shim's own transformed list (CatchUpLog): the caller's list was built
+     * without sequenceDelta events, so it is superseded.
+     */
     summarize(runtime, handle, serializer, catchUpMsgs) {
         const dm = runtime.deltaManager;
         this.updateSeqNumbers(dm.minimumSequenceNumber, dm.lastSequenceNumber);
@@ -330,6 +441,7 @@ class BatchReplayClient {
         this._check();
         if (!this.engine.summarized) { native().summarize(this.engine.h); this.engine.summarized = true; }
         const blobs = native().getSummary(this.engine.h, this.doc);
+        if (!v1) catchUpMsgs = this.engine.catchUps[this.doc].forSummary(dm.minimumSequenceNumber);
         const names = v1 ? blobs.map((_, i) => (i === 0 ? 'header' : 'body_' + (i - 1))) : ['header', 'body'];
         const tree = {};
         let total = 0;

@@ -268,6 +268,29 @@ napi_value Reset(napi_env env, napi_callback_info info) {
 }
 
 // setMatrix(h, rowsDoc, colsDoc): the two PermutationVectors of one SharedMatrix (mtr_set_matrix)
+napi_value GetDeltas(napi_env env, napi_callback_info info) {
+    // getDeltas(engine, doc) -> Int32Array of [op, pos, len, kind] records (mtr_get_deltas)
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    std::vector<mtr_delta> d(1024);
+    int64_t n = mtr_get_deltas(e, doc, d.data(), int64_t(d.size()));
+    if (n == -1) return throw_engine(env, "mtr_get_deltas");
+    if (n < 0) {
+        d.resize(size_t(-n));
+        n = mtr_get_deltas(e, doc, d.data(), int64_t(d.size()));
+        if (n < 0) return throw_engine(env, "mtr_get_deltas");
+    }
+    void* data = nullptr;
+    napi_value ab, arr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, size_t(n) * sizeof(mtr_delta), &data, &ab));
+    if (n) std::memcpy(data, d.data(), size_t(n) * sizeof(mtr_delta));
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, size_t(n) * 4, ab, 0, &arr));
+    return arr;
+}
 napi_value SetMatrix(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (!get_args(env, info, 3, argv)) return nullptr;
@@ -288,7 +311,8 @@ napi_value Init(napi_env env, napi_value exports) {
         napi_callback cb;
     } fns[] = {{"createEngine", CreateEngine}, {"submitRun", SubmitRun}, {"summarize", Summarize},
                {"getSummary", GetSummary},     {"getText", GetText},     {"docStatus", DocStatus},
-               {"stats", Stats},               {"reset", Reset},         {"setMatrix", SetMatrix}};
+               {"stats", Stats},               {"reset", Reset},         {"setMatrix", SetMatrix},
+               {"getDeltas", GetDeltas}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||
