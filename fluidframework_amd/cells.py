@@ -1,0 +1,181 @@
+"""SharedMatrix cell values and the ``cells`` summary blob, host side.
+
+The engine resolves every set-cell message to a (row handle, col handle) pair on the device -- the
+position adjustment, the split and the handle allocation are the hot part (rows a17/a18) -- and, for a
+matrix tracked for its cells, reports in op order (``mtr_get_deltas``):
+
+* ``MTR_DELTA_CELL`` {op, row handle, col handle}: ``cells.setCell(rowHandle, colHandle, value)``
+  happened (SharedMatrix.processCore, packages/dds/matrix/src/matrix.ts:676-692);
+* ``MTR_DELTA_RECYCLE`` {op, first handle, count} on a vector's document: zamboni unlinked a segment
+  and its handles went back to the free list, so their row / column of cells is cleared
+  (onRowHandlesRecycled / onColHandlesRecycled, matrix.ts:722-734).
+
+The values themselves are opaque JSON the host already holds, so the cell store lives here:
+:class:`SparseArray2D` restates packages/dds/matrix/src/sparsearray2d.ts -- a 4-level, 256-way
+Morton-keyed trie whose *allocated levels* show in the summary (levels are never freed, cleared
+cells become ``null``) -- and :class:`CellMatrixLog` pairs it with the matrix message packer.
+"""
+from __future__ import annotations
+
+from typing import Any
+
+import numpy as np
+
+from . import abi
+from .batch import Interner, MatrixLog
+from .jsjson import js_stringify, parse, to_utf8
+
+DELTA_CELL = abi.OP_SETCELL  # include/mtr_types.h MTR_DELTA_CELL
+DELTA_RECYCLE = 32           # MTR_DELTA_RECYCLE
+
+
+def _spread8(x: int) -> int:  # x8ToInterlacedX16 (sparsearray2d.ts:13-20)
+    j = x
+    j = (j | (j << 4)) & 0x0F0F
+    j = (j | (j << 2)) & 0x3333
+    j = (j | (j << 1)) & 0x5555
+    return j
+
+
+_SPREAD = [_spread8(i) for i in range(256)]
+
+
+def _spread16(x: int) -> int:  # interlaceBitsX16 of the low 16 bits
+    return (_SPREAD[(x >> 8) & 0xFF] << 16) | _SPREAD[x & 0xFF]
+
+
+def row_bits(row: int) -> int:  # r0ToMorton16
+    return (_spread16(row) << 1) & 0xFFFFFFFF
+
+
+def col_bits(col: int) -> int:  # c0ToMorton16
+    return _spread16(col)
+
+
+def morton(row: int, col: int) -> int:  # r0c0ToMorton2x16
+    return row_bits(row) | col_bits(col)
+
+
+def _bytes(x: int) -> tuple[int, int, int, int]:  # byte0 .. byte3 (most significant first)
+    return (x >> 24) & 0xFF, (x >> 16) & 0xFF, (x >> 8) & 0xFF, x & 0xFF
+
+
+class SparseArray2D:
+    """The reference's cell trie with JavaScript array semantics: ``None`` is ``undefined`` (a hole
+    or a cleared cell; JSON.stringify writes both as ``null``)."""
+
+    def __init__(self, root: list | None = None) -> None:
+        self.root: list = [None] if root is None else root
+
+    @staticmethod
+    def _level(parent: list, key: int) -> list:  # getLevel: allocate a 256-entry level on first use
+        if key >= len(parent):
+            parent.extend([None] * (key + 1 - len(parent)))
+        lv = parent[key]
+        if lv is None:
+            lv = parent[key] = [None] * 256
+        return lv
+
+    def set_cell(self, row: int, col: int, value: Any) -> None:
+        hi = morton(row >> 16, col >> 16)
+        b0, b1, b2, b3 = _bytes(morton(row, col))
+        lv = self._level(self._level(self._level(self._level(self.root, hi), b0), b1), b2)
+        lv[b3] = value
+
+    def get_cell(self, row: int, col: int) -> Any:
+        hi = morton(row >> 16, col >> 16)
+        lv = self.root[hi] if hi < len(self.root) else None
+        for b in _bytes(morton(row, col)):
+            if lv is None:
+                return None
+            lv = lv[b]
+        return lv
+
+    def _clear(self, hi_mask: int, hi_bits: int, lo: int, mask8: int) -> None:
+        """Clear every cell whose key matches `bits` on `mask` (one row: the odd Morton bits, one
+        column: the even ones), walking only allocated levels (clearRows / clearCols)."""
+        b = _bytes(lo)
+        keys = [[k for k in range(256) if (k & mask8) == b[i]] for i in range(4)]
+        for hi, l0 in enumerate(self.root):
+            if l0 is None or (hi & hi_mask) != hi_bits:
+                continue
+            for k0 in keys[0]:
+                l1 = l0[k0]
+                if l1 is None:
+                    continue
+                for k1 in keys[1]:
+                    l2 = l1[k1]
+                    if l2 is None:
+                        continue
+                    for k2 in keys[2]:
+                        l3 = l2[k2]
+                        if l3 is None:
+                            continue
+                        for k3 in keys[3]:
+                            l3[k3] = None
+
+    def clear_rows(self, row_start: int, count: int) -> None:
+        for row in range(row_start, row_start + count):
+            self._clear(0xAAAAAAAA, row_bits(row >> 16), row_bits(row), 0xAA)
+
+    def clear_cols(self, col_start: int, count: int) -> None:
+        for col in range(col_start, col_start + count):
+            self._clear(0x55555555, col_bits(col >> 16), col_bits(col), 0x55)
+
+    def snapshot(self) -> list:
+        return self.root
+
+
+class CellMatrixLog(MatrixLog):
+    """A MatrixLog that also keeps the matrix's cells: every op it packs is flagged MTR_F_DELTA (the
+    engine then reports cell writes and handle recycling for this matrix), and ``resolve`` replays
+    the records of the last batch into the cell store."""
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.cells = SparseArray2D()
+        self.pending = SparseArray2D()  # pending local writes: always empty for an observer
+        self.values: dict[int, Any] = {}
+
+    def message(self, msg: dict, interner: Interner) -> None:
+        lo = len(self.ops)
+        super().message(msg, interner)
+        for k in range(lo, len(self.ops)):
+            rec = self.ops[k]
+            self.ops[k] = (rec[0], rec[1] | abi.F_DELTA) + tuple(rec[2:])
+            if rec[0] == abi.OP_SETCELL:
+                contents = msg["contents"]
+                if isinstance(contents, str):
+                    contents = parse(contents)
+                self.values[k] = contents.get("value")  # `const { value } = contents`
+
+    def resolve(self, rows: np.ndarray, cols: np.ndarray) -> None:
+        """Apply the last batch's records (engine.deltas(rows doc), engine.deltas(cols doc)) in op
+        order; within one op the rows records come first (a vector op touches one vector)."""
+        recs = [(int(r["op"]), 0, i, r) for i, r in enumerate(rows)] + [(int(r["op"]), 1, i, r) for i, r in enumerate(cols)]
+        recs.sort(key=lambda x: (x[0], x[1], x[2]))
+        for op, which, _, r in recs:
+            kind, a, b = int(r["kind"]), int(r["pos"]), int(r["len"])
+            if kind == DELTA_CELL:
+                self.cells.set_cell(a, b, self.values[op])
+            elif kind == DELTA_RECYCLE:
+                if which == 0:
+                    self.cells.clear_rows(a, b)
+                    self.pending.clear_rows(a, b)
+                else:
+                    self.cells.clear_cols(a, b)
+                    self.pending.clear_cols(a, b)
+            else:
+                raise ValueError(f"unexpected matrix record kind {kind}")
+        self.values = {}
+
+    def cells_blob(self) -> bytes:
+        """The ``cells`` blob of SharedMatrix.summarizeCore (matrix.ts:458-462):
+        JSON.stringify([cells.snapshot(), pending.snapshot()])."""
+        return to_utf8(js_stringify([self.cells.snapshot(), self.pending.snapshot()]))
+
+    def load_cells(self, blob: str | bytes) -> None:
+        """SparseArray2D.load of both tries (matrix.ts:621-631; nullToUndefined)."""
+        cells, pending = parse(blob.decode() if isinstance(blob, bytes) else blob)
+        self.cells = SparseArray2D(cells)
+        self.pending = SparseArray2D(pending)

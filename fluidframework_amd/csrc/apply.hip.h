@@ -201,6 +201,7 @@ struct St {
     int htop;  // seq of the LRU heap's top entry (valid while heapn > 0)
     int heap_need;
     int dused;
+    int cur_op;  // index of the op being applied (delta-reporting instantiations only)
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
 
@@ -960,7 +961,10 @@ struct Eng {
     // HandleTable.free of handles a, a+1, ..., a+n-1 in that order (onMaintenance UNLINK frees a
     // segment's handles in ascending order, permutationvector.ts:418-443): handles[a] = old head,
     // handles[a+q] = a+q-1, head = a+n-1
-    static MTR_DI void free_handles(D& L, int a, int n) {
+    static MTR_DI void free_handles(D& L, St& s, int a, int n) {
+        // a matrix tracked for its cells: the host clears the recycled handles' rows / cols
+        // (onRowHandlesRecycled / onColHandlesRecycled, matrix.ts:722-734)
+        if (DL && L.dcap > 0) put_record(L, s, s.cur_op, a, n, MTR_DELTA_RECYCLE);
         const gptr<int32_t> h = handles(L);
         const int head = uni(h[0]);
         for (int q = lane_id(); q < n; q += 64) h[a + q] = q == 0 ? head : a + q - 1;
@@ -1023,7 +1027,7 @@ struct Eng {
                         L.meta[k] = m | M_DEL;  // UNLINK
                         wsync();
                         const uint32_t tk = rdlane(vt, t);
-                        if (PM && tk != uint32_t(MTR_HANDLE_UNALLOCATED)) free_handles(L, int(tk), rdlane(vl, t));
+                        if (PM && tk != uint32_t(MTR_HANDLE_UNALLOCATED)) free_handles(L, s, int(tk), rdlane(vl, t));
                     }
                     prev = -1;
                 } else if (rdlane(vs, t) <= minseq) {
@@ -1130,7 +1134,7 @@ struct Eng {
         if (PM) {  // UNLINK frees the segment's handles, in leaf order
             for (uint64_t um = __ballot(unlink && vt != uint32_t(MTR_HANDLE_UNALLOCATED)); um; um &= um - 1) {
                 const int l = first_lane(um);
-                free_handles(L, int(rdlane(vt, l)), rdlane(vl, l));
+                free_handles(L, s, int(rdlane(vt, l)), rdlane(vl, l));
             }
         }
         const int kept = __popcll(__ballot(in && !pre && !unlink && !link));
@@ -1481,7 +1485,7 @@ struct Eng {
         if (marker) m |= M_MARKER;
         else m |= (nl ? M_NL : 0u) | (nonl ? M_NONL : 0u);
         if (op.flags & MTR_F_NOREF) m |= M_NOREF;
-        if (DL && (op.flags & MTR_F_DELTA)) m |= M_TOUCH;
+        if (DL && !PM && (op.flags & MTR_F_DELTA)) m |= M_TOUCH;
         if (S == 0) {
             s.height = 1;
             m = set_bnd(m, 1);
@@ -1889,6 +1893,22 @@ struct Eng {
     // The ranges of a SequenceDeltaEvent (sequenceDeltaEvent.ts): every M_TOUCH leaf in tree order
     // with its position in the local view (Client.getPosition: removed segments count 0) and its
     // cachedLength; clears the marks.
+    // one mtr_delta record written by lane 0 (wave-uniform bookkeeping)
+    static MTR_DI void put_record(D& L, St& s, int op, int a, int b, uint32_t kind) {
+        if (s.dused >= L.dcap) {
+            s.status = MTR_ERR_CAPACITY;
+            return;
+        }
+        if (lane_id() == 0) {
+            const gptr<uint32_t> r = L.gdelta + 4 * size_t(s.dused);
+            r[0] = uint32_t(op);
+            r[1] = uint32_t(a);
+            r[2] = uint32_t(b);
+            r[3] = kind;
+        }
+        s.dused++;
+    }
+
     static MTR_DI void emit_deltas(D& L, const KParams& P, St& s, int gidx, uint32_t kind) {
         const int S = s.nseg;
         const int ln = lane_id();
@@ -1934,6 +1954,7 @@ struct Eng {
     // (s.status != MTR_OK; s.fail_op = gidx).
     static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
                                 uint32_t pf, int gidx) {
+        if (DL) s.cur_op = gidx;
         if (!G && !P.gen && s.collab && L.lhcap < P.hcap) {  // (record mode never yields: ops are drawn once)
             // LRU pushes this op can make (one per touched leaf block): if the launch's LDS heap
             // could overflow, stop before the op and ask the next launch for a larger heap
@@ -2008,7 +2029,7 @@ struct Eng {
                 split_at(L, s, op.pos1);
                 split_at(L, s, op.pos2);
                 range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload,
-                           DL && (op.flags & MTR_F_DELTA) != 0);
+                           DL && !PM && (op.flags & MTR_F_DELTA) != 0);
                 zop = s.collab;
                 break;
             }
@@ -2028,7 +2049,7 @@ struct Eng {
                 break;
         }
         // mergeTreeDeltaCallback (mergeTree.ts:1414, 1943, 2028) fires before zamboni
-        if (DL && (op.flags & MTR_F_DELTA) && s.status == MTR_OK &&
+        if (DL && !PM && (op.flags & MTR_F_DELTA) && s.status == MTR_OK &&
             (op.type == MTR_OP_INSERT || op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE))
             emit_deltas(L, P, s, gidx, op.type);
         // zamboniSegments after the op (mergeTree.ts:1420-1426, 1948-1952, 2042-2046), then
@@ -2136,7 +2157,7 @@ struct Eng {
     // segment without a handle is split to [pos, pos + 1) (walkSegments with splitRange ->
     // MergeTree.mapRange, mergeTree.ts:2451-2469: `if (start)` skips the split at 0) and that
     // one-position segment gets the next handle (HandleTable.allocate)
-    static MTR_DI void allocated_handle(D& L, const KParams& P, St& s, int pos) {
+    static MTR_DI int allocated_handle(D& L, const KParams& P, St& s, int pos) {
         View v;
         v.ref = s.curseq;
         v.client = uint32_t(s.local);
@@ -2146,17 +2167,20 @@ struct Eng {
             const int i = lower_bound_E(L, s, pos + 1);
             if (i >= s.nseg) {  // "Trying to get handle of out-of-bounds position!"
                 s.status = MTR_ERR_ASSERT | 0x027;
-                return;
+                return -1;
             }
-            if (uniu(L.text[i]) != uint32_t(MTR_HANDLE_UNALLOCATED)) return;  // already has a handle
+            const uint32_t t = uniu(L.text[i]);
+            if (t != uint32_t(MTR_HANDLE_UNALLOCATED))  // already has a handle: segment.start + offset
+                return int(t) + pos - (i > 0 ? (uni(L.E[i - 1]) & EMASK) : 0);
         }
         if (pos) split_at(L, s, pos);
         split_at(L, s, pos + 1);
         const int i = lower_bound_E(L, s, pos + 1);
         const int h = alloc_handle(L, P, s);
-        if (s.status != MTR_OK) return;
+        if (s.status != MTR_OK) return -1;
         L.text[i] = uint32_t(h);
         wsync();
+        return h;
     }
 
     // A matrix pair: the rows vector's op list drives the rows (L0, s0) and cols (L1, s1)
@@ -2192,8 +2216,11 @@ struct Eng {
                 if (r >= 0) {
                     const int c = adjust_position(L1, P, s1, op.pos2, v1);
                     if (c >= 0) {
-                        allocated_handle(L0, P, s0, r);
-                        allocated_handle(L1, P, s1, c);
+                        const int rh = allocated_handle(L0, P, s0, r);
+                        const int ch = allocated_handle(L1, P, s1, c);
+                        // the cell write (cells.setCell(rowHandle, colHandle, value), matrix.ts:686-689)
+                        if (DL && (op.flags & MTR_F_DELTA) && s0.status == MTR_OK && s1.status == MTR_OK)
+                            put_record(L0, s0, cursor + k, rh, ch, MTR_DELTA_CELL);
                     }
                 }
                 if (s0.status != MTR_OK) s0.fail_op = cursor + k;
@@ -2227,12 +2254,12 @@ __global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
 
 // SharedMatrix pairs: one wave applies a matrix's op list to its two PermutationVectors, each with
 // its own LDS region of `pair_region` bytes (HBM-resident arrays in global mode)
-template <bool G>
+template <bool G, bool DL = false>
 __global__ void __launch_bounds__(NT) apply_pair_kernel(KParams P, uint32_t pair_region) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
-    Eng<G, true>::run_pair(smem, pair_region, P, d);
+    Eng<G, true, 0, DL>::run_pair(smem, pair_region, P, d);
 }
 
 }  // namespace mtr

@@ -357,27 +357,45 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
         upload(e, e->client_bytes, b->client_bytes, size_t(b->client_off[ncl - 1])))
         return -1;
     e->h_val_eq.assign(b->val_eq, b->val_eq + b->n_vals);
-    // delta ranges (MTR_F_DELTA): per-document slices sized by an exact bound of this batch's ranges
-    // (an insert reports its one segment; a remove / annotate at most one range per unit of its range
-    // and per segment)
+    // delta records (MTR_F_DELTA): per-document slices sized by an exact bound of this batch's records.
+    // SharedString: an insert reports its one segment; a remove / annotate at most one range per unit
+    // of its range and per segment.  SharedMatrix tracked for its cells (any flagged op): one record
+    // per flagged set-cell, and per vector one per unlinked segment -- at most the segments present
+    // at the batch start plus two per op (split + insert / load)
     e->has_delta = false;
     e->h_doff.assign(size_t(b->n_docs) + 1, 0);
     bool any = false;
     for (uint64_t i = 0; i < b->n_ops && !any; i++) any = (b->ops[i].flags & MTR_F_DELTA) != 0;
-    for (uint32_t d = 0; any && d < b->n_docs; d++) {
-        const mtr_doc_desc& dd = b->docs[d];
-        uint64_t need = 0;
-        // (record mode submits op lists that are only written on the device: n_ops bounds the scan)
-        const uint64_t end = std::min<uint64_t>(dd.op_begin + dd.op_count, b->n_ops);
-        for (uint64_t i = dd.op_begin; i < end; i++) {
-            const mtr_op& op = b->ops[i];
-            if (!(op.flags & MTR_F_DELTA)) continue;
-            if (op.type == MTR_OP_INSERT) need += 1;
-            else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE)
-                need += uint64_t(std::min<int64_t>(std::max<int64_t>(int64_t(op.pos2) - op.pos1, 0),
-                                                   int64_t(e->caps.max_segments)));
+    if (any) {
+        std::vector<uint64_t> need(b->n_docs, 0);
+        for (uint32_t d = 0; d < b->n_docs; d++) {
+            const mtr_doc_desc& dd = b->docs[d];
+            const uint32_t kind = d < e->h_kind.size() ? e->h_kind[d] : 0;
+            if (kind == 2) continue;  // a cols vector: sized with its rows document
+            // (record mode submits op lists that are only written on the device: n_ops bounds the scan)
+            const uint64_t end = std::min<uint64_t>(dd.op_begin + dd.op_count, b->n_ops);
+            bool flagged = false;
+            for (uint64_t i = dd.op_begin; i < end; i++) {
+                const mtr_op& op = b->ops[i];
+                if (!(op.flags & MTR_F_DELTA)) continue;
+                flagged = true;
+                if (kind == 1) {
+                    if (op.type == MTR_OP_SETCELL) need[d] += 1;
+                } else if (op.type == MTR_OP_INSERT) {
+                    need[d] += 1;
+                } else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) {
+                    need[d] += uint64_t(std::min<int64_t>(std::max<int64_t>(int64_t(op.pos2) - op.pos1, 0),
+                                                          int64_t(e->caps.max_segments)));
+                }
+            }
+            if (kind == 1 && flagged) {
+                const uint64_t recycle = uint64_t(e->caps.max_segments) + 2 * uint64_t(dd.op_count);
+                need[d] += recycle;
+                const uint32_t d1 = e->h_part[d];
+                if (d1 < b->n_docs) need[d1] += recycle;
+            }
         }
-        e->h_doff[d + 1] = e->h_doff[d] + need;
+        for (uint32_t d = 0; d < b->n_docs; d++) e->h_doff[d + 1] = e->h_doff[d] + need[d];
     }
     if (e->h_doff[b->n_docs]) {
         e->has_delta = true;
@@ -491,6 +509,10 @@ static int run_impl(mtr_engine* e, int gen) {
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_kernel<false, 0, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_kernel<true, 0, true>,
@@ -569,8 +591,14 @@ static int run_impl(mtr_engine* e, int gen) {
                     return MTR_ERR_UNSUPPORTED;
                 }
                 const uint32_t region = uint32_t(lds / 2);
-                if (P.global_mode) apply_pair_kernel<true><<<cnt, NT, lds, st>>>(P, region);
-                else apply_pair_kernel<false><<<cnt, NT, lds, st>>>(P, region);
+                if (P.doff) {  // a matrix tracked for its cells
+                    if (P.global_mode) apply_pair_kernel<true, true><<<cnt, NT, lds, st>>>(P, region);
+                    else apply_pair_kernel<false, true><<<cnt, NT, lds, st>>>(P, region);
+                } else if (P.global_mode) {
+                    apply_pair_kernel<true><<<cnt, NT, lds, st>>>(P, region);
+                } else {
+                    apply_pair_kernel<false><<<cnt, NT, lds, st>>>(P, region);
+                }
             } else if (P.doff) {  // a batch with MTR_F_DELTA ops: the delta-reporting instantiation
                 if (P.global_mode) apply_kernel<true, 0, true><<<cnt, NT, lds, st>>>(P);
                 else apply_kernel<false, 0, true><<<cnt, NT, lds, st>>>(P);

@@ -66,11 +66,12 @@ int mtr_run(mtr_engine* e);
  * (PermutationVector.summarize, permutationvector.ts:310-325).  Persistent across mtr_reset. */
 int mtr_set_matrix(mtr_engine* e, uint32_t rows_doc, uint32_t cols_doc);
 
-/* The delta ranges (mtr_delta) of the MTR_F_DELTA ops of the last submitted batch for one document,
- * in op order (SequenceDeltaEvent for SharedSegmentSequence's catch-up transformation,
- * sequence.ts:697-736).  Returns the count, or -(count) if cap is too small.  mtr_submit sizes each
- * document's buffer by an exact bound: 1 per flagged insert, min(pos2 - pos1, max_segments) per
- * flagged remove / annotate. */
+/* The delta records (mtr_delta) of the MTR_F_DELTA ops of the last submitted batch for one document,
+ * in op order: for a SharedString the SequenceDeltaEvent ranges SharedSegmentSequence turns into
+ * catch-up ops (sequence.ts:697-736); for a SharedMatrix vector document the MTR_DELTA_CELL /
+ * MTR_DELTA_RECYCLE records of its cell tracking (include/mtr_types.h).  Returns the count, or
+ * -(count) if cap is too small.  mtr_submit sizes each document's buffer by an exact bound (see
+ * mtr_submit in mtr_engine.hip). */
 int64_t mtr_get_deltas(mtr_engine* e, uint32_t doc, mtr_delta* out, int64_t cap);
 
 /* Build every document's summary blobs on the device (Client.summarize). Async except for

@@ -62,6 +62,14 @@ enum {
  * (Client.getPosition) and its cachedLength; ranges come in tree order (SortedSegmentSet by ordinal).
  * kind: MTR_OP_INSERT (the inserted segment), MTR_OP_REMOVE (segments this op removed first),
  * MTR_OP_ANNOTATE (every annotated segment). */
+/* mtr_delta.kind of a SharedMatrix document tracked for its cells (any op of the matrix flagged
+ * MTR_F_DELTA): on the rows document, one MTR_DELTA_CELL record per flagged set-cell that wrote a cell
+ * (pos = row handle, len = col handle; cells.setCell, matrix.ts:686-689); on each vector's document,
+ * one MTR_DELTA_RECYCLE record per segment whose handles zamboni freed (pos = first handle,
+ * len = count; onRowHandlesRecycled / onColHandlesRecycled, matrix.ts:722-734). */
+#define MTR_DELTA_CELL MTR_OP_SETCELL
+#define MTR_DELTA_RECYCLE 32
+
 typedef struct mtr_delta {
     uint32_t op;
     int32_t  pos;

@@ -544,8 +544,11 @@ class Tree {
                     } else {
                         // UNLINK; a PermutationVector frees the segment's handles in order
                         // (onMaintenance, permutationvector.ts:418-443)
-                        if (s->perm && s->start >= 1)
+                        if (s->perm && s->start >= 1) {
+                            if (recycleLog)  // onRowHandlesRecycled / onColHandlesRecycled, matrix.ts:722-734
+                                deltas.push_back({curOpIndex, s->start, s->len, MTR_DELTA_RECYCLE});
                             for (int h = 0; h < s->len; h++) freeHandle(s->start + h);
+                        }
                         s->parent = nullptr;
                     }
                     prev = nullptr;
@@ -725,6 +728,7 @@ class Tree {
     // SequenceDeltaEvent ranges of MTR_F_DELTA ops (sequenceDeltaEvent.ts: position = getPosition
     // at the local view when the delta callback fires, before zamboni; tree order)
     bool deltaOn = false;
+    bool recycleLog = false;  // a matrix vector tracked for its cells (MTR_DELTA_RECYCLE records)
     uint32_t curOpIndex = 0;
     std::vector<mtr_delta> deltas;
     void recordDeltas(const std::vector<Seg*>& segs, uint32_t kind) {
@@ -1167,6 +1171,8 @@ struct oracle_doc {
             const int rh = tree.getAllocatedHandle(r);
             const int ch = cols.getAllocatedHandle(c);
             if (rh < 1 || ch < 1) return MTR_ERR_ASSERT | 0x022;  // "row and/or col handles are invalid"
+            if (op.flags & MTR_F_DELTA)  // cells.setCell(rowHandle, colHandle, value), matrix.ts:686-689
+                tree.deltas.push_back({tree.curOpIndex, rh, ch, MTR_DELTA_CELL});
             return tree.status != MTR_OK ? tree.status : cols.status;
         }
         return (op.flags & MTR_F_COLS) ? cols.apply(op, dd) : tree.apply(op, dd);
@@ -1206,10 +1212,16 @@ int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint
     d->cols.tabs.b = b;
     const mtr_doc_desc& dd = b->docs[doc_index];
     if (op_hi > dd.op_count) op_hi = dd.op_count;
+    if (d->matrix) {  // the engine tracks a matrix's cells in a batch with any flagged op
+        bool any = false;
+        for (uint32_t i = op_lo; i < op_hi; i++) any = any || (b->ops[dd.op_begin + i].flags & MTR_F_DELTA);
+        t.recycleLog = d->cols.recycleLog = any;
+    }
     for (uint32_t i = op_lo; i < op_hi; i++) {
         const mtr_op& op = b->ops[dd.op_begin + i];
         t.curOpIndex = i;
-        t.deltaOn = (op.flags & MTR_F_DELTA) != 0;
+        d->cols.curOpIndex = i;
+        t.deltaOn = !d->matrix && (op.flags & MTR_F_DELTA) != 0;
         int st = d->matrix ? d->applyMatrix(op, dd) : t.apply(op, dd);
         t.deltaOn = false;
         if (st != MTR_OK) return st;
@@ -1218,7 +1230,7 @@ int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint
 }
 
 int64_t oracle_doc_deltas(oracle_doc* d, mtr_delta* out, int64_t cap) {
-    std::vector<mtr_delta>& v = d->tree.deltas;
+    std::vector<mtr_delta>& v = d->view().deltas;
     const int64_t n = int64_t(v.size());
     if (n > cap) return -n;
     if (n) std::memcpy(out, v.data(), size_t(n) * sizeof(mtr_delta));

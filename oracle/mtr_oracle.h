@@ -47,8 +47,9 @@ int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_ind
  * Returns number of leaves (or -(needed) if cap too small); *height = tree height. */
 int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap_leaves, int32_t* height);
 
-/* The SequenceDeltaEvent ranges of the MTR_F_DELTA ops applied since the last call (then cleared),
- * as the engine's mtr_get_deltas reports them.  Returns the count or -(count). */
+/* The delta records of the MTR_F_DELTA ops applied since the last call (then cleared), as the
+ * engine's mtr_get_deltas reports them: SequenceDeltaEvent ranges, or for a matrix the selected
+ * vector's cell / recycle records.  Returns the count or -(count). */
 int64_t oracle_doc_deltas(oracle_doc* d, mtr_delta* out, int64_t cap);
 
 /* Collaboration window state: out[0]=minSeq out[1]=currentSeq out[2]=#heap entries out[3]=#leaves */

@@ -186,3 +186,218 @@ def test_matrix_engine_matches_oracle(writers, lag, ops):
             oe, oh = o.export()
             assert gh == oh and np.array_equal(ge, oe), f"matrix {m} vector {w}: leaves differ"
             assert eng.summary(d) == o.summarize(gb, m), f"matrix {m} vector {w}: summary bytes differ"
+
+
+# ---------------------------------------------------------------- cells
+
+from fluidframework_amd.cells import CellMatrixLog, SparseArray2D, morton  # noqa: E402
+
+
+def _morton_slow(row, col):
+    """Bit-by-bit restatement of r0c0ToMorton2x16 (sparsearray2d.ts:30-31): row bit i -> 2i+1,
+    col bit i -> 2i, of the low 16 bits."""
+    k = 0
+    for i in range(16):
+        k |= ((row >> i) & 1) << (2 * i + 1)
+        k |= ((col >> i) & 1) << (2 * i)
+    return k
+
+
+def test_sparsearray2d_morton_and_layout():
+    for r, c in [(0, 0), (1, 1), (1, 2), (0x1234, 0x5678), (0xFFFF, 0), (70000, 3)]:
+        assert morton(r, c) == _morton_slow(r & 0xFFFF, c & 0xFFFF)
+    a = SparseArray2D()
+    a.set_cell(1, 1, "x")   # key 3
+    a.set_cell(1, 2, "y")   # key 6
+    lvl3 = [None] * 256
+    lvl3[3], lvl3[6] = "x", "y"
+    pad = lambda x: [x] + [None] * 255  # noqa: E731
+    assert a.snapshot() == [pad(pad(pad(lvl3)))]
+    assert a.get_cell(1, 2) == "y" and a.get_cell(2, 1) is None
+    # clearing keeps every allocated level (levels are never freed) and only nulls the cells
+    a.set_cell(300, 5, 7)
+    a.clear_rows(1, 1)
+    assert a.get_cell(1, 1) is None and a.get_cell(1, 2) is None and a.get_cell(300, 5) == 7
+    assert a.snapshot()[0][0][0][0] == [None] * 256
+    a.clear_cols(5, 1)
+    assert a.get_cell(300, 5) is None
+    # a handle above 65535 lands in root[keyHi]: the root array grows with holes (JSON null)
+    b = SparseArray2D()
+    b.set_cell(0x10000, 0, True)
+    assert len(b.snapshot()) == 3 and b.snapshot()[0] is None and b.get_cell(0x10000, 0) is True
+
+
+def _cell_msgs(log, it, msgs):
+    for m in msgs:
+        log.message(m, it)
+
+
+def test_known_answer_cells_blob():
+    """The KAT matrix (test_known_answer_handle_allocation): setCell(1, 1) writes cell (row handle 1,
+    col handle 1) and setCell(1, 0) writes (1, 2) -> keys 3 and 6 of one level chain; no pending
+    writes -> the second trie is [null]."""
+    it = Interner()
+    log = CellMatrixLog()
+    log.start_collab("observer")
+    _cell_msgs(log, it, [
+        _msg(1, 0, "A", {"target": "rows", "type": 0, "pos1": 0, "seg": [3, 7]}),
+        _msg(2, 1, "A", {"target": "cols", "type": 0, "pos1": 0, "seg": [2, 9]}),
+        _msg(3, 2, "B", {"type": 2, "row": 1, "col": 1, "value": "x"}),
+        _msg(4, 2, "B", {"type": 2, "row": 1, "col": 0, "value": {"v": [1, 2.5]}}),
+    ])
+    b = build_batch([log], it)
+    o = _oracle(b)
+    rows, cols = o.select(0).deltas(), o.select(1).deltas()
+    assert [tuple(int(x) for x in r) for r in rows] == [(3, 1, 1, abi.OP_SETCELL), (4, 1, 2, abi.OP_SETCELL)]
+    assert len(cols) == 0
+    log.resolve(rows, cols)
+    lvl3 = ["null"] * 256
+    lvl3[3], lvl3[6] = '"x"', '{"v":[1,2.5]}'
+    pad = lambda x: "[" + ",".join([x] + ["null"] * 255) + "]"  # noqa: E731
+    assert log.cells_blob() == ("[[" + pad(pad(pad("[" + ",".join(lvl3) + "]"))) + "],[null]]").encode()
+
+
+def test_known_answer_recycled_handles_clear_cells():
+    """test_known_answer_recycling_and_coalescing with values: the removed row's handle 3 is freed
+    when the MSN passes its removal (seq 8) -> its cell is cleared; rows 0 and 1 keep theirs."""
+    it = Interner()
+    log = CellMatrixLog()
+    log.start_collab("observer")
+    msgs = [
+        _msg(1, 0, "A", {"target": "rows", "type": 0, "pos1": 0, "seg": [4, -1]}),
+        _msg(2, 1, "A", {"target": "cols", "type": 0, "pos1": 0, "seg": [1, -1]}),
+    ] + [_msg(s, 2, "A", {"type": 2, "row": r, "col": 0, "value": s}) for s, r in ((3, 0), (4, 1), (5, 2))] + [
+        _msg(6, 5, "A", {"target": "rows", "type": 1, "pos1": 2, "pos2": 3}, msn=5),
+        _msg(7, 6, "A", {"target": "rows", "type": 0, "pos1": 3, "seg": [1, -1]}, msn=6),
+    ]
+    _cell_msgs(log, it, msgs)
+    b = build_batch([log], it)
+    o = _oracle(b)
+    log.resolve(o.select(0).deltas(), o.select(1).deltas())
+    assert [log.cells.get_cell(h, 1) for h in (1, 2, 3)] == [3, 4, 5]
+    _cell_msgs(log, it, [_msg(8, 7, "A", {"target": "rows", "type": 0, "pos1": 0, "seg": [1, -1]}, msn=7)])
+    b = build_batch([log], it)
+    assert o.apply(b, 0) == 0
+    rows = o.select(0).deltas()
+    assert [tuple(int(x) for x in r) for r in rows] == [(0, 3, 1, 32)]
+    log.resolve(rows, o.select(1).deltas())
+    assert [log.cells.get_cell(h, 1) for h in (1, 2, 3)] == [3, 4, None]
+
+
+def matrix_messages(batch, doc, rng):
+    """Rebuild a generated matrix's messages (tests only); set-cell values are seeded JSON."""
+    dd = batch.docs[doc]
+    ops = batch.ops[int(dd["op_begin"]): int(dd["op_begin"]) + int(dd["op_count"])]
+    names = ["observer"] + [f"client-{k}" for k in range(1, int(dd["n_clients"]))]
+    msgs, group, observer = [], [], None
+    for op in ops:
+        t = int(op["type"])
+        m = dict(seq=int(op["seq"]), ref=int(op["ref_seq"]), client=names[int(op["client"])], msn=int(op["min_seq"]))
+        if t == abi.OP_START_COLLAB:
+            observer = names[int(op["client"])]
+            continue
+        if t == abi.OP_SETCELL:
+            v = [int(rng.integers(100)), "s%d" % rng.integers(10), {"k": [1, None, "z"]}, None][int(rng.integers(4))]
+            msgs.append(_msg(m["seq"], m["ref"], m["client"],
+                             {"type": 2, "row": int(op["pos1"]), "col": int(op["pos2"]), "value": v}, m["msn"]))
+            continue
+        target = "cols" if op["flags"] & abi.F_COLS else "rows"
+        if t == abi.OP_INSERT:
+            group.append({"pos1": int(op["pos1"]), "seg": [int(op["payload2"]), -1], "type": 0})
+        elif t == abi.OP_REMOVE:
+            group.append({"pos1": int(op["pos1"]), "pos2": int(op["pos2"]), "type": 1})
+        else:
+            raise AssertionError(t)
+        if op["flags"] & abi.F_LAST:
+            c = group[0] if len(group) == 1 else {"ops": group, "type": 3}
+            c = dict(c, target=target) if len(group) == 1 else {"target": target, **c}
+            msgs.append(_msg(m["seq"], m["ref"], m["client"], c, m["msn"]))
+            group = []
+    return observer, msgs
+
+
+def _oracle_cells(observer, msgs, chunk):
+    it = Interner()
+    log = CellMatrixLog()
+    log.start_collab(observer)
+    o = OracleDoc(options(), matrix=True)
+    for k in range(0, len(msgs), chunk):
+        for m in msgs[k:k + chunk]:
+            log.message(m, it)
+        b = build_batch([log], it)
+        assert o.apply(b, 0) == 0
+        log.resolve(o.select(0).deltas(), o.select(1).deltas())
+    return log, o, b
+
+
+@pytest.mark.parametrize("writers,lag", [(8, 16), (16, 64)])
+def test_cells_track_handle_recycling(writers, lag):
+    """Seeded C4-mix matrices: the cell store never holds a value at a freed handle, every live
+    cell's handles are owned by segments, and the oracle's records replayed in one batch or in
+    chunks give the same cells blob."""
+    cfg = matrix_cfg(4, 1500, writers=writers, max_lag=lag)
+    tabs = tables(writers=writers)
+    gb, _, status = generate_matrix(cfg, tabs, 0, 4, threads=4)
+    assert (status == 0).all()
+    n_recycled = 0
+    for d in range(4):
+        observer, msgs = matrix_messages(gb, d, np.random.default_rng(d))
+        whole, o, b = _oracle_cells(observer, msgs, len(msgs))
+        parts, _, _ = _oracle_cells(observer, msgs, 211)
+        assert whole.cells_blob() == parts.cells_blob()
+        owned = []
+        for w in (0, 1):
+            ex, _ = o.select(w).export()
+            owned.append({h for r in ex if r[6] >= 1 for h in range(int(r[6]), int(r[6]) + int(r[0]))})
+        root = whole.cells.snapshot()
+        for k0, l1 in enumerate(root[0]):
+            for k1, l2 in enumerate(l1 or []):
+                for k2, l3 in enumerate(l2 or []):
+                    for k3, v in enumerate(l3 or []):
+                        if v is None:
+                            continue
+                        key = (k0 << 24) | (k1 << 16) | (k2 << 8) | k3
+                        row = sum(((key >> (2 * i + 1)) & 1) << i for i in range(16))
+                        col = sum(((key >> (2 * i)) & 1) << i for i in range(16))
+                        assert row in owned[0] and col in owned[1]
+        n_recycled += whole.cells_blob().count(b"null")
+    assert n_recycled > 0
+
+
+@pytest.mark.gpu
+def test_matrix_cell_records_match_oracle():
+    """Cell tracking on the device: per vector, the engine's MTR_DELTA_CELL / MTR_DELTA_RECYCLE records
+    equal the oracle's, and the cells blobs the two drive are byte-identical."""
+    from fluidframework_amd.batch import matrix_logs
+    from fluidframework_amd.engine import Engine
+
+    n, nops = 32, 2000
+    cfg = matrix_cfg(n, nops, writers=8, max_lag=16)
+    tabs = tables(writers=8)
+    gb, _, status = generate_matrix(cfg, tabs, 0, n, threads=8)
+    assert (status == 0).all()
+    feeds = [matrix_messages(gb, m, np.random.default_rng(m)) for m in range(n)]
+    eng = Engine(2 * n, max_segments=2 * nops + 128, heap_entries=2 * nops + 128, text_units=1 << 15,
+                 prop_words=1024, remover_cells=4096, ops_per_launch=64)
+    for m in range(n):
+        eng.set_matrix(2 * m, 2 * m + 1)
+    it = Interner()
+    logs = []
+    for observer, _ in feeds:
+        lg = CellMatrixLog()
+        lg.start_collab(observer)
+        logs.append(lg)
+    chunk = 617
+    for k in range(0, max(len(f[1]) for f in feeds), chunk):
+        for lg, (_, msgs) in zip(logs, feeds):
+            for msg in msgs[k:k + chunk]:
+                lg.message(msg, it)
+        cols = [lg.cols_log() for lg in logs]
+        b = build_batch([x for pair in zip(logs, cols) for x in pair], it)
+        eng.apply(b)
+        for m, lg in enumerate(logs):
+            assert eng.status(2 * m)[0] == 0 and eng.status(2 * m + 1)[0] == 0
+            lg.resolve(eng.deltas(2 * m), eng.deltas(2 * m + 1))
+    for m, (observer, msgs) in enumerate(feeds):
+        ref, _, _ = _oracle_cells(observer, msgs, chunk)
+        assert logs[m].cells_blob() == ref.cells_blob(), f"matrix {m}: cells blob differs"
