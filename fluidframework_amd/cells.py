@@ -179,3 +179,16 @@ class CellMatrixLog(MatrixLog):
         cells, pending = parse(blob.decode() if isinstance(blob, bytes) else blob)
         self.cells = SparseArray2D(cells)
         self.pending = SparseArray2D(pending)
+
+
+def matrix_summary(engine, rows_doc: int, cols_doc: int, log: CellMatrixLog) -> dict:
+    """SharedMatrix.summarizeCore (matrix.ts:449-464) as a nested {name: bytes | dict} tree:
+    ``rows`` / ``cols`` = PermutationVector.summarize (permutationvector.ts:310-325: the V1
+    ``segments`` tree and the ``handleTable`` blob), ``cells`` = the cell tries.  Call after
+    engine.summarize()."""
+    def vector(doc):
+        blobs = engine.summary(doc)
+        segs = {("header" if i == 0 else f"body_{i - 1}"): b for i, b in enumerate(blobs[:-1])}
+        return {"segments": segs, "handleTable": blobs[-1]}
+
+    return {"rows": vector(rows_doc), "cols": vector(cols_doc), "cells": log.cells_blob()}

@@ -398,6 +398,12 @@ def test_matrix_cell_records_match_oracle():
         for m, lg in enumerate(logs):
             assert eng.status(2 * m)[0] == 0 and eng.status(2 * m + 1)[0] == 0
             lg.resolve(eng.deltas(2 * m), eng.deltas(2 * m + 1))
+    eng.summarize()
+    from fluidframework_amd.cells import matrix_summary
     for m, (observer, msgs) in enumerate(feeds):
-        ref, _, _ = _oracle_cells(observer, msgs, chunk)
+        ref, o, rb = _oracle_cells(observer, msgs, chunk)
         assert logs[m].cells_blob() == ref.cells_blob(), f"matrix {m}: cells blob differs"
+        tree = matrix_summary(eng, 2 * m, 2 * m + 1, logs[m])
+        for w, name in ((0, "rows"), (1, "cols")):
+            blobs = o.select(w).summarize(rb, 0)
+            assert list(tree[name]["segments"].values()) + [tree[name]["handleTable"]] == blobs
