@@ -317,7 +317,7 @@ struct ProfScope {
 // no permutation code; CAP: the launch's LDS leaf capacity as a compile-time constant (0 = runtime),
 // which puts every leaf array at a constant LDS offset (ds_read/ds_write immediate offsets from one
 // per-lane address instead of a base register and an address add per array)
-template <bool G, bool PM = false, int CAP = 0, bool DL = false>
+template <bool G, bool PM = false, int CAP = 0, bool DL = false, bool GN = false>
 struct Eng {
     using D = Doc<G>;
     template <class T>
@@ -863,6 +863,38 @@ struct Eng {
         }
     }
 
+    // Concatenation of a merge chain's texts: chain units [c0, total) go to dst + p, unit p taken
+    // from the piece (a lane in `pieces`, chain offset `off`, arena offset `vt`) that covers it.
+    // Every lane copies units c0 + lane, c0 + lane + 64, ...: the loads of a batch of 8 rounds
+    // are all in flight before its stores (one HBM round trip per 512 units, not per 8 units of
+    // one lane's piece).
+    static MTR_DI void copy_chain(const D& L, uint32_t dst, int c0, int total, uint64_t pieces, uint32_t vt,
+                                  int off) {
+        const int ln = lane_id();
+        for (int b0 = c0; b0 < total; b0 += 8 * 64) {
+            uint16_t u[8];
+            uint32_t src[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) src[q] = NONE32;
+            for (uint64_t pm = pieces; pm; pm &= pm - 1) {  // pieces in chain order: the last start <= p wins
+                const int j = first_lane(pm);
+                const int pj = rdlane(off, j);
+                const uint32_t tj = rdlane(vt, j);
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int pos = b0 + 64 * q + ln;
+                    if (pos >= pj) src[q] = tj + uint32_t(pos - pj);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (b0 + 64 * q + ln < total) u[q] = L.gtext[src[q]];
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (b0 + 64 * q + ln < total) L.gtext[dst + uint32_t(b0 + 64 * q + ln)] = u[q];
+        }
+    }
+
     // prev.append(seg) (textSegment.ts:99-103): text of b follows text of a.  Updates L.len/L.text
     // of a; the caller keeps M_NL.
     static MTR_DI void text_append(D& L, const KParams& P, St& s, int a, int b) {
@@ -1126,7 +1158,10 @@ struct Eng {
         } else {
             link = link && !((vm | pm) & M_MARKER) && !(pm & M_NL);
         }
-        if (link && vp != pp) link = props_match(L.gprop, gp(P.val_eq), pp, vp);
+        if (__ballot(link && vp != pp)) {
+            PROF(P_X1);
+            if (link && vp != pp) link = props_match(L.gprop, gp(P.val_eq), pp, vp);
+        }
         if (!PM && __ballot(link && vl > kGranularity)) return -1;
         const bool unlink = !pre && removed && vr <= minseq;
         const uint64_t lm = __ballot(link);
@@ -1162,6 +1197,7 @@ struct Eng {
                     wsync();
                     continue;
                 }
+                PROF(P_X2);
                 const uint32_t th = rdlane(vt, h);
                 const int lh = rdlane(vl, h);
                 const bool mine = ((mem >> ln) & 1) != 0;
@@ -1175,8 +1211,9 @@ struct Eng {
                         s.status = MTR_ERR_CAPACITY;
                         return kept;
                     }
-                    const bool copy = mine || (!tail && ln == h);
-                    if (copy) copy_units(L, base + uint32_t(off), vt, vl);
+                    // the copied pieces: the members, and the head unless its text already ends
+                    // the arena; all 64 lanes copy the chain's units [c0, total) together
+                    copy_chain(L, base, tail ? lh : 0, total, (tail ? 0 : (uint64_t(1) << h)) | mem, vt, off);
                     s.textused = int(base) + total;
                 }
                 const uint32_t me = rdlane(vm, e), mh = rdlane(vm, h);
@@ -1233,7 +1270,12 @@ struct Eng {
             // surviving leaf may now repeat its block's start marker).
             int cs = rs1, ce = re1;
             for (int l = 2; l <= H; l++) {  // packParent chain
-                const int ps = block_start(L, cs, l), pe = block_end(L, s, ce - 1, l);
+                int ps, pe;
+                {
+                    PROF(P_FETCH);
+                    ps = block_start(L, cs, l);
+                    pe = block_end(L, s, ce - 1, l);
+                }
                 const int top = bnd_of(uniu(L.meta[ps]));
                 cs = ps;
                 ce = pe;
@@ -1242,6 +1284,7 @@ struct Eng {
                     // packParent scours every child of P again -- including the block just
                     // scoured: scourNode is not idempotent (a dropped tombstone no longer resets
                     // the merge candidate), zamboni.ts:68-73,122-193.
+                    PROF(P_SPLIT1);
                     if (pe - ps > 64 || scour_par(L, P, s, ps, pe) < 0) scour_range(L, P, s, ps, pe);
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
@@ -1758,7 +1801,7 @@ struct Eng {
 #ifdef MTR_PROF
             for (int q = 0; q < P_COUNT; q++) L.sc->prof[q] = 0;
 #endif
-            if (P.gen) st_struct(L.gst, ld_struct<mtr_synth_state>(gp(P.gen_state) + d));
+            if (GN) st_struct(L.gst, ld_struct<mtr_synth_state>(gp(P.gen_state) + d));
         }
         if (!G) {  // stage the leaves and the heap into LDS
             const int S = s.nseg;
@@ -1819,7 +1862,7 @@ struct Eng {
             h.heap_need = s.heap_need;
             h.dused = s.dused;
             st_struct(hp, h);
-            if (P.gen) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
+            if (GN) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
 #ifdef MTR_PROF
             for (int q = 0; q < P_COUNT; q++) atomicAdd(&g_prof[q], L.sc->prof[q]);
 #endif
@@ -1870,7 +1913,7 @@ struct Eng {
             L.hseq = (A<int>)(take(4 * size_t(lhcap)));
             L.huid = (A<uint32_t>)(take(4 * size_t(lhcap)));
             L.sc = (lptr<Sc>)(take(sizeof(Sc)));
-            L.gst = (lptr<mtr_synth_state>)(P.gen ? take(sizeof(mtr_synth_state)) : p);
+            L.gst = (lptr<mtr_synth_state>)(GN ? take(sizeof(mtr_synth_state)) : p);
             L.cap = cap;
             L.lhcap = lhcap;
         }
@@ -1955,7 +1998,7 @@ struct Eng {
     static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
                                 uint32_t pf, int gidx) {
         if (DL) s.cur_op = gidx;
-        if (!G && !P.gen && s.collab && L.lhcap < P.hcap) {  // (record mode never yields: ops are drawn once)
+        if (!G && !GN && s.collab && L.lhcap < P.hcap) {  // (record mode never yields: ops are drawn once)
             // LRU pushes this op can make (one per touched leaf block): if the launch's LDS heap
             // could overflow, stop before the op and ask the next launch for a larger heap
             int need = 0;
@@ -2098,7 +2141,7 @@ struct Eng {
         for (int k = 0; k < n_ops; k++) {
             PROF(P_OP);
             mtr_op op;
-            if (P.gen) {
+            if (GN) {
                 gen_op(L, P, s, dd, cursor + k);
                 op = uni_struct(ld_struct<mtr_op>(ops + k));
                 pre = false;
@@ -2240,12 +2283,17 @@ struct Eng {
     }
 };
 
-template <bool G, int CAP = 0, bool DL = false>
-__global__ void __launch_bounds__(NT) apply_kernel(KParams P) {
+// GN: record mode (synthetic workloads, untimed) as its own instantiation, so the replay kernels
+// carry no generator code or generator state
+#ifndef MTR_WPE
+#define MTR_WPE 5
+#endif
+template <bool G, int CAP = 0, bool DL = false, bool GN = false>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MTR_WPE))) apply_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
-    Eng<G, false, CAP, DL>::run(smem, P, d);
+    Eng<G, false, CAP, DL, GN>::run(smem, P, d);
 }
 
 // leaf capacities with a compile-time LDS layout (apply_kernel<false, CAP>); other capacities use

@@ -517,6 +517,10 @@ static int run_impl(mtr_engine* e, int gen) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_kernel<true, 0, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_kernel<false, 0, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_kernel<true, 0, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 #define MTR_CAP_ATTR(C)                                                                                   \
     (void)hipFuncSetAttribute((const void*)apply_kernel<false, C>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                               160 * 1024);
@@ -599,6 +603,9 @@ static int run_impl(mtr_engine* e, int gen) {
                 } else {
                     apply_pair_kernel<false><<<cnt, NT, lds, st>>>(P, region);
                 }
+            } else if (P.gen) {  // record mode: the generating instantiation
+                if (P.global_mode) apply_kernel<true, 0, false, true><<<cnt, NT, lds, st>>>(P);
+                else apply_kernel<false, 0, false, true><<<cnt, NT, lds, st>>>(P);
             } else if (P.doff) {  // a batch with MTR_F_DELTA ops: the delta-reporting instantiation
                 if (P.global_mode) apply_kernel<true, 0, true><<<cnt, NT, lds, st>>>(P);
                 else apply_kernel<false, 0, true><<<cnt, NT, lds, st>>>(P);
