@@ -198,17 +198,18 @@ def test_summarize_load_continue_on_device():
         assert eng.summary(n + d) == orcs[d].summarize(b, n + d)
 
 
-def test_c5_shaped_hbm_resident():
-    """Config C5's shape at test scale: documents pre-grown through a summary load
-    (20k header segments, reloadFromSegments), then 64 writers with lags up to 4096 keeping the MSN
-    far behind (deep collaboration window).  The documents exceed LDS, so the engine runs them
-    HBM-resident (apply_kernel<true>); leaves, tree shape and summary bytes equal the oracle's."""
+@pytest.mark.parametrize("n,grow,ops", [(8, 20000, 2000), (2, 200000, 300)], ids=["20k-segments", "200k-segments"])
+def test_c5_shaped_hbm_resident(n, grow, ops):
+    """Config C5's shape: documents pre-grown through a summary load (20k, and C5's
+    full 200k header segments, reloadFromSegments), then 64 writers with lags up to 4096 keeping the
+    MSN far behind (deep collaboration window).  The documents exceed LDS, so the engine runs them
+    HBM-resident (apply_kernel<true>); leaves, tree shape and summary bytes equal the oracle's.  The
+    full-size case keeps the op count small: each op scans all 200k leaves."""
     import time
 
     from fluidframework_amd.synth import make_cfg, tables
     from oracle.oracle import generate
 
-    n, grow, ops = 8, 20000, 2000
     cfg = make_cfg(n, ops, writers=64, max_lag=4096, text_cap=2 * grow + ops * 18 + 16)
     tabs = tables(writers=64)
     b, _, status = generate(cfg, tabs, 0, n, threads=8, grow=grow)
