@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--ops", type=int, default=None, help="sequenced messages per document (preset)")
     ap.add_argument("--writers", type=int, default=None)
     ap.add_argument("--max-lag", type=int, default=None)
-    ap.add_argument("--ops-per-launch", type=int, default=24)
+    ap.add_argument("--ops-per-launch", type=int, default=48)
     ap.add_argument("--cpu-sample-docs", type=int, default=0,
                     help="default: about 60M messages of documents (~8 s on 16 host threads)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -122,6 +122,8 @@ def main():
     barrier()
 
     st = eng.stats()  # counters of the last step
+    if st["ops"] != n * (ops + 1):  # every document applied its whole log (START_COLLAB + messages)
+        raise SystemExit(f"the step applied {st['ops']} op records, expected {n * (ops + 1)}")
     hashes = eng.hashes(n)
     messages = n * ops
     run_digest = shard.digest(hashes)

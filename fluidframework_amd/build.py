@@ -15,7 +15,8 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 ENGINE_SRC = ["mtr_engine.hip"]
-ENGINE_DEPS = ["apply.hip.h", "summary.hip.h", "mtr_engine.hip"]
+ENGINE_DEPS = ["apply.hip.h", "summary.hip.h", "mtr_engine.hip", "apply_caps.hip"]
+CAP_PARTS = 3  # kCapParts in apply.hip.h
 
 
 def _stale(target, deps):
@@ -30,8 +31,24 @@ def build_engine(force=False, verbose=False, prof=False):
     deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", h)
                                                            for h in ("mtr.h", "mtr_types.h", "mtr_synth.h", "mtr_digest.h")]
     if force or _stale(out, deps):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wno-unused-result"] + (["-DMTR_PROF"] if prof else []) + ["-o", out] + [os.path.join(CSRC, f) for f in ENGINE_SRC]
+        # translation units compiled in parallel (the fixed-capacity kernels in CAP_PARTS parts), then linked
+        flags = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
+            (["-DMTR_PROF"] if prof else [])
+        objdir = os.path.join(HERE, "build_prof" if prof else "build")
+        os.makedirs(objdir, exist_ok=True)
+        units = [(os.path.join(CSRC, f), os.path.join(objdir, f + ".o"), []) for f in ENGINE_SRC]
+        units += [(os.path.join(CSRC, "apply_caps.hip"), os.path.join(objdir, f"apply_caps_{q}.o"), [f"-DMTR_CAP_PART={q}"])
+                  for q in range(CAP_PARTS)]
+        procs = []
+        for src, obj, extra in units:
+            cmd = flags + extra + ["-c", "-o", obj, src]
+            if verbose:
+                print(" ".join(cmd))
+            procs.append(subprocess.Popen(cmd))
+        rcs = [p.wait() for p in procs]
+        if any(rcs):
+            raise subprocess.CalledProcessError(max(rcs), "hipcc")
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + [u[1] for u in units]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -422,13 +422,14 @@ struct Eng {
         const int ln = lane_id();
         int carry = 0;
         for (int base = 0; base < S; base += 64) {
-            // leaf slots up to the next multiple of 64 exist (capacities are multiples of 64):
-            // every lane evaluates, lanes past the last leaf contribute 0 and store harmlessly
+            // every lane evaluates (reads past the last leaf stay inside the LDS allocation);
+            // lanes past the last leaf contribute 0 and store nothing (capacities are multiples
+            // of 32, so the round's top slots may belong to the next array)
             const int i = base + ln;
             const int x0 = vis_len(L, i, v, newlen, s.minseq, i < S);
             const int x = i < S ? x0 : 0;
             const int inc = wave_incl_scan(max(x, 0));
-            L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
+            if (i < S) L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
             carry += rdlane(inc, 63);
         }
         wsync();
@@ -1998,7 +1999,10 @@ struct Eng {
     static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
                                 uint32_t pf, int gidx) {
         if (DL) s.cur_op = gidx;
-        if (!G && !GN && s.collab && L.lhcap < P.hcap) {  // (record mode never yields: ops are drawn once)
+        // (record mode never yields: ops are drawn once; matrix pairs never do: their launches have
+        // room for every op)
+        if (!G && !GN && !PM && s.nseg + 2 >= L.cap && L.cap < P.segcap) return false;  // yield: more leaf room
+        if (!G && !GN && s.collab && L.lhcap < P.hcap) {
             // LRU pushes this op can make (one per touched leaf block): if the launch's LDS heap
             // could overflow, stop before the op and ask the next launch for a larger heap
             int need = 0;
@@ -2296,9 +2300,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MTR_WPE
     Eng<G, false, CAP, DL, GN>::run(smem, P, d);
 }
 
-// leaf capacities with a compile-time LDS layout (apply_kernel<false, CAP>); other capacities use
-// the runtime layout (CAP = 0)
-#define MTR_FIXED_CAPS(X) X(128) X(192) X(256) X(320) X(384) X(448) X(512) X(640) X(768)
+// leaf capacities with a compile-time LDS layout (apply_kernel<false, CAP>, instantiated in
+// apply_caps.hip, kCapParts translation units); other capacities use the runtime layout (CAP = 0)
+constexpr int kCapParts = 3;
+bool launch_fixed_cap_p0(int cap, uint32_t grid, size_t lds, hipStream_t st, const KParams& P);
+bool launch_fixed_cap_p1(int cap, uint32_t grid, size_t lds, hipStream_t st, const KParams& P);
+bool launch_fixed_cap_p2(int cap, uint32_t grid, size_t lds, hipStream_t st, const KParams& P);
+#define MTR_FIXED_CAPS(X) \
+    X(64) X(96) X(128) X(160) X(192) X(224) X(256) X(288) X(320) X(352) X(384) X(416) X(448) X(480) X(512) X(576) X(640) X(768)
 
 // SharedMatrix pairs: one wave applies a matrix's op list to its two PermutationVectors, each with
 // its own LDS region of `pair_region` bytes (HBM-resident arrays in global mode)

@@ -66,6 +66,7 @@ struct DevBuf {
 };
 
 int round64(int x) { return std::max(64, (x + 63) & ~63); }
+int round32(int x) { return std::max(64, (x + 31) & ~31); }
 
 }  // namespace
 
@@ -164,11 +165,10 @@ __global__ void scan_state_kernel(const DocHdr* h, const mtr_doc_desc* docs, uin
 // Classes [kClasses, 2 kClasses) hold matrix pairs (rows vector documents), classed by the larger
 // of the two vectors; they launch apply_pair_kernel with two LDS regions.
 constexpr int kClasses = 64;
-constexpr int kClassLeaves = 64;
 constexpr int kAllClasses = 2 * kClasses;
 __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t n,
                                                       const uint32_t* dkind, const uint32_t* dpart, int32_t* cls,
-                                                      uint32_t* list) {
+                                                      uint32_t* list, int class_leaves) {
     // block-local histogram in LDS, then one global atomic per (block, class): the per-document
     // atomics on a handful of addresses would serialise at the memory side
     __shared__ int lcnt[kAllClasses], lmax[kAllClasses], lheap[kAllClasses], lbase[kAllClasses];
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
                 heapn = max(heapn, max(y.heapn, y.heap_need));
                 base = kClasses;
             }
-            c = base + min(kClasses - 1, nseg / kClassLeaves);
+            c = base + min(kClasses - 1, nseg / class_leaves);
             rank = atomicAdd(&lcnt[c], 1);
             atomicMax(&lmax[c], nseg);
             atomicMax(&lheap[c], heapn);
@@ -521,11 +521,6 @@ static int run_impl(mtr_engine* e, int gen) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_kernel<true, 0, false, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-#define MTR_CAP_ATTR(C)                                                                                   \
-    (void)hipFuncSetAttribute((const void*)apply_kernel<false, C>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                              160 * 1024);
-        MTR_FIXED_CAPS(MTR_CAP_ATTR)
-#undef MTR_CAP_ATTR
         (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
     });
@@ -534,6 +529,17 @@ static int run_impl(mtr_engine* e, int gen) {
         const char* v = std::getenv("MTR_LDS_LIMIT");
         return v ? std::min<size_t>(size_t(std::atoll(v)), 160 * 1024) : size_t(160 * 1024);
     }();
+    // Size classes of `class_leaves` leaves (SharedString classes: LDS sized to the class's largest
+    // document plus `slack` leaves; a document that runs out of room yields before the op and is
+    // classed again next round).  Tuning knobs: MTR_CLASS_LEAVES, MTR_SLACK.
+    static const int class_leaves = [] {
+        const char* v = std::getenv("MTR_CLASS_LEAVES");
+        return v ? std::max(16, std::atoi(v)) : 64;
+    }();
+    static const int slack_env = [] {
+        const char* v = std::getenv("MTR_SLACK");
+        return v ? std::max(0, std::atoi(v)) : -1;
+    }();
     const size_t ncls = 1 + 3 * kAllClasses;
     if (e->cls.ensure(ncls) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
     if (!e->h_cls) HIPCHK(hipHostMalloc((void**)&e->h_cls, ncls * sizeof(int32_t), hipHostMallocDefault));
@@ -541,7 +547,7 @@ static int run_impl(mtr_engine* e, int gen) {
     for (;;) {
         HIPCHK(hipMemsetAsync(e->cls.p, 0, ncls * sizeof(int32_t), e->stream));
         classify_kernel<<<(e->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, e->n_docs, e->dkind.p,
-                                                                           e->dpart.p, e->cls.p, e->dlist.p);
+                                                                           e->dpart.p, e->cls.p, e->dlist.p, class_leaves);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(cls, e->cls.p, ncls * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
@@ -555,11 +561,17 @@ static int run_impl(mtr_engine* e, int gen) {
             const bool pair = c >= kClasses;              // SharedString classes, largest documents first
             const int cnt = cls[1 + 3 * c], maxseg = cls[2 + 3 * c], maxheap = cls[3 + 3 * c];
             if (cnt <= 0) continue;
-            int cap = round64(maxseg + 2 * k + 8);
+            // replay launches of SharedString documents yield when their leaves or LRU heap could
+            // overflow the launch's LDS, so they get `slack` leaves of room; matrix pairs (setCell
+            // splits) and record mode (ops drawn once) keep room for every op of the launch
+            const bool tight = !pair && !P.gen;
+            const int slack = slack_env >= 0 ? slack_env : 8;
+            int cap = tight ? round32(maxseg + slack + 8) : round64(maxseg + 2 * k + 8);
             if (cap > P.segcap) cap = P.segcap;
             // LRU heap: what the class holds now plus room for this launch's pushes; a document that
             // could overflow it stops before the op and asks for more (DocHdr.heap_need)
-            int lhcap = std::min<int>(P.hcap, std::max(cap / 8, round64(maxheap + 2 * k + 8)));
+            int lhcap = std::min<int>(P.hcap, std::max(cap / 8, tight ? round32(maxheap + slack + 8)
+                                                                       : round64(maxheap + 2 * k + 8)));
             size_t lds = lds_bytes(cap, lhcap, P.gen != 0);
             if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             P.global_mode = 0;
@@ -573,8 +585,8 @@ static int run_impl(mtr_engine* e, int gen) {
                 lds = lds_bytes_global_mode();
                 if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             }
-            const int kk = std::max(1, std::min(k, (cap - maxseg - 8) / 2));
-            if (cap - maxseg - 8 < 2) stuck = true;
+            const int kk = tight && !P.global_mode ? k : std::max(1, std::min(k, (cap - maxseg - 8) / 2));
+            if (cap - maxseg - 8 < 2 && cap >= P.segcap) stuck = true;  // no room and no larger LDS class
             P.cap = cap;
             P.lhcap = lhcap;
             P.ops_this_launch = kk;
@@ -612,16 +624,10 @@ static int run_impl(mtr_engine* e, int gen) {
             } else if (P.global_mode) {
                 apply_kernel<true><<<cnt, NT, lds, st>>>(P);
             } else {
-                switch (cap) {
-#define MTR_CAP_CASE(C)                                     \
-    case C:                                                 \
-        apply_kernel<false, C><<<cnt, NT, lds, st>>>(P);    \
-        break;
-                    MTR_FIXED_CAPS(MTR_CAP_CASE)
-#undef MTR_CAP_CASE
-                    default:
-                        apply_kernel<false><<<cnt, NT, lds, st>>>(P);
-                }
+                if (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
+                    !launch_fixed_cap_p1(cap, uint32_t(cnt), lds, st, P) &&
+                    !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P))
+                    apply_kernel<false><<<cnt, NT, lds, st>>>(P);
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e->kev[2 * nl + 1], st));
@@ -644,7 +650,7 @@ static int run_impl(mtr_engine* e, int gen) {
         }
         if (stuck) {
             set_err("document exceeds the leaf capacity");
-            break;
+            return MTR_ERR_CAPACITY;
         }
     }
     e->summarized = false;
