@@ -59,14 +59,18 @@ template <bool W>
 struct LW {
     gptr<uint8_t> p;  // document output base (write pass)
     int64_t n;        // position
+    // a long text body written by the whole wave (wave_body): skip > = 0 leaves that many bytes
+    // for it and records where it starts
+    int64_t skip = -1;
+    int64_t body_at = -1;
     MTR_DI void put(uint32_t c) {
         if (W) p[n] = uint8_t(c);
         n++;
     }
     template <size_t N>
     MTR_DI void lit(const char (&s)[N]) {
-        if (W) {
-#pragma unroll
+        if (W) {  // a rolled loop: unrolled, every literal's stores held their addresses in VGPRs
+#pragma unroll 1
             for (size_t i = 0; i + 1 < N; i++) p[n + int64_t(i)] = uint8_t(s[i]);
         }
         n += int64_t(N - 1);
@@ -325,10 +329,15 @@ MTR_DI void w_segjson(LW<W>& w, const SDoc& D, const SParams& P, int s, int e) {
     }
     if (pr != NONE32) w.lit("{\"text\":");
     w.put('"');
-    int hi = -1;
-    for (int k = s; k < e; k++)
-        if (k == s || D.kind[k] == 1) w_units(w, D, D.text[k], int(D.len[k]), hi);
-    w.flush_hi(hi);
+    if (w.skip >= 0) {  // the body is the wave's (wave_body)
+        w.body_at = w.n;
+        w.n += w.skip;
+    } else {
+        int hi = -1;
+        for (int k = s; k < e; k++)
+            if (k == s || D.kind[k] == 1) w_units(w, D, D.text[k], int(D.len[k]), hi);
+        w.flush_hi(hi);
+    }
     w.put('"');
     if (pr != NONE32) {
         w.lit(",\"props\":");
@@ -379,6 +388,76 @@ MTR_DI void w_spec(LW<W>& w, const SDoc& D, const SParams& P, const mtr_doc_desc
         w.put(']');
     }
     w.put('}');
+}
+
+// ------------------------------------------------------------------ wave-parallel text bodies
+// JSON.stringify bytes of one UTF-16 unit c of a string body given its neighbours in the body
+// (NOU = none): the greedy surrogate pairing of LW::unit is local -- a low surrogate pairs iff the
+// unit before it is a high surrogate, a high one iff the unit after it is a low surrogate.
+constexpr uint32_t NOU = 0xffffffffu;
+MTR_DI bool is_hi(uint32_t u) { return u >= 0xD800 && u <= 0xDBFF; }
+MTR_DI bool is_lo(uint32_t u) { return u >= 0xDC00 && u <= 0xDFFF; }
+MTR_DI int unit_bytes(uint32_t p, uint32_t c, uint32_t n) {
+    if (c >= 0x20 && c < 0x80) return (c == '"' || c == '\\') ? 2 : 1;
+    if (c < 0x20) return (c == '\b' || c == '\f' || c == '\n' || c == '\r' || c == '\t') ? 2 : 6;
+    if (is_lo(c)) return (p != NOU && is_hi(p)) ? 0 : 6;
+    if (is_hi(c)) return (n != NOU && is_lo(n)) ? 4 : 6;
+    return c < 0x800 ? 2 : 3;
+}
+MTR_DI void unit_write(gptr<uint8_t> o, uint32_t p, uint32_t c, uint32_t n) {
+    LW<true> w{o, 0};
+    if (is_lo(c) && p != NOU && is_hi(p)) return;
+    if (is_hi(c) && n != NOU && is_lo(n)) {
+        w.utf8(0x10000 + ((c - 0xD800) << 10) + (n - 0xDC00));
+        return;
+    }
+    if (is_hi(c) || is_lo(c)) {
+        w.hex4(c);
+        return;
+    }
+    int hi = -1;
+    w.unit(c, hi);
+}
+// the body of spec [s, e) (pieces: leaf s and the kind-1 leaves after it, concatenated) by all
+// 64 lanes, one unit per lane per round: byte counts, a wave scan for offsets, then each lane
+// writes its unit (W).  Returns the body's byte count.
+template <bool W>
+MTR_DI int64_t wave_body(const SDoc& D, int s, int e, gptr<uint8_t> out) {
+    const int ln = lane_id();
+    int64_t nb = 0;
+    uint32_t prev = NOU;  // last unit of the previous non-empty piece
+    for (int k = s; k < e; k++) {
+        if (k != s && D.kind[k] != 1) continue;
+        const int L = int(uniu(D.len[k]));
+        if (L <= 0) continue;
+        const uint32_t t = uniu(D.text[k]);
+        uint32_t after = NOU;  // first unit of the next non-empty piece
+        for (int k2 = k + 1; k2 < e; k2++)
+            if (D.kind[k2] == 1 && uni(int(D.len[k2])) > 0) {
+                after = uniu(uint32_t(D.gtext[uniu(D.text[k2])]));
+                break;
+            }
+        for (int u0 = 0; u0 < L; u0 += 64) {
+            const int i = u0 + ln;
+            const bool in = i < L;
+            const uint32_t c = in ? uint32_t(D.gtext[t + uint32_t(i)]) : NOU;
+            uint32_t pu = uint32_t(__shfl(int(c), max(ln - 1, 0)));
+            if (ln == 0) pu = u0 == 0 ? prev : uint32_t(D.gtext[t + uint32_t(u0 - 1)]);
+            uint32_t nu = uint32_t(__shfl(int(c), min(ln + 1, 63)));
+            if (i + 1 >= L) nu = after;
+            else if (ln == 63) nu = uint32_t(D.gtext[t + uint32_t(i + 1)]);
+            const int b = in ? unit_bytes(pu, c, nu) : 0;
+            const int incl = wave_incl_scan(b);
+            if (W && in && b) unit_write(out + (nb + incl - b), pu, c, nu);
+            nb += rdlane(incl, 63);
+        }
+        prev = uniu(uint32_t(D.gtext[t + uint32_t(L - 1)]));
+    }
+    return nb;
+}
+// a spec whose body the wave writes: a text segment (not a marker) longer than one round
+MTR_DI bool long_body(const SDoc& D, int s, uint32_t slen) {
+    return !D.perm && slen > 64u && !(D.meta[s] & M_MARKER);
 }
 
 // blob wrappers.  V1: snapshotV1.ts:122-178 + serializeAsMaxSupportedVersion; legacy:
@@ -568,9 +647,18 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
                     if (k == s || D.kind[k] == 1) length += int(D.len[k]);
             }
             LW<false> w{(gptr<uint8_t>)nullptr, 0};
+            if (long_body(D, s, uint32_t(length))) w.skip = 0;  // counted by the wave below
             w_spec(w, D, P, dd, s, e);
             D.slen[g] = uint32_t(length);
             D.sbytes[g] = uint32_t(w.n);
+        }
+        wsync();
+        const bool lb = g < nspec && long_body(D, int(D.start[g]), D.slen[g]);
+        for (uint64_t lm = __ballot(lb); lm; lm &= lm - 1) {  // long bodies: all lanes on one spec
+            const int l = first_lane(lm);
+            const int s = int(uniu(D.start[g0 + l])), e = int(uniu(D.start[g0 + l + 1]));
+            const int64_t nb = wave_body<false>(D, s, e, (gptr<uint8_t>)nullptr);
+            if (ln == l) D.sbytes[g] += uint32_t(nb);
         }
     }
     wsync();
@@ -712,11 +800,26 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
             const bool act = g < bs + bc;
             const int x = act ? int(D.sbytes[g]) + (g > bs ? 1 : 0) : 0;
             const int incl = wave_incl_scan(x);
+            int64_t body_at = -1;
             if (act) {
                 LW<true> w{base, pos + incl - x};
                 if (g > bs) w.put(',');
                 const int s = int(D.start[g]), e = int(D.start[g + 1]);
+                if (long_body(D, s, D.slen[g])) {  // lay out around the body, which the wave writes
+                    LW<false> c{(gptr<uint8_t>)nullptr, 0};
+                    c.skip = 0;
+                    w_spec(c, D, P, dd, s, e);
+                    w.skip = int64_t(D.sbytes[g]) - c.n;
+                }
                 w_spec(w, D, P, dd, s, e);
+                body_at = w.body_at;
+            }
+            wsync();
+            for (uint64_t lm = __ballot(body_at >= 0); lm; lm &= lm - 1) {
+                const int l = first_lane(lm);
+                const int s = int(uniu(D.start[g0 + l])), e = int(uniu(D.start[g0 + l + 1]));
+                const uint32_t lo = uint32_t(rdlane(uint32_t(body_at), l)), hi = uint32_t(rdlane(uint32_t(body_at >> 32), l));
+                wave_body<true>(D, s, e, base + int64_t((uint64_t(hi) << 32) | lo));
             }
             pos += rdlane(incl, 63);
         }
@@ -774,13 +877,16 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
     if (ln == 0) P.out_hash[d] = hsh;
 }
 
+#ifndef MTR_SWPE
+#define MTR_SWPE 8
+#endif
 __global__ void __launch_bounds__(64) summary_size_kernel(SParams P) {
     const uint32_t d = blockIdx.x;
     if (d >= P.n_docs) return;
     summary_size_doc(P, d);
 }
 
-__global__ void __launch_bounds__(64) summary_write_kernel(SParams P) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTR_SWPE))) summary_write_kernel(SParams P) {
     const uint32_t d = blockIdx.x;
     if (d >= P.n_docs) return;
     summary_write_doc(P, d);
