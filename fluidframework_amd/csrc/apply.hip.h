@@ -176,6 +176,7 @@ struct KParams {
     mtr_synth_state* gen_state;  // [doc]
     mtr_op* gen_ops;             // == ops, writable
     uint16_t* gen_text;          // == btext, writable
+    unsigned long long* prof;    // [P_COUNT] phase-timer sums (-DMTR_PROF builds)
 };
 
 // phase-timer slots (-DMTR_PROF builds)
@@ -293,7 +294,6 @@ __host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
 // Phase timers (builds with -DMTR_PROF only): lane-0 clock cycles per phase, summed over
 // documents into g_prof (mtr_profile()).
 #ifdef MTR_PROF
-__device__ unsigned long long g_prof[P_COUNT];
 struct ProfScope {
     lptr<Sc> sc;
     int id;
@@ -615,8 +615,8 @@ struct Eng {
         int k = ++s.heapn;
         while (k > 1) {
             const int ps = uni(L.hseq[k >> 1]);
+            const uint32_t pu = uniu(L.huid[k >> 1]);  // loaded with the seq: one round per level
             if (!(ps - sq > 0)) break;
-            const uint32_t pu = uniu(L.huid[k >> 1]);
             L.hseq[k] = ps;
             L.huid[k] = pu;
             k >>= 1;
@@ -638,19 +638,21 @@ struct Eng {
         int k = 1;
         s.htop = ls;
         while ((k << 1) <= n) {
+            // both children's (seq, uid) in one round of loads (slot n + 1 may be stale: unused)
             int j = k << 1;
             int sj = uni(L.hseq[j]);
-            if (j < n) {
-                const int sj1 = uni(L.hseq[j + 1]);
-                if (sj - sj1 > 0) {
-                    j++;
-                    sj = sj1;
-                }
+            const int sj1 = uni(L.hseq[j + 1]);
+            uint32_t uj = uniu(L.huid[j]);
+            const uint32_t uj1 = uniu(L.huid[j + 1]);
+            if (j < n && sj - sj1 > 0) {
+                j++;
+                sj = sj1;
+                uj = uj1;
             }
             if (ls - sj <= 0) break;
             if (k == 1) s.htop = sj;
             L.hseq[k] = sj;
-            L.huid[k] = uniu(L.huid[j]);
+            L.huid[k] = uj;
             k = j;
         }
         L.hseq[k] = ls;
@@ -1865,7 +1867,9 @@ struct Eng {
             st_struct(hp, h);
             if (GN) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
 #ifdef MTR_PROF
-            for (int q = 0; q < P_COUNT; q++) atomicAdd(&g_prof[q], L.sc->prof[q]);
+            // (a buffer, not a __device__ symbol: the kernels live in several code objects)
+            if (P.prof)
+                for (int q = 0; q < P_COUNT; q++) atomicAdd(&P.prof[q], L.sc->prof[q]);
 #endif
             if (s.ops_done) {  // this document's counters (no cross-document atomics)
                 const gptr<unsigned long long> st = gp(P.stat_ops) + size_t(d) * 4;

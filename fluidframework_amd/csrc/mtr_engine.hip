@@ -102,6 +102,7 @@ struct mtr_engine {
     std::vector<uint64_t> h_doff;
     bool has_delta = false;
     DevBuf<int32_t> red;              // small reduction buffer
+    DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
     DevBuf<uint32_t> dlist;           // [class][n_docs] document lists of one apply round
     int32_t* h_cls = nullptr;         // pinned host copy of cls
@@ -493,6 +494,13 @@ static int run_impl(mtr_engine* e, int gen) {
     P.dkind = e->dkind.p;
     P.dpart = e->dpart.p;
     P.gen = gen;
+#ifdef MTR_PROF
+    if (!e->prof.p) {
+        if (e->prof.ensure(32)) return -1;
+        HIPCHK(hipMemset(e->prof.p, 0, 32 * sizeof(unsigned long long)));
+    }
+    P.prof = e->prof.p;
+#endif
     if (gen) {
         P.gen_cfg = e->gcfg;
         P.gen_state = e->gstate.p;
@@ -1005,11 +1013,11 @@ int mtr_profile(mtr_engine* e, uint64_t* out, int32_t n, int32_t reset) {
     unsigned long long v[32] = {0};
 #ifdef MTR_PROF
     if (hipStreamSynchronize(e->stream) != hipSuccess) return MTR_ERR_ASSERT;
-    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(mtr::g_prof), sizeof(v)) != hipSuccess) return MTR_ERR_ASSERT;
-    if (reset) {
-        unsigned long long z[32] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(mtr::g_prof), z, sizeof(z)) != hipSuccess) return MTR_ERR_ASSERT;
+    if (!e->prof.p) {
+        if (e->prof.ensure(32) || hipMemset(e->prof.p, 0, sizeof(v)) != hipSuccess) return MTR_ERR_ASSERT;
     }
+    if (hipMemcpy(v, e->prof.p, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return MTR_ERR_ASSERT;
+    if (reset && hipMemset(e->prof.p, 0, sizeof(v)) != hipSuccess) return MTR_ERR_ASSERT;
 #else
     (void)reset;
 #endif
