@@ -32,7 +32,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: chip-level para
 PRESETS = {
     "C2": dict(docs=10_000, ops=5_000, writers=16, max_lag=64),
     "C3": dict(docs=100_000, ops=1_000, writers=8, max_lag=32),
+    # SharedMatrix replay: docs = matrices (two PermutationVector documents each), 20 % row/col
+    # splices (insert 12 : remove 8) and 80 % setCell
+    "C4": dict(docs=1_000, ops=20_000, writers=8, max_lag=64),
 }
+MATRIX = {"C4"}
 
 
 def parse():
@@ -78,15 +82,26 @@ def main():
     from fluidframework_amd.synth import make_cfg, tables
 
     n, ops = a.docs, a.ops
+    matrix = a.config in MATRIX
     tabs = tables(writers=a.writers)
     doc_lo, _ = shard.doc_range(rank, world, n)
-    cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=doc_lo)
-    text_units = 2 * int(cfg.text_cap) + 1024
-    eng = Engine(n, device=local, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=text_units,
-                 prop_words=16384, remover_cells=4096, ops_per_launch=a.ops_per_launch)
+    if matrix:
+        cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, weights=(12, 8, 80), max_text=4, max_range=3,
+                       doc_base=doc_lo, text_cap=0)
+        # handle tables live in the text arena of a vector document (<= positions ever inserted)
+        eng = Engine(2 * n, device=local, max_segments=2 * ops + 128, heap_entries=2 * ops + 128,
+                     text_units=2 * ops + 1024, prop_words=1024, remover_cells=8192, ops_per_launch=a.ops_per_launch)
+    else:
+        cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=doc_lo)
+        text_units = 2 * int(cfg.text_cap) + 1024
+        eng = Engine(n, device=local, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=text_units,
+                     prop_words=16384, remover_cells=4096, ops_per_launch=a.ops_per_launch)
 
     t0 = time.time()
-    eng.generate(cfg, tabs)  # untimed: record the op logs on the device
+    if matrix:  # untimed: record the op logs on the device
+        eng.generate_matrix(cfg, tabs)
+    else:
+        eng.generate(cfg, tabs)
     gen_s = time.time() - t0
     gen_stats = eng.stats()
     if gen_stats["bad_docs"]:
@@ -124,7 +139,7 @@ def main():
     st = eng.stats()  # counters of the last step
     if st["ops"] != n * (ops + 1):  # every document applied its whole log (START_COLLAB + messages)
         raise SystemExit(f"the step applied {st['ops']} op records, expected {n * (ops + 1)}")
-    hashes = eng.hashes(n)
+    hashes = eng.hashes(2 * n if matrix else n)
     messages = n * ops
     run_digest = shard.digest(hashes)
     if dist is not None:  # the only collective: counters + summary digests over RCCL/xGMI
@@ -156,7 +171,7 @@ def main():
             traffic = None
     roofline = {
         "bound": "hbm",
-        "kernel": "mtr::apply_kernel",
+        "kernel": "mtr::apply_pair_kernel" if matrix else "mtr::apply_kernel",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -169,26 +184,32 @@ def main():
         "note": "achieved = algorithmic bytes of a step / apply wall time of the step; a round's size-class "
                 "launches overlap on 4 streams, so avg_launch_ms (each launch's own HIP-event duration, "
                 "comparable to rocprof) x launches exceeds the wall time",
-        "model": "B_op = 16*S_d(t) + 32 + 2*L_ins (SURVEY.md 8d)",
+        "model": "B_op = 16*S_d(t) + 32 + 2*L_ins (SURVEY.md 8d)" + (
+            "; setCell: S_d = leaves of both vectors (two position resolutions)" if matrix else ""),
     }
 
     cpu = None
     bit_exact = {"checked_docs": 0, "equal": 0}
     if not a.no_cpu_baseline and world == 1:
-        from oracle.oracle import replay_batch
+        from oracle.oracle import replay_batch, replay_matrix_batch
 
         k = min(a.cpu_sample_docs or max(1, 60_000_000 // ops), n)
-        sample = eng.download(0, k)
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        secs, ohash, ost = replay_batch(sample, 0, k, threads)
-        eq = int((ohash == hashes[:k]).sum())
+        if matrix:  # a matrix is equal when both of its vectors' summaries are
+            sample = eng.download_matrix(0, k)
+            secs, ohash, ost = replay_matrix_batch(sample, 0, k, threads)
+            eq = int((ohash == hashes[:2 * k]).reshape(k, 2).all(axis=1).sum())
+        else:
+            sample = eng.download(0, k)
+            secs, ohash, ost = replay_batch(sample, 0, k, threads)
+            eq = int((ohash == hashes[:k]).sum())
         bit_exact = {"checked_docs": k, "equal": eq, "oracle_errors": int((ost != 0).sum())}
         cpu = {
             "value": round(k * ops / secs, 1),
             "unit": "ops/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"first {k} of the {n} documents ({k * ops} messages), replay + V1 summary, one document "
+            "sample": f"first {k} of the {n} {'matrices' if matrix else 'documents'} ({k * ops} messages), replay + V1 summary, one document "
                       f"per task on {threads} host threads (reference-algorithm C++ restatement, not Node)",
             "seconds": round(secs, 3),
         }
@@ -206,7 +227,10 @@ def main():
         "dtype": "int32",
         "data": "synthetic: seeded recipe include/mtr_synth.h recorded on the device (record mode)",
         "config": {
-            "workload": f"{a.config}: {n} docs/GPU x {ops} ops, {a.writers} writers, lag<={a.max_lag}, V1 summaries",
+            "workload": (f"{a.config}: {n} SharedMatrix docs/GPU (2 PermutationVectors each) x {ops} ops, 20% row/col "
+                         f"splices + 80% setCell, {a.writers} writers, lag<={a.max_lag}, V1 segments + handleTable"
+                         if matrix else
+                         f"{a.config}: {n} docs/GPU x {ops} ops, {a.writers} writers, lag<={a.max_lag}, V1 summaries"),
             "docs_per_gpu": n,
             "ops_per_doc": ops,
             "writers": a.writers,

@@ -2234,6 +2234,48 @@ struct Eng {
         return h;
     }
 
+    // record mode for a matrix pair: draw op `idx` from the SharedMatrix recipe
+    // (mtr_synth_matrix_finish) with the writer's exact view lengths of both vectors -- the same
+    // lengths the oracle's generator takes from nodeLength(root, refSeq, clientId)
+    static MTR_DI void gen_pair_op(D& L0, D& L1, const KParams& P, St& s0, St& s1, const mtr_doc_desc& dd, int idx) {
+        const gptr<mtr_op> rec = gp(P.gen_ops) + dd.op_begin + idx;
+        if (idx == 0) {
+            if (threadIdx.x == 0) {
+                mtr_op z{};
+                z.type = MTR_OP_START_COLLAB;
+                st_struct(rec, z);
+            }
+            wsync();
+            return;
+        }
+        if (threadIdx.x == 0) {
+            mtr_op op;
+            mtr_synth_state st = ld_struct<mtr_synth_state>(L0.gst);
+            mtr_synth_begin(&P.gen_cfg, &st, idx, &op);
+            st_struct(L0.gst, st);
+            L0.sc->gen_ref = op.ref_seq;
+            L0.sc->gen_client = op.client;
+            st_struct(rec, op);
+        }
+        wsync();
+        View v;
+        v.ref = uni(L0.sc->gen_ref);
+        v.client = enc_client(uni(L0.sc->gen_client));
+        v.local = 0;
+        prefix(L0, s0, v, P.new_length_calc);
+        const int lr = s0.nseg > 0 ? (uni(L0.E[s0.nseg - 1]) & EMASK) : 0;
+        prefix(L1, s1, v, P.new_length_calc);
+        const int lc = s1.nseg > 0 ? (uni(L1.E[s1.nseg - 1]) & EMASK) : 0;
+        if (threadIdx.x == 0) {
+            mtr_op op = ld_struct<mtr_op>(rec);
+            mtr_synth_state st = ld_struct<mtr_synth_state>(L0.gst);
+            mtr_synth_matrix_finish(&P.gen_cfg, &st, lr, lc, &op);
+            st_struct(L0.gst, st);
+            st_struct(rec, op);
+        }
+        wsync();
+    }
+
     // A matrix pair: the rows vector's op list drives the rows (L0, s0) and cols (L1, s1)
     // PermutationVectors (SharedMatrix.processCore, matrix.ts:636-693, remote branch).
     static MTR_DI void run_pair(char* smem, size_t region, const KParams& P, uint32_t d) {
@@ -2251,11 +2293,13 @@ struct Eng {
         s1.ops_done = 0;
         const gptr<const mtr_op> ops = gp(P.ops) + dd.op_begin + cursor;
         for (int k = 0; k < n_ops; k++) {
+            if (GN) gen_pair_op(L0, L1, P, s0, s1, dd, cursor + k);
             const mtr_op op = uni_struct(ld_struct<mtr_op>(ops + k));
             bool ok = true;
             if (op.type == MTR_OP_START_COLLAB) {  // didAttach / onConnect start both vectors (matrix.ts:514-532)
                 ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k) && apply_op(L1, P, s1, op, dd, false, 0, cursor + k);
             } else if (op.type == MTR_OP_SETCELL) {
+                s0.sum_s += (unsigned long long)(s0.nseg + s1.nseg);  // both vectors are resolved
                 View v;
                 v.ref = op.ref_seq;
                 v.client = enc_client(int(int16_t(op.client)));
@@ -2285,6 +2329,8 @@ struct Eng {
             if (!ok) break;
             s0.ops_done = k + 1;
         }
+        s0.sum_s += s1.sum_s;  // the matrix's counters are kept with its rows document
+        s1.sum_s = 0;
         store_doc(L0, P, s0, d);
         s1.ops_done = 0;  // the cols vector's op cursor stays at 0 (it has no op list of its own)
         store_doc(L1, P, s1, d1);
@@ -2315,12 +2361,12 @@ bool launch_fixed_cap_p2(int cap, uint32_t grid, size_t lds, hipStream_t st, con
 
 // SharedMatrix pairs: one wave applies a matrix's op list to its two PermutationVectors, each with
 // its own LDS region of `pair_region` bytes (HBM-resident arrays in global mode)
-template <bool G, bool DL = false>
+template <bool G, bool DL = false, bool GN = false>
 __global__ void __launch_bounds__(NT) apply_pair_kernel(KParams P, uint32_t pair_region) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
-    Eng<G, true, 0, DL>::run_pair(smem, pair_region, P, d);
+    Eng<G, true, 0, DL, GN>::run_pair(smem, pair_region, P, d);
 }
 
 }  // namespace mtr

@@ -531,6 +531,10 @@ static int run_impl(mtr_engine* e, int gen) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     });
     // documents whose class needs more LDS than this stay HBM-resident (MTR_LDS_LIMIT, bytes; tuning knob)
     static const size_t lds_limit = [] {
@@ -610,12 +614,11 @@ static int run_impl(mtr_engine* e, int gen) {
             }
             HIPCHK(hipEventRecord(e->kev[2 * nl], st));
             if (pair) {
-                if (P.gen) {
-                    set_err("record mode does not generate matrix documents");
-                    return MTR_ERR_UNSUPPORTED;
-                }
                 const uint32_t region = uint32_t(lds / 2);
-                if (P.doff) {  // a matrix tracked for its cells
+                if (P.gen) {  // record mode (mtr_generate_matrix)
+                    if (P.global_mode) apply_pair_kernel<true, false, true><<<cnt, NT, lds, st>>>(P, region);
+                    else apply_pair_kernel<false, false, true><<<cnt, NT, lds, st>>>(P, region);
+                } else if (P.doff) {  // a matrix tracked for its cells
                     if (P.global_mode) apply_pair_kernel<true, true><<<cnt, NT, lds, st>>>(P, region);
                     else apply_pair_kernel<false, true><<<cnt, NT, lds, st>>>(P, region);
                 } else if (P.global_mode) {
@@ -703,6 +706,63 @@ int mtr_generate(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch* table
     if (run_impl(e, 1) != MTR_OK) return -1;
     synth_text_count_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(e->gstate.p, e->docs.p, n);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return MTR_OK;
+}
+
+// matrix m's generator state lives with its rows vector (engine document 2m), seeded as matrix m
+__global__ void synth_init_matrix_kernel(mtr_synth_cfg cfg, mtr_synth_state* st, uint32_t n) {
+    uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < 2 * n) mtr_synth_init(&cfg, d / 2, &st[d]);
+}
+
+int mtr_generate_matrix(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch* tables) {
+    HIPCHK(hipSetDevice(e->device));
+    const uint32_t n = cfg->n_docs, per = cfg->ops_per_doc + 1;
+    if (2ull * n > e->max_docs || cfg->writers > MTR_SYNTH_MAX_WRITERS || cfg->writers + 1 > 0xfd) {
+        set_err("mtr_generate_matrix: bad configuration");
+        return MTR_ERR_BAD_OP;
+    }
+    for (uint32_t m = 0; m < n; m++) {  // pair the vectors (mtr_set_matrix) unless already paired so
+        const uint32_t r = 2 * m, c = 2 * m + 1;
+        if (e->h_kind[r] == 1 && e->h_part[r] == c) continue;
+        if (e->h_kind[r] || e->h_kind[c]) {
+            set_err("mtr_generate_matrix: documents 2m, 2m+1 are paired otherwise");
+            return MTR_ERR_BAD_OP;
+        }
+        e->h_kind[r] = 1;
+        e->h_kind[c] = 2;
+        e->h_part[r] = c;
+        e->h_part[c] = r;
+    }
+    HIPCHK(hipMemcpyAsync(e->dkind.p, e->h_kind.data(), e->h_kind.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          e->stream));
+    HIPCHK(hipMemcpyAsync(e->dpart.p, e->h_part.data(), e->h_part.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          e->stream));
+    std::vector<mtr_doc_desc> docs(2 * size_t(n));
+    for (uint32_t m = 0; m < n; m++) {
+        for (uint32_t w = 0; w < 2; w++) {
+            mtr_doc_desc& x = docs[2 * m + w];
+            x.op_begin = uint64_t(m) * per;
+            x.op_count = w == 0 ? per : 0;  // the cols vector has no op list of its own
+            x.text_base = 0;
+            x.text_count = 0;
+            x.client_base = 0;
+            x.n_clients = cfg->writers + 1;
+        }
+    }
+    mtr_batch b = *tables;
+    b.n_docs = 2 * n;
+    b.docs = docs.data();
+    b.n_ops = 0;
+    b.n_text = 0;
+    if (mtr_reset(e) != MTR_OK || mtr_submit(e, &b) != MTR_OK) return -1;
+    if (e->ops.ensure(size_t(n) * per) || e->btext.ensure(1) || e->gstate.ensure(2 * size_t(n))) return -1;
+    e->gcfg = *cfg;
+    e->gcfg.text_cap = 0;  // the matrix recipe draws no text
+    synth_init_matrix_kernel<<<(2 * n + 255) / 256, 256, 0, e->stream>>>(*cfg, e->gstate.p, n);
+    HIPCHK(hipGetLastError());
+    if (run_impl(e, 1) != MTR_OK) return -1;
     HIPCHK(hipStreamSynchronize(e->stream));
     return MTR_OK;
 }

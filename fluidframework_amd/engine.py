@@ -74,6 +74,8 @@ def lib():
         L.mtr_profile.restype = C.c_int
         L.mtr_generate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mtr_generate.restype = C.c_int
+        L.mtr_generate_matrix.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.mtr_generate_matrix.restype = C.c_int
         L.mtr_download_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_uint64]
         L.mtr_download_batch.restype = C.c_int
@@ -142,6 +144,26 @@ class Engine:
         self._tabs = tabs
         self._cfg = cfg
         self._check(lib().mtr_generate(self.h, C.byref(cfg), C.addressof(tabs.c)), "mtr_generate")
+
+    def generate_matrix(self, cfg, tabs):
+        """Record mode for SharedMatrix logs (mtr_synth_matrix_finish): cfg.n_docs matrices, matrix m
+        = engine documents (2m rows, 2m+1 cols); the recorded logs stay on the device for replays."""
+        self._tabs = tabs
+        self._cfg = cfg
+        self._check(lib().mtr_generate_matrix(self.h, C.byref(cfg), C.addressof(tabs.c)), "mtr_generate_matrix")
+
+    def download_matrix(self, lo, hi):
+        """The recorded op lists of matrices [lo, hi) as a host Batch with one document per matrix (the
+        layout of oracle.generate_matrix)."""
+        from .synth import with_docs
+        n = hi - lo
+        per = self._cfg.ops_per_doc + 1
+        docs = np.zeros(2 * n, dtype=abi.DOC_DTYPE)
+        ops = np.zeros(max(n * per, 1), dtype=abi.OP_DTYPE)
+        text = np.zeros(1, dtype="<u2")
+        self._check(lib().mtr_download_batch(self.h, 2 * lo, 2 * hi, docs.ctypes.data, ops.ctypes.data,
+                                             text.ctypes.data, 0), "mtr_download_batch")
+        return with_docs(self._tabs, docs[0::2].copy(), ops[:n * per], text)
 
     def download(self, lo, hi):
         """The recorded batch of documents [lo, hi) as a host Batch (sharing the recipe tables)."""

@@ -121,6 +121,13 @@ int mtr_last_timing(mtr_engine* e, double* out, int32_t n);
 struct mtr_synth_cfg;
 int mtr_generate(mtr_engine* e, const struct mtr_synth_cfg* cfg, const mtr_batch* tables);
 
+/* Record mode for SharedMatrix workloads: cfg->n_docs matrices drawn from the
+ * matrix recipe (mtr_synth_matrix_finish) with the engine's exact view lengths of both vectors.
+ * Matrix m is the pair (rows = engine document 2m, cols = 2m + 1; paired as by mtr_set_matrix) and
+ * its op list is the rows document's; the engine needs max_docs >= 2 * n_docs.  Draws the same logs
+ * as the oracle's oracle_generate_matrix from the same seeds. */
+int mtr_generate_matrix(mtr_engine* e, const struct mtr_synth_cfg* cfg, const mtr_batch* tables);
+
 /* Copy the recorded batch of documents [lo, hi) to the host (compacted: op_begin/text_base are
  * rewritten relative to the copied arrays; text_cap = capacity of `text` in UTF-16 units). */
 int mtr_download_batch(mtr_engine* e, uint32_t lo, uint32_t hi, mtr_doc_desc* docs, mtr_op* ops, uint16_t* text,

@@ -1579,6 +1579,49 @@ double oracle_replay_batch(const mtr_batch* b, const mtr_options* opt, uint32_t 
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// SharedMatrix replay (the CPU leg of the C4 bench and its parity check): matrices [lo, hi) of a
+// batch with one document per matrix (its rows vector's op list, as oracle_generate_matrix writes
+// it), each applied to a fresh matrix observer (SharedMatrix.processCore, matrix.ts:636-693) and
+// summarized per vector (PermutationVector.summarize, permutationvector.ts:310-325).  hashes[2m] /
+// hashes[2m + 1] = digest of the rows / cols vector's blobs; returns wall-clock seconds.
+double oracle_replay_matrix_batch(const mtr_batch* b, const mtr_options* opt, uint32_t lo, uint32_t hi,
+                                  int nthreads, uint64_t* hashes, int32_t* status) {
+    std::atomic<uint32_t> next{lo};
+    auto t0 = std::chrono::steady_clock::now();
+    auto work = [&]() {
+        std::vector<uint8_t> out(1 << 16);
+        std::vector<int64_t> lens(4096);
+        for (;;) {
+            const uint32_t d = next.fetch_add(1);
+            if (d >= hi) break;
+            oracle_doc* doc = oracle_doc_new_matrix(opt);
+            const int st = oracle_doc_apply(doc, b, d, 0, b->docs[d].op_count);
+            for (int w = 0; w < 2; w++) {
+                uint64_t h = 0;
+                if (st == MTR_OK) {
+                    oracle_doc_select(doc, w);
+                    int64_t r;
+                    while ((r = oracle_doc_summarize(doc, b, d, out.data(), int64_t(out.size()), lens.data(), 4096)) < 0)
+                        out.resize(size_t(-r) + 16);
+                    std::vector<std::string> blobs;
+                    int64_t off = 0;
+                    for (int64_t k = 0; k < r; k++) {
+                        blobs.emplace_back(reinterpret_cast<const char*>(out.data() + off), size_t(lens[k]));
+                        off += lens[k];
+                    }
+                    h = summary_hash(blobs);
+                }
+                if (hashes) hashes[2 * size_t(d - lo) + w] = h;
+            }
+            if (status) status[d - lo] = st;
+            oracle_doc_free(doc);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, nthreads); t++) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
 
 // Synthetic op logs (include/mtr_synth.h) with the oracle as the exact simulator.
 // SharedMatrix op logs from the matrix recipe (mtr_synth_matrix_finish), one document per task;

@@ -60,6 +60,12 @@ void oracle_doc_state(oracle_doc* d, int64_t* out);
 double oracle_replay_batch(const mtr_batch* b, const mtr_options* opt, uint32_t lo, uint32_t hi, int nthreads,
                            uint64_t* hashes, int32_t* status);
 
+/* SharedMatrix replay: matrices [lo, hi) of a batch with one document per matrix (as
+ * oracle_generate_matrix writes it); hashes[2m] / hashes[2m+1] = digest of the rows / cols vector's
+ * blobs (the engine's per-document digest of documents 2m / 2m+1).  Returns wall seconds. */
+double oracle_replay_matrix_batch(const mtr_batch* b, const mtr_options* opt, uint32_t lo, uint32_t hi,
+                                  int nthreads, uint64_t* hashes, int32_t* status);
+
 /* Synthetic op logs (include/mtr_synth.h) driven by the oracle: documents [lo, hi); ops_out holds
  * (hi-lo) * (ops_per_doc+1) records, text_out (hi-lo) * cfg->text_cap units.  tables supplies the
  * prop-op / key / value / client tables.  Also digests each document's summary. */

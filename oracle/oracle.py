@@ -55,6 +55,9 @@ def lib():
         L.oracle_replay_batch.restype = C.c_double
         L.oracle_replay_batch.argtypes = [C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32, C.c_int,
                                           C.c_void_p, C.c_void_p]
+        L.oracle_replay_matrix_batch.restype = C.c_double
+        L.oracle_replay_matrix_batch.argtypes = [C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32,
+                                                 C.c_int, C.c_void_p, C.c_void_p]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         _LIB = L
@@ -141,6 +144,18 @@ def replay_batch(batch, lo, hi, threads, opts=None):
     status = np.zeros(n, dtype="<i4")
     secs = lib().oracle_replay_batch(C.addressof(batch.c), C.byref(opts), lo, hi, threads, hashes.ctypes.data,
                                      status.ctypes.data)
+    return secs, hashes, status
+
+
+def replay_matrix_batch(batch, lo, hi, threads, opts=None):
+    """Replay matrices [lo, hi) (one document per matrix) -> (seconds, digests [rows, cols] per
+    matrix, statuses)."""
+    opts = opts or options()
+    n = hi - lo
+    hashes = np.zeros(2 * n, dtype="<u8")
+    status = np.zeros(n, dtype="<i4")
+    secs = lib().oracle_replay_matrix_batch(C.addressof(batch.c), C.byref(opts), lo, hi, threads,
+                                            hashes.ctypes.data, status.ctypes.data)
     return secs, hashes, status
 
 

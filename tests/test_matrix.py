@@ -17,7 +17,7 @@ import pytest
 from fluidframework_amd import abi
 from fluidframework_amd.batch import Interner, MatrixLog, build_batch, matrix_logs
 from fluidframework_amd.synth import make_cfg, tables, with_docs
-from oracle.oracle import OracleDoc, generate_matrix, options
+from oracle.oracle import OracleDoc, generate_matrix, options, replay_matrix_batch, summary_digest
 
 U = abi.HANDLE_UNALLOCATED
 
@@ -186,6 +186,52 @@ def test_matrix_engine_matches_oracle(writers, lag, ops):
             oe, oh = o.export()
             assert gh == oh and np.array_equal(ge, oe), f"matrix {m} vector {w}: leaves differ"
             assert eng.summary(d) == o.summarize(gb, m), f"matrix {m} vector {w}: summary bytes differ"
+
+
+def test_oracle_matrix_replay_digests():
+    """The C4 bench's CPU leg: per-vector digests of a replayed matrix equal the digests of the
+    oracle's own summaries of each vector."""
+    n = 6
+    cfg = matrix_cfg(n, 800)
+    tabs = tables(writers=8)
+    b, _, status = generate_matrix(cfg, tabs, 0, n, threads=4)
+    assert (status == 0).all()
+    _, h, st = replay_matrix_batch(b, 0, n, 4)
+    assert (st == 0).all()
+    for m in range(n):
+        o = _oracle(b, m)
+        for w in (0, 1):
+            assert int(h[2 * m + w]) == summary_digest(o.select(w).summarize(b, m)), f"matrix {m} vector {w}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("writers,lag,ops", [(8, 64, 1500), (16, 16, 1000)])
+def test_matrix_record_mode_matches_oracle_generator(writers, lag, ops):
+    """Record mode for matrices (mtr_generate_matrix, the C4 bench's input): the engine draws the
+    same op logs as the oracle's generator from the same seeds, and replaying them reproduces the
+    oracle's per-vector summaries."""
+    from fluidframework_amd.engine import Engine
+
+    n = 32
+    cfg = matrix_cfg(n, ops, writers=writers, max_lag=lag)
+    tabs = tables(writers=writers)
+    eng = Engine(2 * n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=1 << 12,
+                 prop_words=1024, remover_cells=4096, ops_per_launch=48)
+    eng.generate_matrix(cfg, tabs)
+    gb = eng.download_matrix(0, n)
+    ob, _, status = generate_matrix(cfg, tabs, 0, n, threads=8)
+    assert (status == 0).all()
+    assert np.array_equal(gb.docs["op_count"], ob.docs["op_count"])
+    assert np.array_equal(gb.ops, ob.ops), "recorded matrix logs differ from the oracle generator's"
+    eng.reset()
+    eng.run()
+    eng.summarize()
+    eng.sync()
+    for d in range(2 * n):
+        assert eng.status(d)[0] == 0, f"document {d}: {eng.status(d)}"
+    _, oh, st = replay_matrix_batch(ob, 0, n, 8)
+    assert (st == 0).all()
+    assert np.array_equal(eng.hashes(2 * n), oh)
 
 
 # ---------------------------------------------------------------- cells (SURVEY.md §8 row f3)
