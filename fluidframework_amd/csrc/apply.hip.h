@@ -2189,31 +2189,39 @@ struct Eng {
     // PermutationVector.adjustPosition (permutationvector.ts:232-247): getContainingSegment at the
     // op's (refSeq, clientId) view (mergeTree.ts:795-813), undefined for a removed segment, else
     // its local-view position (getPosition, mergeTree.ts:768-785) plus the offset.  -1 = undefined.
-    static MTR_DI int adjust_position(D& L, const KParams& P, St& s, int pos, const View& v) {
+    // Returns the leaf index (-1 = undefined) and the offset in it; handle_at finishes the job.
+    static MTR_DI View local_view(const St& s) {
+        View v;
+        v.ref = s.curseq;
+        v.client = uint32_t(s.local);
+        v.local = 1;
+        return v;
+    }
+    static MTR_DI int adjust_position(D& L, const KParams& P, St& s, int pos, const View& v, int& off) {
         prefix(L, s, v, P.new_length_calc);
         const int S = s.nseg;
         const int i = lower_bound_E(L, s, pos + 1);  // the leaf whose view range [E - V, E) holds pos
         if (i >= S) return -1;
         if (uni(L.rseq[i]) != RNONE) return -1;
-        const int off = pos - (i > 0 ? (uni(L.E[i - 1]) & EMASK) : 0);
-        int before = 0;  // local-view length of the leaves before i (removed leaves count 0)
-        for (int base = 0; base < i; base += 64) {
-            const int j = base + lane_id();
-            const int x = j < i && L.rseq[min(j, S - 1)] == RNONE ? int(L.len[min(j, S - 1)]) : 0;
-            before += rdlane(wave_incl_scan(x), 63);
-        }
-        return before + off;
+        off = pos - (i > 0 ? (uni(L.E[i - 1]) & EMASK) : 0);
+        return i;
+    }
+    // getAllocatedHandle of the adjusted position (leaf i, offset off): at the local view that
+    // position lies in the same (not removed, visible) leaf at the same offset, so a leaf that has
+    // a handle answers start + off without a local-view scan; otherwise the local position is the
+    // local-view length of the leaves before i (every leaf is acked: those not removed) plus off
+    static MTR_DI int handle_at(D& L, const KParams& P, St& s, int i, int off) {
+        const uint32_t t = uniu(L.text[i]);
+        if (t != uint32_t(MTR_HANDLE_UNALLOCATED)) return int(t) + off;
+        prefix(L, s, local_view(s), P.new_length_calc);
+        return allocated_handle(L, P, s, (i > 0 ? (uni(L.E[i - 1]) & EMASK) : 0) + off, true);
     }
     // PermutationVector.getAllocatedHandle (permutationvector.ts:209-230) at the local view: a
     // segment without a handle is split to [pos, pos + 1) (walkSegments with splitRange ->
     // MergeTree.mapRange, mergeTree.ts:2451-2469: `if (start)` skips the split at 0) and that
     // one-position segment gets the next handle (HandleTable.allocate)
-    static MTR_DI int allocated_handle(D& L, const KParams& P, St& s, int pos) {
-        View v;
-        v.ref = s.curseq;
-        v.client = uint32_t(s.local);
-        v.local = 1;
-        prefix(L, s, v, P.new_length_calc);
+    static MTR_DI int allocated_handle(D& L, const KParams& P, St& s, int pos, bool scanned) {
+        if (!scanned) prefix(L, s, local_view(s), P.new_length_calc);
         {
             const int i = lower_bound_E(L, s, pos + 1);
             if (i >= s.nseg) {  // "Trying to get handle of out-of-bounds position!"
@@ -2307,12 +2315,13 @@ struct Eng {
                 View v1 = v;
                 v.local = (!s0.collab || uint32_t(s0.local) == v.client) ? 1 : 0;
                 v1.local = (!s1.collab || uint32_t(s1.local) == v1.client) ? 1 : 0;
-                const int r = adjust_position(L0, P, s0, op.pos1, v);
-                if (r >= 0) {
-                    const int c = adjust_position(L1, P, s1, op.pos2, v1);
-                    if (c >= 0) {
-                        const int rh = allocated_handle(L0, P, s0, r);
-                        const int ch = allocated_handle(L1, P, s1, c);
+                int roff = 0, coff = 0;
+                const int ri = adjust_position(L0, P, s0, op.pos1, v, roff);
+                if (ri >= 0) {
+                    const int ci = adjust_position(L1, P, s1, op.pos2, v1, coff);
+                    if (ci >= 0) {
+                        const int rh = handle_at(L0, P, s0, ri, roff);
+                        const int ch = handle_at(L1, P, s1, ci, coff);
                         // the cell write (cells.setCell(rowHandle, colHandle, value), matrix.ts:686-689)
                         if (DL && (op.flags & MTR_F_DELTA) && s0.status == MTR_OK && s1.status == MTR_OK)
                             put_record(L0, s0, cursor + k, rh, ch, MTR_DELTA_CELL);
