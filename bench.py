@@ -55,8 +55,12 @@ def parse():
                     help="default: about 60M messages of documents (~8 s on 16 host threads)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-file", default=None,
+                    help="PMC summary of this config (default: profiles/traffic_r01.json, _c4 for C4)")
     a = ap.parse_args()
+    if a.traffic_file is None:
+        name = "traffic_r01.json" if a.config != "C4" else "traffic_r01_c4.json"
+        a.traffic_file = os.path.join(ROOT, "profiles", name)
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)

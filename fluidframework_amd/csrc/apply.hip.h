@@ -435,6 +435,36 @@ struct Eng {
         wsync();
     }
 
+    // the scans of a matrix's two vectors at one op's views in one pass: each round carries two
+    // independent chains of LDS reads and DPP scans, which overlap
+    static MTR_DI void prefix2(D& La, const St& sa, const View& va, D& Lb, const St& sb, const View& vb,
+                               int newlen) {
+        PROF(P_PREFIX);
+        const int Sa = sa.nseg, Sb = sb.nseg;
+        const int ln = lane_id();
+        int ca = 0, cb = 0;
+        for (int base = 0; base < max(Sa, Sb); base += 64) {
+            const int i = base + ln;
+            const bool pa = base < Sa, pb = base < Sb;  // uniform: the vector still has leaves here
+            int xa = 0, xb = 0;
+            if (pa) {
+                const int x0 = vis_len(La, i, va, newlen, sa.minseq, i < Sa);
+                xa = i < Sa ? x0 : 0;
+            }
+            if (pb) {
+                const int x0 = vis_len(Lb, i, vb, newlen, sb.minseq, i < Sb);
+                xb = i < Sb ? x0 : 0;
+            }
+            const int ia = wave_incl_scan(max(xa, 0));
+            const int ib = wave_incl_scan(max(xb, 0));
+            if (i < Sa) La.E[i] = (ca + ia) | (xa < 0 ? int(0x80000000u) : 0);
+            if (i < Sb) Lb.E[i] = (cb + ib) | (xb < 0 ? int(0x80000000u) : 0);
+            ca += rdlane(ia, 63);
+            cb += rdlane(ib, 63);
+        }
+        wsync();
+    }
+
     // ------------------------------------------------------------ data movement
     // move leaves [at, S) (with their scan entries) to [at+1, S+1); rounds of 64 from the top
     static MTR_DI void shift_right1(D& L, const St& s, int at) {
@@ -2197,8 +2227,8 @@ struct Eng {
         v.local = 1;
         return v;
     }
-    static MTR_DI int adjust_position(D& L, const KParams& P, St& s, int pos, const View& v, int& off) {
-        prefix(L, s, v, P.new_length_calc);
+    // (the caller has scanned the vector at the op's view: prefix2)
+    static MTR_DI int adjust_position(D& L, St& s, int pos, int& off) {
         const int S = s.nseg;
         const int i = lower_bound_E(L, s, pos + 1);  // the leaf whose view range [E - V, E) holds pos
         if (i >= S) return -1;
@@ -2316,9 +2346,12 @@ struct Eng {
                 v.local = (!s0.collab || uint32_t(s0.local) == v.client) ? 1 : 0;
                 v1.local = (!s1.collab || uint32_t(s1.local) == v1.client) ? 1 : 0;
                 int roff = 0, coff = 0;
-                const int ri = adjust_position(L0, P, s0, op.pos1, v, roff);
+                // both vectors at the op's view in one pass (the cols scan is unused when the row
+                // is undefined: nothing else reads it)
+                prefix2(L0, s0, v, L1, s1, v1, P.new_length_calc);
+                const int ri = adjust_position(L0, s0, op.pos1, roff);
                 if (ri >= 0) {
-                    const int ci = adjust_position(L1, P, s1, op.pos2, v1, coff);
+                    const int ci = adjust_position(L1, s1, op.pos2, coff);
                     if (ci >= 0) {
                         const int rh = handle_at(L0, P, s0, ri, roff);
                         const int ch = handle_at(L1, P, s1, ci, coff);

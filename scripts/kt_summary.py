@@ -15,7 +15,9 @@ for line in open(os.path.join(d, "kt.log")):
         bench = json.loads(line)
 n = bench["roofline"]["launches_per_step"]
 rows = list(csv.DictReader(open(os.path.join(d, "kt", "kt_kernel_trace.csv"))))
-ak = [r for r in rows if "apply_kernel" in r["Kernel_Name"]][-n:]
+# the timed kernel: apply_kernel (SharedString configs) or apply_pair_kernel (C4 matrices)
+kern = "apply_pair_kernel" if "apply_pair_kernel" in bench["roofline"].get("kernel", "") else "apply_kernel"
+ak = [r for r in rows if kern in r["Kernel_Name"]][-n:]
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in ak]
 t0 = min(int(r["Start_Timestamp"]) for r in ak)
 t1 = max(int(r["End_Timestamp"]) for r in ak)
