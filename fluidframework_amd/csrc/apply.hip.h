@@ -435,34 +435,57 @@ struct Eng {
         wsync();
     }
 
-    // the scans of a matrix's two vectors at one op's views in one pass: each round carries two
-    // independent chains of LDS reads and DPP scans, which overlap
-    static MTR_DI void prefix2(D& La, const St& sa, const View& va, D& Lb, const St& sb, const View& vb,
-                               int newlen) {
+    // getContainingSegment for two vectors at once (a setCell's row and col): two visibility scans
+    // interleaved round by round (independent chains of LDS reads and DPP scans that overlap), each
+    // stopping at the round that reaches its position.  ia / ib = first leaf whose inclusive
+    // visible prefix exceeds pa / pb (S if none, as lower_bound_E(pos + 1)); bfa / bfb = the
+    // visible length before it.  Writes no scan array.
+    static MTR_DI void find2(const D& La, const St& sa, const View& va, int pa, int& ia, int& bfa, const D& Lb,
+                             const St& sb, const View& vb, int pb, int& ib, int& bfb, int newlen) {
         PROF(P_PREFIX);
         const int Sa = sa.nseg, Sb = sb.nseg;
         const int ln = lane_id();
         int ca = 0, cb = 0;
-        for (int base = 0; base < max(Sa, Sb); base += 64) {
+        ia = -1;
+        ib = -1;
+        for (int base = 0;; base += 64) {
+            const bool ga = ia < 0 && base < Sa, gb = ib < 0 && base < Sb;  // uniform
+            if (!ga && ia < 0) { ia = Sa; bfa = ca; }
+            if (!gb && ib < 0) { ib = Sb; bfb = cb; }
+            if (!ga && !gb) break;
             const int i = base + ln;
-            const bool pa = base < Sa, pb = base < Sb;  // uniform: the vector still has leaves here
             int xa = 0, xb = 0;
-            if (pa) {
+            if (ga) {
                 const int x0 = vis_len(La, i, va, newlen, sa.minseq, i < Sa);
-                xa = i < Sa ? x0 : 0;
+                xa = i < Sa ? max(x0, 0) : 0;
             }
-            if (pb) {
+            if (gb) {
                 const int x0 = vis_len(Lb, i, vb, newlen, sb.minseq, i < Sb);
-                xb = i < Sb ? x0 : 0;
+                xb = i < Sb ? max(x0, 0) : 0;
             }
-            const int ia = wave_incl_scan(max(xa, 0));
-            const int ib = wave_incl_scan(max(xb, 0));
-            if (i < Sa) La.E[i] = (ca + ia) | (xa < 0 ? int(0x80000000u) : 0);
-            if (i < Sb) Lb.E[i] = (cb + ib) | (xb < 0 ? int(0x80000000u) : 0);
-            ca += rdlane(ia, 63);
-            cb += rdlane(ib, 63);
+            const int sa_ = wave_incl_scan(xa);
+            const int sb_ = wave_incl_scan(xb);
+            if (ga) {
+                const uint64_t m = __ballot(i < Sa && ca + sa_ > pa);
+                if (m) {
+                    const int l = first_lane(m);
+                    ia = base + l;
+                    bfa = ca + rdlane(sa_ - xa, l);
+                } else {
+                    ca += rdlane(sa_, 63);
+                }
+            }
+            if (gb) {
+                const uint64_t m = __ballot(i < Sb && cb + sb_ > pb);
+                if (m) {
+                    const int l = first_lane(m);
+                    ib = base + l;
+                    bfb = cb + rdlane(sb_ - xb, l);
+                } else {
+                    cb += rdlane(sb_, 63);
+                }
+            }
         }
-        wsync();
     }
 
     // ------------------------------------------------------------ data movement
@@ -2227,13 +2250,11 @@ struct Eng {
         v.local = 1;
         return v;
     }
-    // (the caller has scanned the vector at the op's view: prefix2)
-    static MTR_DI int adjust_position(D& L, St& s, int pos, int& off) {
-        const int S = s.nseg;
-        const int i = lower_bound_E(L, s, pos + 1);  // the leaf whose view range [E - V, E) holds pos
-        if (i >= S) return -1;
+    // (i, before: the leaf whose view range holds pos and the view length before it, from find2)
+    static MTR_DI int adjust_position(D& L, St& s, int pos, int i, int before, int& off) {
+        if (i >= s.nseg) return -1;
         if (uni(L.rseq[i]) != RNONE) return -1;
-        off = pos - (i > 0 ? (uni(L.E[i - 1]) & EMASK) : 0);
+        off = pos - before;
         return i;
     }
     // getAllocatedHandle of the adjusted position (leaf i, offset off): at the local view that
@@ -2346,12 +2367,13 @@ struct Eng {
                 v.local = (!s0.collab || uint32_t(s0.local) == v.client) ? 1 : 0;
                 v1.local = (!s1.collab || uint32_t(s1.local) == v1.client) ? 1 : 0;
                 int roff = 0, coff = 0;
-                // both vectors at the op's view in one pass (the cols scan is unused when the row
-                // is undefined: nothing else reads it)
-                prefix2(L0, s0, v, L1, s1, v1, P.new_length_calc);
-                const int ri = adjust_position(L0, s0, op.pos1, roff);
+                // both vectors at the op's view in one pass (the cols result is unused when the row
+                // is undefined)
+                int fr, br, fc, bc;
+                find2(L0, s0, v, op.pos1, fr, br, L1, s1, v1, op.pos2, fc, bc, P.new_length_calc);
+                const int ri = adjust_position(L0, s0, op.pos1, fr, br, roff);
                 if (ri >= 0) {
-                    const int ci = adjust_position(L1, s1, op.pos2, coff);
+                    const int ci = adjust_position(L1, s1, op.pos2, fc, bc, coff);
                     if (ci >= 0) {
                         const int rh = handle_at(L0, P, s0, ri, roff);
                         const int ch = handle_at(L1, P, s1, ci, coff);
