@@ -365,11 +365,21 @@ struct Eng {
     // nodeLength for a leaf (mergeTree.ts:916-1004): -1 = undefined.  Every lane evaluates the
     // same select chain (no divergent branches); only lanes whose answer depends on a later
     // remover in the overlap list walk it, behind one ballot.
+    // the fields a visibility test reads (loaded apart from the test so scans can issue the next
+    // round's loads early)
+    struct Hot {
+        int len, rseq, seq;
+        uint32_t meta;
+    };
+    static MTR_DI Hot ld_hot(const D& L, int i) { return Hot{L.len[i], L.rseq[i], L.seq[i], L.meta[i]}; }
     static MTR_DI int vis_len(const D& L, int i, const View& v, int newlen, int minseq, bool valid = true) {
-        const int len = L.len[i];
-        const int rseq = L.rseq[i];
-        const uint32_t m = L.meta[i];
-        const int seq = L.seq[i];
+        return vis_hot(L, ld_hot(L, i), i, v, newlen, minseq, valid);
+    }
+    static MTR_DI int vis_hot(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
+        const int len = h.len;
+        const int rseq = h.rseq;
+        const uint32_t m = h.meta;
+        const int seq = h.seq;
         const bool removed = rseq != RNONE;
         if (v.local) {  // localNetLength, mergeTree.ts:613-634
             return removed ? (newlen ? 0 : (rseq > minseq ? 0 : -1)) : len;
@@ -442,25 +452,32 @@ struct Eng {
     // visible length before it.  Writes no scan array.
     static MTR_DI void find2(const D& La, const St& sa, const View& va, int pa, int& ia, int& bfa, const D& Lb,
                              const St& sb, const View& vb, int pb, int& ib, int& bfb, int newlen) {
-        PROF(P_PREFIX);
+#ifdef MTR_PROF
+        ProfScope _prof_scope(La.sc, P_PREFIX);
+#endif
         const int Sa = sa.nseg, Sb = sb.nseg;
         const int ln = lane_id();
         int ca = 0, cb = 0;
         ia = -1;
         ib = -1;
+        // software-pipelined: each round's leaf fields were loaded during the previous round
+        Hot ha = Sa > 0 ? ld_hot(La, ln) : Hot{}, hb = Sb > 0 ? ld_hot(Lb, ln) : Hot{};
         for (int base = 0;; base += 64) {
             const bool ga = ia < 0 && base < Sa, gb = ib < 0 && base < Sb;  // uniform
             if (!ga && ia < 0) { ia = Sa; bfa = ca; }
             if (!gb && ib < 0) { ib = Sb; bfb = cb; }
             if (!ga && !gb) break;
             const int i = base + ln;
+            const Hot ca_h = ha, cb_h = hb;
+            if (ga && base + 64 < Sa) ha = ld_hot(La, i + 64);
+            if (gb && base + 64 < Sb) hb = ld_hot(Lb, i + 64);
             int xa = 0, xb = 0;
             if (ga) {
-                const int x0 = vis_len(La, i, va, newlen, sa.minseq, i < Sa);
+                const int x0 = vis_hot(La, ca_h, i, va, newlen, sa.minseq, i < Sa);
                 xa = i < Sa ? max(x0, 0) : 0;
             }
             if (gb) {
-                const int x0 = vis_len(Lb, i, vb, newlen, sb.minseq, i < Sb);
+                const int x0 = vis_hot(Lb, cb_h, i, vb, newlen, sb.minseq, i < Sb);
                 xb = i < Sb ? max(x0, 0) : 0;
             }
             const int sa_ = wave_incl_scan(xa);
@@ -2354,6 +2371,10 @@ struct Eng {
         for (int k = 0; k < n_ops; k++) {
             if (GN) gen_pair_op(L0, L1, P, s0, s1, dd, cursor + k);
             const mtr_op op = uni_struct(ld_struct<mtr_op>(ops + k));
+#ifdef MTR_PROF  // P_X1 = setCell messages, P_X2 = row/col splices
+            ProfScope _prof_op(L0.sc, P_OP);
+            ProfScope _prof_kind(L0.sc, op.type == MTR_OP_SETCELL ? P_X1 : P_X2);
+#endif
             bool ok = true;
             if (op.type == MTR_OP_START_COLLAB) {  // didAttach / onConnect start both vectors (matrix.ts:514-532)
                 ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k) && apply_op(L1, P, s1, op, dd, false, 0, cursor + k);

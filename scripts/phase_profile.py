@@ -17,12 +17,21 @@ ap.add_argument("--ops", type=int, default=1000)
 ap.add_argument("--writers", type=int, default=8)
 ap.add_argument("--max-lag", type=int, default=32)
 ap.add_argument("--ops-per-launch", type=int, default=256)
+ap.add_argument("--matrix", action="store_true",
+                help="C4-shaped SharedMatrix pairs (x1 = setCell messages, x2 = row/col splices)")
 a = ap.parse_args()
 n, ops = a.docs, a.ops
-cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag)
-eng = Engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
-             prop_words=16384, remover_cells=4096, ops_per_launch=a.ops_per_launch)
-eng.generate(cfg, tables(writers=a.writers))
+if a.matrix:
+    cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, weights=(12, 8, 80), max_text=4, max_range=3,
+                   text_cap=0)
+    eng = Engine(2 * n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * ops + 1024,
+                 prop_words=1024, remover_cells=8192, ops_per_launch=a.ops_per_launch)
+    eng.generate_matrix(cfg, tables(writers=a.writers))
+else:
+    cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag)
+    eng = Engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
+                 prop_words=16384, remover_cells=4096, ops_per_launch=a.ops_per_launch)
+    eng.generate(cfg, tables(writers=a.writers))
 eng.profile(reset=True)
 eng.reset()
 eng.run()
