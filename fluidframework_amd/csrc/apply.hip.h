@@ -431,12 +431,15 @@ struct Eng {
         const int S = s.nseg;
         const int ln = lane_id();
         int carry = 0;
+        Hot h = S > 0 ? ld_hot(L, ln) : Hot{};  // software-pipelined: loaded one round ahead
         for (int base = 0; base < S; base += 64) {
             // every lane evaluates (reads past the last leaf stay inside the LDS allocation);
             // lanes past the last leaf contribute 0 and store nothing (capacities are multiples
             // of 32, so the round's top slots may belong to the next array)
             const int i = base + ln;
-            const int x0 = vis_len(L, i, v, newlen, s.minseq, i < S);
+            const Hot cur = h;
+            if (base + 64 < S) h = ld_hot(L, i + 64);
+            const int x0 = vis_hot(L, cur, i, v, newlen, s.minseq, i < S);
             const int x = i < S ? x0 : 0;
             const int inc = wave_incl_scan(max(x, 0));
             if (i < S) L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
