@@ -30,6 +30,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: chip-level para
 
 # BASELINE.json configs: documents per GPU, messages per document, writers, max lag
 PRESETS = {
+    # the reference's own replay logs (merge-tree/src/test/results, 30 files x 2,040 messages, 2/4/8
+    # clients) as 30 documents, replayed as client.replay.spec.ts:17-71 does
+    "C1": dict(docs=30, ops=2_040, writers=7, max_lag=0),
     "C2": dict(docs=10_000, ops=5_000, writers=16, max_lag=64),
     "C3": dict(docs=100_000, ops=1_000, writers=8, max_lag=32),
     # SharedMatrix replay: docs = matrices (two PermutationVector documents each), 20 % row/col
@@ -89,7 +92,28 @@ def main():
     matrix = a.config in MATRIX
     tabs = tables(writers=a.writers)
     doc_lo, _ = shard.doc_range(rank, world, n)
-    if matrix:
+    fixture_text = None
+    if a.config == "C1":  # reference fixtures, not synthetic: every rank replays the same 30 logs
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from fixtures import load_replay, replay_files, replay_log
+
+        from fluidframework_amd.batch import Interner, build_batch
+
+        groups = [load_replay(p) for p in replay_files()]
+        it = Interner()
+        logs = [replay_log(g, it) for g in groups]
+        for d, gs in enumerate(groups):
+            for g in gs:
+                for m in g["msgs"]:
+                    logs[d].message(m, it)
+        fixture_batch = build_batch(logs, it)
+        fixture_text = [gs[-1]["resultText"] for gs in groups]
+        n = len(groups)
+        fixture_msgs = sum(len(g["msgs"]) for gs in groups for g in gs)
+        ops = fixture_msgs // n
+        eng = Engine(n, device=local, max_segments=8192, heap_entries=8192, text_units=1 << 18,
+                     prop_words=1 << 18, remover_cells=1 << 14, ops_per_launch=a.ops_per_launch)
+    elif matrix:
         cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, weights=(12, 8, 80), max_text=4, max_range=3,
                        doc_base=doc_lo, text_cap=0)
         # handle tables live in the text arena of a vector document (<= positions ever inserted)
@@ -102,7 +126,10 @@ def main():
                      prop_words=16384, remover_cells=4096, ops_per_launch=a.ops_per_launch)
 
     t0 = time.time()
-    if matrix:  # untimed: record the op logs on the device
+    if fixture_text is not None:  # untimed: upload the fixture logs once (replays start from HBM)
+        eng.submit(fixture_batch)
+        eng.sync()
+    elif matrix:  # untimed: record the op logs on the device
         eng.generate_matrix(cfg, tabs)
     else:
         eng.generate(cfg, tabs)
@@ -141,10 +168,17 @@ def main():
     barrier()
 
     st = eng.stats()  # counters of the last step
-    if st["ops"] != n * (ops + 1):  # every document applied its whole log (START_COLLAB + messages)
-        raise SystemExit(f"the step applied {st['ops']} op records, expected {n * (ops + 1)}")
+    if fixture_text is not None:
+        want = len(fixture_batch.ops)
+        bad_text = sum(eng.text(d) != t for d, t in enumerate(fixture_text))
+        if bad_text:
+            raise SystemExit(f"{bad_text} fixture documents end with a text other than the reference's resultText")
+    else:
+        want = n * (ops + 1)  # every document applied its whole log (START_COLLAB + messages)
+    if st["ops"] != want:
+        raise SystemExit(f"the step applied {st['ops']} op records, expected {want}")
     hashes = eng.hashes(2 * n if matrix else n)
-    messages = n * ops
+    messages = n * ops if fixture_text is None else fixture_msgs
     run_digest = shard.digest(hashes)
     if dist is not None:  # the only collective: counters + summary digests over RCCL/xGMI
         r = shard.reduce_run(dist, f"cuda:{local}", elapsed, messages, int(st["bad_docs"]), run_digest)
@@ -199,7 +233,14 @@ def main():
 
         k = min(a.cpu_sample_docs or max(1, 60_000_000 // ops), n)
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        if matrix:  # a matrix is equal when both of its vectors' summaries are
+        if fixture_text is not None:  # the whole fixture set, replayed 10 times (one pass is ~0.2 s)
+            k = n
+            secs = 0.0
+            for _ in range(10):
+                dt, ohash, ost = replay_batch(fixture_batch, 0, k, threads)
+                secs += dt / 10
+            eq = int((ohash == hashes[:k]).sum())
+        elif matrix:  # a matrix is equal when both of its vectors' summaries are
             sample = eng.download_matrix(0, k)
             secs, ohash, ost = replay_matrix_batch(sample, 0, k, threads)
             eq = int((ohash == hashes[:2 * k]).reshape(k, 2).all(axis=1).sum())
@@ -209,7 +250,7 @@ def main():
             eq = int((ohash == hashes[:k]).sum())
         bit_exact = {"checked_docs": k, "equal": eq, "oracle_errors": int((ost != 0).sum())}
         cpu = {
-            "value": round(k * ops / secs, 1),
+            "value": round((messages if fixture_text is not None else k * ops) / secs, 1),
             "unit": "ops/s",
             "cores": threads,
             "kind": "port",
@@ -229,9 +270,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic: seeded recipe include/mtr_synth.h recorded on the device (record mode)",
+        "data": ("reference fixtures (tests/golden/replay, converted from merge-tree/src/test/results)"
+                 if fixture_text is not None else
+                 "synthetic: seeded recipe include/mtr_synth.h recorded on the device (record mode)"),
         "config": {
-            "workload": (f"{a.config}: {n} SharedMatrix docs/GPU (2 PermutationVectors each) x {ops} ops, 20% row/col "
+            "workload": (f"C1: the reference's 30 replay logs (merge-tree/src/test/results) as {n} documents, "
+                         f"{messages} sequenced messages (plus initial text + startOrUpdateCollaboration), final texts "
+                         f"checked against resultText, V1 summaries" if fixture_text is not None else
+                         f"{a.config}: {n} SharedMatrix docs/GPU (2 PermutationVectors each) x {ops} ops, 20% row/col "
                          f"splices + 80% setCell, {a.writers} writers, lag<={a.max_lag}, V1 segments + handleTable"
                          if matrix else
                          f"{a.config}: {n} docs/GPU x {ops} ops, {a.writers} writers, lag<={a.max_lag}, V1 summaries"),
