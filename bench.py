@@ -8,8 +8,14 @@ include/mtr_synth.h), so the timed region starts with every op log resident in H
 
 Single GPU:   python bench.py
 Multi GPU:    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
-Documents are sharded over ranks (weak scaling: every rank replays its own `--docs` documents); the only
-collective is the final RCCL reduction of counters and summary digests.
+Documents are sharded over ranks.  Default strong scaling: `--docs` is the node's total (C3: 100k
+documents split into contiguous equal ranges -- the LPT assignment for documents of one recipe);
+`--scaling weak` gives every rank its own `--docs`.  The only collective is the final RCCL reduction of
+counters and summary digests.
+
+`value` is the device-resident rate (op logs in HBM when the timed region starts, summaries left on the
+device).  The end-to-end rate SURVEY.md 8d defines -- host op upload, apply, summarize, every blob
+back in host memory -- is measured separately on the same documents (`end_to_end`).
 """
 from __future__ import annotations
 
@@ -47,9 +53,13 @@ def parse():
     ap.add_argument("--config", choices=sorted(PRESETS), default="C3",
                     help="workload preset (C3 = the headline metric's 100k-document run)")
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: --docs is the node total (split over ranks); weak: --docs per rank")
+    ap.add_argument("--e2e-steps", type=int, default=2,
+                    help="timed end-to-end steps (host upload -> blobs on host); 0 = skip")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--docs", type=int, default=None, help="documents per GPU (preset)")
+    ap.add_argument("--docs", type=int, default=None, help="documents: node total (strong) or per GPU (weak)")
     ap.add_argument("--ops", type=int, default=None, help="sequenced messages per document (preset)")
     ap.add_argument("--writers", type=int, default=None)
     ap.add_argument("--max-lag", type=int, default=None)
@@ -68,6 +78,71 @@ def parse():
         if getattr(a, k) is None:
             setattr(a, k, v)
     return a
+
+
+def end_to_end(eng, n, steps, messages, matrix, hashes):
+    """SURVEY.md 8d's end-to-end time: the host hands the op logs over (one upload from page-locked
+    memory), the engine applies and summarizes, and every blob of every document lands in host memory
+    (one bulk download, mtr_get_summaries).  The op logs are the recorded ones, downloaded once
+    (untimed) into pinned host memory.  Reported beside the device-resident headline, never as it."""
+    import time as _t
+
+    from fluidframework_amd.engine import pinned
+
+    if matrix:
+        return None  # (matrix pairs: the vectors' op lists are not a standalone host batch)
+    t0 = _t.perf_counter()
+    hb = eng.download(0, n, pinned_memory=True)
+    prep_s = _t.perf_counter() - t0
+    out = pinned(int(eng.summary_bytes()) + 8 * n + 4096, "u1")
+    times, parts = [], []
+    for i in range(steps + 1):  # the first is untimed (warm)
+        t0 = _t.perf_counter()
+        eng.reset()
+        eng.submit(hb)
+        eng.sync()
+        t1 = _t.perf_counter()
+        eng.run()
+        eng.summarize()
+        eng.sync()
+        t2 = _t.perf_counter()
+        buf, off = eng.summaries(0, n, out=out)
+        t3 = _t.perf_counter()
+        if i:
+            times.append(t3 - t0)
+            parts.append((t1 - t0, t2 - t1, t3 - t2))
+    if eng.stats()["bad_docs"]:
+        raise SystemExit("end-to-end replay left documents in an error state")
+    if not np.array_equal(eng.hashes(n), hashes[:n]):
+        raise SystemExit("end-to-end replay produced different summaries than the device-resident steps")
+    total = int(off[-1])
+    if total != eng.summary_bytes():  # (per document: count word, lengths, blob bytes)
+        raise SystemExit("bulk summary download is short")
+    for d in (0, n // 2, n - 1):  # the bulk records equal the per-document reads
+        if _bulk_record(buf, off, d) != eng.summary(d):
+            raise SystemExit(f"bulk summary record of document {d} differs")
+    t = float(np.mean(times))
+    up, dev, down = (float(np.mean([p[q] for p in parts])) for q in range(3))
+    return {
+        "value": round(messages / t, 1),
+        "unit": "ops/s",
+        "ms_per_step": round(1000 * t, 3),
+        "upload_ms": round(1000 * up, 3),
+        "apply_summarize_ms": round(1000 * dev, 3),
+        "download_ms": round(1000 * down, 3),
+        "upload_bytes": int(hb.ops.nbytes + hb.text.nbytes + hb.docs.nbytes),
+        "download_bytes": total,
+        "steps": steps,
+        "host_batch_prep_s": round(prep_s, 2),
+        "note": "host op upload (page-locked) -> apply -> summarize -> every blob in host memory "
+                "(one bulk copy); same documents and summaries as the headline",
+    }
+
+
+def _bulk_record(buf, off, d):
+    from fluidframework_amd.engine import Engine
+
+    return Engine.split_record(buf, int(off[d]), int(off[d + 1]))
 
 
 def main():
@@ -91,7 +166,11 @@ def main():
     n, ops = a.docs, a.ops
     matrix = a.config in MATRIX
     tabs = tables(writers=a.writers)
-    doc_lo, _ = shard.doc_range(rank, world, n)
+    if a.scaling == "strong" and a.config != "C1":
+        doc_lo, doc_hi = shard.strong_range(rank, world, n)
+        n = doc_hi - doc_lo
+    else:
+        doc_lo, _ = shard.doc_range(rank, world, n)
     fixture_text = None
     if a.config == "C1":  # reference fixtures, not synthetic: every rank replays the same 30 logs
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -198,33 +277,69 @@ def main():
     b_step = 16.0 * st["sum_leaves_before_op"] + 32.0 * messages + 2.0 * st["text_units_inserted"]
     apply_s = apply_ms / 1000.0 / a.steps
     launches_per_step = max(1, launches // a.steps)
-    achieved = b_step / apply_s / 1e9 if apply_s > 0 else 0.0
-    traffic = None
+    kernel_s = kernel_ms / 1000.0 / a.steps  # sum of the apply launches' own durations per step
+    b_launch = b_step / launches_per_step
+    avg_launch_s = kernel_ms / 1000.0 / max(1, launches)
+    # the prescribed figure: algorithmic bytes per launch / that launch's average duration (HIP events
+    # on the launch's own stream; rocprof's per-dispatch average agrees, profiles/)
+    achieved = b_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    # the same bytes over the apply span: a round's size-class launches overlap on 4 streams, so the
+    # span (= rocprof's first-start..last-end of the step's apply dispatches) is shorter than the sum
+    achieved_span = b_step / apply_s / 1e9 if apply_s > 0 else 0.0
+    traffic = pmc = None
     if os.path.exists(a.traffic_file):
         try:
             tf = json.load(open(a.traffic_file))
             if tf.get("docs") == n and tf.get("ops") == ops:
                 traffic = tf.get("hbm_bytes_per_launch")
+                pmc = tf
         except (OSError, ValueError):
-            traffic = None
+            traffic = pmc = None
+    issue = None
+    if pmc is not None:
+        ipo = pmc.get("insts_per_op", {})
+        issue = {
+            "source": os.path.relpath(a.traffic_file, ROOT),
+            "insts_per_op": round(sum(ipo.values()), 1),
+            "salu_per_op": round(ipo.get("salu", 0.0), 1),
+            "valu_per_op": round(ipo.get("valu", 0.0), 1),
+            "lds_per_op": round(ipo.get("lds", 0.0), 1),
+            "wave_cycles_waiting": round(pmc.get("wait_any_frac", 0.0), 3),
+            "wave_cycles_issuing": round(pmc.get("active_inst_frac", 0.0), 3),
+            "lds_bank_conflict_rate": round(pmc.get("lds_bank_conflict_rate", 0.0), 4),
+            "counter_hbm_gbs": round(traffic * launches_per_step / apply_s / 1e9, 1) if traffic and apply_s > 0
+            else None,
+        }
     roofline = {
         "bound": "hbm",
+        "limiter": "per-wave issue latency: one wave per document applies its ops in order (a chain of "
+                   "dependent LDS round trips, ballots and scalar control per op); waves per SIMD are "
+                   "capped by VGPRs and LDS per document. HBM sees only stage-in/out and arenas "
+                   "(counter_hbm_gbs), so the HBM roofline is the flat-pass B_op model's, not the traffic's",
         "kernel": "mtr::apply_pair_kernel" if matrix else "mtr::apply_kernel",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "algorithmic_bytes_per_launch": b_step / launches_per_step,
+        "achieved_span": round(achieved_span, 2),
+        "frac_span": round(achieved_span / HBM_PEAK_GBS, 4),
+        "algorithmic_bytes_per_launch": b_launch,
         "avg_launch_ms": kernel_ms / max(1, launches),
         "launches_per_step": launches_per_step,
         "apply_wall_ms_per_step": apply_ms / a.steps,
-        "note": "achieved = algorithmic bytes of a step / apply wall time of the step; a round's size-class "
-                "launches overlap on 4 streams, so avg_launch_ms (each launch's own HIP-event duration, "
-                "comparable to rocprof) x launches exceeds the wall time",
+        "kernel_sum_ms_per_step": 1000.0 * kernel_s,
+        "issue": issue,
+        "note": "frac = algorithmic bytes per launch / average launch duration (the prescribed per-launch "
+                "figure); frac_span = the step's algorithmic bytes / the apply span (launches of a round "
+                "overlap on 4 streams); traffic = PMC HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)",
         "model": "B_op = 16*S_d(t) + 32 + 2*L_ins (SURVEY.md 8d)" + (
             "; setCell: S_d = leaves of both vectors (two position resolutions)" if matrix else ""),
     }
+
+    e2e = None
+    if a.e2e_steps > 0 and world == 1 and fixture_text is None:
+        e2e = end_to_end(eng, n, a.e2e_steps, messages, matrix, hashes)
 
     cpu = None
     bit_exact = {"checked_docs": 0, "equal": 0}
@@ -249,6 +364,8 @@ def main():
             secs, ohash, ost = replay_batch(sample, 0, k, threads)
             eq = int((ohash == hashes[:k]).sum())
         bit_exact = {"checked_docs": k, "equal": eq, "oracle_errors": int((ost != 0).sum())}
+        if eq != k or bit_exact["oracle_errors"]:
+            raise SystemExit(f"summaries differ from the CPU oracle: {bit_exact}")
         cpu = {
             "value": round((messages if fixture_text is not None else k * ops) / secs, 1),
             "unit": "ops/s",
@@ -267,7 +384,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling if a.config != "C1" else "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": ("reference fixtures (tests/golden/replay, converted from merge-tree/src/test/results)"
@@ -280,14 +397,17 @@ def main():
                          f"{a.config}: {n} SharedMatrix docs/GPU (2 PermutationVectors each) x {ops} ops, 20% row/col "
                          f"splices + 80% setCell, {a.writers} writers, lag<={a.max_lag}, V1 segments + handleTable"
                          if matrix else
-                         f"{a.config}: {n} docs/GPU x {ops} ops, {a.writers} writers, lag<={a.max_lag}, V1 summaries"),
+                         f"{a.config}: {n} docs/GPU ({a.docs} {'per GPU' if a.scaling == 'weak' else 'in all'}) x {ops} ops, "
+                         f"{a.writers} writers, lag<={a.max_lag}, V1 summaries"),
             "docs_per_gpu": n,
+            "docs_total": int(n * world) if a.scaling == "weak" or a.config == "C1" else int(a.docs),
             "ops_per_doc": ops,
             "writers": a.writers,
             "max_lag": a.max_lag,
-            "parallelism": f"doc-sharded x{world}",
+            "parallelism": f"doc-sharded x{world} ({a.scaling if a.config != 'C1' else 'replicas'})",
         },
         "roofline": roofline,
+        "end_to_end": e2e,
         "cpu_baseline": cpu,
         "bit_exact_sample": bit_exact,
         "detail": {

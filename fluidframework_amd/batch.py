@@ -30,6 +30,11 @@ class Unsupported(Exception):
     """A message uses a feature the engine does not implement (document must fall back)."""
 
 
+# short client ids one engine document can hold (include/mtr_types.h MTR_MAX_CLIENTS): the engine
+# keeps a short id in 8 bits; a document that registers more stays on the TypeScript Client
+MAX_CLIENTS = 253
+
+
 class Interner:
     """Global key / value / prop-op tables (ids are stable across batches)."""
 
@@ -88,11 +93,20 @@ class DocLog:
     collaborating: bool = False
 
     def short_id(self, long_id: str) -> int:
+        """Client.getOrAddShortClientId (client.ts:673-677)."""
         i = self.client_ix.get(long_id)
         if i is None:
-            i = len(self.clients)
-            self.client_ix[long_id] = i
-            self.clients.append(long_id)
+            i = self.add_long_id(long_id)
+        return i
+
+    def add_long_id(self, long_id: str) -> int:
+        """Client.addLongClientId (client.ts:685-688): always a new short id (re-adding a known long
+        id re-points it, as clientNameToIds.put does)."""
+        if len(self.clients) >= MAX_CLIENTS:
+            raise Unsupported(f"more than {MAX_CLIENTS} client ids in one document")
+        i = len(self.clients)
+        self.client_ix[long_id] = i
+        self.clients.append(long_id)
         return i
 
     def _text(self, s: str) -> tuple[int, int]:
@@ -138,13 +152,23 @@ class DocLog:
     def local_annotate(self, start: int, end: int, props: dict, interner: Interner) -> None:
         self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, 0, 0, 0, start, end, interner.propop(props), 0))
 
-    def start_collab(self, long_id: str, min_seq: int = 0, current_seq: int = 0) -> None:
-        """Client.startOrUpdateCollaboration (client.ts:1133-1155)."""
+    def start_collab(self, long_id: str | None, min_seq: int = 0, current_seq: int = 0) -> None:
+        """Client.startOrUpdateCollaboration (client.ts:1133-1155): an undefined id keeps the client
+        local (detached container); the first id registers a new short id (addLongClientId, even for
+        a long id seen before) and starts collaboration as that client; a later id renames the
+        observer (its short id now maps back to the new long id, and both long ids map to it)."""
+        if long_id is None:
+            return
         if self.observer_id is None:
             self.observer_id = long_id
-            me = self.short_id(long_id)
+            me = self.add_long_id(long_id)
             self.collaborating = True
             self.ops.append((abi.OP_START_COLLAB, 0, me, current_seq, 0, min_seq, 0, 0, 0, 0))
+        else:
+            me = self.client_ix[self.observer_id]
+            self.observer_id = long_id
+            self.client_ix[long_id] = me
+            self.clients[me] = long_id
 
     # -- loading a summary (SnapshotLoader, snapshotLoader.ts:41-257)
     def _snapshot_seg(self, spec: Any, interner: Interner, op_type: int, flags: int) -> None:

@@ -141,12 +141,27 @@ __global__ void reset_kernel(DocHdr* h, uint32_t n) {
     h[d] = z;
 }
 
-__global__ void cursor_reset_kernel(DocHdr* h, uint32_t n) {
+__global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_t n) {
     uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d < n) {
         h[d].op_cursor = 0;
         h[d].dused = 0;  // delta ranges are per batch
+        // more short client ids than the engine's 8-bit client field holds: the document stays on
+        // the TypeScript Client (MTR_MAX_CLIENTS)
+        if (docs[d].n_clients > MTR_MAX_CLIENTS && h[d].status == MTR_OK) {
+            h[d].status = MTR_ERR_UNSUPPORTED;
+            h[d].fail_op = 0;
+        }
     }
+}
+
+// any op of the batch flagged MTR_F_DELTA (the host sizes delta buffers only when one is)
+__global__ void any_delta_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    bool any = false;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        any = any || (ops[i].flags & MTR_F_DELTA) != 0;
+    if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(out, 1);
 }
 
 // out[0] = max nseg, out[1] = max remaining ops, out[2] = max heapn
@@ -366,7 +381,16 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
     e->has_delta = false;
     e->h_doff.assign(size_t(b->n_docs) + 1, 0);
     bool any = false;
-    for (uint64_t i = 0; i < b->n_ops && !any; i++) any = (b->ops[i].flags & MTR_F_DELTA) != 0;
+    if (b->n_ops) {  // one pass over the uploaded ops on the device instead of the host
+        HIPCHK(hipMemsetAsync(e->red.p, 0, sizeof(int32_t), e->stream));
+        const uint64_t blocks = std::min<uint64_t>((b->n_ops + 255) / 256, 4096);
+        any_delta_kernel<<<uint32_t(blocks), 256, 0, e->stream>>>(e->ops.p, b->n_ops, e->red.p);
+        HIPCHK(hipGetLastError());
+        int32_t flag = 0;
+        HIPCHK(hipMemcpyAsync(&flag, e->red.p, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        any = flag != 0;
+    }
     if (any) {
         std::vector<uint64_t> need(b->n_docs, 0);
         for (uint32_t d = 0; d < b->n_docs; d++) {
@@ -404,19 +428,12 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
         HIPCHK(hipMemcpyAsync(e->doff.p, e->h_doff.data(), (size_t(b->n_docs) + 1) * sizeof(uint64_t),
                               hipMemcpyHostToDevice, e->stream));
     }
-    cursor_reset_kernel<<<(b->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, b->n_docs);
-    HIPCHK(hipGetLastError());
+    if (b->n_docs) {  // (an empty batch launches nothing: a 0-block grid is an invalid launch)
+        cursor_reset_kernel<<<(b->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, b->n_docs);
+        HIPCHK(hipGetLastError());
+    }
     e->summarized = false;
     return MTR_OK;
-}
-
-static int read_state(mtr_engine* e, int32_t out[3]) {
-    HIPCHK(hipMemsetAsync(e->red.p, 0, 4 * sizeof(int32_t), e->stream));
-    scan_state_kernel<<<(e->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, e->n_docs, e->red.p);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, e->red.p, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    return 0;
 }
 
 static int run_impl(mtr_engine* e, int gen);
@@ -684,6 +701,7 @@ int mtr_generate(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch* table
         return MTR_ERR_BAD_OP;
     }
     const uint32_t n = cfg->n_docs, per = cfg->ops_per_doc + 1;
+    if (n == 0) return mtr_reset(e);
     std::vector<mtr_doc_desc> docs(n);
     for (uint32_t d = 0; d < n; d++) {
         docs[d].op_begin = uint64_t(d) * per;
@@ -723,6 +741,7 @@ int mtr_generate_matrix(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch
         set_err("mtr_generate_matrix: bad configuration");
         return MTR_ERR_BAD_OP;
     }
+    if (n == 0) return mtr_reset(e);
     for (uint32_t m = 0; m < n; m++) {  // pair the vectors (mtr_set_matrix) unless already paired so
         const uint32_t r = 2 * m, c = 2 * m + 1;
         if (e->h_kind[r] == 1 && e->h_part[r] == c) continue;
@@ -777,13 +796,56 @@ int mtr_download_batch(mtr_engine* e, uint32_t lo, uint32_t hi, mtr_doc_desc* do
     }
     std::vector<mtr_doc_desc> dd(hi - lo);
     if (hi > lo) HIPCHK(hipMemcpy(dd.data(), e->docs.p + lo, (hi - lo) * sizeof(mtr_doc_desc), hipMemcpyDeviceToHost));
-    uint64_t op_at = 0, text_at = 0;
+    // op lists: one copy per run of documents whose lists are adjacent on the device (a recorded
+    // batch is one run); empty lists (matrix cols vectors) never break a run
+    uint64_t op_at = 0, text_at = 0, text_need = 0;
+    if (ops) {
+        uint64_t run_src = 0, run_dst = 0, run_n = 0;
+        for (uint32_t i = 0; i < hi - lo; i++) {
+            const mtr_doc_desc& x = dd[i];
+            if (x.op_count == 0) continue;
+            if (run_n && x.op_begin != run_src + run_n) {
+                HIPCHK(hipMemcpy(ops + run_dst, e->ops.p + run_src, run_n * sizeof(mtr_op), hipMemcpyDeviceToHost));
+                run_n = 0;
+            }
+            if (!run_n) {
+                run_src = x.op_begin;
+                run_dst = op_at;
+            }
+            run_n += x.op_count;
+            op_at += x.op_count;
+        }
+        if (run_n) HIPCHK(hipMemcpy(ops + run_dst, e->ops.p + run_src, run_n * sizeof(mtr_op), hipMemcpyDeviceToHost));
+    }
+    for (uint32_t i = 0; i < hi - lo; i++) text_need += dd[i].text_count;
+    if (text && text_need && text_need <= text_cap) {
+        // texts: one copy of the span when the gaps between documents are small, then compacted
+        uint64_t t0 = UINT64_MAX, t1 = 0;
+        for (uint32_t i = 0; i < hi - lo; i++)
+            if (dd[i].text_count) {
+                t0 = std::min<uint64_t>(t0, dd[i].text_base);
+                t1 = std::max<uint64_t>(t1, dd[i].text_base + dd[i].text_count);
+            }
+        if (t1 - t0 <= 4 * text_need + (1u << 20)) {
+            std::vector<uint16_t> span(t1 - t0);
+            HIPCHK(hipMemcpy(span.data(), e->btext.p + t0, span.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < hi - lo; i++) {
+                std::memcpy(text + text_at, span.data() + (dd[i].text_base - t0), dd[i].text_count * sizeof(uint16_t));
+                text_at += dd[i].text_count;
+            }
+        } else {
+            for (uint32_t i = 0; i < hi - lo; i++) {
+                if (dd[i].text_count)
+                    HIPCHK(hipMemcpy(text + text_at, e->btext.p + dd[i].text_base, dd[i].text_count * sizeof(uint16_t),
+                                     hipMemcpyDeviceToHost));
+                text_at += dd[i].text_count;
+            }
+        }
+    }
+    op_at = 0;
+    text_at = 0;
     for (uint32_t i = 0; i < hi - lo; i++) {
         mtr_doc_desc x = dd[i];
-        if (ops) HIPCHK(hipMemcpy(ops + op_at, e->ops.p + x.op_begin, x.op_count * sizeof(mtr_op), hipMemcpyDeviceToHost));
-        if (text && text_at + x.text_count <= text_cap && x.text_count)
-            HIPCHK(hipMemcpy(text + text_at, e->btext.p + x.text_base, x.text_count * sizeof(uint16_t),
-                             hipMemcpyDeviceToHost));
         x.op_begin = op_at;
         x.text_base = text_at;
         op_at += x.op_count;
@@ -874,19 +936,43 @@ int mtr_sync(mtr_engine* e) {
     return MTR_OK;
 }
 
-int64_t mtr_get_summary(mtr_engine* e, uint32_t doc, uint8_t* out, int64_t cap, int64_t* blob_len, int32_t max_blobs) {
+// one document's summary record in the output buffer: u32 nb, u32 len[nb], blob bytes
+static int summary_record(mtr_engine* e, uint32_t doc, std::vector<uint8_t>& buf) {
     if (!e->summarized || doc >= e->n_docs) {
         set_err("no summary for this document (call mtr_summarize first)");
         return -1;
     }
-    (void)hipSetDevice(e->device);
-    const int64_t sz = e->h_size[doc];
-    std::vector<uint8_t> buf(static_cast<size_t>(sz));
-    if (hipMemcpy(buf.data(), e->out.p + e->h_off[doc], size_t(sz), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    buf.resize(size_t(e->h_size[doc]));
+    HIPCHK(hipMemcpy(buf.data(), e->out.p + e->h_off[doc], buf.size(), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int mtr_summary_info(mtr_engine* e, uint32_t doc, int64_t* n_blobs, int64_t* n_bytes) {
+    if (!e->summarized || doc >= e->n_docs) {
+        set_err("no summary for this document (call mtr_summarize first)");
+        return -1;
+    }
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint32_t nb = 0;
+    HIPCHK(hipMemcpy(&nb, e->out.p + e->h_off[doc], 4, hipMemcpyDeviceToHost));
+    if (n_blobs) *n_blobs = nb;
+    if (n_bytes) *n_bytes = e->h_size[doc] - 4 - 4 * int64_t(nb);
+    return MTR_OK;
+}
+
+int64_t mtr_get_summary(mtr_engine* e, uint32_t doc, uint8_t* out, int64_t cap, int64_t* blob_len, int32_t max_blobs) {
+    std::vector<uint8_t> buf;
+    if (summary_record(e, doc, buf)) return -1;
     uint32_t nb;
     std::memcpy(&nb, buf.data(), 4);
-    const int64_t payload = sz - 4 - 4 * int64_t(nb);
-    if (payload > cap || int32_t(nb) > max_blobs) return -payload;
+    const int64_t payload = int64_t(buf.size()) - 4 - 4 * int64_t(nb);
+    if (payload > cap || int64_t(nb) > int64_t(max_blobs) || (payload > 0 && !out) || !blob_len) {
+        set_err("mtr_get_summary: buffers smaller than mtr_summary_info reports");
+        return MTR_SUMMARY_TOO_SMALL;
+    }
     int64_t off = 4 + 4 * int64_t(nb);
     int64_t w = 0;
     for (uint32_t k = 0; k < nb; k++) {
@@ -898,6 +984,42 @@ int64_t mtr_get_summary(mtr_engine* e, uint32_t doc, uint8_t* out, int64_t cap, 
         w += len;
     }
     return int64_t(nb);
+}
+
+int64_t mtr_get_summaries(mtr_engine* e, uint32_t lo, uint32_t hi, uint8_t* out, int64_t cap, int64_t* doc_off) {
+    if (!e->summarized || hi > e->n_docs || lo > hi) {
+        set_err("mtr_get_summaries: bad range or no summary (call mtr_summarize first)");
+        return -1;
+    }
+    if (lo == hi) {
+        if (doc_off) doc_off[0] = 0;
+        return 0;
+    }
+    const int64_t base = e->h_off[lo];
+    const int64_t total = e->h_off[hi - 1] + e->h_size[hi - 1] - base;  // documents are laid out in order
+    if (total > cap) return -total;
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(out, e->out.p + base, size_t(total), hipMemcpyDeviceToHost));
+    if (doc_off) {
+        for (uint32_t d = lo; d < hi; d++) doc_off[d - lo] = e->h_off[d] - base;
+        doc_off[hi - lo] = total;
+    }
+    return total;
+}
+
+void* mtr_host_alloc(uint64_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<uint64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+        set_err("hipHostMalloc failed for " + std::to_string(bytes) + " bytes");
+        return nullptr;
+    }
+    return p;
+}
+
+int mtr_host_free(void* p) {
+    if (p && hipHostFree(p) != hipSuccess) return -1;
+    return MTR_OK;
 }
 
 int mtr_summary_hashes(mtr_engine* e, uint64_t* out, uint32_t n_docs) {

@@ -51,6 +51,14 @@ def lib():
         L.mtr_submit.restype = C.c_int
         L.mtr_get_summary.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]
         L.mtr_get_summary.restype = C.c_int64
+        L.mtr_summary_info.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.mtr_summary_info.restype = C.c_int
+        L.mtr_get_summaries.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p]
+        L.mtr_get_summaries.restype = C.c_int64
+        L.mtr_host_alloc.argtypes = [C.c_uint64]
+        L.mtr_host_alloc.restype = C.c_void_p
+        L.mtr_host_free.argtypes = [C.c_void_p]
+        L.mtr_host_free.restype = C.c_int
         L.mtr_summary_hashes.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
         L.mtr_summary_hashes.restype = C.c_int
         L.mtr_summary_bytes.argtypes = [C.c_void_p]
@@ -85,6 +93,32 @@ def lib():
 
 def _err() -> str:
     return (lib().mtr_last_error() or b"").decode(errors="replace")
+
+
+class _Pinned:
+    """Owner of one mtr_host_alloc block (freed when the last array view goes away)."""
+
+    def __init__(self, nbytes):
+        self.p = lib().mtr_host_alloc(max(int(nbytes), 1))
+        if not self.p:
+            raise EngineError(f"mtr_host_alloc failed: {_err()}")
+        self.nbytes = max(int(nbytes), 1)
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            lib().mtr_host_free(self.p)
+            self.p = None
+
+
+def pinned(shape, dtype) -> np.ndarray:
+    """A numpy array in page-locked host memory (mtr_host_alloc): op uploads and summary downloads
+    from it run at full PCIe rate."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+    owner = _Pinned(n * dt.itemsize)
+    buf = (C.c_uint8 * owner.nbytes).from_address(owner.p)
+    buf._owner = owner  # the array holds `buf`, `buf` holds the owner
+    return np.frombuffer(buf, dtype=dt, count=n).reshape(shape)
 
 
 class Engine:
@@ -165,35 +199,69 @@ class Engine:
                                              text.ctypes.data, 0), "mtr_download_batch")
         return with_docs(self._tabs, docs[0::2].copy(), ops[:n * per], text)
 
-    def download(self, lo, hi):
-        """The recorded batch of documents [lo, hi) as a host Batch (sharing the recipe tables)."""
+    def download(self, lo, hi, pinned_memory=False):
+        """The recorded batch of documents [lo, hi) as a host Batch (sharing the recipe tables); with
+        pinned_memory the op and text arrays live in page-locked memory (full-rate uploads)."""
         from .synth import with_docs
         n = hi - lo
         per = self._cfg.ops_per_doc + 1
+        alloc = (lambda k, dt: pinned(k, dt)) if pinned_memory else (lambda k, dt: np.zeros(k, dtype=dt))
         docs = np.zeros(n, dtype=abi.DOC_DTYPE)
-        ops = np.zeros(n * per, dtype=abi.OP_DTYPE)
+        ops = alloc(n * per, abi.OP_DTYPE)
         cap = n * int(self._cfg.text_cap)
-        text = np.zeros(max(cap, 1), dtype="<u2")
+        text = alloc(max(cap, 1), "<u2")
         self._check(lib().mtr_download_batch(self.h, lo, hi, docs.ctypes.data, ops.ctypes.data, text.ctypes.data, cap),
                     "mtr_download_batch")
         used = int(docs["text_base"][-1] + docs["text_count"][-1]) if n else 0
-        return with_docs(self._tabs, docs, ops, text[:max(used, 1)].copy())
+        text = text[:max(used, 1)] if pinned_memory else text[:max(used, 1)].copy()
+        return with_docs(self._tabs, docs, ops, text)
 
     def summary(self, doc) -> list[bytes]:
-        cap = 1 << 16
-        while True:
-            out = np.zeros(cap, dtype="u1")
-            lens = np.zeros(4096, dtype="<i8")
-            r = lib().mtr_get_summary(self.h, doc, out.ctypes.data, cap, lens.ctypes.data, 4096)
-            if r >= 0:
-                res, off = [], 0
-                for k in range(r):
-                    res.append(out[off:off + lens[k]].tobytes())
-                    off += int(lens[k])
-                return res
-            if r == -1:
-                raise EngineError(_err())
-            cap = -r + 16
+        nb, nbytes = C.c_int64(0), C.c_int64(0)
+        self._check(lib().mtr_summary_info(self.h, doc, C.byref(nb), C.byref(nbytes)), "mtr_summary_info")
+        out = np.zeros(max(nbytes.value, 1), dtype="u1")
+        lens = np.zeros(max(nb.value, 1), dtype="<i8")
+        r = lib().mtr_get_summary(self.h, doc, out.ctypes.data, out.size, lens.ctypes.data, nb.value)
+        if r < 0:
+            raise EngineError(f"mtr_get_summary failed ({r}): {_err()}")
+        res, off = [], 0
+        for k in range(r):
+            res.append(out[off:off + lens[k]].tobytes())
+            off += int(lens[k])
+        return res
+
+    def summaries(self, lo=0, hi=None, out=None):
+        """Every blob of documents [lo, hi) in one device-to-host copy (mtr_get_summaries).  Returns
+        (buffer, doc_off): document lo + i's record is buffer[doc_off[i]:doc_off[i + 1]] = u32 blob
+        count nb, nb u32 lengths, the blob bytes.  `out` (a u1 array, e.g. pinned) is reused when big
+        enough."""
+        hi = self._n_docs() if hi is None else hi
+        doc_off = np.zeros(hi - lo + 1, dtype="<i8")
+        need = lib().mtr_get_summaries(self.h, lo, hi, None, 0, doc_off.ctypes.data)
+        if need == -1:
+            raise EngineError(_err())
+        need = -need if need < 0 else need
+        if out is None or out.size < need:
+            out = np.zeros(max(need, 1), dtype="u1")
+        r = lib().mtr_get_summaries(self.h, lo, hi, out.ctypes.data, out.size, doc_off.ctypes.data)
+        if r < 0:
+            raise EngineError(f"mtr_get_summaries failed ({r}): {_err()}")
+        return out, doc_off
+
+    @staticmethod
+    def split_record(buf, a, b) -> list[bytes]:
+        """The blobs of one document record of :meth:`summaries`."""
+        nb = int(np.frombuffer(buf[a:a + 4].tobytes(), "<u4")[0])
+        lens = np.frombuffer(buf[a + 4:a + 4 + 4 * nb].tobytes(), "<u4")
+        res, off = [], a + 4 + 4 * nb
+        for n in lens:
+            res.append(buf[off:off + int(n)].tobytes())
+            off += int(n)
+        assert off == b, "malformed summary record"
+        return res
+
+    def _n_docs(self):
+        return int(self.stats()["docs"])
 
     def hashes(self, n=None) -> np.ndarray:
         n = self.max_docs if n is None else n

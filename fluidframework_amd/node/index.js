@@ -35,6 +35,7 @@ const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_R
     START_COLLAB: 12 };
 const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, DELTA: 64 };
 const NULL_VALUE = 0xFFFFFFFF;
+const MAX_CLIENTS = 253;  // include/mtr_types.h MTR_MAX_CLIENTS: short ids per engine document
 const NOT_INDEX = 0xFFFFFFFF;
 const STATUS = { OK: 0, INSERT_FAILED: 1, BAD_OP: 2, CAPACITY: 3, UNSUPPORTED: 4, ASSERT: 0x1000 };
 // protocol-definitions SummaryType
@@ -125,9 +126,15 @@ class DocLog {
         this.observerId = undefined; this.clients = []; this.clientIx = new Map();
         this.ops = []; this.text = []; this.collaborating = false;
     }
-    shortId(longId) {  // Client.getOrAddShortClientId, client.ts:673-688
-        let i = this.clientIx.get(longId);
-        if (i === undefined) { i = this.clients.length; this.clientIx.set(longId, i); this.clients.push(longId); }
+    shortId(longId) {  // Client.getOrAddShortClientId, client.ts:673-677
+        const i = this.clientIx.get(longId);
+        return i === undefined ? this.addLongId(longId) : i;
+    }
+    addLongId(longId) {  // Client.addLongClientId, client.ts:685-688: always a new short id
+        if (this.clients.length >= MAX_CLIENTS) throw new UnsupportedError('more than ' + MAX_CLIENTS + ' client ids');
+        const i = this.clients.length;
+        this.clientIx.set(longId, i);
+        this.clients.push(longId);
         return i;
     }
     _text(s) {
@@ -162,11 +169,17 @@ class DocLog {
     localRemove(start, end) { this.push(OP.LOCAL_REMOVE, 0, 0, 0, 0, 0, start, end, 0, 0); }
     localAnnotate(start, end, props, it) { this.push(OP.LOCAL_ANNOTATE, 0, 0, 0, 0, 0, start, end, it.propop(props), 0); }
     startCollab(longId, minSeq, currentSeq) {  // client.ts:1133-1155
+        if (longId === undefined) return;  // detached: stay local until attached
         if (this.observerId === undefined) {
             this.observerId = longId;
-            this.shortId(longId);
+            const me = this.addLongId(longId);
             this.collaborating = true;
-            this.push(OP.START_COLLAB, 0, 0, currentSeq, 0, minSeq, 0, 0, 0, 0);
+            this.push(OP.START_COLLAB, 0, me, currentSeq, 0, minSeq, 0, 0, 0, 0);
+        } else {  // reconnect under a new id: the observer's short id is renamed
+            const me = this.clientIx.get(this.observerId);
+            this.observerId = longId;
+            this.clientIx.set(longId, me);
+            this.clients[me] = longId;
         }
     }
     seqUpdate(min, seq) { this.push(OP.SEQ, F.LAST, 0, seq, seq, min, 0, 0, 0, 0); }

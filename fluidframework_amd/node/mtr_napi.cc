@@ -183,11 +183,11 @@ napi_value GetSummary(napi_env env, napi_callback_info info) {
     if (!e) return nullptr;
     uint32_t doc = 0;
     NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
-    int64_t lens[256];
-    const int64_t need = mtr_get_summary(e, doc, nullptr, 0, lens, 256);  // -(bytes) when cap is too small
-    if (need == -1) return throw_engine(env, "mtr_get_summary");
-    std::vector<uint8_t> buf(size_t(need < 0 ? -need : 0) + 1);
-    const int64_t nb = mtr_get_summary(e, doc, buf.data(), int64_t(buf.size()), lens, 256);
+    int64_t n_blobs = 0, n_bytes = 0;
+    if (mtr_summary_info(e, doc, &n_blobs, &n_bytes) != MTR_OK) return throw_engine(env, "mtr_summary_info");
+    std::vector<int64_t> lens(size_t(n_blobs) + 1);
+    std::vector<uint8_t> buf(size_t(n_bytes) + 1);
+    const int64_t nb = mtr_get_summary(e, doc, buf.data(), int64_t(buf.size()), lens.data(), int32_t(n_blobs));
     if (nb < 0) return throw_engine(env, "mtr_get_summary");
     napi_value arr;
     NAPI_CALL(env, napi_create_array_with_length(env, size_t(nb), &arr));

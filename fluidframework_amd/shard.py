@@ -21,6 +21,42 @@ def doc_range(rank: int, world: int, docs_per_rank: int) -> tuple[int, int]:
     return rank * docs_per_rank, (rank + 1) * docs_per_rank
 
 
+def strong_range(rank: int, world: int, total_docs: int) -> tuple[int, int]:
+    """Strong scaling: the node's `total_docs` documents split into `world` contiguous ranges whose
+    sizes differ by at most one (the LPT assignment for documents of equal cost, e.g. one synthetic
+    recipe)."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world of {world}")
+    base, rem = divmod(total_docs, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def doc_cost(op_counts, seg_estimate) -> np.ndarray:
+    """Estimated apply cost of each document, sum over its ops of the leaves it scans (SURVEY.md 8e:
+    ops x est. S): a document growing from s0 leaves by ~1 leaf per op costs ops * (s0 + ops / 2)."""
+    ops = np.asarray(op_counts, dtype=np.float64)
+    s0 = np.asarray(seg_estimate, dtype=np.float64)
+    return ops * (s0 + ops / 2.0 + 1.0)
+
+
+def lpt_assign(costs, world: int) -> list[np.ndarray]:
+    """Greedy longest-processing-time assignment of documents to ranks: documents in
+    decreasing cost, each to the least-loaded rank (ties: lowest rank).  Returns each rank's document
+    indices in ascending order (their order in the rank's batch)."""
+    import heapq
+
+    costs = np.asarray(costs, dtype=np.float64)
+    order = np.lexsort((np.arange(len(costs)), -costs))  # cost descending, index ascending
+    heap = [(0.0, r) for r in range(world)]
+    out: list[list[int]] = [[] for _ in range(world)]
+    for d in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(int(d))
+        heapq.heappush(heap, (load + float(costs[d]), r))
+    return [np.array(sorted(x), dtype=np.int64) for x in out]
+
+
 def digest(hashes: np.ndarray) -> int:
     """Order- and sharding-independent digest: sum of per-document uint64 hashes mod 2**64."""
     h = np.asarray(hashes, dtype=np.uint64)

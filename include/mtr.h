@@ -81,11 +81,30 @@ int mtr_summarize(mtr_engine* e);
 /* Wait for all queued work on the engine stream. */
 int mtr_sync(mtr_engine* e);
 
+/* Size of one document's summary after mtr_summarize (SnapshotV1/Legacy emit, snapshotV1.ts:122-178,
+ * snapshotlegacy.ts:122-182): *n_blobs = number of blobs, *n_bytes = their total payload bytes.
+ * Callers size the buffers of mtr_get_summary from it.  Returns MTR_OK or -1 (mtr_last_error). */
+int mtr_summary_info(mtr_engine* e, uint32_t doc, int64_t* n_blobs, int64_t* n_bytes);
+
 /* Blobs of one document after mtr_summarize: writes them back-to-back to out (cap bytes),
  * blob_len[k] = bytes of blob k (order: header, body / body_0, body_1, ...).
- * Returns the number of blobs, or -(bytes needed) when cap is too small. */
+ * Returns the number of blobs (>= 1); MTR_SUMMARY_TOO_SMALL when cap or max_blobs is smaller than
+ * mtr_summary_info reports (nothing written); -1 on any other error (mtr_last_error). */
+#define MTR_SUMMARY_TOO_SMALL (-3)
 int64_t mtr_get_summary(mtr_engine* e, uint32_t doc, uint8_t* out, int64_t cap, int64_t* blob_len,
                         int32_t max_blobs);
+
+/* Bulk download of the summaries of documents [lo, hi) in ONE device-to-host copy (a scribe hands
+ * every blob of a batch to storage at once).  Layout: per document, in order, a little-endian u32
+ * blob count nb, nb u32 blob lengths, then the blob bytes.  doc_off[i] (hi - lo + 1 entries) = offset
+ * of document lo + i in out; doc_off[hi - lo] = total bytes.  Returns the total bytes, or -(bytes
+ * needed) when cap is too small (nothing written; a non-empty range always needs >= 8 bytes), or -1
+ * on error.  `out` may be pinned memory from mtr_host_alloc for full PCIe bandwidth. */
+int64_t mtr_get_summaries(mtr_engine* e, uint32_t lo, uint32_t hi, uint8_t* out, int64_t cap, int64_t* doc_off);
+
+/* Page-locked host memory (hipHostMalloc) for op batches and summary downloads; NULL on failure. */
+void* mtr_host_alloc(uint64_t bytes);
+int mtr_host_free(void* p);
 
 /* 64-bit FNV-1a of every document's summary (blob lengths + bytes), n_docs entries. */
 int mtr_summary_hashes(mtr_engine* e, uint64_t* out, uint32_t n_docs);

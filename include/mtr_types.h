@@ -97,6 +97,12 @@ typedef struct mtr_delta {
  */
 #define MTR_CLIENT_NONCOLLAB 0xFFFEu
 
+/* Short client ids a document may register (the engine keeps a short id in 8 bits next to the
+ * LocalClientId / NonCollabClient codes 0xff / 0xfe).  The reference's ids are unbounded
+ * (client.ts:673-688); mtr_submit marks a document with more clients MTR_ERR_UNSUPPORTED (the shim
+ * keeps it on the TypeScript Client) and the host packers refuse it up front. */
+#define MTR_MAX_CLIENTS 253u
+
 typedef struct mtr_op {
     uint8_t  type;     /* MTR_OP_* */
     uint8_t  flags;    /* MTR_F_* */

@@ -1,0 +1,173 @@
+"""GPU tests of the boundary additions and of full-size documents:
+
+* bulk summary download (mtr_get_summaries) against the per-document reads, mtr_summary_info sizing,
+  the MTR_SUMMARY_TOO_SMALL answer, empty batches, the short-client-id cap;
+* documents at C2 (5,000 messages, 16 writers, lag 64) and C4 (20,000 matrix messages) size against
+  the oracle;
+* document sharding through the real engine: two engines holding rank 0 / rank 1's document ranges
+  give the same run digest as one engine holding all of them.
+"""
+import numpy as np
+import pytest
+
+from fluidframework_amd import abi, shard
+from fluidframework_amd.batch import DocLog, Interner, build_batch
+from oracle.oracle import OracleDoc, generate, generate_matrix, options, replay_matrix_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(n_docs, **kw):
+    from fluidframework_amd.engine import Engine
+    caps = dict(max_segments=8192, heap_entries=8192, text_units=1 << 18, prop_words=1 << 18, remover_cells=1 << 14)
+    caps.update(kw)
+    return Engine(n_docs, **caps)
+
+
+def test_bulk_summaries_equal_per_document_reads():
+    from fluidframework_amd.engine import Engine, lib, pinned
+    from fluidframework_amd.synth import make_cfg, tables
+
+    n, ops = 64, 600
+    cfg = make_cfg(n, ops, writers=8, max_lag=32, seed=0xb01c)
+    eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
+                  ops_per_launch=64, chunk_size=256)  # small chunks: several blobs per document
+    eng.generate(cfg, tables(writers=8))
+    eng.reset()
+    eng.run()
+    eng.summarize()
+    out = pinned(eng.summary_bytes() + 64, "u1")
+    buf, off = eng.summaries(0, n, out=out)
+    assert int(off[-1]) == eng.summary_bytes()
+    for d in range(n):
+        assert Engine.split_record(buf, int(off[d]), int(off[d + 1])) == eng.summary(d)
+    # a sub-range starts at offset 0
+    buf2, off2 = eng.summaries(5, 9)
+    for i, d in enumerate(range(5, 9)):
+        assert Engine.split_record(buf2, int(off2[i]), int(off2[i + 1])) == eng.summary(d)
+    # sizing: too-small buffers are refused without writing, never read as a blob count
+    import ctypes as C
+    nb, nbytes = C.c_int64(0), C.c_int64(0)
+    assert lib().mtr_summary_info(eng.h, 3, C.byref(nb), C.byref(nbytes)) == 0
+    assert nb.value == len(eng.summary(3)) and nbytes.value == sum(len(x) for x in eng.summary(3))
+    small = np.zeros(max(nbytes.value - 1, 1), dtype="u1")
+    lens = np.zeros(max(nb.value, 1), dtype="<i8")
+    r = lib().mtr_get_summary(eng.h, 3, small.ctypes.data, small.size, lens.ctypes.data, nb.value)
+    assert r == -3  # MTR_SUMMARY_TOO_SMALL
+    r = lib().mtr_get_summary(eng.h, 3, small.ctypes.data, 1 << 30, lens.ctypes.data, nb.value - 1)
+    assert r == -3
+    need = lib().mtr_get_summaries(eng.h, 0, n, None, 0, None)
+    assert need == -eng.summary_bytes()
+
+
+def test_empty_batch():
+    eng = _engine(4)
+    b = build_batch([], Interner())
+    eng.apply(b)
+    eng.summarize()
+    assert eng.stats()["ops"] == 0
+
+
+def test_too_many_clients_is_unsupported_per_document():
+    """A document with more short ids than the engine's 8-bit client field (MTR_MAX_CLIENTS) is
+    marked unsupported at submit; the other documents of the batch are applied normally."""
+    it = Interner()
+    good, bad = DocLog(), DocLog()
+    for log in (good, bad):
+        log.local_insert(0, "hello", it)
+        log.start_collab("observer")
+    # bypass the packer's own refusal (it raises Unsupported at MAX_CLIENTS)
+    bad.clients += [f"c{i}" for i in range(300)]
+    b = build_batch([good, bad], it)
+    eng = _engine(2)
+    eng.apply(b)
+    assert eng.status(0)[0] == abi.MTR_OK and eng.text(0) == "hello"
+    assert eng.status(1)[0] == abi.MTR_ERR_UNSUPPORTED
+
+
+def test_c2_size_documents_match_oracle():
+    """C2-sized documents (5,000 messages, 16 writers, lag <= 64): up to ~1,300 leaves,
+    the largest LDS classes; every summary equals the oracle's."""
+    from fluidframework_amd.synth import make_cfg, tables
+
+    n, ops = 64, 5000
+    cfg = make_cfg(n, ops, writers=16, max_lag=64, seed=0xc2)
+    tabs = tables(writers=16)
+    b, ohash, ost = generate(cfg, tabs, 0, n, threads=16)
+    assert (ost == 0).all()
+    eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 8192,
+                  prop_words=1 << 17, remover_cells=8192, ops_per_launch=48)
+    eng.apply(b)
+    eng.summarize()
+    for d in range(n):
+        st, op = eng.status(d)
+        assert st == 0, f"doc {d}: status {st:#x} at op {op}"
+    ghash = eng.hashes(n)
+    bad = np.nonzero(ghash != ohash)[0]
+    if bad.size:
+        d = int(bad[0])
+        orc = OracleDoc(options())
+        assert orc.apply(b, d) == 0
+        assert eng.summary(d) == orc.summarize(b, d)
+    assert bad.size == 0
+    st = eng.stats()
+    assert st["max_leaves"] > 700, st  # the test reaches the large classes
+
+
+def test_c4_size_matrices_match_oracle():
+    """C4-sized SharedMatrix documents (20,000 messages per matrix, 20 % row/col splices,
+    80 % setCell, lag <= 64): both vectors' summaries (segments + handleTable) equal the oracle's."""
+    from test_matrix import expand_pairs, matrix_cfg
+    from fluidframework_amd.synth import tables
+
+    n, ops = 16, 20000
+    cfg = matrix_cfg(n, ops, writers=8, max_lag=64)
+    tabs = tables(writers=8)
+    gb, _, status = generate_matrix(cfg, tabs, 0, n, threads=16)
+    assert (status == 0).all()
+    b = expand_pairs(gb, tabs)
+    eng = _engine(2 * n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * ops + 1024,
+                  prop_words=1024, remover_cells=8192, ops_per_launch=48)
+    for m in range(n):
+        eng.set_matrix(2 * m, 2 * m + 1)
+    eng.apply(b)
+    eng.summarize()
+    for d in range(2 * n):
+        st, op = eng.status(d)
+        assert st == 0, f"document {d}: status {st:#x} at op {op}"
+    _, oh, st = replay_matrix_batch(gb, 0, n, 16)
+    assert (st == 0).all()
+    assert np.array_equal(eng.hashes(2 * n), oh)
+
+
+def test_two_engines_as_two_ranks_equal_one_engine():
+    """Document sharding through the real engine: rank 0 / rank 1 of a strong-scaling split (two
+    engines on device 0, each recording and replaying its own document range) reduce to the same run
+    digest and message count as one engine holding every document."""
+    from fluidframework_amd.synth import make_cfg, tables
+
+    total, ops = 300, 500
+    tabs = tables(writers=8)
+    digests, msgs = [], 0
+    for rank in range(2):
+        lo, hi = shard.strong_range(rank, 2, total)
+        cfg = make_cfg(hi - lo, ops, writers=8, max_lag=32, doc_base=lo)
+        eng = _engine(hi - lo, max_segments=2 * ops + 128, heap_entries=2 * ops + 128,
+                      text_units=2 * int(cfg.text_cap) + 1024, ops_per_launch=48)
+        eng.generate(cfg, tabs)
+        eng.reset()
+        eng.run()
+        eng.summarize()
+        assert eng.stats()["bad_docs"] == 0
+        digests.append(shard.digest(eng.hashes(hi - lo)))
+        msgs += (hi - lo) * ops
+        eng.close()
+    cfg = make_cfg(total, ops, writers=8, max_lag=32)
+    one = _engine(total, max_segments=2 * ops + 128, heap_entries=2 * ops + 128,
+                  text_units=2 * int(cfg.text_cap) + 1024, ops_per_launch=48)
+    one.generate(cfg, tabs)
+    one.reset()
+    one.run()
+    one.summarize()
+    assert msgs == total * ops
+    assert (sum(digests) & shard.MASK64) == shard.digest(one.hashes(total))

@@ -12,7 +12,8 @@ import numpy as np
 import pytest
 
 from fixtures import load_replay, replay_files, replay_log
-from fluidframework_amd.batch import Interner, build_batch
+from fluidframework_amd import abi
+from fluidframework_amd.batch import MAX_CLIENTS, DocLog, Interner, Unsupported, build_batch
 from oracle.oracle import OracleDoc, options
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -66,12 +67,70 @@ def _py_batch(paths):
     return build_batch(logs, it)
 
 
-def test_js_packer_matches_python_packer():
+def _py_batch_pre(paths, pre):
+    """The --pre mode of tests/node/pack_batch.js: messages before startOrUpdateCollaboration, an
+    undefined-id call (stays local), then a reconnect under a new id halfway (client.ts:1133-1155)."""
+    it = Interner()
+    logs = []
+    for p in paths:
+        groups = load_replay(p)
+        log = DocLog()
+        if groups[0]["initialText"]:
+            log.local_insert(0, groups[0]["initialText"], it)
+        msgs = [m for g in groups for m in g["msgs"]]
+        for m in msgs[:pre]:
+            log.message(m, it)
+        log.start_collab(None)
+        log.start_collab("A")
+        half = pre + (len(msgs) - pre) // 2
+        for m in msgs[pre:half]:
+            log.message(m, it)
+        log.start_collab("observer-2")
+        for m in msgs[half:]:
+            log.message(m, it)
+        last = msgs[-1]
+        log.seq_update(last["minimumSequenceNumber"], last["sequenceNumber"])
+        logs.append(log)
+    return build_batch(logs, it)
+
+
+def test_start_collab_semantics():
+    """addLongClientId always registers a new short id at startOrUpdateCollaboration (even for a known
+    long id), an undefined id keeps the client local, a second id renames the observer."""
+    it = Interner()
+    log = DocLog()
+    log.message({"clientId": "A", "type": "join", "sequenceNumber": 1, "referenceSequenceNumber": 0,
+                 "minimumSequenceNumber": 0}, it)
+    log.start_collab(None)
+    assert not log.collaborating and log.clients == ["A"]
+    log.start_collab("A")
+    assert log.clients == ["A", "A"] and log.client_ix["A"] == 1
+    assert log.ops[-1][0] == abi.OP_START_COLLAB and log.ops[-1][2] == 1  # the op carries the new short id
+    log.start_collab("B")
+    assert log.clients == ["A", "B"] and log.client_ix["A"] == 1 and log.client_ix["B"] == 1
+    assert log.observer_id == "B"
+    n = len(log.ops)
+    log.start_collab("C")  # renames again; never a second START_COLLAB record
+    assert len(log.ops) == n and log.clients == ["A", "C"]
+
+
+def test_client_cap_is_unsupported():
+    it = Interner()
+    log = DocLog()
+    for i in range(MAX_CLIENTS):
+        log.short_id(f"c{i}")
+    with pytest.raises(Unsupported):
+        log.short_id("one-too-many")
+
+
+@pytest.mark.parametrize("pre", [-1, 5])
+def test_js_packer_matches_python_packer(pre):
     paths = replay_files()[:6]
     _addon()
-    js = json.loads(_node([os.path.join(HERE, "node", "pack_batch.js")] + paths))
+    js = json.loads(_node([os.path.join(HERE, "node", "pack_batch.js")] + (["--pre", str(pre)] if pre >= 0 else [])
+                          + paths))
     raw = {k: base64.b64decode(v) for k, v in js.items()}
-    py = _py_batch(paths)
+    py = _py_batch(paths) if pre < 0 else _py_batch_pre(paths, pre)
 
     def arr(name, dtype):
         return np.frombuffer(raw[name], dtype=dtype)

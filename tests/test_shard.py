@@ -76,3 +76,32 @@ def test_two_ranks_gloo_match_single_process():
     assert r["bad_docs"] == 0 and not status.any()
     assert r["elapsed"] == float(world)  # max over ranks
     assert r["digest"] == shard.digest(hashes)
+
+
+def test_strong_ranges_cover_every_document_once():
+    for total in (0, 1, 7, 100_000, 100_003):
+        for world in (1, 2, 3, 4, 8):
+            rs = [shard.strong_range(r, world, total) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            sizes = [hi - lo for lo, hi in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_lpt_assignment_balances_estimated_cost():
+    """Greedy LPT over Σ(ops × est. S): every document once, and the most loaded rank
+    carries at most 4/3 of the optimum's bound (max(mean load, largest document))."""
+    rng = np.random.default_rng(5)
+    ops = rng.integers(10, 5000, size=997)
+    seg = rng.integers(0, 3000, size=997)
+    costs = shard.doc_cost(ops, seg)
+    for world in (1, 2, 4, 8):
+        parts = shard.lpt_assign(costs, world)
+        allv = np.sort(np.concatenate(parts))
+        assert np.array_equal(allv, np.arange(len(costs)))
+        loads = np.array([costs[p].sum() for p in parts])
+        bound = max(costs.sum() / world, costs.max())
+        assert loads.max() <= 4 / 3 * bound + 1e-6
+    # equal costs: the assignment is the equal-size split
+    parts = shard.lpt_assign(np.ones(10), 4)
+    assert sorted(len(p) for p in parts) == [2, 2, 3, 3]
