@@ -26,15 +26,18 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_engine(force=False, verbose=False, prof=False):
-    out = os.path.join(HERE, "libmtr_prof.so" if prof else "libmtr.so")
+def build_engine(force=False, verbose=False, prof=False, variant=None, extra=()):
+    """libmtr.so; prof: the phase-timer build (libmtr_prof.so); variant: an experiment build
+    libmtr_<variant>.so with extra compiler flags (selected at run time with MTR_LIB)."""
+    name = "libmtr_prof.so" if prof else (f"libmtr_{variant}.so" if variant else "libmtr.so")
+    out = os.path.join(HERE, name)
     deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", h)
                                                            for h in ("mtr.h", "mtr_types.h", "mtr_synth.h", "mtr_digest.h")]
     if force or _stale(out, deps):
         # translation units compiled in parallel (the fixed-capacity kernels in CAP_PARTS parts), then linked
         flags = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
-            (["-DMTR_PROF"] if prof else [])
-        objdir = os.path.join(HERE, "build_prof" if prof else "build")
+            (["-DMTR_PROF"] if prof else []) + list(extra)
+        objdir = os.path.join(HERE, "build_prof" if prof else (f"build_{variant}" if variant else "build"))
         os.makedirs(objdir, exist_ok=True)
         units = [(os.path.join(CSRC, f), os.path.join(objdir, f + ".o"), []) for f in ENGINE_SRC]
         units += [(os.path.join(CSRC, "apply_caps.hip"), os.path.join(objdir, f"apply_caps_{q}.o"), [f"-DMTR_CAP_PART={q}"])
@@ -84,5 +87,8 @@ def build_all(force=False, verbose=False):
 if __name__ == "__main__":
     if "--prof" in sys.argv:
         build_engine(force="--force" in sys.argv, verbose=True, prof=True)
+    elif "--variant" in sys.argv:  # python -m fluidframework_amd.build --variant NAME [flags...]
+        i = sys.argv.index("--variant")
+        build_engine(force=True, verbose=False, variant=sys.argv[i + 1], extra=sys.argv[i + 2:])
     else:
         build_all(force="--force" in sys.argv, verbose=True)

@@ -381,32 +381,45 @@ struct Eng {
         const uint32_t m = h.meta;
         const int seq = h.seq;
         const bool removed = rseq != RNONE;
-        if (v.local) {  // localNetLength, mergeTree.ts:613-634
-            return removed ? (newlen ? 0 : (rseq > minseq ? 0 : -1)) : len;
+        if (v.local) {  // localNetLength, mergeTree.ts:613-634 (a uniform branch)
+            const int rl = newlen ? 0 : (rseq > minseq ? 0 : -1);
+            return removed ? rl : len;
         }
-        const bool vis = (m & M_CLIENT_MASK) == v.client || seq <= v.ref;
-        bool inr = removed && ((m >> M_FREM_SHIFT) & 0xffu) == v.client;
+        // Every lane evaluates the same select chain (bitwise predicates: no divergent branches and
+        // no lane masks carried across them); only lanes whose answer depends on a later remover in
+        // the overlap list walk it, behind one ballot.
+        const bool vis = ((m & M_CLIENT_MASK) == v.client) | (seq <= v.ref);
+        const bool first = removed & (((m >> M_FREM_SHIFT) & 0xffu) == v.client);
         // lanes whose result still depends on removedClientIds[1..] (mergeTree.ts:935-1003)
-        const bool walk =
-            valid && removed && !inr && (m & M_OVERLAP) && rseq > v.ref && (newlen ? rseq > minseq : vis);
-        if (__ballot(walk)) {
-            if (walk) {
-                uint32_t cell = rm_get(L, L.uid[i]);
-                while (cell != 0xffffffu) {
-                    const uint32_t w = L.grm[cell];
-                    if ((w >> 24) == v.client) {
-                        inr = true;
-                        break;
-                    }
-                    cell = w & 0xffffffu;
+        const bool walk = valid & removed & !first & ((m & M_OVERLAP) != 0) & (rseq > v.ref) &
+                          (newlen ? rseq > minseq : vis);
+        int inr = first ? 1 : 0;
+        if (__ballot(walk)) inr |= later_remover(L, i, walk, v.client);
+        if (newlen) {  // mergeTree.ts:935-965
+            const int live = vis ? len : 0;
+            const int gone = ((rseq <= v.ref) | (inr != 0)) ? 0 : live;
+            return removed ? (rseq <= minseq ? -1 : gone) : live;
+        }
+        // mergeTree.ts:967-1003
+        const int seen = (removed & (inr != 0)) ? 0 : len;
+        const int r = vis ? seen : (removed ? -1 : 0);
+        return (removed & (rseq <= v.ref)) ? -1 : r;
+    }
+    // 1 when client c is in leaf i's removedClientIds[1..] (the overlap list), for the lanes in `walk`
+    static MTR_DI int later_remover(const D& L, int i, bool walk, uint32_t c) {
+        int inr = 0;
+        if (walk) {
+            uint32_t cell = rm_get(L, L.uid[i]);
+            while (cell != 0xffffffu) {
+                const uint32_t w = L.grm[cell];
+                if ((w >> 24) == c) {
+                    inr = 1;
+                    break;
                 }
+                cell = w & 0xffffffu;
             }
         }
-        if (newlen)  // mergeTree.ts:935-965
-            return removed ? (rseq <= minseq ? -1 : ((rseq <= v.ref || inr) ? 0 : (vis ? len : 0))) : (vis ? len : 0);
-        // mergeTree.ts:967-1003
-        if (removed && rseq <= v.ref) return -1;
-        return vis ? ((removed && inr) ? 0 : len) : (removed ? -1 : 0);
+        return inr;
     }
 
     // root.cachedLength: the local view's length (removed leaves count 0), mergeTree.ts:613-634
@@ -517,12 +530,9 @@ struct Eng {
             const int lo = max(at, hi - 64);
             const int i = lo + lane_id();
             const bool act = i < hi;
-            int a0 = 0, a1 = 0, a2 = 0, a8 = 0;
-            uint32_t a3 = 0, a4 = 0, a5 = 0, a7 = 0;
-            if (act) {
-                a0 = L.len[i]; a1 = L.seq[i]; a2 = L.rseq[i]; a3 = L.meta[i]; a4 = L.text[i];
-                a5 = L.props[i]; a7 = L.uid[i]; a8 = L.E[i];
-            }
+            const int ic = min(i, S - 1);  // (unconditional loads: no divergent branch around them)
+            const int a0 = L.len[ic], a1 = L.seq[ic], a2 = L.rseq[ic], a8 = L.E[ic];
+            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = L.props[ic], a7 = L.uid[ic];
             wsync();
             if (act) {
                 L.len[i + 1] = a0; L.seq[i + 1] = a1; L.rseq[i + 1] = a2; L.meta[i + 1] = a3; L.text[i + 1] = a4;
@@ -542,13 +552,10 @@ struct Eng {
         for (int lo = from; lo < S; lo += 64) {
             const int i = lo + lane_id();
             const bool act = i < S;
-            int a0 = 0, a1 = 0, a2 = 0;
-            uint32_t a3 = M_DEL, a4 = 0, a5 = 0, a7 = 0;
-            if (act) {
-                a0 = L.len[i]; a1 = L.seq[i]; a2 = L.rseq[i]; a3 = L.meta[i];
-                a4 = L.text[i]; a5 = L.props[i]; a7 = L.uid[i];
-            }
-            const bool keep = act && !(a3 & M_DEL);
+            const int ic = min(i, S - 1);
+            const int a0 = L.len[ic], a1 = L.seq[ic], a2 = L.rseq[ic];
+            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = L.props[ic], a7 = L.uid[ic];
+            const bool keep = act & !(a3 & M_DEL);
             const uint64_t km = __ballot(keep);
             wsync();
             if (keep) {
@@ -569,7 +576,8 @@ struct Eng {
         const int S = s.nseg;
         for (int base = 0; base < S; base += 64) {
             const int i = base + lane_id();
-            const uint64_t m = __ballot(i < S && L.uid[min(i, S - 1)] == u);
+            const uint32_t ui = L.uid[min(i, S - 1)];  // unconditional (clamped) load: no divergent branch
+            const uint64_t m = __ballot((i < S) & (ui == u));
             if (m) return base + first_lane(m);
         }
         return -1;
@@ -580,7 +588,8 @@ struct Eng {
     static MTR_DI int block_start(const D& L, int x, int level) {
         for (int base = x;; base -= 64) {
             const int i = base - lane_id();
-            const uint64_t m = __ballot(i <= 0 || bnd_of(L.meta[max(i, 0)]) >= level);
+            const uint32_t mi = L.meta[max(i, 0)];
+            const uint64_t m = __ballot((i <= 0) | (bnd_of(mi) >= level));
             if (m) return max(0, base - first_lane(m));
         }
     }
@@ -589,7 +598,8 @@ struct Eng {
         const int S = s.nseg;
         for (int base = x + 1;; base += 64) {
             const int i = base + lane_id();
-            const uint64_t m = __ballot(i >= S || bnd_of(L.meta[max(min(i, S - 1), 0)]) >= level);
+            const uint32_t mi = L.meta[max(min(i, S - 1), 0)];
+            const uint64_t m = __ballot((i >= S) | (bnd_of(mi) >= level));
             if (m) return base + first_lane(m);
         }
     }
@@ -601,14 +611,16 @@ struct Eng {
             // the hi - lo + 1 candidates in 64 strides: lane 63's probe reaches hi, which qualifies
             const int stride = (hi - lo + 64) >> 6;
             const int idx = lo + (ln + 1) * stride - 1;
-            const uint64_t m = __ballot(idx >= hi || (L.E[min(idx, hi - 1)] & EMASK) >= pos);
+            const int ei = L.E[min(idx, hi - 1)];
+            const uint64_t m = __ballot((idx >= hi) | ((ei & EMASK) >= pos));
             const int k = first_lane(m);  // lane 63 always qualifies
             const int nlo = lo + k * stride;
             hi = min(hi, lo + (k + 1) * stride - 1);
             lo = nlo;
         }
         const int i = lo + ln;
-        const uint64_t m = __ballot(i < hi && (L.E[min(i, max(hi - 1, 0))] & EMASK) >= pos);
+        const int ei = L.E[min(i, max(hi - 1, 0))];
+        const uint64_t m = __ballot((i < hi) & ((ei & EMASK) >= pos));
         return m ? lo + first_lane(m) : hi;
     }
     // number of leaves in [bs, be) with bnd >= minb
@@ -616,7 +628,8 @@ struct Eng {
         int c = 0;
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
-            c += __popcll(__ballot(i < be && bnd_of(L.meta[min(i, be - 1)]) >= minb));
+            const uint32_t mi = L.meta[min(i, be - 1)];
+            c += __popcll(__ballot((i < be) & (bnd_of(mi) >= minb)));
         }
         return c;
     }
@@ -624,7 +637,8 @@ struct Eng {
     static MTR_DI int nth_bnd(const D& L, int bs, int be, int minb, int n) {
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
-            const bool t = i < be && bnd_of(L.meta[min(i, be - 1)]) >= minb;
+            const uint32_t mi = L.meta[min(i, be - 1)];
+            const bool t = (i < be) & (bnd_of(mi) >= minb);
             const uint64_t m = __ballot(t);
             const int pc = __popcll(m);
             if (n < pc) return base + first_lane(__ballot(t && __popcll(m & lanes_below()) == n));
@@ -639,10 +653,11 @@ struct Eng {
         const int S = s.nseg;
         const int ln = lane_id();
         const int i = x - 31 + ln;
-        const bool in = i >= 0 && i < S;
-        const bool b = in && bnd_of(L.meta[in ? i : 0]) >= 1;
-        const uint64_t sm = __ballot(ln <= 31 && (i <= 0 || b));
-        const uint64_t em = __ballot(ln > 31 && (i >= S || b));
+        const bool in = (i >= 0) & (i < S);
+        const uint32_t mi = L.meta[in ? i : 0];
+        const bool b = in & (bnd_of(mi) >= 1);
+        const uint64_t sm = __ballot((ln <= 31) & ((i <= 0) | b));
+        const uint64_t em = __ballot((ln > 31) & ((i >= S) | b));
         bs = sm ? max(0, x - 31 + last_lane(sm)) : block_start(L, x - 32, 1);
         be = em ? x - 31 + first_lane(em) : block_end(L, s, x + 32, 1);
     }
@@ -1097,16 +1112,11 @@ struct Eng {
         uint32_t pmeta = 0, pprops = 0, ptext = 0;
         for (int base = cs; base < ce; base += 64) {
             const int i = base + lane_id();
-            uint32_t vm = M_DEL, vp = 0, vt = 0;
-            int vr = 0, vs = 0, vl = 0;
-            if (i < ce) {
-                vm = L.meta[i];
-                vr = L.rseq[i];
-                vs = L.seq[i];
-                vl = L.len[i];
-                vp = L.props[i];
-                vt = L.text[i];
-            }
+            const int ic = min(i, ce - 1);
+            uint32_t vm = L.meta[ic];
+            const uint32_t vp = L.props[ic], vt = L.text[ic];
+            const int vr = L.rseq[ic], vs = L.seq[ic], vl = L.len[ic];
+            if (i >= ce) vm = M_DEL;
             {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
                 const bool q = !PM && (vm & (M_NLQ | M_DEL | M_MARKER)) == M_NLQ && vl > 0 && vr == RNONE &&
                                vs <= minseq;
@@ -1190,16 +1200,11 @@ struct Eng {
         const int ln = lane_id();
         const int i = cs + ln;
         const bool in = i < ce;
-        uint32_t vm = M_DEL, vp = 0, vt = 0;
-        int vr = RNONE, vs = 0, vl = 0;
-        if (in) {
-            vm = L.meta[i];
-            vr = L.rseq[i];
-            vs = L.seq[i];
-            vl = L.len[i];
-            vp = L.props[i];
-            vt = L.text[i];
-        }
+        const int ic = min(i, ce - 1);
+        const uint32_t vm0 = L.meta[ic], vp = L.props[ic], vt = L.text[ic];
+        const int vr0 = L.rseq[ic], vs = L.seq[ic], vl0 = L.len[ic];
+        uint32_t vm = in ? vm0 : M_DEL;
+        const int vr = in ? vr0 : RNONE, vl = in ? vl0 : 0;
         const bool pre = (vm & M_DEL) != 0;
         const bool removed = vr != RNONE;
         const bool cand = !pre && !removed && vs <= minseq && vl > 0;
@@ -1450,17 +1455,15 @@ struct Eng {
         const int ln = lane_id();
         const int jj = i + ln;
         const bool in = jj < S;
-        int vj = 0, ej = 0, lj = 0, sqj = 0, rsj = 0;
-        uint32_t mj = 0, tj = 0, pj = 0, uj = 0;
-        if (in) {
-            ej = L.E[jj]; mj = L.meta[jj]; lj = L.len[jj]; sqj = L.seq[jj];
-            rsj = L.rseq[jj]; tj = L.text[jj]; pj = L.props[jj]; uj = L.uid[jj];
-            vj = ev(ej, jj > 0 ? L.E[jj - 1] : 0);
-            ej &= EMASK;
-        }
-        const uint64_t em = __ballot(!in || (ln > 0 && bnd_of(mj) >= 1));
+        const int jc = min(jj, S - 1);  // unconditional (clamped) loads
+        const int ej0 = L.E[jc], ep = L.E[max(jc - 1, 0)];
+        const uint32_t mj = L.meta[jc], tj = L.text[jc], pj = L.props[jc], uj = L.uid[jc];
+        const int lj = L.len[jc], sqj = L.seq[jc], rsj = L.rseq[jc];
+        const int vj = ev(ej0, jc > 0 ? ep : 0);
+        const int ej = ej0 & EMASK;
+        const uint64_t em = __ballot(!in | ((ln > 0) & (bnd_of(mj) >= 1)));
         const int be = em ? i + first_lane(em) : block_end(L, s, i + 63, 1);
-        const uint64_t cm = __ballot(jj < be && vj >= 0 && pos < ej);
+        const uint64_t cm = __ballot((jj < be) & (vj >= 0) & (pos < ej));
         if (!cm) return;
         const int jl = first_lane(cm);
         const int j = i + jl;
@@ -1558,22 +1561,20 @@ struct Eng {
                     // one batch of loads over leaves i-31 .. i+32: the leaf block's bounds and the
                     // breakTie candidates (mergeTree.ts:1719-1738) in [i, be)
                     const int w = i - 31 + ln;
-                    const bool inw = w >= 0 && w < S;
-                    int vw = 0, ew = 0, sw = 0;
-                    uint32_t mw = 0;
-                    if (inw) {
-                        ew = L.E[w]; sw = L.seq[w]; mw = L.meta[w];
-                        vw = ev(ew, w > 0 ? L.E[w - 1] : 0);
-                        ew &= EMASK;
-                    }
-                    const bool bw = inw && bnd_of(mw) >= 1;
-                    const uint64_t sm = __ballot(ln <= 31 && (w <= 0 || bw));
-                    const uint64_t em = __ballot(ln > 31 && (w >= S || bw));
+                    const bool inw = (w >= 0) & (w < S);
+                    const int wc = min(max(w, 0), S - 1);  // unconditional (clamped) loads
+                    const int ew0 = L.E[wc], ewp = L.E[max(wc - 1, 0)], sw = L.seq[wc];
+                    const uint32_t mw = L.meta[wc];
+                    const int vw = ev(ew0, wc > 0 ? ewp : 0);
+                    const int ew = ew0 & EMASK;
+                    const bool bw = inw & (bnd_of(mw) >= 1);
+                    const uint64_t sm = __ballot((ln <= 31) & ((w <= 0) | bw));
+                    const uint64_t em = __ballot((ln > 31) & ((w >= S) | bw));
                     if (sm && em) {
                         const int bs = max(0, i - 31 + last_lane(sm));
                         const int be = i - 31 + first_lane(em);
-                        const uint64_t cm =
-                            __ballot(ln >= 31 && w < be && vw >= 0 && (ew > pos || (vw == 0 && seq > sw)));
+                        const uint64_t cm = __ballot((ln >= 31) & (w < be) & (vw >= 0) &
+                                                     ((ew > pos) | ((vw == 0) & (seq > sw))));
                         slot = cm ? i - 31 + first_lane(cm) : be;
                         inherit = slot == bs ? 1 : 0;
                         wbs = bs;
@@ -1737,18 +1738,14 @@ struct Eng {
         for (int base = lower_bound_E(L, s, start + 1); base < S; base += 64) {
             const int j = base + ln;
             const bool in = j < S;
-            int vj = 0, ej = 0, rj = RNONE;
-            uint32_t mj = 0;
-            if (in) {
-                ej = L.E[j];
-                vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
-                ej &= EMASK;
-                mj = L.meta[j];
-                if (is_remove) rj = L.rseq[j];
-            }
-            const uint64_t stop = __ballot(!in || ej - max(vj, 0) >= end);
+            const int jc = min(j, S - 1);  // unconditional (clamped) loads
+            const int ej0 = L.E[jc], ep = L.E[max(jc - 1, 0)], rj = L.rseq[jc];
+            uint32_t mj = L.meta[jc];
+            const int vj = ev(ej0, jc > 0 ? ep : 0);
+            const int ej = ej0 & EMASK;
+            const uint64_t stop = __ballot(!in | (ej - max(vj, 0) >= end));
             const int lim = stop ? first_lane(stop) : 64;
-            const bool act = ln < lim && vj > 0;
+            const bool act = (ln < lim) & (vj > 0);
             const uint64_t am = __ballot(act);
             if (am) {
                 if (is_remove) {
