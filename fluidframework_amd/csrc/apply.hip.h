@@ -185,8 +185,14 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
        P_TAPPEND, P_HEAP, P_OVERFLOW, P_NPACK, P_NMERGE, P_NPMATCH, P_NNLQ, P_SPLIT1, P_INS1, P_FETCH, P_X1, P_X2,
        P_COUNT };
 
-// LDS-side scratch of one document: record-mode broadcast, phase timers
+// Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
+// records, the batch's property tables), kept in LDS and read where used, so they never hold SGPRs
+// across the whole op loop (the loop's scalar state otherwise spills into VGPR lanes)
+enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_N };
+
+// LDS-side scratch of one document: record-mode broadcast, cold pointers, phase timers
 struct Sc {
+    unsigned long long cp[CP_N];
     int gen_ref, gen_client;
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];
@@ -220,11 +226,20 @@ struct Doc {
     A<uint32_t> meta, text, props, uid, huid;
     lptr<Sc> sc;
     lptr<mtr_synth_state> gst;
-    gptr<uint16_t> gtext;
-    gptr<uint32_t> gprop, grm, grt;  // grt: remover-head table (2 words per entry)
-    gptr<uint32_t> gdelta;           // this document's delta ranges (mtr_delta records)
-    int dcap;                        // ... and their capacity in this batch
+    int dcap;  // capacity of this document's delta records in this batch
     int cap, lhcap, rtmask;
+    // cold pointers (read from LDS at the use site, made wave-uniform)
+    MTR_DI unsigned long long cold(int k) const {
+        const unsigned long long v = sc->cp[k];
+        return (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane(int(uint32_t(v))) |
+               ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))) << 32);
+    }
+    MTR_DI gptr<uint16_t> gtext() const { return (gptr<uint16_t>)cold(CP_TEXT); }
+    MTR_DI gptr<uint32_t> gprop() const { return (gptr<uint32_t>)cold(CP_PROP); }
+    MTR_DI gptr<uint32_t> grm() const { return (gptr<uint32_t>)cold(CP_RM); }
+    MTR_DI gptr<uint32_t> grt() const { return (gptr<uint32_t>)cold(CP_RT); }  // remover-head table
+    MTR_DI gptr<uint32_t> gdelta() const { return (gptr<uint32_t>)cold(CP_DELTA); }  // mtr_delta records
+    MTR_DI gptr<const uint32_t> tab(int k) const { return (gptr<const uint32_t>)cold(k); }
 };
 
 MTR_DI int bnd_of(uint32_t m) { return int((m & M_BND_MASK) >> M_BND_SHIFT); }
@@ -328,8 +343,8 @@ struct Eng {
     static MTR_DI uint32_t rm_get(const D& L, uint32_t uid) {
         uint32_t h = rtab_hash(uid) & uint32_t(L.rtmask);
         for (int n = 0; n <= L.rtmask; n++) {
-            const uint32_t k = L.grt[2 * h];
-            if (k == uid + 1) return L.grt[2 * h + 1];
+            const uint32_t k = L.grt()[2 * h];
+            if (k == uid + 1) return L.grt()[2 * h + 1];
             if (k == 0) break;
             h = (h + 1) & uint32_t(L.rtmask);
         }
@@ -339,10 +354,10 @@ struct Eng {
     static MTR_DI bool rm_set(const D& L, uint32_t uid, uint32_t head) {
         uint32_t h = rtab_hash(uid) & uint32_t(L.rtmask);
         for (int n = 0; n <= L.rtmask; n++) {
-            uint32_t k = L.grt[2 * h];
-            if (k == 0) k = atomicCAS((uint32_t*)&L.grt[2 * h], 0u, uid + 1);
+            uint32_t k = L.grt()[2 * h];
+            if (k == 0) k = atomicCAS((uint32_t*)&L.grt()[2 * h], 0u, uid + 1);
             if (k == 0 || k == uid + 1) {
-                L.grt[2 * h + 1] = head;
+                L.grt()[2 * h + 1] = head;
                 return true;
             }
             h = (h + 1) & uint32_t(L.rtmask);
@@ -355,7 +370,7 @@ struct Eng {
         if (!(m & M_OVERLAP)) return false;
         uint32_t cell = rm_get(L, L.uid[i]);
         while (cell != 0xffffffu) {
-            const uint32_t v = L.grm[cell];
+            const uint32_t v = L.grm()[cell];
             if ((v >> 24) == c) return true;
             cell = v & 0xffffffu;
         }
@@ -411,7 +426,7 @@ struct Eng {
         if (walk) {
             uint32_t cell = rm_get(L, L.uid[i]);
             while (cell != 0xffffffu) {
-                const uint32_t w = L.grm[cell];
+                const uint32_t w = L.grm()[cell];
                 if ((w >> 24) == c) {
                     inr = 1;
                     break;
@@ -765,10 +780,10 @@ struct Eng {
         uint32_t dst;
         int propused, status;
     };
-    static MTR_DI PropRes props_apply_serial(gptr<uint32_t> gprop, const KParams& P, int propused,
-                                                              uint32_t old, uint32_t pp) {
+    static MTR_DI PropRes props_apply_serial(const D& L, const KParams& P, int propused, uint32_t old, uint32_t pp) {
         PropRes r{old, propused, MTR_OK};
-        const gptr<const uint32_t> poff = gp(P.propop_off), pkv = gp(P.propop_kv), kix = gp(P.key_index);
+        const gptr<uint32_t> gprop = L.gprop();
+        const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX);
         const uint32_t n_old = old == NONE32 ? 0 : uniu(gprop[old]);
         const uint32_t lo = uniu(poff[pp]), hi = uniu(poff[pp + 1]);
         const uint32_t need = 1 + 2 * (n_old + (hi - lo));
@@ -825,11 +840,11 @@ struct Eng {
     // Wave version: the old set and the op's keys are fetched once (one lane per entry) and the
     // set is edited in registers (lane t = entry t); falls back to the serial form above 64 keys.
     static MTR_DI uint32_t props_apply(D& L, const KParams& P, St& s, uint32_t old, uint32_t pp) {
-        const gptr<const uint32_t> poff = gp(P.propop_off), pkv = gp(P.propop_kv), kix = gp(P.key_index);
-        const int n_old = old == NONE32 ? 0 : int(uniu(L.gprop[old]));
+        const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX);
+        const int n_old = old == NONE32 ? 0 : int(uniu(L.gprop()[old]));
         const int lo = int(uniu(poff[pp])), nq = int(uniu(poff[pp + 1])) - lo;
         if (n_old + nq > 64) {
-            const PropRes r = props_apply_serial(L.gprop, P, s.propused, old, pp);
+            const PropRes r = props_apply_serial(L, P, s.propused, old, pp);
             s.propused = uni(r.propused);
             if (uni(r.status) != MTR_OK) s.status = uni(r.status);
             wsync();
@@ -843,8 +858,8 @@ struct Eng {
         const int ln = lane_id();
         uint32_t wk = 0, wv = 0, wx = MTR_NOT_INDEX, qk = 0, qv = 0, qx = MTR_NOT_INDEX;
         if (ln < n_old) {
-            wk = L.gprop[old + 1 + 2 * ln];
-            wv = L.gprop[old + 2 + 2 * ln];
+            wk = L.gprop()[old + 1 + 2 * ln];
+            wv = L.gprop()[old + 2 + 2 * ln];
         }
         if (ln < nq) {
             qk = pkv[2 * (lo + ln)];
@@ -891,7 +906,7 @@ struct Eng {
             }
         }
         const uint32_t dst = uint32_t(s.propused);
-        const gptr<uint32_t> e = L.gprop + dst;
+        const gptr<uint32_t> e = L.gprop() + dst;
         if (ln < n) {
             e[1 + 2 * ln] = wk;
             e[2 + 2 * ln] = wv;
@@ -906,19 +921,19 @@ struct Eng {
     static MTR_DI bool props_match_w(const D& L, const KParams& P, uint32_t a, uint32_t b) {
         if (a == b) return true;
         if (a == NONE32 || b == NONE32) return false;
-        const int na = int(uniu(L.gprop[a])), nb = int(uniu(L.gprop[b]));
+        const int na = int(uniu(L.gprop()[a])), nb = int(uniu(L.gprop()[b]));
         if (na != nb) return false;
-        const gptr<const uint32_t> veq = gp(P.val_eq);
-        if (na > 64) return __ballot(!props_match(L.gprop, veq, a, b)) == 0;
+        const gptr<const uint32_t> veq = L.tab(CP_VEQ);
+        if (na > 64) return __ballot(!props_match(L.gprop(), veq, a, b)) == 0;
         PROF(P_PMATCH);
         PROF_COUNT(P_NPMATCH);
         const int ln = lane_id();
         uint32_t ka = 0, kb = 0, ea = 0, eb = 0;
         if (ln < na) {
-            ka = L.gprop[a + 1 + 2 * ln];
-            kb = L.gprop[b + 1 + 2 * ln];
-            ea = veq[L.gprop[a + 2 + 2 * ln]];
-            eb = veq[L.gprop[b + 2 + 2 * ln]];
+            ka = L.gprop()[a + 1 + 2 * ln];
+            kb = L.gprop()[b + 1 + 2 * ln];
+            ea = veq[L.gprop()[a + 2 + 2 * ln]];
+            eb = veq[L.gprop()[b + 2 + 2 * ln]];
         }
         bool found = ln >= na, ok = true;
         for (int j = 0; j < nb; j++) {
@@ -938,19 +953,21 @@ struct Eng {
         return la <= kGranularity || lb <= kGranularity;
     }
     static MTR_DI void copy_text(const D& L, uint32_t dst, uint32_t src, int n) {
-        for (int k = lane_id(); k < n; k += 64) L.gtext[dst + k] = L.gtext[src + k];
+        const gptr<uint16_t> t = L.gtext();
+        for (int k = lane_id(); k < n; k += 64) t[dst + k] = t[src + k];
     }
     static MTR_DI int text_end(const St& s, const KParams& P) { return (P.tcap / 2) * (s.texthalf + 1); }
     // one lane's copy of n units: 8 loads in flight, then 8 stores
     static MTR_DI void copy_units(const D& L, uint32_t dst, uint32_t src, int n) {
+        const gptr<uint16_t> t = L.gtext();
         for (int u0 = 0; u0 < n; u0 += 8) {
             uint16_t b[8];
 #pragma unroll
             for (int q = 0; q < 8; q++)
-                if (u0 + q < n) b[q] = L.gtext[src + u0 + q];
+                if (u0 + q < n) b[q] = t[src + u0 + q];
 #pragma unroll
             for (int q = 0; q < 8; q++)
-                if (u0 + q < n) L.gtext[dst + u0 + q] = b[q];
+                if (u0 + q < n) t[dst + u0 + q] = b[q];
         }
     }
 
@@ -962,6 +979,7 @@ struct Eng {
     static MTR_DI void copy_chain(const D& L, uint32_t dst, int c0, int total, uint64_t pieces, uint32_t vt,
                                   int off) {
         const int ln = lane_id();
+        const gptr<uint16_t> t = L.gtext();
         for (int b0 = c0; b0 < total; b0 += 8 * 64) {
             uint16_t u[8];
             uint32_t src[8];
@@ -979,10 +997,10 @@ struct Eng {
             }
 #pragma unroll
             for (int q = 0; q < 8; q++)
-                if (b0 + 64 * q + ln < total) u[q] = L.gtext[src[q]];
+                if (b0 + 64 * q + ln < total) u[q] = t[src[q]];
 #pragma unroll
             for (int q = 0; q < 8; q++)
-                if (b0 + 64 * q + ln < total) L.gtext[dst + uint32_t(b0 + 64 * q + ln)] = u[q];
+                if (b0 + 64 * q + ln < total) t[dst + uint32_t(b0 + 64 * q + ln)] = u[q];
         }
     }
 
@@ -1056,7 +1074,7 @@ struct Eng {
     // ------------------------------------------------------------ HandleTable (matrix/src/handletable.ts)
     // A permutation vector keeps its HandleTable in its (otherwise unused) text arena as int32
     // words; handles[0] is the head of the free list, s.textused the array length.
-    static MTR_DI gptr<int32_t> handles(const D& L) { return (gptr<int32_t>)L.gtext; }
+    static MTR_DI gptr<int32_t> handles(const D& L) { return (gptr<int32_t>)L.gtext(); }
     static MTR_DI int handle_cap(const KParams& P) { return P.tcap / 2; }
     // HandleTable.allocate, handletable.ts:37-42
     static MTR_DI int alloc_handle(D& L, const KParams& P, St& s) {
@@ -1124,7 +1142,7 @@ struct Eng {
                     PROF(P_NLQ);
                     PROF_COUNT(P_NNLQ);
                     if (q) {
-                        const uint16_t u = L.gtext[L.text[i] + uint32_t(vl) - 1];
+                        const uint16_t u = L.gtext()[L.text[i] + uint32_t(vl) - 1];
                         vm = (vm & ~(M_NLQ | M_NL)) | (u == u'\n' ? M_NL : 0u);
                         L.meta[i] = vm;
                     }
@@ -1207,58 +1225,60 @@ struct Eng {
         const int vr = in ? vr0 : RNONE, vl = in ? vl0 : 0;
         const bool pre = (vm & M_DEL) != 0;
         const bool removed = vr != RNONE;
-        const bool cand = !pre && !removed && vs <= minseq && vl > 0;
+        const bool cand = !pre & !removed & (vs <= minseq) & (vl > 0);
         {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
-            const bool q = cand && !PM && (vm & (M_NLQ | M_MARKER)) == M_NLQ;
+            const bool q = cand & !PM & ((vm & (M_NLQ | M_MARKER)) == M_NLQ);
             if (__ballot(q)) {
                 PROF(P_NLQ);
                 PROF_COUNT(P_NNLQ);
                 if (q) {
-                    const uint16_t u = L.gtext[vt + uint32_t(vl) - 1];
+                    const uint16_t u = L.gtext()[vt + uint32_t(vl) - 1];
                     vm = (vm & ~(M_NLQ | M_NL)) | (u == u'\n' ? M_NL : 0u);
                     L.meta[i] = vm;
                 }
                 wsync();
             }
         }
-        const uint64_t nd = __ballot(in && !pre);
-        const uint64_t bm = __ballot(in && i > cs && bnd_of(vm) >= 1);
+        const uint64_t nd = __ballot(in & !pre);
+        const uint64_t bm = __ballot(in & (i > cs) & (bnd_of(vm) >= 1));
         const uint64_t below = nd & lanes_below();
         const int p = below ? last_lane(below) : -1;
         const int ps = p < 0 ? 0 : p;
-        const int pc = __shfl(int(cand), ps);
-        const uint32_t pm = uint32_t(__shfl(int(vm), ps));
+        // the previous leaf's meta word with its candidacy in the spare top bit: one shuffle
+        const uint32_t pmc = uint32_t(__shfl(int(vm | (cand ? 0x80000000u : 0u)), ps));
+        const bool pc = (pmc >> 31) != 0;
+        const uint32_t pm = pmc & 0x7fffffffu;
         const uint32_t pp = uint32_t(__shfl(int(vp), ps));
         const uint64_t upto = (uint64_t(2) << ln) - 1;  // lanes <= ln
         const uint64_t after_p = p < 0 ? ~uint64_t(0) : ~((uint64_t(2) << p) - 1);
-        bool link = cand && p >= 0 && pc && !(bm & upto & after_p);
+        bool link = cand & (p >= 0) & pc & ((bm & upto & after_p) == 0);
         if (PM) {  // handle contiguity with the previous chain member (permutationvector.ts:131-137)
             const uint32_t pt = uint32_t(__shfl(int(vt), ps));
             const int pl = __shfl(vl, ps);
-            link = link && perm_contig(pt, pl, vt);
+            link = link & perm_contig(pt, pl, vt);
         } else {
-            link = link && !((vm | pm) & M_MARKER) && !(pm & M_NL);
+            link = link & !((vm | pm) & M_MARKER) & !(pm & M_NL);
         }
-        if (__ballot(link && vp != pp)) {
+        if (__ballot(link & (vp != pp))) {
             PROF(P_X1);
-            if (link && vp != pp) link = props_match(L.gprop, gp(P.val_eq), pp, vp);
+            if (link & (vp != pp)) link = props_match(L.gprop(), L.tab(CP_VEQ), pp, vp);
         }
-        if (!PM && __ballot(link && vl > kGranularity)) return -1;
-        const bool unlink = !pre && removed && vr <= minseq;
+        if (!PM && __ballot(link & (vl > kGranularity))) return -1;
+        const bool unlink = !pre & removed & (vr <= minseq);
         const uint64_t lm = __ballot(link);
-        if (unlink || link) L.meta[i] = vm | M_DEL;
+        if (unlink | link) L.meta[i] = vm | M_DEL;
         if (PM) {  // UNLINK frees the segment's handles, in leaf order
             for (uint64_t um = __ballot(unlink && vt != uint32_t(MTR_HANDLE_UNALLOCATED)); um; um &= um - 1) {
                 const int l = first_lane(um);
                 free_handles(L, s, int(rdlane(vt, l)), rdlane(vl, l));
             }
         }
-        const int kept = __popcll(__ballot(in && !pre && !unlink && !link));
+        const int kept = __popcll(__ballot(in & !pre & !unlink & !link));
         if (lm) {  // concatenate each chain's text behind its head (prev.append, textSegment.ts:99-103)
-            const uint64_t hm = __ballot(in && !pre && !link);  // chain heads and unmerged leaves
+            const uint64_t hm = __ballot(in & !pre & !link);  // chain heads and unmerged leaves
             // lane offsets inside its chain: inclusive scan of lengths restarted at every head
             const int hd = (hm & upto) ? last_lane(hm & upto) : 0;  // this lane's chain head (chain lanes)
-            const int incl = wave_incl_scan(in && !pre ? vl : 0);
+            const int incl = wave_incl_scan((in & !pre) ? vl : 0);
             const int hbase = __shfl(incl - vl, hd);       // exclusive prefix at the head
             const int off = incl - vl - hbase;             // offset of this piece inside its chain
             uint64_t todo = lm;
@@ -1525,7 +1545,7 @@ struct Eng {
             bool any = false, last = false;
             if (pre) {
                 if (ln < len) {
-                    L.gtext[t0 + ln] = uint16_t(pf);
+                    L.gtext()[t0 + ln] = uint16_t(pf);
                     any = pf == u'\n';
                     last = any && ln == len - 1;
                 }
@@ -1533,7 +1553,7 @@ struct Eng {
                 const gptr<const uint16_t> src = gp(P.btext) + dd.text_base + op.payload;
                 for (int k = ln; k < len; k += 64) {
                     const uint16_t u = src[k];
-                    L.gtext[t0 + k] = u;
+                    L.gtext()[t0 + k] = u;
                     if (u == u'\n') {
                         any = true;
                         last = last || k == len - 1;
@@ -1652,7 +1672,7 @@ struct Eng {
                 uint32_t head = 0xffffffu;
                 for (int k = 1; k < nrem; k++) {
                     const uint32_t cell = uint32_t(s.rmused++);
-                    L.grm[cell] = (enc_client(int(uniu(rl[k]))) << 24) | head;
+                    L.grm()[cell] = (enc_client(int(uniu(rl[k]))) << 24) | head;
                     head = cell;
                 }
                 m |= M_OVERLAP;
@@ -1684,7 +1704,7 @@ struct Eng {
                 return;
             }
             const gptr<const uint16_t> src = gp(P.btext) + dd.text_base + op.payload;
-            for (int k = lane_id(); k < len; k += 64) L.gtext[t0 + k] = src[k];
+            for (int k = lane_id(); k < len; k += 64) L.gtext()[t0 + k] = src[k];
             s.textused = t0 + len;
         }
         uint32_t m = enc_client(int(int16_t(op.client)));
@@ -1762,7 +1782,7 @@ struct Eng {
                         const uint32_t cell = uint32_t(s.rmused + __popcll(om & lanes_below()));
                         const uint32_t uj = L.uid[j];
                         const uint32_t nxt = (mj & M_OVERLAP) ? rm_get(L, uj) : 0xffffffu;
-                        L.grm[cell] = (client << 24) | (nxt & 0xffffffu);
+                        L.grm()[cell] = (client << 24) | (nxt & 0xffffffu);
                         full = !rm_set(L, uj, cell);
                         mj |= M_OVERLAP;
                         L.meta[j] = mj;
@@ -1992,19 +2012,27 @@ struct Eng {
             L.cap = cap;
             L.lhcap = lhcap;
         }
-        L.gtext = gp(P.text) + size_t(d) * P.tcap;
-        L.gprop = gp(P.prop) + size_t(d) * P.pcap;
-        L.grm = gp(P.rm) + size_t(d) * (size_t(P.rcap) + 2 * size_t(P.rtab));
-        L.grt = L.grm + P.rcap;
         L.rtmask = P.rtab - 1;
+        unsigned long long delta = (unsigned long long)P.delta;
+        L.dcap = 0;
         if (P.doff) {
             const uint64_t o = gp(P.doff)[d];
-            L.gdelta = gp(P.delta) + o * 4;
+            delta = (unsigned long long)(P.delta + o * 4);
             L.dcap = int(gp(P.doff)[d + 1] - o);
-        } else {
-            L.gdelta = gp(P.delta);
-            L.dcap = 0;
         }
+        if (threadIdx.x == 0) {
+            const unsigned long long rm = (unsigned long long)(P.rm + size_t(d) * (size_t(P.rcap) + 2 * size_t(P.rtab)));
+            L.sc->cp[CP_TEXT] = (unsigned long long)(P.text + size_t(d) * P.tcap);
+            L.sc->cp[CP_PROP] = (unsigned long long)(P.prop + size_t(d) * P.pcap);
+            L.sc->cp[CP_RM] = rm;
+            L.sc->cp[CP_RT] = rm + 4ull * uint32_t(P.rcap);
+            L.sc->cp[CP_DELTA] = delta;
+            L.sc->cp[CP_POFF] = (unsigned long long)P.propop_off;
+            L.sc->cp[CP_PKV] = (unsigned long long)P.propop_kv;
+            L.sc->cp[CP_KIX] = (unsigned long long)P.key_index;
+            L.sc->cp[CP_VEQ] = (unsigned long long)P.val_eq;
+        }
+        wsync();
     }
 
     // ------------------------------------------------------------ delta ranges
@@ -2018,7 +2046,7 @@ struct Eng {
             return;
         }
         if (lane_id() == 0) {
-            const gptr<uint32_t> r = L.gdelta + 4 * size_t(s.dused);
+            const gptr<uint32_t> r = L.gdelta() + 4 * size_t(s.dused);
             r[0] = uint32_t(op);
             r[1] = uint32_t(a);
             r[2] = uint32_t(b);
@@ -2052,7 +2080,7 @@ struct Eng {
                     return;
                 }
                 if (t) {
-                    const gptr<uint32_t> r = L.gdelta + 4 * size_t(s.dused + __popcll(tm & lanes_below()));
+                    const gptr<uint32_t> r = L.gdelta() + 4 * size_t(s.dused + __popcll(tm & lanes_below()));
                     r[0] = uint32_t(gidx);
                     r[1] = uint32_t(carry + inc - loc);
                     r[2] = uint32_t(len);
