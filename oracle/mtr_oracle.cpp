@@ -7,9 +7,12 @@
 // Differences from the reference that are deliberate and behaviour-neutral:
 //  * Block lengths seen by a remote (refSeq, clientId) view are the sum of the
 //    leaves' nodeLength (undefined counted as 0) instead of
-//    PartialSequenceLengths.getPartialLength (partialLengths.ts:698).  The
-//    reference's own tests assert the two agree (test/testUtils.ts:209-248,
-//    used by test/partialLength.spec.ts); see DESIGN.md "Oracle".
+//    PartialSequenceLengths.getPartialLength (partialLengths.ts:698).  psl.h
+//    restates PartialSequenceLengths and, with oracle_set_psl_check on, the oracle
+//    maintains it at the reference's call sites and compares the two at every
+//    query (tests/test_partial_lengths.py: all golden logs and seeded sets agree;
+//    the one modelled quirk, a leaf-level root's stale own length, is documented
+//    at Tree::pslCheck).
 //  * Ordinals, tiles/range stacks, local references, attribution, pending
 //    segment groups and delta/maintenance events are not modelled: none of them
 //    change the observer's text, segment boundaries or summary bytes.
@@ -23,7 +26,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <atomic>
 #include <chrono>
@@ -44,6 +49,11 @@ constexpr int kUndef = -1;                   // "undefined" node length
 constexpr int64_t kMaxSafe = 9007199254740991LL;
 int g_trace = 0;
 int g_trace_seq = -1;
+// PartialSequenceLengths cross-check (psl.h): off unless a test turns it on
+int g_psl = 0;
+std::atomic<long long> g_psl_checks{0}, g_psl_mismatch{0}, g_psl_rootlag{0};
+std::mutex g_psl_mu;
+std::string g_psl_first;
 #define OTRACE(...)                          \
     do {                                     \
         if (g_trace) printf(__VA_ARGS__);    \
@@ -79,10 +89,12 @@ struct Seg : Node {
     PropMap props;
 };
 
+struct PSL;
 struct Block : Node {
     int childCount = 0;
     Node* children[kMaxNodesInBlock] = {};
     int needsScour = -1;  // -1 undefined, 0 false, 1 true
+    std::shared_ptr<PSL> pl;  // partialLengths (maintained only with the psl.h cross-check on)
     Block() { leaf = false; }
 };
 
@@ -124,6 +136,8 @@ struct Heap {
         }
     }
 };
+
+#include "psl.h"
 
 struct Tables {
     const mtr_batch* b = nullptr;
@@ -283,8 +297,60 @@ class Tree {
             if (n->leaf) return localNetLength(static_cast<const Seg*>(n));
             return blockLocalLength(static_cast<const Block*>(n));
         }
-        if (!n->leaf) return blockRemoteLength(static_cast<const Block*>(n), refSeq, clientId);
+        if (!n->leaf) {
+            const int l = blockRemoteLength(static_cast<const Block*>(n), refSeq, clientId);
+            if (pslOn) pslCheck(static_cast<const Block*>(n), refSeq, clientId, l);
+            return l;
+        }
         return leafRemoteLength(static_cast<const Seg*>(n), refSeq, clientId);
+    }
+
+    // ---------------------------------------------------------------- PartialSequenceLengths (psl.h)
+    // The reference's block length at a remote view is partialLengths.getPartialLength
+    // (mergeTree.ts:928-931); the oracle's is the sum of its leaves.  With the cross-check on, every
+    // block keeps its PartialSequenceLengths, updated where mergeTree.ts / zamboni.ts update it, and
+    // every remote block-length query compares the two (test/testUtils.ts:209-248).
+    bool pslOn = g_psl != 0;
+    //
+    // One reference quirk is modelled, not flagged: a root whose children are leaves never receives
+    // markRangeRemoved's post-order update (depthFirstNodeWalk's first block result is undefined,
+    // mergeTreeNodeWalk.ts:98-105), so its partialLengths miss removes until the next combine and
+    // read high.  The reference reads a root's own partial length only as nodeMap's default end
+    // (legacy extractSync's mapRange, where a high end changes nothing: the walk ends with the leaves)
+    // and in getLength; such queries pass when partial length >= leaf sum (counted in rootlag).
+    void pslCheck(const Block* b, int refSeq, int clientId, int leafSum) const {
+        g_psl_checks++;
+        const bool have = b->pl != nullptr;
+        const int64_t v = have ? b->pl->getPartialLength(refSeq, clientId) : -1;
+        const bool leafRoot = b == root && b->childCount > 0 && b->children[0]->leaf;
+        if (have && leafRoot && v > int64_t(leafSum)) {
+            g_psl_rootlag++;
+            return;
+        }
+        if (!have || v != int64_t(leafSum)) {
+            if (g_psl_mismatch++ == 0) {
+                std::lock_guard<std::mutex> g(g_psl_mu);
+                char buf[256];
+                snprintf(buf, sizeof buf, "op seq %d: %s of %d children at (refSeq %d, client %d): partial length %lld, "
+                         "leaf sum %d%s", curOpSeq, b == root ? "root" : "block", b->childCount, refSeq, clientId,
+                         (long long)v, leafSum, have ? "" : " (no partialLengths)");
+                g_psl_first = buf;
+            }
+        }
+    }
+    // nodeUpdateLengthNewStructure, mergeTree.ts:2183-2189
+    void nodeUpdateLengthNewStructure(Block* b, bool recur = false) {
+        if (pslOn && collaborating) b->pl = pslCombine(b, minSeq, recur);
+    }
+    // blockUpdateLength, mergeTree.ts:2431-2449 (MergeTree.options.incrementalUpdate = true)
+    void blockUpdateLength(Block* b, int seq, int clientId) {
+        if (!pslOn || !collaborating || seq == kUnassignedSeq || seq == kTreeMaintenanceSeq) return;
+        if (b->pl && clientId != kNonCollabClient) pslUpdate(*b->pl, b, seq, clientId, minSeq);
+        else b->pl = pslCombine(b, minSeq, false);
+    }
+    // blockUpdatePathLengths(block, UnassignedSequenceNumber, -1, newStructure = true), mergeTree.ts:2414-2429
+    void blockUpdatePathLengthsNew(Block* b) {
+        for (; b; b = b->parent) nodeUpdateLengthNewStructure(b);
     }
 
     // ------------------------------------------------------------ segments
@@ -414,6 +480,8 @@ class Tree {
             assignChild(nb, node->children[half + i], i);
             node->children[half + i] = nullptr;
         }
+        nodeUpdateLengthNewStructure(node);
+        nodeUpdateLengthNewStructure(nb);
         return nb;
     }
 
@@ -429,7 +497,10 @@ class Tree {
             if (_pos < len || (_pos == len && breakTie(_pos, child, seq))) {
                 if (!child->leaf) {
                     Block* splitNode = insertingWalk(static_cast<Block*>(child), _pos, refSeq, clientId, seq, ctx);
-                    if (splitNode == nullptr) return nullptr;
+                    if (splitNode == nullptr) {  // mergeTree.ts:1778-1784
+                        blockUpdateLength(block, seq, clientId);
+                        return nullptr;
+                    }
                     if (splitNode == unfinished()) {
                         _pos -= len;
                         continue;
@@ -462,7 +533,10 @@ class Tree {
             }
             assignChild(block, newNode, childIndex);
             block->childCount++;
-            if (block->childCount < kMaxNodesInBlock) return nullptr;
+            if (block->childCount < kMaxNodesInBlock) {  // mergeTree.ts:1837-1848
+                blockUpdateLength(block, seq, clientId);
+                return nullptr;
+            }
             return split(block);
         }
         return nullptr;
@@ -476,6 +550,7 @@ class Tree {
             assignChild(nr, root, 0);
             assignChild(nr, splitNode, 1);
             root = nr;
+            nodeUpdateLengthNewStructure(root);
         }
     }
 
@@ -494,20 +569,27 @@ class Tree {
         }
     }
 
-    // nodeMap restricted to its leaf visits, mergeTree.ts:2526-2577 + mergeTreeNodeWalk.ts:35-115.
-    // (The post action only maintains cached/partial lengths, which this oracle recomputes.)
-    template <class F>
-    void nodeMap(int refSeq, int clientId, F&& leaf, int start, int end) {
+    // nodeMap, mergeTree.ts:2526-2577 over depthFirstNodeWalk, mergeTreeNodeWalk.ts:35-115.  Leaf
+    // actions run in walk order (they never change a length the walk reads later: the leaf was
+    // passed, sibling and ancestor lengths were read before).  `post` is the walk's upAction: after
+    // every block the walk descended into (downAction Continue), and on the way up for its ancestors
+    // -- the root included when it holds blocks; a root holding leaves never gets it (the walk's
+    // first block result is undefined, mergeTreeNodeWalk.ts:98-105).
+    struct NoPost {
+        void operator()(Block*) const {}
+    };
+    template <class F, class Post = NoPost>
+    void nodeMap(int refSeq, int clientId, F&& leaf, int start, int end, Post post = Post()) {
         int endPos = end >= 0 ? end : std::max(0, nodeLength(root, refSeq, clientId));
         if (endPos == start) return;
         int pos = 0;
         bool exit = false;
-        std::vector<Seg*> visit;  // collect then apply: leaf actions never change lengths seen later
-        walkMap(root, refSeq, clientId, start, endPos, pos, exit, visit);
-        for (Seg* s : visit) leaf(s);
+        walkMap(root, refSeq, clientId, start, endPos, pos, exit, leaf, post);
+        if (root->childCount > 0 && !root->children[0]->leaf) post(root);
     }
-    void walkMap(Block* b, int refSeq, int clientId, int start, int endPos, int& pos, bool& exit,
-                 std::vector<Seg*>& visit) {
+    template <class F, class Post>
+    void walkMap(Block* b, int refSeq, int clientId, int start, int endPos, int& pos, bool& exit, F& leaf,
+                 Post& post) {
         for (int i = 0; i < b->childCount && !exit; i++) {
             Node* n = b->children[i];
             if (endPos <= pos) {
@@ -522,10 +604,11 @@ class Tree {
                 continue;
             }
             if (n->leaf) {
-                visit.push_back(static_cast<Seg*>(n));
+                leaf(static_cast<Seg*>(n));
                 pos = nextPos;
             } else {
-                walkMap(static_cast<Block*>(n), refSeq, clientId, start, endPos, pos, exit, visit);
+                walkMap(static_cast<Block*>(n), refSeq, clientId, start, endPos, pos, exit, leaf, post);
+                post(static_cast<Block*>(n));
             }
         }
     }
@@ -607,6 +690,7 @@ class Tree {
                 for (int pi = 0; pi < nc; pi++) assignChild(pb, hold[packed++], pi);
                 pb->parent = parent;
                 blocks.push_back(pb);
+                nodeUpdateLengthNewStructure(pb);  // zamboni.ts:103
             }
             for (int j = 0; j < kMaxNodesInBlock; j++) parent->children[j] = nullptr;
             for (int j = 0; j < childCount; j++) assignChild(parent, blocks[j], j);
@@ -616,6 +700,7 @@ class Tree {
             parent->childCount = 0;
         }
         if (underflow(parent) && parent->parent) packParent(parent->parent);
+        else blockUpdatePathLengthsNew(parent);  // zamboni.ts:114-119
     }
 
     // zamboniSegments, zamboni.ts:19-60
@@ -653,6 +738,7 @@ class Tree {
                     block->childCount = newCount;
                     for (int j = 0; j < newCount; j++) assignChild(block, copy[j], j);
                     if (underflow(block) && block->parent) packParent(block->parent);
+                    else blockUpdatePathLengthsNew(block);  // zamboni.ts:52-56
                 }
             }
         }
@@ -763,10 +849,12 @@ class Tree {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
         std::vector<Seg*> fresh;  // removedSegments (mergeTree.ts:1975-2000)
+        bool overwrite = false;   // _overwrite: an overlapping remove rebuilds lengths (mergeTree.ts:1966,2012-2019)
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
                 if (s->removed) {
+                    overwrite = true;
                     if (s->removedSeq == kUnassignedSeq) {
                         s->removedClientIds.insert(s->removedClientIds.begin(), clientId);
                         s->removedSeq = seq;
@@ -783,7 +871,11 @@ class Tree {
                     if (!(s->removedSeq == kUnassignedSeq && clientId == localClientId)) addToLRUSet(s, seq);
                 }
             },
-            start, end);
+            start, end,
+            [&](Block* b) {  // afterMarkRemoved, mergeTree.ts:2012-2019
+                if (overwrite) nodeUpdateLengthNewStructure(b);
+                else blockUpdateLength(b, seq, clientId);
+            });
         recordDeltas(fresh, MTR_OP_REMOVE);  // mergeTree.ts:2026-2031
         if (collaborating && seq != kUnassignedSeq) zamboniSegments();
     }
@@ -897,6 +989,7 @@ class Tree {
                 currentSeq = op.seq;
                 collaborating = true;
                 heap = Heap();
+                nodeUpdateLengthNewStructure(root, true);  // mergeTree.ts:738
                 return status;
             default:
                 return MTR_ERR_BAD_OP;
@@ -928,7 +1021,9 @@ class Tree {
         int p = 0;
         bool exit = false;
         std::vector<Seg*> visit;
-        walkMap(root, refSeq, clientId, pos, pos + 1, p, exit, visit);
+        auto collect = [&](Seg* x) { visit.push_back(x); };
+        NoPost none;
+        walkMap(root, refSeq, clientId, pos, pos + 1, p, exit, collect, none);
         if (!visit.empty()) {
             found = visit[0];
             // position of the leaf in this view: sum of the lengths of the leaves before it
@@ -1180,6 +1275,28 @@ struct oracle_doc {
 };
 
 extern "C" {
+
+void oracle_set_psl_check(int on) {
+    g_psl = on;
+    g_psl_checks = 0;
+    g_psl_mismatch = 0;
+    g_psl_rootlag = 0;
+    std::lock_guard<std::mutex> g(g_psl_mu);
+    g_psl_first.clear();
+}
+
+int64_t oracle_psl_stats(int64_t* out, char* first, int64_t cap) {
+    out[0] = g_psl_checks.load();
+    out[1] = g_psl_mismatch.load();
+    out[2] = g_psl_rootlag.load();
+    std::lock_guard<std::mutex> g(g_psl_mu);
+    if (first && cap > 0) {
+        const size_t n = std::min<size_t>(size_t(cap) - 1, g_psl_first.size());
+        std::memcpy(first, g_psl_first.data(), n);
+        first[n] = 0;
+    }
+    return out[1];
+}
 
 void oracle_set_trace(int on) {
     g_trace = on;
@@ -1438,22 +1555,24 @@ int64_t oracle_doc_summarize(oracle_doc* d, const mtr_batch* b, uint32_t doc_ind
         }
     } else {
         // extractSync, snapshotlegacy.ts:184-255: mapRange(minSeq, NonCollabClient)
+        // (nodeMap with the default end: the root's own length at (minSeq, NonCollabClient))
         std::vector<SpecOut> segs;
         const int cid = kNonCollabClient;
-        for (Seg* s : lv) {
-            int l = t.nodeLength(s, minSeq, cid);
-            if (l == kUndef || l == 0) continue;
-            if (s->seq != kUnassignedSeq && s->seq <= minSeq &&
-                (!s->removed || s->removedSeq == kUnassignedSeq || s->removedSeq > minSeq)) {
-                if (prev.has && Tree::canAppend(&prev.seg, s) && matchProperties(&prev.seg, s, b)) {
-                    prev.seg.text += s->text;
-                    prev.seg.len += s->len;
-                } else {
-                    pushPrev();
-                    takePrev(s);
+        t.nodeMap(
+            minSeq, cid,
+            [&](Seg* s) {
+                if (s->seq != kUnassignedSeq && s->seq <= minSeq &&
+                    (!s->removed || s->removedSeq == kUnassignedSeq || s->removedSeq > minSeq)) {
+                    if (prev.has && Tree::canAppend(&prev.seg, s) && matchProperties(&prev.seg, s, b)) {
+                        prev.seg.text += s->text;
+                        prev.seg.len += s->len;
+                    } else {
+                        pushPrev();
+                        takePrev(s);
+                    }
                 }
-            }
-        }
+            },
+            0, -1);
         pushPrev();
         int64_t totalLen = 0;
         for (auto& sp : specs) totalLen += sp.len;

@@ -85,6 +85,15 @@ int oracle_generate_grown(const struct mtr_synth_cfg* cfg, const mtr_batch* tabl
 int oracle_generate_matrix(const struct mtr_synth_cfg* cfg, const mtr_batch* tables, const mtr_options* opt,
                            uint32_t lo, uint32_t hi, int nthreads, mtr_op* ops_out, uint64_t* hashes, int32_t* status);
 
+/* PartialSequenceLengths cross-check (oracle/psl.h): documents created while it is on keep the
+ * reference's per-block PartialSequenceLengths, updated where mergeTree.ts / zamboni.ts update them,
+ * and every remote block-length query compares getPartialLength with the oracle's leaf sum.
+ * oracle_psl_stats: out[0] = queries checked, out[1] = mismatches (returned), out[2] = queries of a
+ * leaf-level root whose partial length read high (a reference quirk, see psl.h / pslCheck); `first`
+ * receives a description of the first mismatch. */
+void oracle_set_psl_check(int on);
+int64_t oracle_psl_stats(int64_t* out, char* first, int64_t cap);
+
 /* Debug: print zamboni decisions to stdout */
 void oracle_set_trace(int on);
 

@@ -58,10 +58,35 @@ def lib():
         L.oracle_replay_matrix_batch.restype = C.c_double
         L.oracle_replay_matrix_batch.argtypes = [C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32,
                                                  C.c_int, C.c_void_p, C.c_void_p]
+        L.oracle_set_psl_check.argtypes = [C.c_int]
+        L.oracle_psl_stats.restype = C.c_int64
+        L.oracle_psl_stats.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         _LIB = L
     return _LIB
+
+
+class psl_check:
+    """Context manager: oracle documents created inside keep the reference's PartialSequenceLengths
+    and compare every remote block-length query with the leaf sum (oracle/psl.h).  `.stats()` ->
+    (queries checked, mismatches, first mismatch); `.rootlag` = leaf-level root queries that read high
+    (the reference's stale-root quirk, harmless where the reference reads it)."""
+
+    def __enter__(self):
+        lib().oracle_set_psl_check(1)
+        return self
+
+    def stats(self):
+        out = np.zeros(3, dtype="<i8")
+        buf = C.create_string_buffer(512)
+        lib().oracle_psl_stats(out.ctypes.data, buf, 512)
+        self.rootlag = int(out[2])
+        return int(out[0]), int(out[1]), buf.value.decode()
+
+    def __exit__(self, *exc):
+        lib().oracle_set_psl_check(0)
+        return False
 
 
 def options(new_length_calc=False, snapshot_v1=True, chunk_size=10000):
