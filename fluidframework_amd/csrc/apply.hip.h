@@ -476,6 +476,66 @@ struct Eng {
         wsync();
     }
 
+    // getContainingSegment of one document (mergeTree.ts:787-813: nodeMap over [pos, pos + 1)): i = the
+    // first leaf whose inclusive visible prefix exceeds pos (S if none), before = the visible length
+    // ahead of it.  Writes no scan array.
+    static MTR_DI void find1(const D& L, const St& s, const View& v, int pos, int& i_out, int& before, int newlen) {
+        const int S = s.nseg;
+        const int ln = lane_id();
+        int c = 0;
+        i_out = S;
+        before = 0;
+        for (int base = 0; base < S; base += 64) {
+            const int i = base + ln;
+            const Hot h = ld_hot(L, min(i, S - 1));
+            const int x0 = vis_hot(L, h, i, v, newlen, s.minseq, i < S);
+            const int x = (i < S) ? max(x0, 0) : 0;
+            const int inc = wave_incl_scan(x);
+            const uint64_t m = __ballot((i < S) & (c + inc > pos));
+            if (m) {
+                const int l = first_lane(m);
+                i_out = base + l;
+                before = c + rdlane(inc - x, l);
+                return;
+            }
+            c += rdlane(inc, 63);
+        }
+        before = c;
+    }
+
+    // Client.getContainingSegment(pos, {referenceSequenceNumber, clientId}) (client.ts:1065-1078) on a
+    // document's HBM state: out = mtr_segment_info (include/mtr.h) of the leaf holding pos, leaf -1
+    // when no segment covers pos in that view
+    static MTR_DI void containing(char* smem, const KParams& P, uint32_t d, int pos, int ref, int client, int32_t* out) {
+        D L;
+        carve(L, smem, P, d);
+        St s;
+        load_doc(L, P, s, d);
+        View v;
+        v.ref = ref;
+        v.client = enc_client(client);
+        v.local = (!s.collab || uint32_t(s.local) == v.client) ? 1 : 0;
+        int i, before;
+        find1(L, s, v, pos, i, before, P.new_length_calc);
+        if (lane_id() == 0) {
+            if (i >= s.nseg || pos < 0) {
+                out[0] = -1;
+            } else {
+                const uint32_t m = L.meta[i];
+                out[0] = i;
+                out[1] = pos - before;
+                out[2] = L.len[i];
+                out[3] = L.seq[i];
+                out[4] = dec_client(m & M_CLIENT_MASK);
+                out[5] = L.rseq[i] == RNONE ? -1 : L.rseq[i];
+                out[6] = (m & M_MARKER) ? 1 : 0;
+                out[7] = int(L.text[i]);
+                out[8] = int(L.props[i]);
+                out[9] = before;
+            }
+        }
+    }
+
     // getContainingSegment for two vectors at once (a setCell's row and col): two visibility scans
     // interleaved round by round (independent chains of LDS reads and DPP scans that overlap), each
     // stopping at the round that reaches its position.  ia / ib = first leaf whose inclusive

@@ -101,7 +101,7 @@ struct mtr_engine {
     DevBuf<uint64_t> doff;            // [doc + 1] record offsets into delta (exact per-batch bound)
     std::vector<uint64_t> h_doff;
     bool has_delta = false;
-    DevBuf<int32_t> red;              // small reduction buffer
+    DevBuf<int32_t> red;              // small reduction / query-result buffer
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
     DevBuf<uint32_t> dlist;           // [class][n_docs] document lists of one apply round
@@ -224,6 +224,13 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
     if (c >= 0) list[size_t(c) * n + lbase[c] + rank] = d;
 }
 
+// one getContainingSegment query on a document's HBM state (mtr_get_containing_segment)
+__global__ void __launch_bounds__(NT) containing_kernel(KParams P, uint32_t d, int pos, int ref, int client,
+                                                        int32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    Eng<true>::containing(smem, P, d, pos, ref, client, out);
+}
+
 template <class T>
 static int upload(mtr_engine* e, DevBuf<T>& dst, const T* src, size_t n) {
     if (dst.ensure(n)) return -1;
@@ -274,7 +281,7 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
     }
     if (e->hdr.ensure(D) || e->seg.ensure(D * NF * c.max_segments) || e->heap.ensure(D * 2 * c.heap_entries) ||
         e->text.ensure(D * c.text_units) || e->prop.ensure(D * c.prop_words) || e->rm.ensure(D * (c.remover_cells + 2 * size_t(e->rtab))) ||
-        e->stat.ensure(D * 4) || e->red.ensure(4)) {
+        e->stat.ensure(D * 4) || e->red.ensure(16)) {
         mtr_engine_destroy(e);
         return nullptr;
     }
@@ -1088,6 +1095,53 @@ int64_t mtr_get_text(mtr_engine* e, uint32_t doc, uint16_t* out, int64_t cap) {
         }
     }
     return n;
+}
+
+int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
+                               mtr_segment_info* info, uint16_t* text, int64_t text_cap) {
+    HIPCHK(hipSetDevice(e->device));
+    if (doc >= e->max_docs || !info) {
+        set_err("mtr_get_containing_segment: bad document");
+        return -1;
+    }
+    KParams P{};
+    P.hdr = e->hdr.p;
+    P.seg = e->seg.p;
+    P.heap = e->heap.p;
+    P.text = e->text.p;
+    P.prop = e->prop.p;
+    P.rm = e->rm.p;
+    P.segcap = int(e->caps.max_segments);
+    P.hcap = int(e->caps.heap_entries);
+    P.tcap = int(e->caps.text_units);
+    P.pcap = int(e->caps.prop_words);
+    P.rcap = int(e->caps.remover_cells);
+    P.rtab = e->rtab;
+    P.new_length_calc = e->opt.new_length_calc;
+    P.n_docs = e->n_docs;
+    if (e->red.ensure(16)) return -1;
+    containing_kernel<<<1, NT, lds_bytes_global_mode(), e->stream>>>(P, doc, pos, ref_seq, client, e->red.p);
+    HIPCHK(hipGetLastError());
+    int32_t r[10];
+    HIPCHK(hipMemcpyAsync(r, e->red.p, sizeof(r), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    std::memset(info, 0, sizeof(*info));
+    info->leaf = r[0];
+    if (r[0] < 0) return MTR_OK;
+    info->offset = r[1];
+    info->length = r[2];
+    info->seq = r[3];
+    info->client = r[4];
+    info->removed_seq = r[5];
+    info->marker = r[6];
+    info->ref_type = r[7];
+    info->props = r[8];
+    info->start = r[9];
+    const bool has_text = !info->marker && e->h_kind[doc] == 0;
+    if (text && has_text && info->length > 0 && text_cap >= info->length)
+        HIPCHK(hipMemcpy(text, e->text.p + size_t(doc) * e->caps.text_units + uint32_t(r[7]),
+                         size_t(info->length) * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    return MTR_OK;
 }
 
 int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index) {

@@ -32,6 +32,12 @@ class MtrCaps(C.Structure):
     ]
 
 
+class SegmentInfo(C.Structure):
+    """include/mtr.h: mtr_segment_info"""
+    _fields_ = [(n, C.c_int32) for n in ("leaf", "offset", "length", "seq", "client", "removed_seq", "marker",
+                                         "ref_type", "props", "start")]
+
+
 def lib():
     """Load libmtr.so (never falls back to anything else)."""
     global _LIB
@@ -65,6 +71,9 @@ def lib():
         L.mtr_summary_bytes.restype = C.c_int64
         L.mtr_get_text.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.mtr_get_text.restype = C.c_int64
+        L.mtr_get_containing_segment.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
+                                                 C.POINTER(SegmentInfo), C.c_void_p, C.c_int64]
+        L.mtr_get_containing_segment.restype = C.c_int
         L.mtr_doc_status.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_int32)]
         L.mtr_doc_status.restype = C.c_int
         L.mtr_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
@@ -292,6 +301,19 @@ class Engine:
                 break
             cap = -n
         return out[:n]
+
+    def containing_segment(self, doc, pos, ref_seq, client):
+        """Client.getContainingSegment(pos, {referenceSequenceNumber, clientId}) on the device:
+        None when no segment covers pos, else a dict of mtr_segment_info fields plus the text."""
+        info = SegmentInfo()
+        text = np.zeros(1 << 16, dtype="<u2")
+        self._check(lib().mtr_get_containing_segment(self.h, doc, pos, ref_seq, client, C.byref(info),
+                                                     text.ctypes.data, text.size), "mtr_get_containing_segment")
+        if info.leaf < 0:
+            return None
+        r = {n: getattr(info, n) for n, _ in SegmentInfo._fields_}
+        r["text"] = None if info.marker else text[:info.length].tobytes().decode("utf-16-le", "surrogatepass")
+        return r
 
     def status(self, doc):
         op = C.c_int32(-1)

@@ -32,8 +32,8 @@ function native() {
 
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
-    START_COLLAB: 12 };
-const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, DELTA: 64 };
+    START_COLLAB: 12, SETCELL: 14 };
+const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, COLS: 32, DELTA: 64 };
 const NULL_VALUE = 0xFFFFFFFF;
 const MAX_CLIENTS = 253;  // include/mtr_types.h MTR_MAX_CLIENTS: short ids per engine document
 const NOT_INDEX = 0xFFFFFFFF;
@@ -215,6 +215,62 @@ class DocLog {
     }
 }
 
+/*
+ * SharedMatrix (SharedMatrix.processCore, matrix/src/matrix.ts:636-693, remote branch): vector ops
+ * (contents.target "rows" / "cols") are merge-tree ops on that PermutationVector, whose segment specs
+ * are [length, start] (permutationvector.ts:45-48; the remote start is discarded on INSERT); a set-cell
+ * message is one SETCELL record.  Both vectors share the rows log's client table.  Mirrors
+ * fluidframework_amd/batch.py MatrixLog record for record.
+ */
+class MatrixDocLog extends DocLog {
+    message(msg, it) {
+        const cid = msg.clientId === null || msg.clientId === undefined ? 'null' : String(msg.clientId);
+        if (msg.type !== 'op') return;  // SharedMatrix has no MSN handler of its own
+        if (cid === this.observerId) throw new UnsupportedError('message authored by the observer (local ack path)');
+        const short = this.shortId(cid);
+        const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
+        let contents = msg.contents;
+        if (typeof contents === 'string') contents = JSON.parse(contents);
+        const target = contents.target;
+        if (target === undefined || target === null) {  // MatrixOp.set (matrix/src/ops.ts:8-12)
+            if (contents.type !== 2) throw new UnsupportedError('matrix message without a target');
+            this.push(OP.SETCELL, 0, short, seq, ref, msn, contents.row, contents.col, 0, 0);
+            return;
+        }
+        if (target !== 'rows' && target !== 'cols') throw new UnsupportedError('matrix target ' + target);
+        const tf = target === 'cols' ? F.COLS : 0;
+        const members = contents.type === 3 ? contents.ops : [contents];
+        if (members.length === 0) { this.push(OP.SEQ, F.LAST | tf, short, seq, ref, msn, 0, 0, 0, 0); return; }
+        members.forEach((op, i) => {
+            const last = (i === members.length - 1 ? F.LAST : 0) | tf;
+            if ('relativePos1' in op || 'relativePos2' in op) throw new UnsupportedError('relative positions');
+            if (op.type === 0) {
+                const seg = op.seg;
+                if (seg === undefined || seg === null) { this.push(OP.SEQ, last, short, seq, ref, msn, 0, 0, 0, 0); return; }
+                if (!Array.isArray(seg) || seg.length !== 2) throw new UnsupportedError('PermutationSegment spec');
+                this.push(OP.INSERT, last, short, seq, ref, msn, op.pos1, -1, 0, seg[0]);
+            } else if (op.type === 1) {
+                this.push(OP.REMOVE, last, short, seq, ref, msn, op.pos1, op.pos2, 0, 0);
+            } else {
+                throw new UnsupportedError('vector op type ' + op.type);
+            }
+        });
+    }
+    colsLog() {  // the cols vector's engine document: no ops of its own, the same client table
+        const c = new DocLog();
+        c.observerId = this.observerId;
+        c.clients = this.clients.slice();
+        c.clientIx = new Map(this.clientIx);
+        return c;
+    }
+}
+/** Engine document order for matrices: [rows 0, cols 0, rows 1, cols 1, ...] (pair 2m / 2m+1). */
+function matrixLogs(logs) {
+    const out = [];
+    for (const m of logs) { out.push(m); out.push(m.colsLog()); }
+    return out;
+}
+
 function offsets(chunks) {
     const off = new Uint32Array(chunks.length + 1);
     for (let i = 0; i < chunks.length; i++) off[i + 1] = off[i] + chunks[i].length;
@@ -381,12 +437,44 @@ class BatchReplayEngine {
         this.catchUps.push(new CatchUpLog());
         return new BatchReplayClient(this, this.logs.length - 1);
     }
-    flush() {  // apply every queued message of every document
-        if (!this.dirty) return;
-        native().submitRun(this.h, buildBatch(this.logs, this.interner));
+    createMatrix() {  // a SharedMatrix: its rows and cols PermutationVectors as engine documents 2k, 2k+1
+        if (this.logs.length + 2 > this.maxDocs) throw new Error('engine is full');
+        const rows = this.logs.length;
+        const log = new MatrixDocLog();
+        this.logs.push(log, log.colsLog());
+        this.catchUps.push(new CatchUpLog(), new CatchUpLog());
+        native().setMatrix(this.h, rows, rows + 1);
+        return new BatchMatrixClient(this, rows);
+    }
+    _batch() {
+        this.logs.forEach((l, d) => {  // cols vectors share their rows log's client table
+            if (l instanceof MatrixDocLog) this.logs[d + 1] = l.colsLog();
+        });
+        return buildBatch(this.logs, this.interner);
+    }
+    _afterRun() {
         this.catchUps.forEach((c, d) => { if (c.pending.length) c.resolve(native().getDeltas(this.h, d)); });
         this.dirty = false;
         this.summarized = false;
+    }
+    flush() {  // apply every queued message of every document
+        if (!this.dirty) return;
+        native().submitRun(this.h, this._batch());
+        this._afterRun();
+    }
+    /**
+     * The asynchronous flush: the batch is applied on a worker thread (N-API async work) and the
+     * returned promise settles when the GPU is done, so the event loop keeps serving meanwhile.  Other
+     * calls on this engine throw until it settles (await it).
+     */
+    async flushAsync() {
+        if (!this.dirty) return;
+        await native().submitRunAsync(this.h, this._batch());
+        this._afterRun();
+    }
+    async summarizeAllAsync() {  // every document's blobs, built on a worker thread
+        await this.flushAsync();
+        if (!this.summarized) { await native().summarizeAsync(this.h); this.summarized = true; }
     }
 }
 
@@ -441,6 +529,34 @@ class BatchReplayClient {
     }
     getLength() { return this.getText().length; }
     /**
+     * Client.getContainingSegment(pos, sequenceArgs) (client.ts:1065-1078): the segment holding pos in
+     * the view of sequenceArgs = {referenceSequenceNumber, clientId} (default: this client's current
+     * view), found on the device.  -> {segment: {text | marker, cachedLength, seq, clientId, removedSeq,
+     * properties index}, offset} with both undefined when no segment covers pos.
+     */
+    getContainingSegment(pos, sequenceArgs) {
+        this.engine.flush();
+        this._check();
+        let ref, client;
+        if (sequenceArgs === undefined) {  // getClientSequenceArgsForMessage, client.ts:598-630
+            ref = this.currentSeq;
+            client = this.log.collaborating ? this.log.clientIx.get(this.log.observerId) : -1;
+        } else {
+            ref = sequenceArgs.referenceSequenceNumber;
+            const cid = sequenceArgs.clientId === null || sequenceArgs.clientId === undefined ? 'null'
+                : String(sequenceArgs.clientId);
+            client = this.log.shortId(cid);  // getOrAddShortClientId
+        }
+        const r = native().getContainingSegment(this.engine.h, this.doc, pos, ref, client);
+        if (r === null) return { segment: undefined, offset: undefined };
+        const longId = (c) => (c >= 0 ? this.log.clients[c] : 'original');
+        const segment = { cachedLength: r.length, seq: r.seq, clientId: longId(r.client), leafIndex: r.leaf,
+            removedSeq: r.removedSeq < 0 ? undefined : r.removedSeq, propertySet: r.props < 0 ? undefined : r.props };
+        if (r.marker) segment.marker = { refType: r.refType };
+        else segment.text = r.text;
+        return { segment, offset: r.offset };
+    }
+    /**
      * Client.summarize (client.ts:966-1000) -> ISummaryTreeWithStats.  In the legacy format the
      * catch-up messages are the shim's own transformed list (CatchUpLog): the caller's list was built
      * without sequenceDelta events, so it is superseded.
@@ -453,6 +569,19 @@ class BatchReplayClient {
         this.engine.flush();
         this._check();
         if (!this.engine.summarized) { native().summarize(this.engine.h); this.engine.summarized = true; }
+        return this._summaryTree(catchUpMsgs, dm, handle, serializer, v1);
+    }
+    /** summarize on a worker thread: resolves to the same ISummaryTreeWithStats. */
+    async summarizeAsync(runtime, handle, serializer, catchUpMsgs) {
+        const dm = runtime.deltaManager;
+        this.updateSeqNumbers(dm.minimumSequenceNumber, dm.lastSequenceNumber);
+        const v1 = !!this.engine.options.snapshotV1;
+        if (v1 && catchUpMsgs !== undefined && catchUpMsgs.length > 0) throw new Error('0x03f');
+        await this.engine.summarizeAllAsync();
+        this._check();
+        return this._summaryTree(catchUpMsgs, dm, handle, serializer, v1);
+    }
+    _summaryTree(catchUpMsgs, dm, handle, serializer, v1) {
         const blobs = native().getSummary(this.engine.h, this.doc);
         if (!v1) catchUpMsgs = this.engine.catchUps[this.doc].forSummary(dm.minimumSequenceNumber);
         const names = v1 ? blobs.map((_, i) => (i === 0 ? 'header' : 'body_' + (i - 1))) : ['header', 'body'];
@@ -472,5 +601,30 @@ class BatchReplayClient {
     }
 }
 
-module.exports = { BatchReplayEngine, BatchReplayClient, Interner, DocLog, buildBatch, UnsupportedError, OP, F,
-    SummaryType, native };
+/**
+ * A SharedMatrix observer (matrix/src/matrix.ts:636-693, remote branch) on a pair of engine documents:
+ * applyMsg queues vector / set-cell messages; summarizeVectors returns each PermutationVector's summary
+ * (V1 segments blobs + handleTable, permutationvector.ts:310-325).  (Cell values are host-side state;
+ * the Python mirror fluidframework_amd/cells.py builds the cells blob from the engine's cell records.)
+ */
+class BatchMatrixClient {
+    constructor(engine, rowsDoc) { this.engine = engine; this.doc = rowsDoc; this.log = engine.logs[rowsDoc]; }
+    startOrUpdateCollaboration(longClientId, minSeq, currentSeq) {
+        this.log.startCollab(longClientId, minSeq || 0, currentSeq || 0);
+        this.engine.dirty = true;
+    }
+    applyMsg(msg) { this.log.message(msg, this.engine.interner); this.engine.dirty = true; }
+    summarizeVectors() {
+        this.engine.flush();
+        for (const d of [this.doc, this.doc + 1]) {
+            const st = native().docStatus(this.engine.h, d);
+            if (st[0] !== STATUS.OK) throw new Error('engine status ' + st[0] + ' at op ' + st[1]);
+        }
+        if (!this.engine.summarized) { native().summarize(this.engine.h); this.engine.summarized = true; }
+        const vec = (d) => native().getSummary(this.engine.h, d).map((b) => b.toString('utf8'));
+        return { rows: vec(this.doc), cols: vec(this.doc + 1) };
+    }
+}
+
+module.exports = { BatchReplayEngine, BatchReplayClient, BatchMatrixClient, Interner, DocLog, MatrixDocLog, matrixLogs,
+    buildBatch, UnsupportedError, OP, F, SummaryType, native };

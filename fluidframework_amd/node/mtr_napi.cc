@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -39,10 +40,18 @@ bool get_args(napi_env env, napi_callback_info info, size_t want, napi_value* ar
     return true;
 }
 
+// engines with an asynchronous run / summarize in flight (only the JS thread touches this set: work is
+// queued and completed there); every other entry point refuses a busy engine
+std::set<mtr_engine*> g_busy;
+
 mtr_engine* engine_of(napi_env env, napi_value v) {
     void* p = nullptr;
     if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
         napi_throw_type_error(env, nullptr, "not an engine handle (destroyed?)");
+        return nullptr;
+    }
+    if (g_busy.count(static_cast<mtr_engine*>(p))) {
+        napi_throw_error(env, nullptr, "engine busy: await the pending submitRunAsync / summarizeAsync first");
         return nullptr;
     }
     return static_cast<mtr_engine*>(p);
@@ -124,14 +133,8 @@ napi_value CreateEngine(napi_env env, napi_callback_info info) {
 
 // submit(h, batch) then apply: Client.applyMsg for every packed message (client.ts:858-887).
 // The batch object carries the arrays of include/mtr_types.h (see index.js buildBatch).
-napi_value SubmitRun(napi_env env, napi_callback_info info) {
-    napi_value argv[2];
-    if (!get_args(env, info, 2, argv)) return nullptr;
-    mtr_engine* e = engine_of(env, argv[0]);
-    if (!e) return nullptr;
-    mtr_batch b{};
+bool parse_batch(napi_env env, napi_value o, mtr_batch& b) {
     size_t n = 0;
-    const napi_value o = argv[1];
     bool ok = arr_prop(env, o, "docs", &b.docs, &n);
     b.n_docs = uint32_t(n);
     ok = ok && arr_prop(env, o, "ops", &b.ops, &n);
@@ -151,15 +154,157 @@ napi_value SubmitRun(napi_env env, napi_callback_info info) {
     ok = ok && arr_prop(env, o, "valEq", &b.val_eq, &n);
     ok = ok && arr_prop(env, o, "clientOff", &b.client_off, &n);
     ok = ok && arr_prop(env, o, "clientBytes", &b.client_bytes, &n);
-    if (!ok) {
-        napi_throw_type_error(env, nullptr, "malformed batch (see include/mtr_types.h)");
-        return nullptr;
-    }
+    if (!ok) napi_throw_type_error(env, nullptr, "malformed batch (see include/mtr_types.h)");
+    return ok;
+}
+
+napi_value SubmitRun(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    mtr_batch b{};
+    if (!parse_batch(env, argv[1], b)) return nullptr;
     // the host arrays belong to the JS heap: the copy must finish before returning
     if (mtr_submit(e, &b) != MTR_OK || mtr_sync(e) != MTR_OK) return throw_engine(env, "mtr_submit");
     if (mtr_run(e) != MTR_OK || mtr_sync(e) != MTR_OK) return throw_engine(env, "mtr_run");
     napi_value r;
     NAPI_CALL(env, napi_get_undefined(env, &r));
+    return r;
+}
+
+// ---- asynchronous forms (napi_async_work + promise): the Node event loop keeps running while the
+// GPU applies a batch / builds the summaries ("mtr_run async")
+struct AsyncJob {
+    napi_async_work work = nullptr;
+    napi_deferred deferred = nullptr;
+    napi_ref keep = nullptr;  // the batch object: its arrays must outlive the host->device copies
+    mtr_engine* e = nullptr;
+    mtr_batch b{};
+    bool summarize = false;
+    int rc = 0;
+    std::string err;
+};
+
+void job_execute(napi_env, void* data) {  // worker thread: no N-API calls here
+    AsyncJob* j = static_cast<AsyncJob*>(data);
+    if (j->summarize) {
+        if (mtr_summarize(j->e) != MTR_OK || mtr_sync(j->e) != MTR_OK) {
+            j->rc = -1;
+            j->err = std::string("mtr_summarize: ") + mtr_last_error();
+        }
+        return;
+    }
+    if (mtr_submit(j->e, &j->b) != MTR_OK || mtr_sync(j->e) != MTR_OK) {
+        j->rc = -1;
+        j->err = std::string("mtr_submit: ") + mtr_last_error();
+    } else if (mtr_run(j->e) != MTR_OK || mtr_sync(j->e) != MTR_OK) {
+        j->rc = -1;
+        j->err = std::string("mtr_run: ") + mtr_last_error();
+    }
+}
+
+void job_complete(napi_env env, napi_status, void* data) {  // JS thread
+    AsyncJob* j = static_cast<AsyncJob*>(data);
+    g_busy.erase(j->e);
+    if (j->keep) napi_delete_reference(env, j->keep);
+    napi_value v;
+    if (j->rc == 0) {
+        napi_get_undefined(env, &v);
+        napi_resolve_deferred(env, j->deferred, v);
+    } else {
+        napi_value msg;
+        napi_create_string_utf8(env, j->err.c_str(), NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, nullptr, msg, &v);
+        napi_reject_deferred(env, j->deferred, v);
+    }
+    napi_delete_async_work(env, j->work);
+    delete j;
+}
+
+napi_value queue_job(napi_env env, AsyncJob* j, const char* name) {
+    napi_value promise, res;
+    if (napi_create_promise(env, &j->deferred, &promise) != napi_ok ||
+        napi_create_string_utf8(env, name, NAPI_AUTO_LENGTH, &res) != napi_ok ||
+        napi_create_async_work(env, nullptr, res, job_execute, job_complete, j, &j->work) != napi_ok ||
+        napi_queue_async_work(env, j->work) != napi_ok) {
+        if (j->keep) napi_delete_reference(env, j->keep);
+        delete j;
+        napi_throw_error(env, nullptr, "cannot queue asynchronous engine work");
+        return nullptr;
+    }
+    g_busy.insert(j->e);
+    return promise;
+}
+
+// submitRunAsync(h, batch) -> Promise: submitRun on a worker thread
+napi_value SubmitRunAsync(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    AsyncJob* j = new AsyncJob();
+    j->e = e;
+    if (!parse_batch(env, argv[1], j->b) || napi_create_reference(env, argv[1], 1, &j->keep) != napi_ok) {
+        delete j;
+        return nullptr;
+    }
+    return queue_job(env, j, "mtr_submit_run");
+}
+
+// summarizeAsync(h) -> Promise: summarize on a worker thread
+napi_value SummarizeAsync(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    AsyncJob* j = new AsyncJob();
+    j->e = e;
+    j->summarize = true;
+    return queue_job(env, j, "mtr_summarize");
+}
+
+// getContainingSegment(h, doc, pos, refSeq, client) -> null | {leaf, offset, length, seq, client,
+// removedSeq, marker, refType, props, start, text}   (client.ts:1065, on the device)
+napi_value GetContainingSegment(napi_env env, napi_callback_info info) {
+    napi_value argv[5];
+    if (!get_args(env, info, 5, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0;
+    int32_t pos = 0, ref = 0, client = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    NAPI_CALL(env, napi_get_value_int32(env, argv[2], &pos));
+    NAPI_CALL(env, napi_get_value_int32(env, argv[3], &ref));
+    NAPI_CALL(env, napi_get_value_int32(env, argv[4], &client));
+    mtr_segment_info si{};
+    std::vector<uint16_t> text(1 << 16);
+    if (mtr_get_containing_segment(e, doc, pos, ref, client, &si, text.data(), int64_t(text.size())) != MTR_OK)
+        return throw_engine(env, "mtr_get_containing_segment");
+    napi_value r;
+    if (si.leaf < 0) {
+        NAPI_CALL(env, napi_get_null(env, &r));
+        return r;
+    }
+    NAPI_CALL(env, napi_create_object(env, &r));
+    const struct {
+        const char* k;
+        int32_t v;
+    } f[] = {{"leaf", si.leaf},   {"offset", si.offset},         {"length", si.length}, {"seq", si.seq},
+             {"client", si.client}, {"removedSeq", si.removed_seq}, {"marker", si.marker}, {"refType", si.ref_type},
+             {"props", si.props}, {"start", si.start}};
+    for (const auto& x : f) {
+        napi_value v;
+        NAPI_CALL(env, napi_create_int32(env, x.v, &v));
+        NAPI_CALL(env, napi_set_named_property(env, r, x.k, v));
+    }
+    napi_value t;
+    if (!si.marker && si.length <= int32_t(text.size())) {
+        NAPI_CALL(env, napi_create_string_utf16(env, reinterpret_cast<const char16_t*>(text.data()), size_t(si.length), &t));
+    } else {
+        NAPI_CALL(env, napi_get_null(env, &t));
+    }
+    NAPI_CALL(env, napi_set_named_property(env, r, "text", t));
     return r;
 }
 
@@ -312,7 +457,8 @@ napi_value Init(napi_env env, napi_value exports) {
     } fns[] = {{"createEngine", CreateEngine}, {"submitRun", SubmitRun}, {"summarize", Summarize},
                {"getSummary", GetSummary},     {"getText", GetText},     {"docStatus", DocStatus},
                {"stats", Stats},               {"reset", Reset},         {"setMatrix", SetMatrix},
-               {"getDeltas", GetDeltas}};
+               {"getDeltas", GetDeltas},       {"submitRunAsync", SubmitRunAsync},
+               {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||

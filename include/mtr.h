@@ -115,6 +115,26 @@ int64_t mtr_summary_bytes(mtr_engine* e);
 /* Local-view text of one document (UTF-16 units); returns length (writes <= cap units). */
 int64_t mtr_get_text(mtr_engine* e, uint32_t doc, uint16_t* out, int64_t cap);
 
+/* Client.getContainingSegment(pos, {referenceSequenceNumber, clientId}) (client.ts:1065-1078 ->
+ * mergeTree.ts:787-813): the segment holding position pos in the (ref_seq, client) view, found on the
+ * device (one wave scans the document's visibility in that view).  client: a short id, -1
+ * (LocalClientId) or -2 (NonCollabClient).  text (cap units, may be NULL) receives a text segment's
+ * units.  Returns MTR_OK with info->leaf = -1 when no segment covers pos. */
+typedef struct mtr_segment_info {
+    int32_t leaf;        /* index of the leaf in tree order, -1 = none */
+    int32_t offset;      /* pos - the segment's start in the view (getContainingSegment's offset) */
+    int32_t length;      /* cachedLength */
+    int32_t seq;         /* segment.seq */
+    int32_t client;      /* segment.clientId: short id, -1 LocalClientId, -2 NonCollabClient */
+    int32_t removed_seq; /* removedSeq, -1 = not removed */
+    int32_t marker;      /* 1 = Marker (text holds nothing; ref_type holds its refType) */
+    int32_t ref_type;    /* marker refType / PermutationSegment start handle / text arena offset */
+    int32_t props;       /* property-set index in the document's arena, -1 = none */
+    int32_t start;       /* the segment's position in the view */
+} mtr_segment_info;
+int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
+                               mtr_segment_info* info, uint16_t* text, int64_t text_cap);
+
 /* Per-document status: MTR_OK or an MTR_ERR_* code; *op_index = op that failed (or -1). */
 int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index);
 

@@ -1364,6 +1364,21 @@ int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap) {
     return n;
 }
 
+int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32_t client, int32_t* out) {
+    Tree& t = d->view();
+    int off = 0;
+    Seg* s = t.containingSegment(pos, ref_seq, client, off);
+    if (!s) {
+        out[0] = -1;
+        return -1;
+    }
+    out[0] = t.leafIndex(s);
+    out[1] = off;
+    out[2] = s->len;
+    out[3] = pos - off;
+    return out[0];
+}
+
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client) {
     if (!d->view().pendingLoad.empty()) d->view().reloadFromSegments();
     return d->view().nodeLength(d->view().root, ref_seq, client);

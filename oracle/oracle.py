@@ -61,6 +61,8 @@ def lib():
         L.oracle_set_psl_check.argtypes = [C.c_int]
         L.oracle_psl_stats.restype = C.c_int64
         L.oracle_psl_stats.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+        L.oracle_doc_containing.restype = C.c_int32
+        L.oracle_doc_containing.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         _LIB = L
@@ -156,6 +158,12 @@ class OracleDoc:
         out = np.zeros(4, dtype="<i8")
         lib().oracle_doc_state(self.h, out.ctypes.data)
         return out
+
+    def containing(self, pos, ref_seq, client):
+        """getContainingSegment -> (leaf index or -1, offset, cachedLength, segment start)."""
+        out = np.zeros(4, dtype="<i4")
+        lib().oracle_doc_containing(self.h, pos, ref_seq, client, out.ctypes.data)
+        return tuple(int(x) for x in out) if out[0] >= 0 else (-1, 0, 0, 0)
 
     def length(self, ref_seq, client):
         return lib().oracle_doc_length(self.h, ref_seq, client)

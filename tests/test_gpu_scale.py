@@ -171,3 +171,49 @@ def test_two_engines_as_two_ranks_equal_one_engine():
     one.summarize()
     assert msgs == total * ops
     assert (sum(digests) & shard.MASK64) == shard.digest(one.hashes(total))
+
+
+def test_containing_segment_matches_oracle():
+    """Client.getContainingSegment(pos, {referenceSequenceNumber, clientId}) on the device
+    (mtr_get_containing_segment) equals the oracle's nodeMap over [pos, pos + 1) at every queried view:
+    the reference replay logs stopped mid-collaboration, views from the MSN to the current seq, every
+    client, every position (and one past the end)."""
+    import random
+
+    from fixtures import load_replay, replay_files, replay_log
+
+    files = [p for p in replay_files() if "clients_8" in p][:5]
+    it = Interner()
+    logs, orcs = [], []
+    for p in files:
+        groups = load_replay(p)
+        log = replay_log(groups, it)
+        for g in groups[:40]:
+            for m in g["msgs"]:
+                log.message(m, it)
+        logs.append(log)
+    b = build_batch(logs, it)
+    eng = _engine(len(files))
+    eng.apply(b)
+    rng = random.Random(7)
+    n_checked = 0
+    for d in range(len(files)):
+        o = OracleDoc(options())
+        assert o.apply(b, d) == 0
+        st = o.state()
+        min_seq, cur = int(st[0]), int(st[1])
+        n_clients = int(b.docs["n_clients"][d])
+        for _ in range(120):
+            ref = rng.randint(min_seq, cur)
+            client = rng.randint(0, n_clients - 1)
+            L = o.length(ref, client)
+            pos = rng.randint(0, max(L, 0))
+            got = eng.containing_segment(d, pos, ref, client)
+            exp = o.containing(pos, ref, client)
+            if exp[0] < 0:
+                assert got is None, (d, pos, ref, client, got)
+                continue
+            assert got is not None, (d, pos, ref, client, exp)
+            assert (got["leaf"], got["offset"], got["length"], got["start"]) == exp, (d, pos, ref, client)
+            n_checked += 1
+    assert n_checked > 400

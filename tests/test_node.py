@@ -47,12 +47,13 @@ def test_addon_loads_and_fails_loudly_without_a_gpu():
                  NODE_DIR])
     lines = out.strip().splitlines()
     assert json.loads(lines[0]) == sorted(["createEngine", "submitRun", "summarize", "getSummary", "getText",
-                                           "docStatus", "stats", "reset", "setMatrix", "getDeltas"])
+                                           "docStatus", "stats", "reset", "setMatrix", "getDeltas",
+                                           "submitRunAsync", "summarizeAsync", "getContainingSegment"])
     if lines[1] != "ENGINE":  # no HIP device here: construction must throw, never fall back
         assert lines[1].startswith("ERR mtr_engine_create")
 
 
-def _py_batch(paths):
+def _py_batch(paths, return_logs=False):
     it = Interner()
     logs = []
     for p in paths:
@@ -64,7 +65,8 @@ def _py_batch(paths):
         last = groups[-1]["msgs"][-1]
         log.seq_update(last["minimumSequenceNumber"], last["sequenceNumber"])
         logs.append(log)
-    return build_batch(logs, it)
+    b = build_batch(logs, it)
+    return (b, logs) if return_logs else b
 
 
 def _py_batch_pre(paths, pre):
@@ -198,3 +200,120 @@ def test_legacy_catchup_through_node_host(tmp_path):
         assert r["names"][-1] == "catchupOps" and len(got) == len(exp)
         assert got == exp, f"doc {d}: legacy summary with catch-up differs"
         assert r["text"] == ref.doc.text()
+
+
+def _compare_batch(raw, py):
+    assert raw["docs"] == py.docs.tobytes()
+    assert raw["ops"] == py.ops.tobytes()
+    assert np.array_equal(np.frombuffer(raw["clientOff"], dtype="<u4"), py.client_off)
+    n = int(py.client_off[-1])
+    assert raw["clientBytes"][:n] == py.client_bytes.tobytes()[:n]
+
+
+def _matrix_feeds(n, ops):
+    from test_matrix import matrix_cfg, matrix_messages
+    from fluidframework_amd.synth import tables
+    from oracle.oracle import generate_matrix
+
+    gb, _, status = generate_matrix(matrix_cfg(n, ops, writers=8, max_lag=16), tables(writers=8), 0, n, threads=n)
+    assert (status == 0).all()
+    return [dict(zip(("observer", "msgs"), matrix_messages(gb, d, np.random.default_rng(d)))) for d in range(n)]
+
+
+def test_js_matrix_packer_matches_python_packer(tmp_path):
+    """MatrixDocLog + matrixLogs (the Node SharedMatrix packer) produce the batch MatrixLog + matrix_logs do:
+    vector ops (single and grouped) with F_COLS, set-cell records, the shared client table."""
+    from fluidframework_amd.batch import MatrixLog, matrix_logs
+
+    _addon()
+    feeds = _matrix_feeds(4, 600)
+    f = tmp_path / "feeds.json"
+    f.write_text(json.dumps(feeds))
+    raw = {k: base64.b64decode(v) for k, v in json.loads(_node([os.path.join(HERE, "node", "matrix_engine.js"),
+                                                                 "--pack", str(f)])).items()}
+    it = Interner()
+    logs = []
+    for fd in feeds:
+        lg = MatrixLog()
+        lg.start_collab(fd["observer"])
+        for m in fd["msgs"]:
+            lg.message(m, it)
+        logs.append(lg)
+    py = build_batch(matrix_logs(logs), it)
+    assert py.n_docs == 8 and int(py.docs["op_count"][1::2].sum()) == 0
+    _compare_batch(raw, py)
+
+
+@pytest.mark.gpu
+def test_matrix_through_node_host(tmp_path):
+    """BatchMatrixClient: C4-mix matrices applied in chunks through Node; both PermutationVectors'
+    summaries (segments + handleTable) equal the oracle's."""
+    from oracle.oracle import OracleDoc
+    from fluidframework_amd.batch import MatrixLog
+
+    _addon()
+    feeds = _matrix_feeds(6, 1500)
+    f = tmp_path / "feeds.json"
+    f.write_text(json.dumps(feeds))
+    res = json.loads(_node([os.path.join(HERE, "node", "matrix_engine.js"), "--run", str(f), "389"], timeout=300))
+    for d, fd in enumerate(feeds):
+        it = Interner()
+        lg = MatrixLog()
+        lg.start_collab(fd["observer"])
+        for m in fd["msgs"]:
+            lg.message(m, it)
+        b = build_batch([lg], it)
+        o = OracleDoc(options(), matrix=True)
+        assert o.apply(b, 0) == 0
+        for w, name in ((0, "rows"), (1, "cols")):
+            got = [base64.b64decode(x) for x in res[d][name]]
+            assert got == o.select(w).summarize(b, 0), f"matrix {d} {name}: summary differs"
+
+
+@pytest.mark.gpu
+def test_async_host_and_containing_segment(tmp_path):
+    """flushAsync / summarizeAsync (napi_async_work + promises): the engine is refused while a run is in
+    flight, the event loop keeps turning, texts and summaries equal the oracle's; getContainingSegment
+    with and without sequenceArgs equals the oracle's nodeMap at every queried (pos, refSeq, client)."""
+    import random
+
+    paths = [p for p in replay_files() if "clients_8" in p][:4] or replay_files()[:4]
+    _addon()
+    b, logs = _py_batch(paths, return_logs=True)
+    rng = random.Random(11)
+    queries, expect = [], []
+    for d, log in enumerate(logs):
+        o = OracleDoc(options())
+        assert o.apply(b, d) == 0
+        min_seq, cur = (int(x) for x in o.state()[:2])
+        clients = [c for c, name in enumerate(log.clients) if log.client_ix[name] == c]
+        qs, ex = [], []
+        for _ in range(80):
+            ref, c = rng.randint(min_seq, cur), rng.choice(clients)
+            pos = rng.randint(0, max(int(o.length(ref, c)), 0))
+            qs.append([pos, ref, log.clients[c]])
+            ex.append(o.containing(pos, ref, c))
+        me = log.client_ix[log.observer_id]
+        for pos in (0, len(o.text()) // 2, len(o.text())):  # no sequenceArgs: the observer's current view
+            qs.append([pos])
+            ex.append(o.containing(pos, cur, me))
+        queries.append(qs)
+        expect.append(ex)
+    f = tmp_path / "queries.json"
+    f.write_text(json.dumps(queries))
+    res = json.loads(_node([os.path.join(HERE, "node", "async_engine.js"), str(f)] + paths, timeout=300))
+    assert res["checks"] == sum(len(load_replay(p)) for p in paths)
+    assert res["busy"] > 0
+    n_hit = 0
+    for r, ex in zip(res["result"], expect):
+        orc = OracleDoc(options())
+        assert orc.apply(b, r["doc"]) == 0
+        assert [base64.b64decode(x) for x in r["blobs"]] == orc.summarize(b, r["doc"])
+        for got, e in zip(r["answers"], ex):
+            if e[0] < 0:
+                assert got is None
+                continue
+            assert got is not None and got[:3] == [e[0], e[1], e[2]], (r["doc"], got, e)
+            assert got[3] in (-1, e[2])  # text segments carry their text
+            n_hit += 1
+    assert n_hit > 250
