@@ -15,6 +15,16 @@ OP_LOCAL_ANNOTATE = 10
 OP_START_COLLAB = 12
 OP_LOAD = 13
 OP_SETCELL = 14
+OP_RELPOS = 15
+REL_BEFORE = 1
+REL_OFFSET = 2
+COMB_NONE, COMB_REWRITE, COMB_INCR, COMB_CONSENSUS, COMB_KEEP = 0, 1, 2, 3, 4
+VEQ_NEVER = 0x80000000
+VEQ_FALSY = 0x40000000
+VEQ_INCR_STR = 0x20000000
+VEQ_CONS_MUT = 0x10000000
+VEQ_CLASS = 0x0FFFFFFF
+PROPS_NEVER = 0x80000000
 HANDLE_UNALLOCATED = -0x80000000
 CLIENT_NONCOLLAB = 0xFFFE
 
@@ -25,6 +35,7 @@ F_NOREF = 8
 F_APPEND = 16
 F_COLS = 32
 F_DELTA = 64
+F_REL = 128
 
 NULL_VALUE = 0xFFFFFFFF
 NOT_INDEX = 0xFFFFFFFF

@@ -10,9 +10,12 @@ message handling the reference does on the JS thread:
   ``{text, props}`` object or a ``{marker: {refType}, props}`` object.
 * GROUP ops (ops.ts:113) become several records with one sequence number.
 
-Property keys/values are interned into global tables (see include/mtr_types.h).  Features outside
-the observer path (relative positions, combining ops, messages authored by the observer itself) make
-the document ``unsupported`` (the reference-side shim keeps such documents on the TypeScript Client).
+Property keys/values are interned into global tables (see include/mtr_types.h).  Remote annotates
+with a ``combiningOp`` are encoded per include/mtr_types.h (MTR_COMB_*); ``relativePos1/2`` become
+MTR_OP_RELPOS records resolved by the engine against the marker the id maps to.  Features outside the
+observer path (messages authored by the observer itself, combining results that are not plain JSON
+values, marker ids whose mapping depends on block-update order) make the document ``unsupported``
+(the reference-side shim keeps such documents on the TypeScript Client).
 """
 from __future__ import annotations
 
@@ -23,7 +26,8 @@ from typing import Any, Iterable
 import numpy as np
 
 from . import abi
-from .jsjson import array_index, eq_key, js_key_order, js_string, js_stringify, parse, plain_value, to_utf8
+from .jsjson import (array_index, eq_key, js_key_order, js_string, js_stringify, js_truthy, parse, plain_value, to_utf8,
+                     utf16_less)
 
 
 class Unsupported(Exception):
@@ -47,6 +51,41 @@ class Interner:
         self.val_eq: list[int] = []
         self.eq_ids: dict[str, int] = {}
         self.propops: list[list[tuple[int, int]]] = []
+        self.never: dict[str, int] = {}  # never-equal values (NaN, {value: undefined, seq}) by JSON text
+
+    def _add_value(self, s: str, eq: int) -> int:
+        i = len(self.val_bytes)
+        self.val_bytes.append(to_utf8(s))
+        self.val_eq.append(eq)
+        return i
+
+    @staticmethod
+    def value_flags(v: Any) -> int:
+        """MTR_VEQ_* bits of a JSON value (include/mtr_types.h)."""
+        f = 0
+        if not js_truthy(v):
+            f |= abi.VEQ_FALSY
+        if isinstance(v, (str, list, dict)):  # value + undefined concatenates (properties.ts:39)
+            f |= abi.VEQ_INCR_STR
+        if isinstance(v, dict):
+            sq = v.get("seq")
+            if isinstance(sq, (int, float)) and not isinstance(sq, bool) and sq == -1:
+                f |= abi.VEQ_CONS_MUT  # consensus would set cv.seq in place (properties.ts:56-60)
+        return f
+
+    def never_value(self, s: str) -> int:
+        """A value matchProperties never matches, not even with itself (NaN -> "null"; a consensus value
+        {value: undefined, seq} -> '{"seq":N}'): its own class, flagged MTR_VEQ_NEVER."""
+        i = self.never.get(s)
+        if i is None:
+            e = len(self.eq_ids)
+            self.eq_ids["never#%d" % e] = e
+            i = self._add_value(s, e | abi.VEQ_NEVER)
+            self.never[s] = i
+        return i
+
+    def nan(self) -> int:
+        return self.never_value("null")
 
     def key(self, k: str) -> int:
         i = self.keys.get(k)
@@ -66,18 +105,87 @@ class Interner:
         s = js_stringify(v)
         i = self.vals.get(s)
         if i is None:
-            i = len(self.val_bytes)
-            self.vals[s] = i
-            self.val_bytes.append(to_utf8(s))
             ek = eq_key(v)
             e = self.eq_ids.setdefault(ek, len(self.eq_ids))
-            self.val_eq.append(e)
+            i = self._add_value(s, e | self.value_flags(v))
+            self.vals[s] = i
         return i
 
     def propop(self, props: dict) -> int:
         pairs = [(self.key(k), self.value(props[k])) for k in js_key_order(props.keys())]
         self.propops.append(pairs)
         return len(self.propops) - 1
+
+    def combining(self, props: dict, co: Any, seq: int) -> tuple[int, int]:
+        """A remote annotate with combiningOp `co` -> (prop-op, payload2) per include/mtr_types.h."""
+        if not isinstance(props, dict):
+            raise Unsupported("annotate props")
+        if not js_truthy(co):  # `op ? op : undefined` (segmentPropertiesManager.ts:93-94)
+            return self.propop(props), abi.COMB_NONE
+        if not isinstance(co, dict):
+            raise Unsupported("combiningOp")
+        name = co.get("name")
+        if name == "rewrite":
+            return self.propop(props), abi.COMB_REWRITE
+        mode = {"incr": abi.COMB_INCR, "consensus": abi.COMB_CONSENSUS}.get(name, abi.COMB_KEEP)
+        absent = self._value_or_null(combine_absent(co, seq))
+        pairs = [(self.key(k), absent) for k in js_key_order(props.keys())]
+        self.propops.append(pairs)
+        return len(self.propops) - 1, mode | ((self.nan() << 3) if mode == abi.COMB_INCR else 0)
+
+    def _value_or_null(self, r: Any) -> int:
+        if r is _NAN:
+            return self.nan()
+        if isinstance(r, _Never):
+            return self.never_value(r.json)
+        if r is None:  # combine gave null: `delete oldProps[key]` (absent stays absent)
+            return abi.NULL_VALUE
+        return self.value(r)
+
+
+class _Never:
+    def __init__(self, json_text: str) -> None:
+        self.json = json_text
+
+
+_NAN = object()
+_JS_UNDEF = object()
+
+
+def combine_absent(co: dict, seq: int) -> Any:
+    """combine(co, undefined, undefined, seq) (properties.ts:24-69) for a key the segment lacks: the
+    value the key takes (a JSON value, None = null, _NAN, or a _Never value)."""
+    cur = co.get("defaultValue", _JS_UNDEF)
+    name = co.get("name")
+    if name == "incr":
+        if cur is _JS_UNDEF or cur is None or isinstance(cur, (bool, int, float)):
+            return _NAN  # NaN < minValue is false: no clamp
+        if not isinstance(cur, str):
+            raise Unsupported("incr of a non-primitive default value")
+        r = cur + "undefined"
+        mv = co.get("minValue", _JS_UNDEF)
+        if mv is not _JS_UNDEF and js_truthy(mv):
+            if isinstance(mv, str):
+                if utf16_less(r, mv):
+                    r = mv
+            elif not isinstance(mv, (int, float)) or isinstance(mv, bool):
+                raise Unsupported("incr minValue comparison")
+            # string < number: ToNumber("...undefined") is NaN -> false
+        return r
+    if name == "consensus":
+        if cur is _JS_UNDEF:
+            return _Never('{"seq":%d}' % seq)  # {value: undefined, seq}: JSON.stringify drops `value`
+        if cur is None:
+            raise Unsupported("consensus on a null default (TypeError in the reference)")
+        if isinstance(cur, dict):
+            sq = cur.get("seq")
+            if isinstance(sq, (int, float)) and not isinstance(sq, bool) and sq == -1:
+                cur = dict(cur)
+                cur["seq"] = seq
+        return cur
+    if cur is _JS_UNDEF:
+        raise Unsupported("combiningOp without a default leaves an explicit undefined property")
+    return cur
 
 
 @dataclass
@@ -91,6 +199,11 @@ class DocLog:
     text: list[int] = field(default_factory=list)
     unsupported: str | None = None
     collaborating: bool = False
+    # MergeTree.idToSegment (mergeTree.ts:549,668) as the host sees it: id key -> marker ordinal
+    n_markers: int = 0
+    marker_ids: dict = field(default_factory=dict)
+    marker_dup: set = field(default_factory=set)  # ids mapped to two markers: block-update order decides
+    marker_id_annotated: bool = False              # an annotate touched "markerId": remapped by blockUpdate
 
     def short_id(self, long_id: str) -> int:
         """Client.getOrAddShortClientId (client.ts:673-677)."""
@@ -115,7 +228,66 @@ class DocLog:
         self.text.extend(u.tolist())
         return off, len(u)
 
-    def _seg(self, spec: Any, interner: Interner) -> tuple[int, int, int, int]:
+    @staticmethod
+    def _id_key(v: Any):
+        """Map key of a marker id (SameValueZero; objects only match themselves: never from JSON)."""
+        if isinstance(v, bool):
+            return ("b", v)
+        if isinstance(v, (int, float)):
+            return ("n", float(v))
+        if isinstance(v, str):
+            return ("s", v)
+        return None
+
+    def _map_marker(self, props: Any) -> int:
+        """Marker.getId (mergeTreeNodes.ts:612-617) truthy -> mapIdToSegment: the new marker ordinal + 1
+        for the record's payload2 (0 = no id)."""
+        if not isinstance(props, dict) or not js_truthy(props.get("markerId")):
+            return 0
+        k = self._id_key(props["markerId"])
+        o = self.n_markers
+        self.n_markers += 1
+        if k is not None:
+            if k in self.marker_ids:
+                self.marker_dup.add(k)
+            self.marker_ids[k] = o
+        return o + 1
+
+    def _relpos(self, rp: Any, which: int, short: int, seq: int, ref: int, msn: int) -> None:
+        """getValidOpRange's posFromRelativePos (client.ts:527-545, mergeTree.ts:1371-1395) -> one
+        MTR_OP_RELPOS record ahead of the op."""
+        if not isinstance(rp, dict):
+            raise Unsupported("relative position")
+        rid = rp.get("id")
+        k = self._id_key(rid) if js_truthy(rid) else None
+        if k is None or k not in self.marker_ids:
+            raise Unsupported("relative position without a mapped marker (position -1)")
+        if k in self.marker_dup or self.marker_id_annotated:
+            raise Unsupported("relative position on a marker id remapped by block updates")
+        off = rp.get("offset", _JS_UNDEF)
+        flags = abi.REL_BEFORE if js_truthy(rp.get("before")) else 0
+        if off is not _JS_UNDEF:
+            if off is None:  # pos += null adds 0
+                off = 0
+            if isinstance(off, bool) or not isinstance(off, (int, float)) or off != int(off):
+                raise Unsupported("relative position offset")
+            flags |= abi.REL_OFFSET
+            off = int(off)
+        else:
+            off = 0
+        self.ops.append((abi.OP_RELPOS, 0, short, seq, ref, msn, self.marker_ids[k], which, off & 0xFFFFFFFF, flags))
+
+    def _position(self, op: dict, key: str, which: int, short: int, seq: int, ref: int, msn: int) -> int:
+        """op.pos1 / op.pos2, or its relativePos (resolved by the engine): the record's field value."""
+        v = op.get(key, _JS_UNDEF)
+        if v is _JS_UNDEF and js_truthy(op.get("relative" + key[0].upper() + key[1:])):
+            self._relpos(op["relative" + key[0].upper() + key[1:]], which, short, seq, ref, msn)
+            return 0
+        if v is _JS_UNDEF or v is None or isinstance(v, bool) or not isinstance(v, (int, float)):
+            raise Unsupported(f"op without a usable {key}")
+        return int(v)
+
+    def _seg(self, spec: Any, interner: Interner, map_marker: bool = True) -> tuple[int, int, int, int]:
         """-> (flags, payload, payload2, propop)"""
         if isinstance(spec, str):
             off, n = self._text(spec)
@@ -138,7 +310,7 @@ class DocLog:
             if props is not None:
                 flags |= abi.F_PROPS
                 pp = interner.propop(props)
-            return flags, int(ref), 0, pp
+            return flags, int(ref), self._map_marker(props) if map_marker else 0, pp
         raise Unsupported("unrecognized segment spec")
 
     # -- non-collaborating local edits (pre-attach SharedString / TestClient.insertTextLocal)
@@ -173,8 +345,12 @@ class DocLog:
     # -- loading a summary (SnapshotLoader, snapshotLoader.ts:41-257)
     def _snapshot_seg(self, spec: Any, interner: Interner, op_type: int, flags: int) -> None:
         """specToSegment with merge info (snapshotLoader.ts:88-128) -> one LOAD / APPEND record."""
+        # a loaded live marker is mapped by reloadFromSegments' blockUpdate (addNodeReferences,
+        # mergeTree.ts:297-306, localNetLength > 0 only); a body segment by blockInsert (:1655-1662)
+        removed = isinstance(spec, dict) and "json" in spec and spec.get("removedSeq") is not None
+        live = op_type != abi.OP_LOAD or not removed
         if isinstance(spec, dict) and "json" in spec:  # hasMergeInfo, snapshotChunks.ts:80-84
-            f, p1, p2, pp = self._seg(spec["json"], interner)
+            f, p1, p2, pp = self._seg(spec["json"], interner, map_marker=live)
             client = self.short_id(spec["client"]) if spec.get("client") is not None else abi.CLIENT_NONCOLLAB
             seq = int(spec["seq"]) if spec.get("seq") is not None else 0
             removers = []
@@ -184,7 +360,7 @@ class DocLog:
                 removers = [self.short_id(x) for x in spec["removedClientIds"]]
             rseq = int(spec["removedSeq"]) if spec.get("removedSeq") is not None else -1
         else:
-            f, p1, p2, pp = self._seg(spec, interner)
+            f, p1, p2, pp = self._seg(spec, interner, map_marker=live)
             client, seq, removers, rseq = abi.CLIENT_NONCOLLAB, 0, [], -1
         roff = len(self.text)
         self.text.extend(removers)
@@ -249,27 +425,33 @@ class DocLog:
         for i, op in enumerate(members):
             last = abi.F_LAST if i == len(members) - 1 else 0
             t = op.get("type")
-            if "relativePos1" in op or "relativePos2" in op:
-                raise Unsupported("relative positions")
             if t == 0:
                 seg = op.get("seg")
                 if seg is None:
                     # applyInsertOp returns early; only updateSeqNumbers runs
                     self.ops.append((abi.OP_SEQ, last, short, seq, ref, msn, 0, 0, 0, 0))
                     continue
+                n0 = len(self.ops)
+                pos1 = self._position(op, "pos1", 1, short, seq, ref, msn)
+                rel = abi.F_REL if len(self.ops) > n0 else 0
                 flags, p1, p2, pp = self._seg(seg, interner)
-                self.ops.append((abi.OP_INSERT, flags | last, short, seq, ref, msn, int(op["pos1"]), pp, p1, p2))
+                self.ops.append((abi.OP_INSERT, flags | last | rel, short, seq, ref, msn, pos1, pp, p1, p2))
             elif t == 1:
-                self.ops.append(
-                    (abi.OP_REMOVE, last, short, seq, ref, msn, int(op["pos1"]), int(op["pos2"]), 0, 0)
-                )
+                n0 = len(self.ops)
+                pos1 = self._position(op, "pos1", 1, short, seq, ref, msn)
+                pos2 = self._position(op, "pos2", 2, short, seq, ref, msn)
+                rel = abi.F_REL if len(self.ops) > n0 else 0
+                self.ops.append((abi.OP_REMOVE, last | rel, short, seq, ref, msn, pos1, pos2, 0, 0))
             elif t == 2:
-                if op.get("combiningOp") is not None:
-                    raise Unsupported("combining ops")
-                pp = interner.propop(op["props"])
-                self.ops.append(
-                    (abi.OP_ANNOTATE, last, short, seq, ref, msn, int(op["pos1"]), int(op["pos2"]), pp, 0)
-                )
+                props = op.get("props")
+                if isinstance(props, dict) and "markerId" in props:
+                    self.marker_id_annotated = True
+                n0 = len(self.ops)
+                pos1 = self._position(op, "pos1", 1, short, seq, ref, msn)
+                pos2 = self._position(op, "pos2", 2, short, seq, ref, msn)
+                rel = abi.F_REL if len(self.ops) > n0 else 0
+                pp, comb = interner.combining(props, op.get("combiningOp"), seq)
+                self.ops.append((abi.OP_ANNOTATE, last | rel, short, seq, ref, msn, pos1, pos2, pp, comb))
             else:
                 raise Unsupported(f"op type {t}")
 

@@ -194,6 +194,8 @@ enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP
 struct Sc {
     unsigned long long cp[CP_N];
     int gen_ref, gen_client;
+    int rel[2];   // positions resolved by MTR_OP_RELPOS records for the next (MTR_F_REL) op
+    int relmask;  // which of rel[] are pending: bit 0 pos1, bit 1 pos2
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];
 #endif
@@ -267,20 +269,28 @@ MTR_DI void wsync() {
 }
 // inclusive add-scan over the 64 lanes: DPP row shifts within rows of 16, then row broadcasts
 MTR_DI int wave_incl_scan(int x) {
-    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
-    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
-    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
-    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    // (bound_ctrl: lanes shifted in from outside the row read 0 -- the same sums as a 0 old value,
+    // but each step folds into one v_add_u32_dpp even while x stays live)
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
     x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
     x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return x;
 }
 
-// matchProperties (properties.ts:71-105) with values compared by equivalence class
+// matchProperties (properties.ts:71-105) with values compared by equivalence class; a value flagged
+// MTR_VEQ_NEVER (NaN, a consensus {value: undefined, seq}) matches nothing, not even itself, so a set
+// holding one -- its leaf-side index carries MTR_PROPS_NEVER -- does not match itself either
+constexpr uint32_t PN_MASK = ~MTR_PROPS_NEVER;
+MTR_DI bool pset_never(uint32_t a) { return a != NONE32 && (a & MTR_PROPS_NEVER) != 0; }
 template <class PA, class PB>
 __device__ bool props_match(PA gprop, PB val_eq, uint32_t a, uint32_t b) {
-    if (a == b) return true;
+    if (a == b) return !pset_never(a);
     if (a == NONE32 || b == NONE32) return false;
+    a &= PN_MASK;
+    b &= PN_MASK;
     const uint32_t na = gprop[a], nb = gprop[b];
     if (na != nb) return false;
     for (uint32_t i = 0; i < na; i++) {
@@ -288,7 +298,8 @@ __device__ bool props_match(PA gprop, PB val_eq, uint32_t a, uint32_t b) {
         bool found = false;
         for (uint32_t j = 0; j < nb; j++)
             if (gprop[b + 1 + 2 * j] == k) {
-                if (val_eq[gprop[a + 2 + 2 * i]] != val_eq[gprop[b + 2 + 2 * j]]) return false;
+                const uint32_t ea = val_eq[gprop[a + 2 + 2 * i]];
+                if (ea != val_eq[gprop[b + 2 + 2 * j]] || (ea & MTR_VEQ_NEVER)) return false;
                 found = true;
                 break;
             }
@@ -360,6 +371,24 @@ struct Eng {
                 L.grt()[2 * h + 1] = head;
                 return true;
             }
+            h = (h + 1) & uint32_t(L.rtmask);
+        }
+        return false;
+    }
+
+    // MergeTree.idToSegment (mergeTree.ts:549,668): marker ordinal -> the marker's uid, kept in the
+    // remover-head table under key 0x80000000 | ordinal (uids stay below 2^31)
+    static MTR_DI bool mk_set(const D& L, uint32_t ordinal, uint32_t uid) { return rm_set(L, 0x80000000u | ordinal, uid); }
+    static MTR_DI bool mk_get(const D& L, uint32_t ordinal, uint32_t& uid) {
+        const uint32_t key = 0x80000000u | ordinal;
+        uint32_t h = rtab_hash(key) & uint32_t(L.rtmask);
+        for (int n = 0; n <= L.rtmask; n++) {
+            const uint32_t k = uniu(L.grt()[2 * h]);
+            if (k == key + 1) {
+                uid = uniu(L.grt()[2 * h + 1]);
+                return true;
+            }
+            if (k == 0) break;
             h = (h + 1) & uint32_t(L.rtmask);
         }
         return false;
@@ -530,7 +559,7 @@ struct Eng {
                 out[5] = L.rseq[i] == RNONE ? -1 : L.rseq[i];
                 out[6] = (m & M_MARKER) ? 1 : 0;
                 out[7] = int(L.text[i]);
-                out[8] = int(L.props[i]);
+                out[8] = L.props[i] == NONE32 ? -1 : int(L.props[i] & PN_MASK);
                 out[9] = before;
             }
         }
@@ -840,11 +869,17 @@ struct Eng {
         uint32_t dst;
         int propused, status;
     };
-    static MTR_DI PropRes props_apply_serial(const D& L, const KParams& P, int propused, uint32_t old, uint32_t pp) {
+    static __device__ __attribute__((noinline)) PropRes props_apply_serial(const D& L, const KParams& P, int propused,
+                                                                         uint32_t old, uint32_t pp,
+                                             uint32_t comb) {
         PropRes r{old, propused, MTR_OK};
         const gptr<uint32_t> gprop = L.gprop();
-        const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX);
-        const uint32_t n_old = old == NONE32 ? 0 : uniu(gprop[old]);
+        const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX),
+                                   veq = L.tab(CP_VEQ);
+        const uint32_t mode = comb & 7u, nanv = comb >> 3;
+        const bool never_old = pset_never(old);
+        old &= PN_MASK;
+        const uint32_t n_old = old == (NONE32 & PN_MASK) ? 0u : uniu(gprop[old]);
         const uint32_t lo = uniu(poff[pp]), hi = uniu(poff[pp + 1]);
         const uint32_t need = 1 + 2 * (n_old + (hi - lo));
         if (uint32_t(propused) + need > uint32_t(P.pcap)) {
@@ -855,14 +890,43 @@ struct Eng {
         const gptr<uint32_t> e = gprop + dst;
         uint32_t n = n_old;
         for (uint32_t k = 0; k < 2 * n_old; k++) e[1 + k] = gprop[old + 1 + k];
+        if (mode == MTR_COMB_REWRITE) {  // old keys whose new value is absent or falsy go first (:109-123)
+            uint32_t w = 0;
+            for (uint32_t k = 0; k < n; k++) {
+                const uint32_t key = uniu(e[1 + 2 * k]), val = uniu(e[2 + 2 * k]);
+                bool keep = false;
+                for (uint32_t q = lo; q < hi; q++)
+                    if (uniu(pkv[2 * q]) == key) {
+                        const uint32_t nv = uniu(pkv[2 * q + 1]);
+                        keep = nv != MTR_NULL_VALUE && !(uniu(veq[nv]) & MTR_VEQ_FALSY);
+                        break;
+                    }
+                if (keep) {
+                    e[1 + 2 * w] = key;
+                    e[2 + 2 * w] = val;
+                    w++;
+                }
+            }
+            n = w;
+        }
         for (uint32_t q = lo; q < hi; q++) {
-            const uint32_t key = uniu(pkv[2 * q]), val = uniu(pkv[2 * q + 1]);
+            const uint32_t key = uniu(pkv[2 * q]);
+            uint32_t val = uniu(pkv[2 * q + 1]);
             int at = -1;
             for (uint32_t k = 0; k < n; k++)
                 if (uniu(e[1 + 2 * k]) == key) {
                     at = int(k);
                     break;
                 }
+            if (mode >= MTR_COMB_INCR && at >= 0) {  // combine(op, prev, undefined, seq), properties.ts:24-69
+                const uint32_t prev = uniu(e[2 + 2 * at]), f = uniu(veq[prev]);
+                if ((mode == MTR_COMB_INCR && (f & MTR_VEQ_INCR_STR)) ||
+                    (mode == MTR_COMB_CONSENSUS && (f & MTR_VEQ_CONS_MUT))) {
+                    r.status = MTR_ERR_UNSUPPORTED;
+                    return r;
+                }
+                val = mode == MTR_COMB_INCR ? nanv : prev;
+            }
             if (val == MTR_NULL_VALUE) {
                 if (at >= 0) {
                     for (uint32_t k = uint32_t(at); k + 1 < n; k++) {
@@ -891,20 +955,27 @@ struct Eng {
                 n++;
             }
         }
+        uint32_t never = 0;
+        if (mode >= MTR_COMB_INCR || never_old)
+            for (uint32_t k = 0; k < n; k++)
+                if (uniu(veq[uniu(e[2 + 2 * k])]) & MTR_VEQ_NEVER) never = MTR_PROPS_NEVER;
         e[0] = n;
         r.propused = propused + int(1 + 2 * n);
-        r.dst = dst;
+        r.dst = dst | never;
         return r;
     }
 
     // Wave version: the old set and the op's keys are fetched once (one lane per entry) and the
     // set is edited in registers (lane t = entry t); falls back to the serial form above 64 keys.
-    static MTR_DI uint32_t props_apply(D& L, const KParams& P, St& s, uint32_t old, uint32_t pp) {
+    // comb: the annotate's MTR_COMB_* mode | NaN value id << 3 (include/mtr_types.h).
+    static MTR_DI uint32_t props_apply(D& L, const KParams& P, St& s, uint32_t old, uint32_t pp, uint32_t comb = 0) {
         const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX);
-        const int n_old = old == NONE32 ? 0 : int(uniu(L.gprop()[old]));
+        const bool never_old = pset_never(old);
+        const uint32_t oi = old & PN_MASK;  // the set's arena offset
+        const int n_old = old == NONE32 ? 0 : int(uniu(L.gprop()[oi]));
         const int lo = int(uniu(poff[pp])), nq = int(uniu(poff[pp + 1])) - lo;
         if (n_old + nq > 64) {
-            const PropRes r = props_apply_serial(L, P, s.propused, old, pp);
+            const PropRes r = props_apply_serial(L, P, s.propused, old, pp, comb);
             s.propused = uni(r.propused);
             if (uni(r.status) != MTR_OK) s.status = uni(r.status);
             wsync();
@@ -915,11 +986,12 @@ struct Eng {
             s.status = MTR_ERR_CAPACITY;
             return old;
         }
+        const uint32_t mode = comb & 7u, nanv = comb >> 3;
         const int ln = lane_id();
         uint32_t wk = 0, wv = 0, wx = MTR_NOT_INDEX, qk = 0, qv = 0, qx = MTR_NOT_INDEX;
         if (ln < n_old) {
-            wk = L.gprop()[old + 1 + 2 * ln];
-            wv = L.gprop()[old + 2 + 2 * ln];
+            wk = L.gprop()[oi + 1 + 2 * ln];
+            wv = L.gprop()[oi + 2 + 2 * ln];
         }
         if (ln < nq) {
             qk = pkv[2 * (lo + ln)];
@@ -928,9 +1000,40 @@ struct Eng {
         if (ln < n_old) wx = kix[wk];
         if (ln < nq) qx = kix[qk];
         int n = n_old;
+        if (mode == MTR_COMB_REWRITE) {  // old keys whose new value is absent or falsy go first (:109-123)
+            bool keep = false;
+            for (int q = 0; q < nq; q++) {
+                const uint32_t key = rdlane(qk, q), val = rdlane(qv, q);
+                const bool truthy = val != MTR_NULL_VALUE && !(L.tab(CP_VEQ)[val] & MTR_VEQ_FALSY);
+                if (wk == key) keep = truthy;
+            }
+            // drop the others, highest first, lanes above each moving down one
+            for (uint64_t del = __ballot(ln < n && !keep); del; ) {
+                const int at = last_lane(del);
+                del &= ~(uint64_t(1) << at);
+                const uint32_t dk = __shfl(wk, min(ln + 1, 63)), dv = __shfl(wv, min(ln + 1, 63)),
+                               dx = __shfl(wx, min(ln + 1, 63));
+                if (ln >= at) {
+                    wk = dk;
+                    wv = dv;
+                    wx = dx;
+                }
+                n--;
+            }
+        }
         for (int q = 0; q < nq; q++) {
-            const uint32_t key = rdlane(qk, q), val = rdlane(qv, q), ix = rdlane(qx, q);
+            const uint32_t key = rdlane(qk, q), ix = rdlane(qx, q);
+            uint32_t val = rdlane(qv, q);
             const uint64_t hit = __ballot(ln < n && wk == key);
+            if (mode >= MTR_COMB_INCR && hit) {  // combine(op, prev, undefined, seq), properties.ts:24-69
+                const uint32_t prev = rdlane(wv, first_lane(hit)), f = uniu(L.tab(CP_VEQ)[prev]);
+                if ((mode == MTR_COMB_INCR && (f & MTR_VEQ_INCR_STR)) ||
+                    (mode == MTR_COMB_CONSENSUS && (f & MTR_VEQ_CONS_MUT))) {
+                    s.status = MTR_ERR_UNSUPPORTED;
+                    return old;
+                }
+                val = mode == MTR_COMB_INCR ? nanv : prev;
+            }
             if (val == MTR_NULL_VALUE) {
                 if (hit) {  // delete entry `at`: lanes above it move down one
                     const int at = first_lane(hit);
@@ -965,6 +1068,11 @@ struct Eng {
                 n++;
             }
         }
+        uint32_t never = 0;
+        if (mode >= MTR_COMB_INCR || never_old) {  // a never-equal value survives: flag the index
+            const bool nv = ln < n && (L.tab(CP_VEQ)[wv] & MTR_VEQ_NEVER) != 0;
+            if (__ballot(nv)) never = MTR_PROPS_NEVER;
+        }
         const uint32_t dst = uint32_t(s.propused);
         const gptr<uint32_t> e = L.gprop() + dst;
         if (ln < n) {
@@ -974,13 +1082,15 @@ struct Eng {
         e[0] = uint32_t(n);
         s.propused += 1 + 2 * n;
         wsync();
-        return dst;
+        return dst | never;
     }
 
     // matchProperties on the wave: one lane per key of `a`, `b`'s keys broadcast by readlane
     static MTR_DI bool props_match_w(const D& L, const KParams& P, uint32_t a, uint32_t b) {
-        if (a == b) return true;
+        if (a == b) return !pset_never(a);
         if (a == NONE32 || b == NONE32) return false;
+        a &= PN_MASK;
+        b &= PN_MASK;
         const int na = int(uniu(L.gprop()[a])), nb = int(uniu(L.gprop()[b]));
         if (na != nb) return false;
         const gptr<const uint32_t> veq = L.tab(CP_VEQ);
@@ -1000,7 +1110,7 @@ struct Eng {
             const uint32_t kj = rdlane(kb, j), ej = rdlane(eb, j);
             if (ka == kj && ln < na) {
                 found = true;
-                ok = ea == ej;
+                ok = ea == ej && !(ea & MTR_VEQ_NEVER);
             }
         }
         return __ballot(!(found && ok)) == 0;
@@ -1323,6 +1433,7 @@ struct Eng {
             PROF(P_X1);
             if (link & (vp != pp)) link = props_match(L.gprop(), L.tab(CP_VEQ), pp, vp);
         }
+        link = link & !((vp == pp) & pset_never(vp));  // a shared set holding a never-equal value
         if (!PM && __ballot(link & (vl > kGranularity))) return -1;
         const bool unlink = !pre & removed & (vr <= minseq);
         const uint64_t lm = __ballot(link);
@@ -1705,6 +1816,10 @@ struct Eng {
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[slot] = pr;
         L.uid[slot] = uint32_t(s.uidnext++);
+        if (marker && op.payload2 != 0) {  // mapIdToSegment (mergeTree.ts:1655-1662)
+            if (lane_id() == 0 && !mk_set(L, op.payload2 - 1, uint32_t(s.uidnext - 1))) s.status = MTR_ERR_CAPACITY;
+            s.status = uni(s.status);
+        }
         wsync();
         s.nseg = S + 1;
         const int xbs = S == 0 ? 0 : overflow_fix(L, s, slot, wbs, wbe);
@@ -1780,6 +1895,10 @@ struct Eng {
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[i] = pr;
         L.uid[i] = uint32_t(s.uidnext++);
+        if (marker && op.payload2 != 0) {  // reloadFromSegments' blockUpdate maps live markers (mergeTree.ts:297-306)
+            if (lane_id() == 0 && !mk_set(L, op.payload2 - 1, uint32_t(s.uidnext - 1))) s.status = MTR_ERR_CAPACITY;
+            s.status = uni(s.status);
+        }
         wsync();
         s.nseg = i + 1;
         set_merge_info(L, P, s, i, op, dd);
@@ -1808,7 +1927,7 @@ struct Eng {
     // visible length > 0 inside [start, end), on the current scan arrays, 64 leaves per round.
     // The walk stops at the first leaf whose view start (E - max(V,0), nondecreasing) is >= end.
     static MTR_DI void range_walk(D& L, const KParams& P, St& s, const View& v, int start, int end, int seq,
-                                  uint32_t client, int is_remove, uint32_t pp, bool dl) {
+                                  uint32_t client, int is_remove, uint32_t pp, uint32_t comb, bool dl) {
         PROF(P_RANGE);
         if (end == start) return;
         const int S = s.nseg;
@@ -1861,7 +1980,7 @@ struct Eng {
                     while (pend) {
                         const uint32_t o = rdlane(old, first_lane(pend));
                         const uint64_t sel = __ballot(act && old == o);
-                        const uint32_t nw = props_apply(L, P, s, o, pp);
+                        const uint32_t nw = props_apply(L, P, s, o, pp, comb);
                         if (act && old == o) L.props[j] = nw;
                         pend &= ~sel;
                     }
@@ -1951,6 +2070,7 @@ struct Eng {
             s.textused = 1;
         }
         if (threadIdx.x == 0) {
+            L.sc->relmask = 0;
 #ifdef MTR_PROF
             for (int q = 0; q < P_COUNT; q++) L.sc->prof[q] = 0;
 #endif
@@ -2161,6 +2281,13 @@ struct Eng {
     static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
                                 uint32_t pf, int gidx) {
         if (DL) s.cur_op = gidx;
+        // positions resolved by the MTR_OP_RELPOS records ahead of this op (getValidOpRange, client.ts:527-545)
+        int pos1 = op.pos1, pos2 = op.pos2;
+        if (op.flags & MTR_F_REL) {
+            const int rm = uni(L.sc->relmask);
+            if (rm & 1) pos1 = uni(L.sc->rel[0]);
+            if ((rm & 2) && op.type != MTR_OP_INSERT) pos2 = uni(L.sc->rel[1]);
+        }
         // (record mode never yields: ops are drawn once; matrix pairs never do: their launches have
         // room for every op)
         if (!G && !GN && !PM && s.nseg + 2 >= L.cap && L.cap < P.segcap) return false;  // yield: more leaf room
@@ -2169,7 +2296,7 @@ struct Eng {
             // could overflow, stop before the op and ask the next launch for a larger heap
             int need = 0;
             if (op.type == MTR_OP_INSERT) need = 1;
-            else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) need = min(max(op.pos2 - op.pos1, 0), s.nseg + 2);
+            else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) need = min(max(pos2 - pos1, 0), s.nseg + 2);
             if (need && s.heapn + need + 1 >= L.lhcap) {
                 s.heap_need = s.heapn + need + 2;
                 return false;
@@ -2186,6 +2313,10 @@ struct Eng {
         if (s.status != MTR_OK) {
             s.fail_op = gidx;
             return false;
+        }
+        if (op.flags & MTR_F_REL) {  // consumed
+            if (lane_id() == 0) L.sc->relmask = 0;
+            wsync();
         }
         if (op.type == MTR_OP_LOAD) {  // SnapshotLoader.loadHeader segment
             load_leaf(L, P, s, op, dd);
@@ -2218,12 +2349,15 @@ struct Eng {
             v.client = client;
             v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
         }
+        // the op's view scan (one call site: every position-taking op starts with it)
+        if (op.type <= MTR_OP_ANNOTATE || (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE) ||
+            op.type == MTR_OP_RELPOS)
+            prefix(L, s, v, P.new_length_calc);
         switch (op.type) {
             case MTR_OP_INSERT:
             case MTR_OP_LOCAL_INSERT: {
-                int pos = op.pos1;
+                int pos = pos1;
                 if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
-                prefix(L, s, v, P.new_length_calc);
                 split_at(L, s, pos);
                 insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf);
                 zop = s.collab;
@@ -2234,16 +2368,38 @@ struct Eng {
             case MTR_OP_ANNOTATE:
             case MTR_OP_LOCAL_ANNOTATE: {
                 const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
-                prefix(L, s, v, P.new_length_calc);
-                split_at(L, s, op.pos1);
-                split_at(L, s, op.pos2);
-                range_walk(L, P, s, v, op.pos1, op.pos2, seq, client, is_remove, op.payload,
-                           DL && !PM && (op.flags & MTR_F_DELTA) != 0);
+                split_at(L, s, pos1);
+                split_at(L, s, pos2);
+                range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
+                           op.type == MTR_OP_ANNOTATE ? op.payload2 : 0u, DL && !PM && (op.flags & MTR_F_DELTA) != 0);
                 zop = s.collab;
                 break;
             }
             case MTR_OP_SEQ:
                 break;
+            case MTR_OP_RELPOS: {  // posFromRelativePos, mergeTree.ts:1371-1395, for the next (MTR_F_REL) op
+                uint32_t mu = 0;
+                int p = -1;
+                if (mk_get(L, uint32_t(op.pos1), mu)) {
+                    // getPosition (mergeTree.ts:768-785): the view lengths ahead of the marker, 0 once
+                    // zamboni unlinked it
+                    const int x = find_uid(L, s, mu);
+                    p = x > 0 ? (uni(L.E[x - 1]) & EMASK) : 0;
+                    const int off = (op.payload2 & MTR_REL_OFFSET) ? int(op.payload) : 0;
+                    p = (op.payload2 & MTR_REL_BEFORE) ? p - off : p + 1 + off;  // marker.cachedLength = 1
+                }
+                if (p < 0) {
+                    s.status = MTR_ERR_UNSUPPORTED;  // the reference goes on with position -1
+                } else {
+                    const int w = op.pos2 == 2 ? 1 : 0;
+                    if (lane_id() == 0) {
+                        L.sc->rel[w] = p;
+                        L.sc->relmask |= 1 << w;
+                    }
+                    wsync();
+                }
+                break;
+            }
             case MTR_OP_START_COLLAB:
                 if (!s.collab) {
                     s.collab = 1;
@@ -2338,6 +2494,8 @@ struct Eng {
             if (!apply_op(L, P, s, op, dd, pre, pf, cursor + k)) break;
             s.ops_done = k + 1;
         }
+        // a launch never ends between MTR_OP_RELPOS records and their op: the next one re-runs them
+        s.ops_done -= __popc(uint32_t(uni(L.sc->relmask)));
         // a batch that ends with header segments: build the tree now (queries read it next)
         if (s.height == 0 && s.status == MTR_OK && cursor + s.ops_done >= int(dd.op_count)) finish_load(L, s);
         store_doc(L, P, s, d);

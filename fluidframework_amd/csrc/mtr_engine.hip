@@ -1176,8 +1176,8 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
             }
         }
         uint32_t h = 0;
-        const uint32_t pr = hd.seg[F_PROPS * sc + i];
-        if (pr != NONE32) {
+        const uint32_t pr = hd.seg[F_PROPS * sc + i] & ~MTR_PROPS_NEVER;  // (index flag)
+        if (hd.seg[F_PROPS * sc + i] != NONE32) {
             h = 2166136261u ^ 1u;
             for (uint32_t q = 0; q < hd.prop[pr]; q++) {  // same hash as the oracle export
                 const uint32_t v = hd.prop[pr + 2 + 2 * q];

@@ -268,6 +268,7 @@ MTR_DI void w_client(LW<W>& w, const SParams& P, const mtr_doc_desc& dd, uint32_
 template <bool W>
 MTR_DI void w_props(LW<W>& w, const SDoc& D, const SParams& P, uint32_t pr) {
     w.put('{');
+    pr &= PN_MASK;  // (the index may carry MTR_PROPS_NEVER)
     const uint32_t n = D.gprop[pr];
     for (uint32_t i = 0; i < n; i++) {
         if (i) w.put(',');
@@ -582,6 +583,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
             link = link && (p_tx == uint32_t(MTR_HANDLE_UNALLOCATED) ? tx == uint32_t(MTR_HANDLE_UNALLOCATED)
                                                                      : tx == p_tx + uint32_t(p_len));
         if (link && pr != p_pr) link = props_match(D.gprop, veq, p_pr, pr);
+        if (link && pr == p_pr) link = !pset_never(pr);
         if (!D.perm && __ballot(link && len > kGranularity)) {  // accumulated-length clause, in order
             uint64_t lm = __ballot(link);
             int acc = c_valid && c_k1 ? c_acc : 0;

@@ -200,3 +200,21 @@ def eq_key(v: Any) -> str:
     if isinstance(v, dict):
         return "{" + ",".join(json.dumps(k) + ":" + eq_key(v[k]) for k in sorted(v.keys())) + "}"
     raise TypeError(f"unsupported JSON value {type(v)}")
+
+
+def js_truthy(v: Any) -> bool:
+    """ToBoolean of a JSON.parse value (None is JSON null)."""
+    if v is None:
+        return False
+    if isinstance(v, bool):
+        return v
+    if isinstance(v, (int, float)):
+        return v == v and v != 0
+    if isinstance(v, str):
+        return len(v) > 0
+    return True
+
+
+def utf16_less(a: str, b: str) -> bool:
+    """a < b for two JS strings (code-unit order)."""
+    return a.encode("utf-16-be", "surrogatepass") < b.encode("utf-16-be", "surrogatepass")

@@ -32,8 +32,11 @@ function native() {
 
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
-    START_COLLAB: 12, SETCELL: 14 };
-const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, COLS: 32, DELTA: 64 };
+    START_COLLAB: 12, SETCELL: 14, RELPOS: 15 };
+const REL = { BEFORE: 1, OFFSET: 2 };
+const COMB = { NONE: 0, REWRITE: 1, INCR: 2, CONSENSUS: 3, KEEP: 4 };
+const VEQ = { NEVER: 0x80000000, FALSY: 0x40000000, INCR_STR: 0x20000000, CONS_MUT: 0x10000000 };
+const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, COLS: 32, DELTA: 64, REL: 128 };
 const NULL_VALUE = 0xFFFFFFFF;
 const MAX_CLIENTS = 253;  // include/mtr_types.h MTR_MAX_CLIENTS: short ids per engine document
 const NOT_INDEX = 0xFFFFFFFF;
@@ -80,12 +83,83 @@ function plainValue(v, nested) {
 
 const utf8 = (s) => Buffer.from(s, 'utf8');
 
+// MTR_VEQ_* bits of a JSON value (include/mtr_types.h)
+function valueFlags(v) {
+    let f = 0;
+    if (!v) f |= VEQ.FALSY;
+    if (typeof v === 'string' || (v !== null && typeof v === 'object')) f |= VEQ.INCR_STR;  // v + undefined concatenates
+    if (v !== null && typeof v === 'object' && !Array.isArray(v) && v.seq === -1) f |= VEQ.CONS_MUT;
+    return f >>> 0;
+}
+
+const NAN = { nan: true };  // combine results that are not JSON values
+class Never { constructor(json) { this.json = json; } }
+
+// combine(co, undefined, undefined, seq) (properties.ts:24-69) for a key the segment lacks
+function combineAbsent(co, seq) {
+    const cur = co.defaultValue;
+    if (co.name === 'incr') {
+        if (cur === undefined || cur === null || typeof cur === 'number' || typeof cur === 'boolean') return NAN;
+        if (typeof cur !== 'string') throw new UnsupportedError('incr of a non-primitive default value');
+        let r = cur + 'undefined';
+        const mv = co.minValue;
+        if (mv) {
+            if (typeof mv === 'string') { if (r < mv) r = mv; } else if (typeof mv !== 'number') {
+                throw new UnsupportedError('incr minValue comparison');
+            }
+        }
+        return r;
+    }
+    if (co.name === 'consensus') {
+        if (cur === undefined) return new Never('{"seq":' + seq + '}');  // {value: undefined, seq}
+        if (cur === null) throw new UnsupportedError('consensus on a null default (TypeError in the reference)');
+        if (typeof cur === 'object' && !Array.isArray(cur) && cur.seq === -1) return Object.assign({}, cur, { seq });
+        return cur;
+    }
+    if (cur === undefined) throw new UnsupportedError('combiningOp without a default leaves an explicit undefined property');
+    return cur;
+}
+
 /** Global key / value / prop-op tables (ids stable across batches). */
 class Interner {
     constructor() {
         this.keys = new Map(); this.keyBytes = []; this.keyIndex = [];
         this.vals = new Map(); this.valBytes = []; this.valEq = []; this.eqIds = new Map();
-        this.propops = [];
+        this.propops = []; this.never = new Map();
+    }
+    _addValue(s, eq) {
+        const i = this.valBytes.length;
+        this.valBytes.push(utf8(s));
+        this.valEq.push(eq >>> 0);
+        return i;
+    }
+    neverValue(s) {  // matchProperties never matches it, not even with itself
+        let i = this.never.get(s);
+        if (i === undefined) {
+            const e = this.eqIds.size;
+            this.eqIds.set('never#' + e, e);
+            i = this._addValue(s, (e | VEQ.NEVER) >>> 0);
+            this.never.set(s, i);
+        }
+        return i;
+    }
+    nan() { return this.neverValue('null'); }
+    _valueOrNull(r) {
+        if (r === NAN) return this.nan();
+        if (r instanceof Never) return this.neverValue(r.json);
+        if (r === null) return NULL_VALUE;
+        return this.value(r);
+    }
+    // a remote annotate with combiningOp co -> [propop, payload2] (include/mtr_types.h MTR_COMB_*)
+    combining(props, co, seq) {
+        if (props === null || typeof props !== 'object' || Array.isArray(props)) throw new UnsupportedError('annotate props');
+        if (!co) return [this.propop(props), COMB.NONE];
+        if (typeof co !== 'object' || Array.isArray(co)) throw new UnsupportedError('combiningOp');
+        if (co.name === 'rewrite') return [this.propop(props), COMB.REWRITE];
+        const mode = co.name === 'incr' ? COMB.INCR : (co.name === 'consensus' ? COMB.CONSENSUS : COMB.KEEP);
+        const absent = this._valueOrNull(combineAbsent(co, seq));
+        this.propops.push(Object.keys(props).map((k) => [this.key(k), absent]));
+        return [this.propops.length - 1, mode === COMB.INCR ? (mode | (this.nan() << 3)) >>> 0 : mode];
     }
     key(k) {
         let i = this.keys.get(k);
@@ -104,13 +178,11 @@ class Interner {
         const s = JSON.stringify(v);
         let i = this.vals.get(s);
         if (i === undefined) {
-            i = this.valBytes.length;
-            this.vals.set(s, i);
-            this.valBytes.push(utf8(s));
             const ek = eqKey(v);
             let e = this.eqIds.get(ek);
             if (e === undefined) { e = this.eqIds.size; this.eqIds.set(ek, e); }
-            this.valEq.push(e);
+            i = this._addValue(s, (e | valueFlags(v)) >>> 0);
+            this.vals.set(s, i);
         }
         return i;
     }
@@ -125,6 +197,50 @@ class DocLog {
     constructor() {
         this.observerId = undefined; this.clients = []; this.clientIx = new Map();
         this.ops = []; this.text = []; this.collaborating = false;
+        // MergeTree.idToSegment (mergeTree.ts:549,668) as the host sees it: id key -> marker ordinal
+        this.nMarkers = 0; this.markerIds = new Map(); this.markerDup = new Set(); this.markerIdAnnotated = false;
+    }
+    static _idKey(v) {  // SameValueZero keys; objects only match themselves (never from JSON)
+        if (typeof v === 'boolean') return 'b' + v;
+        if (typeof v === 'number') return 'n' + String(v === 0 ? 0 : v);
+        if (typeof v === 'string') return 's' + v;
+        return null;
+    }
+    _mapMarker(props) {  // Marker.getId truthy -> mapIdToSegment: ordinal + 1 (0 = no id)
+        if (!props || typeof props !== 'object' || !props.markerId) return 0;
+        const k = DocLog._idKey(props.markerId);
+        const o = this.nMarkers++;
+        if (k !== null) {
+            if (this.markerIds.has(k)) this.markerDup.add(k);
+            this.markerIds.set(k, o);
+        }
+        return o + 1;
+    }
+    _relpos(rp, which, short, seq, ref, msn) {  // posFromRelativePos, mergeTree.ts:1371-1395
+        if (!rp || typeof rp !== 'object') throw new UnsupportedError('relative position');
+        const k = rp.id ? DocLog._idKey(rp.id) : null;
+        if (k === null || !this.markerIds.has(k)) throw new UnsupportedError('relative position without a mapped marker (position -1)');
+        if (this.markerDup.has(k) || this.markerIdAnnotated) {
+            throw new UnsupportedError('relative position on a marker id remapped by block updates');
+        }
+        let off = rp.offset, flags = rp.before ? REL.BEFORE : 0;
+        if (off !== undefined) {
+            if (off === null) off = 0;  // pos += null adds 0
+            if (typeof off !== 'number' || !Number.isInteger(off)) throw new UnsupportedError('relative position offset');
+            flags |= REL.OFFSET;
+        } else {
+            off = 0;
+        }
+        this.push(OP.RELPOS, 0, short, seq, ref, msn, this.markerIds.get(k), which, off >>> 0, flags);
+    }
+    _position(op, key, which, short, seq, ref, msn) {  // op.pos1 / op.pos2, or its relativePos (client.ts:527-545)
+        const v = op[key], rk = 'relative' + key[0].toUpperCase() + key.slice(1);
+        if (v === undefined && op[rk]) {
+            this._relpos(op[rk], which, short, seq, ref, msn);
+            return 0;
+        }
+        if (typeof v !== 'number') throw new UnsupportedError('op without a usable ' + key);
+        return Math.trunc(v);
     }
     shortId(longId) {  // Client.getOrAddShortClientId, client.ts:673-677
         const i = this.clientIx.get(longId);
@@ -142,7 +258,7 @@ class DocLog {
         for (let i = 0; i < s.length; i++) this.text.push(s.charCodeAt(i));
         return [off, s.length];
     }
-    _seg(spec, it) {  // specToSegment, sequence/src/sequenceFactory.ts:26-38 -> [flags, payload, payload2, propop]
+    _seg(spec, it, mapMarker = true) {  // specToSegment, sequence/src/sequenceFactory.ts:26-38 -> [flags, payload, payload2, propop]
         if (typeof spec === 'string') { const t = this._text(spec); return [0, t[0], t[1], -1]; }
         if (spec && typeof spec === 'object' && 'text' in spec) {
             const t = this._text(spec.text);
@@ -155,7 +271,7 @@ class DocLog {
             if (ref === undefined || ref === null) { flags |= F.NOREF; ref = 0; }
             let pp = -1;
             if (spec.props !== undefined && spec.props !== null) { flags |= F.PROPS; pp = it.propop(spec.props); }
-            return [flags, ref >>> 0, 0, pp];
+            return [flags, ref >>> 0, mapMarker ? this._mapMarker(spec.props) : 0, pp];
         }
         throw new UnsupportedError('unrecognized segment spec');
     }
@@ -195,19 +311,30 @@ class DocLog {
         if (members.length === 0) { this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
         members.forEach((op, i) => {
             const last = i === members.length - 1 ? F.LAST : 0;
-            if ('relativePos1' in op || 'relativePos2' in op) throw new UnsupportedError('relative positions');
             if (op.type === 0) {
                 if (op.seg === undefined || op.seg === null) {  // applyInsertOp returns early
                     this.push(OP.SEQ, last, short, seq, ref, msn, 0, 0, 0, 0);
                     return;
                 }
+                const n0 = this.ops.length;
+                const pos1 = this._position(op, 'pos1', 1, short, seq, ref, msn);
+                const rel = this.ops.length > n0 ? F.REL : 0;
                 const s = this._seg(op.seg, it);
-                this.push(OP.INSERT, s[0] | last, short, seq, ref, msn, op.pos1, s[3], s[1], s[2]);
+                this.push(OP.INSERT, s[0] | last | rel, short, seq, ref, msn, pos1, s[3], s[1], s[2]);
             } else if (op.type === 1) {
-                this.push(OP.REMOVE, last, short, seq, ref, msn, op.pos1, op.pos2, 0, 0);
+                const n0 = this.ops.length;
+                const pos1 = this._position(op, 'pos1', 1, short, seq, ref, msn);
+                const pos2 = this._position(op, 'pos2', 2, short, seq, ref, msn);
+                const rel = this.ops.length > n0 ? F.REL : 0;
+                this.push(OP.REMOVE, last | rel, short, seq, ref, msn, pos1, pos2, 0, 0);
             } else if (op.type === 2) {
-                if (op.combiningOp !== undefined && op.combiningOp !== null) throw new UnsupportedError('combining ops');
-                this.push(OP.ANNOTATE, last, short, seq, ref, msn, op.pos1, op.pos2, it.propop(op.props), 0);
+                if (op.props && typeof op.props === 'object' && 'markerId' in op.props) this.markerIdAnnotated = true;
+                const n0 = this.ops.length;
+                const pos1 = this._position(op, 'pos1', 1, short, seq, ref, msn);
+                const pos2 = this._position(op, 'pos2', 2, short, seq, ref, msn);
+                const rel = this.ops.length > n0 ? F.REL : 0;
+                const c = it.combining(op.props, op.combiningOp, seq);
+                this.push(OP.ANNOTATE, last | rel, short, seq, ref, msn, pos1, pos2, c[0], c[1]);
             } else {
                 throw new UnsupportedError('op type ' + op.type);
             }
@@ -502,6 +629,18 @@ class BatchReplayClient {
     applyMsg(msg, local) {
         if (local) throw new UnsupportedError('local (acked) ops are outside the observer path');
         this._queue(() => {
+            if (!this.engine.options.snapshotV1 && msg.type === 'op' &&
+                msg.referenceSequenceNumber !== msg.sequenceNumber - 1) {
+                let c = msg.contents;
+                if (typeof c === 'string') c = JSON.parse(c);
+                for (const m of c.type === 3 ? (c.ops || []) : [c]) {
+                    // the catch-up transform needs each member's post-op values / one record per member
+                    if (m.combiningOp || m.relativePos1 || m.relativePos2) {
+                        throw new UnsupportedError('a lagging message with a combining annotate or a relative position ' +
+                            'in the legacy format');
+                    }
+                }
+            }
             const lo = this.log.ops.length;
             this.log.message(msg, this.engine.interner);
             if (!this.engine.options.snapshotV1 && msg.type === 'op') this.engine.catchUps[this.doc].add(msg, this.log, lo);

@@ -193,6 +193,14 @@ class SequenceLog(DocLog):
         if msg.get("type") != "op" or not self.legacy:
             super().message(msg, interner)
             return
+        if int(msg["referenceSequenceNumber"]) != int(msg["sequenceNumber"]) - 1:
+            c = msg["contents"]
+            c = parse(c) if isinstance(c, str) else c
+            for m in (c.get("ops") or []) if c.get("type") == 3 else [c]:
+                # the catch-up transform needs each member's post-op values / one record per member
+                if m.get("combiningOp") or m.get("relativePos1") or m.get("relativePos2"):
+                    raise Unsupported("a lagging message with a combining annotate or a relative position "
+                                      "in the legacy format")
         lo = len(self.ops)
         super().message(msg, interner)
         hi = len(self.ops)

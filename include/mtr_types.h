@@ -35,12 +35,51 @@ enum {
     MTR_OP_LOAD = 13,           /* a snapshot header segment (SnapshotLoader.loadHeader, snapshotLoader.ts:130-167):
                                    consecutive LOAD records are built into the tree bottom-up by
                                    MergeTree.reloadFromSegments (mergeTree.ts:678-728) before the next record */
-    MTR_OP_SETCELL = 14         /* SharedMatrix set-cell message (matrix.ts:636-693, remote branch): pos1 = row,
+    MTR_OP_SETCELL = 14,        /* SharedMatrix set-cell message (matrix.ts:636-693, remote branch): pos1 = row,
                                    pos2 = col at (ref_seq, client); resolves both positions
                                    (PermutationVector.adjustPosition, permutationvector.ts:232-247) and, when both
                                    are live, allocates row and col handles (getAllocatedHandle, :209-230).
                                    No updateSeqNumbers on either vector. */
+    MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
+                                   MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
+                                   (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for
+                                   an id no marker was ever mapped to (position -1); pos2 = 1 or 2, the position of the
+                                   next op (flagged MTR_F_REL) it replaces; payload = relativePos.offset (int32);
+                                   payload2 = MTR_REL_*.
+                                   Position = getPosition(marker) (+ 1 + offset unless `before`, else - offset);
+                                   a marker zamboni unlinked has position 0 (its parent is gone). A resolved
+                                   position < 0 makes the document MTR_ERR_UNSUPPORTED. */
 };
+
+/* MTR_OP_RELPOS payload2 */
+enum { MTR_REL_BEFORE = 1, MTR_REL_OFFSET = 2 };
+
+/*
+ * Marker ordinals (MergeTree.idToSegment, mergeTree.ts:549,668): an insert / load record of a Marker whose
+ * props carry a truthy "markerId" (Marker.getId, mergeTreeNodes.ts:612-617) has payload2 = ordinal + 1, the
+ * host's per-document count of such markers; the engine maps ordinal -> segment.  The host resolves
+ * relativePos.id to the latest ordinal mapped under that id.
+ *
+ * Remote annotate with a combiningOp (PropertiesManager.addProperties, segmentPropertiesManager.ts:60-157):
+ * payload2 = MTR_COMB_* | (NaN value id << 3).  For "rewrite" the prop-op is the op's props; keys of the old
+ * set whose new value is absent or falsy are deleted first (:109-123).  For the other names the op's props
+ * values are ignored (combine(op, prev, undefined, seq), properties.ts:24-69): the prop-op holds, per key in
+ * op order, the value the key takes when it is absent (combine of the default, computed by the host; the
+ * null value = stays absent); a present value becomes NaN (incr) or stays (consensus / other names).
+ */
+enum { MTR_COMB_NONE = 0, MTR_COMB_REWRITE = 1, MTR_COMB_INCR = 2, MTR_COMB_CONSENSUS = 3, MTR_COMB_KEEP = 4 };
+
+/* val_eq[v] high bits: value flags read by the combining rules and matchProperties; the low 28 bits
+ * are the equivalence class */
+#define MTR_VEQ_NEVER 0x80000000u   /* never equal, even to itself (NaN; {value: undefined, seq}) */
+#define MTR_VEQ_FALSY 0x40000000u   /* !value (false, 0, -0, "") */
+#define MTR_VEQ_INCR_STR 0x20000000u /* value + undefined is not NaN (string, object, array): unsupported */
+#define MTR_VEQ_CONS_MUT 0x10000000u /* object whose "seq" is -1 (consensus mutates it in place): unsupported */
+#define MTR_VEQ_CLASS 0x0fffffffu
+/* engine-internal: a leaf's property-set index carries this bit when the set holds a MTR_VEQ_NEVER
+ * value, so a set shared by two leaves (split halves, one annotate's memoized result) does not match
+ * itself without reading it */
+#define MTR_PROPS_NEVER 0x80000000u
 
 /* op.flags */
 enum {
@@ -52,9 +91,10 @@ enum {
                           (SnapshotLoader.loadBody append, snapshotLoader.ts:221-256) */
     MTR_F_COLS = 32,   /* matrix documents: the vector op targets the cols PermutationVector (contents.target
                           "cols", matrix.ts:645-651); without it, the rows vector */
-    MTR_F_DELTA = 64   /* report this op's delta ranges (mtr_get_deltas): the SequenceDeltaEvent ranges
+    MTR_F_DELTA = 64,  /* report this op's delta ranges (mtr_get_deltas): the SequenceDeltaEvent ranges
                           SharedSegmentSequence.processMergeTreeMsg turns into catch-up ops for lagging
                           messages in the legacy format (sequence.ts:120-173, 697-736) */
+    MTR_F_REL = 128    /* pos1 and/or pos2 come from the MTR_OP_RELPOS records right ahead of this op */
 };
 
 /* One delta range of an MTR_F_DELTA op (ISequenceDeltaRange, sequenceDeltaEvent.ts): the op's

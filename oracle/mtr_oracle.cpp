@@ -27,6 +27,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -87,6 +88,7 @@ struct Seg : Node {
     bool hasProps = false;           // properties !== undefined
     bool hasPropMgr = false;         // propertyManager !== undefined
     PropMap props;
+    uint32_t markerOrdinal = 0;      // host marker ordinal + 1 of a Marker with a truthy markerId (0 = none)
 };
 
 struct PSL;
@@ -179,7 +181,10 @@ bool matchProperties(const Seg* a, const Seg* b, const mtr_batch* bt) {
             bool found = false;
             for (auto& kb : b->props.kv)
                 if (kb.first == ka.first) {
-                    if (bt->val_eq[kb.second] != bt->val_eq[ka.second]) return false;
+                    // never-equal values (NaN, {value: undefined, seq}) fail `b[key] !== a[key]` / the
+                    // recursive b[key] === undefined test even against themselves
+                    if (bt->val_eq[kb.second] != bt->val_eq[ka.second] || (bt->val_eq[ka.second] & MTR_VEQ_NEVER))
+                        return false;
                     found = true;
                     break;
                 }
@@ -774,14 +779,52 @@ class Tree {
     }
 
     // ------------------------------------------------------------ ops
-    // properties: PropertiesManager.addProperties without combining ops
-    // (segmentPropertiesManager.ts:60-157), BaseSegment.addProperties (mergeTreeNodes.ts:385-406)
-    void addProperties(Seg* s, uint32_t propop) {
+    // properties: PropertiesManager.addProperties (segmentPropertiesManager.ts:60-157) for an observer
+    // (no pending local keys: shouldModifyKey is always true), BaseSegment.addProperties
+    // (mergeTreeNodes.ts:385-406).  comb = MTR_COMB_* | NaN value id << 3 (include/mtr_types.h).
+    void addProperties(Seg* s, uint32_t propop, uint32_t comb = 0) {
         const mtr_batch* b = tabs.b;
+        const uint32_t mode = comb & 7u, nanv = comb >> 3;
         s->hasPropMgr = true;
         s->hasProps = true;
-        for (uint32_t i = b->propop_off[propop]; i < b->propop_off[propop + 1]; i++) {
+        const uint32_t lo = b->propop_off[propop], hi = b->propop_off[propop + 1];
+        if (mode == MTR_COMB_REWRITE) {  // delete old keys whose new value is falsy (:109-123)
+            std::vector<std::pair<uint32_t, uint32_t>> kept;
+            for (auto& kv : s->props.kv) {
+                bool truthy = false;
+                for (uint32_t i = lo; i < hi; i++)
+                    if (b->propop_kv[2 * i] == kv.first) {
+                        const uint32_t v = b->propop_kv[2 * i + 1];
+                        truthy = v != MTR_NULL_VALUE && !(b->val_eq[v] & MTR_VEQ_FALSY);
+                        break;
+                    }
+                if (truthy) kept.push_back(kv);
+            }
+            s->props.kv.swap(kept);
+        }
+        for (uint32_t i = lo; i < hi; i++) {
             uint32_t k = b->propop_kv[2 * i], v = b->propop_kv[2 * i + 1];
+            if (mode >= MTR_COMB_INCR) {  // newValue = combine(op, previousValue, undefined, seq), :145-147
+                const std::pair<uint32_t, uint32_t>* prev = nullptr;
+                for (auto& kv : s->props.kv)
+                    if (kv.first == k) prev = &kv;
+                if (prev) {
+                    const uint32_t f = b->val_eq[prev->second];
+                    if (mode == MTR_COMB_INCR) {
+                        if (f & MTR_VEQ_INCR_STR) {  // string / object + undefined: a new string
+                            status = MTR_ERR_UNSUPPORTED;
+                            return;
+                        }
+                        v = nanv;  // number + undefined
+                    } else {
+                        if (mode == MTR_COMB_CONSENSUS && (f & MTR_VEQ_CONS_MUT)) {  // cv.seq = seq in place
+                            status = MTR_ERR_UNSUPPORTED;
+                            return;
+                        }
+                        v = prev->second;
+                    }
+                }  // absent: the host's combine of the default (or null: stays absent)
+            }
             if (v == MTR_NULL_VALUE)
                 propDelete(s->props, k);
             else
@@ -802,6 +845,7 @@ class Tree {
             s->refType = int(op.payload);
             s->noRef = (op.flags & MTR_F_NOREF) != 0;
             s->len = 1;
+            s->markerOrdinal = op.payload2;
         } else {
             const uint16_t* t = tabs.b->text + dd.text_base + op.payload;
             s->text.assign(reinterpret_cast<const char16_t*>(t), op.payload2);
@@ -828,6 +872,7 @@ class Tree {
         if (seg->len > 0) {
             seg->seq = seq;
             seg->clientId = clientId;
+            if (seg->markerOrdinal) idToSegment[seg->markerOrdinal - 1] = seg;  // blockInsert, mergeTree.ts:1655-1662
             InsertContext ctx{LeafMode::Insert, seg, true};
             Block* splitNode = insertingWalk(root, pos, refSeq, clientId, seq, ctx);
             if (seg->parent == nullptr) {
@@ -881,14 +926,14 @@ class Tree {
     }
 
     // annotateRange, mergeTree.ts:1895-1953
-    void annotateRange(int start, int end, uint32_t propop, int refSeq, int clientId, int seq) {
+    void annotateRange(int start, int end, uint32_t propop, int refSeq, int clientId, int seq, uint32_t comb = 0) {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
         std::vector<Seg*> touched;
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
-                addProperties(s, propop);
+                addProperties(s, propop, comb);
                 touched.push_back(s);
                 if (collaborating && seq != kUnassignedSeq) addToLRUSet(s, seq);
             },
@@ -945,10 +990,32 @@ class Tree {
             if (collaborating) return MTR_ERR_ASSERT | 0x049;  // "Trying to reload from segments while collaborating!"
             Seg* s = segmentFromSpec(op, dd);
             setMergeInfo(s, op, dd);
+            // reloadFromSegments' blockUpdate maps live markers (addNodeReferences, mergeTree.ts:297-306);
+            // the host gives a removed one no ordinal
+            if (s->markerOrdinal) idToSegment[s->markerOrdinal - 1] = s;
             pendingLoad.push_back(s);
             return status;
         }
         if (!pendingLoad.empty()) reloadFromSegments();
+        int pos1 = op.pos1, pos2 = op.pos2;
+        if (op.type == MTR_OP_RELPOS) {  // getValidOpRange -> posFromRelativePos (client.ts:527-545, mergeTree.ts:1371-1395)
+            int p = -1;
+            auto it = idToSegment.find(uint32_t(op.pos1));
+            if (it != idToSegment.end()) {
+                p = getPosition(it->second, op.ref_seq, op.client);
+                const int off = (op.payload2 & MTR_REL_OFFSET) ? int(op.payload) : 0;
+                p = (op.payload2 & MTR_REL_BEFORE) ? p - off : p + it->second->len + off;
+            }
+            if (p < 0) return MTR_ERR_UNSUPPORTED;  // the reference goes on with position -1
+            relPos[op.pos2 == 2 ? 1 : 0] = p;
+            relMask |= op.pos2 == 2 ? 2 : 1;
+            return status;
+        }
+        if (op.flags & MTR_F_REL) {  // the positions the MTR_OP_RELPOS records ahead resolved
+            if (relMask & 1) pos1 = relPos[0];
+            if ((relMask & 2) && op.type != MTR_OP_INSERT) pos2 = relPos[1];
+            relMask = 0;
+        }
         switch (op.type) {
             case MTR_OP_INSERT: {
                 Seg* s = segmentFromSpec(op, dd);
@@ -957,14 +1024,14 @@ class Tree {
                     insertSegments(blockLocalLength(root), s, kUniversalSeq, opClient(op), op.seq);
                     return status;
                 }
-                insertSegments(op.pos1, s, op.ref_seq, op.client, op.seq);
+                insertSegments(pos1, s, op.ref_seq, op.client, op.seq);
                 break;
             }
             case MTR_OP_REMOVE:
-                markRangeRemoved(op.pos1, op.pos2, op.ref_seq, op.client, op.seq);
+                markRangeRemoved(pos1, pos2, op.ref_seq, op.client, op.seq);
                 break;
             case MTR_OP_ANNOTATE:
-                annotateRange(op.pos1, op.pos2, op.payload, op.ref_seq, op.client, op.seq);
+                annotateRange(pos1, pos2, op.payload, op.ref_seq, op.client, op.seq, op.payload2);
                 break;
             case MTR_OP_SEQ:
                 break;
@@ -1038,6 +1105,25 @@ class Tree {
             offset = pos - before;
         }
         return found;
+    }
+    // MergeTree.idToSegment (mergeTree.ts:549,668) by host marker ordinal; never unmapped
+    std::unordered_map<uint32_t, Seg*> idToSegment;
+    int relPos[2] = {0, 0};
+    int relMask = 0;
+    // getPosition, mergeTree.ts:768-785: the preceding siblings' nodeLength (undefined = 0) up the
+    // parent chain; an unlinked segment (parent undefined, zamboni.ts:146,170) is at 0
+    int getPosition(Seg* seg, int refSeq, int clientId) {
+        int total = 0;
+        Node* prev = seg;
+        for (Block* parent = seg->parent; parent; prev = parent, parent = parent->parent) {
+            for (int i = 0; i < parent->childCount; i++) {
+                Node* child = parent->children[i];
+                if (child == prev) break;
+                const int l = nodeLength(child, refSeq, clientId);
+                if (l > 0) total += l;
+            }
+        }
+        return total;
     }
     // getPosition at the local view, mergeTree.ts:768-785
     int localPosition(Seg* seg) {
@@ -1377,6 +1463,13 @@ int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32
     out[2] = s->len;
     out[3] = pos - off;
     return out[0];
+}
+
+int32_t oracle_doc_marker_position(oracle_doc* d, uint32_t ordinal, int32_t ref_seq, int32_t client) {
+    if (!d->view().pendingLoad.empty()) d->view().reloadFromSegments();
+    Tree& t = d->view();
+    auto it = t.idToSegment.find(ordinal);
+    return it == t.idToSegment.end() ? -1 : t.getPosition(it->second, ref_seq, client);
 }
 
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client) {

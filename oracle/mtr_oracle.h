@@ -103,6 +103,8 @@ int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32
 
 /* Length of the doc in the (ref_seq, client) view (MergeTree.getLength, mergeTree.ts:757) */
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client);
+/* MergeTree.getPosition (mergeTree.ts:768-785) of the marker mapped to a host marker ordinal, -1 if none */
+int32_t oracle_doc_marker_position(oracle_doc* d, uint32_t ordinal, int32_t ref_seq, int32_t client);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,8 @@ def lib():
         L.oracle_psl_stats.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
         L.oracle_doc_containing.restype = C.c_int32
         L.oracle_doc_containing.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
+        L.oracle_doc_marker_position.restype = C.c_int32
+        L.oracle_doc_marker_position.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         _LIB = L
@@ -164,6 +166,10 @@ class OracleDoc:
         out = np.zeros(4, dtype="<i4")
         lib().oracle_doc_containing(self.h, pos, ref_seq, client, out.ctypes.data)
         return tuple(int(x) for x in out) if out[0] >= 0 else (-1, 0, 0, 0)
+
+    def marker_position(self, ordinal, ref_seq, client):
+        """getPosition of the marker mapped to a host marker ordinal at (refSeq, clientId); -1 if none."""
+        return lib().oracle_doc_marker_position(self.h, ordinal, ref_seq, client)
 
     def length(self, ref_seq, client):
         return lib().oracle_doc_length(self.h, ref_seq, client)
