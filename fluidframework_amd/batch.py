@@ -514,6 +514,68 @@ class MatrixLog(DocLog):
             else:
                 raise Unsupported(f"vector op type {t}")
 
+    # -- loading a matrix from its summary (SharedMatrix.loadCore, matrix.ts:611-631)
+    def _perm_seg(self, spec: Any, op_type: int, flags: int) -> None:
+        """PermutationSegment.fromJSONObject of a snapshot spec [length, start] (permutationvector.ts:45-48)
+        with its merge info (SnapshotLoader.specToSegment, snapshotLoader.ts:88-128): the start is kept."""
+        client, seq, removers, rseq = abi.CLIENT_NONCOLLAB, 0, [], -1
+        if isinstance(spec, dict) and "json" in spec:
+            client = self.short_id(spec["client"]) if spec.get("client") is not None else abi.CLIENT_NONCOLLAB
+            seq = int(spec["seq"]) if spec.get("seq") is not None else 0
+            if spec.get("removedClient") is not None:
+                removers = [self.short_id(spec["removedClient"])]
+            if spec.get("removedClientIds") is not None:
+                removers = [self.short_id(x) for x in spec["removedClientIds"]]
+            rseq = int(spec["removedSeq"]) if spec.get("removedSeq") is not None else -1
+            spec = spec["json"]
+        if not (isinstance(spec, list) and len(spec) == 2 and all(isinstance(x, (int, float)) for x in spec)):
+            raise Unsupported("PermutationSegment spec")
+        roff = len(self.text)
+        self.text.extend(removers)
+        self.ops.append((op_type, flags, client, seq, rseq, len(removers), roff, -1, int(spec[1]) & 0xFFFFFFFF,
+                         int(spec[0])))
+
+    def load_summary(self, tree: dict, long_id: str, interner: Interner) -> None:
+        """rows.load then cols.load (PermutationVector.load, permutationvector.ts:327-345): the handle
+        table, the V1 header segments, startOrUpdateCollaboration(long_id, minSeq, seq) from that
+        vector's header, its body segments.  `tree`: {"rows" | "cols": {"segments": {blob id: blob},
+        "handleTable": blob}} (cells: CellMatrixLog)."""
+        me = None
+        for name, tf in (("rows", 0), ("cols", abi.F_COLS)):
+            vec = tree[name]
+            ht = vec["handleTable"]
+            ht = parse(ht.decode() if isinstance(ht, bytes) else ht) if isinstance(ht, (str, bytes)) else ht
+            if not isinstance(ht, list) or not ht:
+                raise Unsupported("handle table")
+            off = len(self.text)
+            for h in ht:
+                h = int(h) & 0xFFFFFFFF
+                self.text.extend((h & 0xFFFF, h >> 16))
+            self.ops.append((abi.OP_HANDLES, tf, 0, 0, 0, 0, len(ht), 0, off, 0))
+            segs = vec["segments"]
+
+            def blob(k):
+                x = segs[k]
+                return parse(x.decode() if isinstance(x, bytes) else x) if isinstance(x, (str, bytes)) else x
+
+            header = blob("header")
+            if header.get("version") != "1":  # PermutationVector forces newMergeTreeSnapshotFormat
+                raise Unsupported("matrix vector summary not in the V1 format")
+            for spec in header["segments"]:
+                self._perm_seg(spec, abi.OP_LOAD, tf)
+            meta = header["headerMetadata"]
+            seq = int(meta["sequenceNumber"])
+            msn = meta.get("minSequenceNumber")
+            if me is None:
+                me = self.add_long_id(long_id)
+            self.ops.append((abi.OP_START_COLLAB, abi.F_APPEND | tf, me, seq, 0, int(msn) if msn is not None else seq,
+                             0, 0, 0, 0))
+            for md in meta["orderedChunkMetadata"][1:]:
+                for spec in blob(md["id"])["segments"]:
+                    self._perm_seg(spec, abi.OP_INSERT, abi.F_APPEND | tf)
+        self.observer_id = long_id
+        self.collaborating = True
+
     def cols_log(self) -> DocLog:
         """The cols vector's engine document: no ops of its own, the same client table."""
         return DocLog(observer_id=self.observer_id, clients=list(self.clients), client_ix=dict(self.client_ix))

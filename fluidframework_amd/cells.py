@@ -174,6 +174,11 @@ class CellMatrixLog(MatrixLog):
         JSON.stringify([cells.snapshot(), pending.snapshot()])."""
         return to_utf8(js_stringify([self.cells.snapshot(), self.pending.snapshot()]))
 
+    def load_summary(self, tree: dict, long_id: str, interner: Interner) -> None:
+        """SharedMatrix.loadCore (matrix.ts:611-631): both vectors, then the cell tries."""
+        super().load_summary(tree, long_id, interner)
+        self.load_cells(tree["cells"])
+
     def load_cells(self, blob: str | bytes) -> None:
         """SparseArray2D.load of both tries (matrix.ts:621-631; nullToUndefined)."""
         cells, pending = parse(blob.decode() if isinstance(blob, bytes) else blob)

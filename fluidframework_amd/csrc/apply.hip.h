@@ -346,6 +346,10 @@ struct ProfScope {
 template <bool G, bool PM = false, int CAP = 0, bool DL = false, bool GN = false>
 struct Eng {
     using D = Doc<G>;
+    // the rare records (MTR_OP_RELPOS / MTR_F_REL, MTR_OP_HANDLES, combining annotates, marker ordinals)
+    // are compiled into the runtime-capacity and matrix instantiations only; the host launches those for a
+    // batch holding any (mtr_submit's op scan), so the fixed-capacity replay kernels carry none of it
+    static constexpr bool X = CAP == 0 || PM;
     template <class T>
     using A = typename D::template A<T>;
 
@@ -377,21 +381,37 @@ struct Eng {
     }
 
     // MergeTree.idToSegment (mergeTree.ts:549,668): marker ordinal -> the marker's uid, kept in the
-    // remover-head table under key 0x80000000 | ordinal (uids stay below 2^31)
-    static MTR_DI bool mk_set(const D& L, uint32_t ordinal, uint32_t uid) { return rm_set(L, 0x80000000u | ordinal, uid); }
-    static MTR_DI bool mk_get(const D& L, uint32_t ordinal, uint32_t& uid) {
+    // remover-head table under key 0x80000000 | ordinal (uids stay below 2^31).  Out of line: rare.
+    static MTR_DI bool mk_put(gptr<uint32_t> rt, uint32_t rtmask, uint32_t ordinal,
+                                                           uint32_t uid) {
         const uint32_t key = 0x80000000u | ordinal;
-        uint32_t h = rtab_hash(key) & uint32_t(L.rtmask);
-        for (int n = 0; n <= L.rtmask; n++) {
-            const uint32_t k = uniu(L.grt()[2 * h]);
-            if (k == key + 1) {
-                uid = uniu(L.grt()[2 * h + 1]);
+        uint32_t h = rtab_hash(key) & rtmask;
+        for (uint32_t n = 0; n <= rtmask; n++) {
+            uint32_t k = rt[2 * h];
+            if (k == 0) k = atomicCAS((uint32_t*)&rt[2 * h], 0u, key + 1);
+            if (k == 0 || k == key + 1) {
+                rt[2 * h + 1] = uid;
                 return true;
             }
-            if (k == 0) break;
-            h = (h + 1) & uint32_t(L.rtmask);
+            h = (h + 1) & rtmask;
         }
         return false;
+    }
+    static MTR_DI bool mk_set(const D& L, uint32_t ordinal, uint32_t uid) {
+        return mk_put(L.grt(), uint32_t(L.rtmask), ordinal, uid);
+    }
+    // -> uid | 1 << 32 when mapped, 0 when not
+    static MTR_DI uint64_t mk_look(gptr<const uint32_t> rt, uint32_t rtmask,
+                                                                uint32_t ordinal) {
+        const uint32_t key = 0x80000000u | ordinal;
+        uint32_t h = rtab_hash(key) & rtmask;
+        for (uint32_t n = 0; n <= rtmask; n++) {
+            const uint32_t k = uniu(rt[2 * h]);
+            if (k == key + 1) return uint64_t(uniu(rt[2 * h + 1])) | (uint64_t(1) << 32);
+            if (k == 0) break;
+            h = (h + 1) & rtmask;
+        }
+        return 0;
     }
 
     static MTR_DI bool in_removers(const D& L, int i, uint32_t m, uint32_t c) {
@@ -869,7 +889,12 @@ struct Eng {
         uint32_t dst;
         int propused, status;
     };
-    static __device__ __attribute__((noinline)) PropRes props_apply_serial(const D& L, const KParams& P, int propused,
+    #ifdef MTR_SERIAL_INLINE
+    static MTR_DI
+#else
+    static __device__ __attribute__((noinline))
+#endif
+    PropRes props_apply_serial(const D& L, const KParams& P, int propused,
                                                                          uint32_t old, uint32_t pp,
                                              uint32_t comb) {
         PropRes r{old, propused, MTR_OK};
@@ -966,15 +991,13 @@ struct Eng {
     }
 
     // Wave version: the old set and the op's keys are fetched once (one lane per entry) and the
-    // set is edited in registers (lane t = entry t); falls back to the serial form above 64 keys.
-    // comb: the annotate's MTR_COMB_* mode | NaN value id << 3 (include/mtr_types.h).
+    // set is edited in registers (lane t = entry t).  Combining annotates (comb: MTR_COMB_* | NaN id << 3),
+    // sets holding a never-equal value and sets above 64 keys take the out-of-line serial form.
     static MTR_DI uint32_t props_apply(D& L, const KParams& P, St& s, uint32_t old, uint32_t pp, uint32_t comb = 0) {
         const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX);
-        const bool never_old = pset_never(old);
-        const uint32_t oi = old & PN_MASK;  // the set's arena offset
-        const int n_old = old == NONE32 ? 0 : int(uniu(L.gprop()[oi]));
+        const int n_old = old == NONE32 ? 0 : int(uniu(L.gprop()[old & PN_MASK]));
         const int lo = int(uniu(poff[pp])), nq = int(uniu(poff[pp + 1])) - lo;
-        if (n_old + nq > 64) {
+        if (n_old + nq > 64 || (X && comb != 0) || pset_never(old)) {
             const PropRes r = props_apply_serial(L, P, s.propused, old, pp, comb);
             s.propused = uni(r.propused);
             if (uni(r.status) != MTR_OK) s.status = uni(r.status);
@@ -986,12 +1009,11 @@ struct Eng {
             s.status = MTR_ERR_CAPACITY;
             return old;
         }
-        const uint32_t mode = comb & 7u, nanv = comb >> 3;
         const int ln = lane_id();
         uint32_t wk = 0, wv = 0, wx = MTR_NOT_INDEX, qk = 0, qv = 0, qx = MTR_NOT_INDEX;
         if (ln < n_old) {
-            wk = L.gprop()[oi + 1 + 2 * ln];
-            wv = L.gprop()[oi + 2 + 2 * ln];
+            wk = L.gprop()[old + 1 + 2 * ln];
+            wv = L.gprop()[old + 2 + 2 * ln];
         }
         if (ln < nq) {
             qk = pkv[2 * (lo + ln)];
@@ -1000,40 +1022,9 @@ struct Eng {
         if (ln < n_old) wx = kix[wk];
         if (ln < nq) qx = kix[qk];
         int n = n_old;
-        if (mode == MTR_COMB_REWRITE) {  // old keys whose new value is absent or falsy go first (:109-123)
-            bool keep = false;
-            for (int q = 0; q < nq; q++) {
-                const uint32_t key = rdlane(qk, q), val = rdlane(qv, q);
-                const bool truthy = val != MTR_NULL_VALUE && !(L.tab(CP_VEQ)[val] & MTR_VEQ_FALSY);
-                if (wk == key) keep = truthy;
-            }
-            // drop the others, highest first, lanes above each moving down one
-            for (uint64_t del = __ballot(ln < n && !keep); del; ) {
-                const int at = last_lane(del);
-                del &= ~(uint64_t(1) << at);
-                const uint32_t dk = __shfl(wk, min(ln + 1, 63)), dv = __shfl(wv, min(ln + 1, 63)),
-                               dx = __shfl(wx, min(ln + 1, 63));
-                if (ln >= at) {
-                    wk = dk;
-                    wv = dv;
-                    wx = dx;
-                }
-                n--;
-            }
-        }
         for (int q = 0; q < nq; q++) {
-            const uint32_t key = rdlane(qk, q), ix = rdlane(qx, q);
-            uint32_t val = rdlane(qv, q);
+            const uint32_t key = rdlane(qk, q), val = rdlane(qv, q), ix = rdlane(qx, q);
             const uint64_t hit = __ballot(ln < n && wk == key);
-            if (mode >= MTR_COMB_INCR && hit) {  // combine(op, prev, undefined, seq), properties.ts:24-69
-                const uint32_t prev = rdlane(wv, first_lane(hit)), f = uniu(L.tab(CP_VEQ)[prev]);
-                if ((mode == MTR_COMB_INCR && (f & MTR_VEQ_INCR_STR)) ||
-                    (mode == MTR_COMB_CONSENSUS && (f & MTR_VEQ_CONS_MUT))) {
-                    s.status = MTR_ERR_UNSUPPORTED;
-                    return old;
-                }
-                val = mode == MTR_COMB_INCR ? nanv : prev;
-            }
             if (val == MTR_NULL_VALUE) {
                 if (hit) {  // delete entry `at`: lanes above it move down one
                     const int at = first_lane(hit);
@@ -1068,11 +1059,6 @@ struct Eng {
                 n++;
             }
         }
-        uint32_t never = 0;
-        if (mode >= MTR_COMB_INCR || never_old) {  // a never-equal value survives: flag the index
-            const bool nv = ln < n && (L.tab(CP_VEQ)[wv] & MTR_VEQ_NEVER) != 0;
-            if (__ballot(nv)) never = MTR_PROPS_NEVER;
-        }
         const uint32_t dst = uint32_t(s.propused);
         const gptr<uint32_t> e = L.gprop() + dst;
         if (ln < n) {
@@ -1082,7 +1068,7 @@ struct Eng {
         e[0] = uint32_t(n);
         s.propused += 1 + 2 * n;
         wsync();
-        return dst | never;
+        return dst;
     }
 
     // matchProperties on the wave: one lane per key of `a`, `b`'s keys broadcast by readlane
@@ -1245,6 +1231,10 @@ struct Eng {
     // A permutation vector keeps its HandleTable in its (otherwise unused) text arena as int32
     // words; handles[0] is the head of the free list, s.textused the array length.
     static MTR_DI gptr<int32_t> handles(const D& L) { return (gptr<int32_t>)L.gtext(); }
+    // HandleTable.load's entries (two UTF-16 units each, low half first), out of line (rare)
+    static MTR_DI void load_handles(gptr<const uint16_t> src, gptr<int32_t> dst, int n) {
+        for (int k = lane_id(); k < n; k += 64) dst[k] = int32_t(uint32_t(src[2 * k]) | (uint32_t(src[2 * k + 1]) << 16));
+    }
     static MTR_DI int handle_cap(const KParams& P) { return P.tcap / 2; }
     // HandleTable.allocate, handletable.ts:37-42
     static MTR_DI int alloc_handle(D& L, const KParams& P, St& s) {
@@ -1809,14 +1799,17 @@ struct Eng {
         L.seq[slot] = seq;
         L.rseq[slot] = RNONE;
         L.meta[slot] = m;
-        // PermutationSegment: start reset to unallocated on INSERT (permutationvector.ts:354-361)
-        L.text[slot] = marker ? op.payload : (PM ? uint32_t(MTR_HANDLE_UNALLOCATED) : uint32_t(t0));
+        // PermutationSegment: start reset to unallocated on INSERT (permutationvector.ts:354-361) -- not for a
+        // snapshot body segment (no delta callback while loading, mergeTree.ts:1410-1418)
+        L.text[slot] = marker ? op.payload
+                              : (PM ? ((op.flags & MTR_F_APPEND) ? op.payload : uint32_t(MTR_HANDLE_UNALLOCATED))
+                                    : uint32_t(t0));
         if (!marker && !PM) s.textused = t0 + len;
         uint32_t pr = NONE32;
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[slot] = pr;
         L.uid[slot] = uint32_t(s.uidnext++);
-        if (marker && op.payload2 != 0) {  // mapIdToSegment (mergeTree.ts:1655-1662)
+        if (X && marker && op.payload2 != 0) {  // mapIdToSegment (mergeTree.ts:1655-1662)
             if (lane_id() == 0 && !mk_set(L, op.payload2 - 1, uint32_t(s.uidnext - 1))) s.status = MTR_ERR_CAPACITY;
             s.status = uni(s.status);
         }
@@ -1869,11 +1862,11 @@ struct Eng {
             s.nseg = 0;
             s.height = 0;
         }
-        const bool marker = (op.flags & MTR_F_MARKER) != 0;
+        const bool marker = !PM && (op.flags & MTR_F_MARKER) != 0;
         const int len = marker ? 1 : int(op.payload2);
         const int i = s.nseg;
         const int t0 = s.textused;
-        if (!marker) {
+        if (!marker && !PM) {
             if (t0 + len > text_end(s, P)) {
                 s.status = MTR_ERR_CAPACITY;
                 return;
@@ -1884,18 +1877,19 @@ struct Eng {
         }
         uint32_t m = enc_client(int(int16_t(op.client)));
         if (marker) m |= M_MARKER;
-        else m |= M_NLQ;
+        else if (!PM) m |= M_NLQ;
         if (op.flags & MTR_F_NOREF) m |= M_NOREF;
         L.len[i] = len;
         L.seq[i] = op.seq;
         L.rseq[i] = RNONE;
         L.meta[i] = m;
-        L.text[i] = marker ? op.payload : uint32_t(t0);
+        // PermutationSegment: the start handle of the spec [length, start] is kept (no reset on load)
+        L.text[i] = (marker || PM) ? op.payload : uint32_t(t0);
         uint32_t pr = NONE32;
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[i] = pr;
         L.uid[i] = uint32_t(s.uidnext++);
-        if (marker && op.payload2 != 0) {  // reloadFromSegments' blockUpdate maps live markers (mergeTree.ts:297-306)
+        if (X && marker && op.payload2 != 0) {  // reloadFromSegments' blockUpdate maps live markers (mergeTree.ts:297-306)
             if (lane_id() == 0 && !mk_set(L, op.payload2 - 1, uint32_t(s.uidnext - 1))) s.status = MTR_ERR_CAPACITY;
             s.status = uni(s.status);
         }
@@ -2283,7 +2277,7 @@ struct Eng {
         if (DL) s.cur_op = gidx;
         // positions resolved by the MTR_OP_RELPOS records ahead of this op (getValidOpRange, client.ts:527-545)
         int pos1 = op.pos1, pos2 = op.pos2;
-        if (op.flags & MTR_F_REL) {
+        if (X && (op.flags & MTR_F_REL)) {
             const int rm = uni(L.sc->relmask);
             if (rm & 1) pos1 = uni(L.sc->rel[0]);
             if ((rm & 2) && op.type != MTR_OP_INSERT) pos2 = uni(L.sc->rel[1]);
@@ -2314,7 +2308,7 @@ struct Eng {
             s.fail_op = gidx;
             return false;
         }
-        if (op.flags & MTR_F_REL) {  // consumed
+        if (X && (op.flags & MTR_F_REL)) {  // consumed
             if (lane_id() == 0) L.sc->relmask = 0;
             wsync();
         }
@@ -2349,15 +2343,14 @@ struct Eng {
             v.client = client;
             v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
         }
-        // the op's view scan (one call site: every position-taking op starts with it)
-        if (op.type <= MTR_OP_ANNOTATE || (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE) ||
-            op.type == MTR_OP_RELPOS)
-            prefix(L, s, v, P.new_length_calc);
+        // (each op type calls the view scan itself: one hoisted call site measured 2.5 % slower at C3)
+        if (X && op.type == MTR_OP_RELPOS) prefix(L, s, v, P.new_length_calc);
         switch (op.type) {
             case MTR_OP_INSERT:
             case MTR_OP_LOCAL_INSERT: {
                 int pos = pos1;
                 if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
+                prefix(L, s, v, P.new_length_calc);
                 split_at(L, s, pos);
                 insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf);
                 zop = s.collab;
@@ -2368,6 +2361,7 @@ struct Eng {
             case MTR_OP_ANNOTATE:
             case MTR_OP_LOCAL_ANNOTATE: {
                 const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
+                prefix(L, s, v, P.new_length_calc);
                 split_at(L, s, pos1);
                 split_at(L, s, pos2);
                 range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
@@ -2377,16 +2371,30 @@ struct Eng {
             }
             case MTR_OP_SEQ:
                 break;
+            case MTR_OP_HANDLES: {  // HandleTable.load (handletable.ts:88): handles = the summary's array
+                const int n = op.pos1;
+                if (!X || !PM || s.collab || n < 1) {
+                    s.status = MTR_ERR_BAD_OP;
+                } else if (n > handle_cap(P)) {
+                    s.status = MTR_ERR_CAPACITY;
+                } else {
+                    load_handles(gp(P.btext) + dd.text_base + op.payload, handles(L), n);
+                    s.textused = n;
+                    wsync();
+                }
+                break;
+            }
             case MTR_OP_RELPOS: {  // posFromRelativePos, mergeTree.ts:1371-1395, for the next (MTR_F_REL) op
-                uint32_t mu = 0;
+                // the marker's getPosition (mergeTree.ts:768-785) at the op's view: the view lengths of the
+                // leaves ahead of it, 0 once zamboni unlinked it; then + cachedLength (1) + offset, or
+                // - offset when `before`; -1 when no marker is mapped to the ordinal
+                const uint64_t mu = X ? mk_look(L.grt(), uint32_t(L.rtmask), uint32_t(op.pos1)) : 0;
                 int p = -1;
-                if (mk_get(L, uint32_t(op.pos1), mu)) {
-                    // getPosition (mergeTree.ts:768-785): the view lengths ahead of the marker, 0 once
-                    // zamboni unlinked it
-                    const int x = find_uid(L, s, mu);
+                if (mu >> 32) {
+                    const int x = find_uid(L, s, uint32_t(mu));
                     p = x > 0 ? (uni(L.E[x - 1]) & EMASK) : 0;
                     const int off = (op.payload2 & MTR_REL_OFFSET) ? int(op.payload) : 0;
-                    p = (op.payload2 & MTR_REL_BEFORE) ? p - off : p + 1 + off;  // marker.cachedLength = 1
+                    p = (op.payload2 & MTR_REL_BEFORE) ? p - off : p + 1 + off;
                 }
                 if (p < 0) {
                     s.status = MTR_ERR_UNSUPPORTED;  // the reference goes on with position -1
@@ -2495,7 +2503,7 @@ struct Eng {
             s.ops_done = k + 1;
         }
         // a launch never ends between MTR_OP_RELPOS records and their op: the next one re-runs them
-        s.ops_done -= __popc(uint32_t(uni(L.sc->relmask)));
+        if (X) s.ops_done -= __popc(uint32_t(uni(L.sc->relmask)));
         // a batch that ends with header segments: build the tree now (queries read it next)
         if (s.height == 0 && s.status == MTR_OK && cursor + s.ops_done >= int(dd.op_count)) finish_load(L, s);
         store_doc(L, P, s, d);
@@ -2622,7 +2630,9 @@ struct Eng {
             ProfScope _prof_kind(L0.sc, op.type == MTR_OP_SETCELL ? P_X1 : P_X2);
 #endif
             bool ok = true;
-            if (op.type == MTR_OP_START_COLLAB) {  // didAttach / onConnect start both vectors (matrix.ts:514-532)
+            if (op.type == MTR_OP_START_COLLAB && !(op.flags & MTR_F_APPEND)) {
+                // didAttach / onConnect start both vectors (matrix.ts:514-532); with MTR_F_APPEND, one
+                // vector's SnapshotLoader start (below, by MTR_F_COLS)
                 ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k) && apply_op(L1, P, s1, op, dd, false, 0, cursor + k);
             } else if (op.type == MTR_OP_SETCELL) {
                 s0.sum_s += (unsigned long long)(s0.nseg + s1.nseg);  // both vectors are resolved

@@ -101,6 +101,7 @@ struct mtr_engine {
     DevBuf<uint64_t> doff;            // [doc + 1] record offsets into delta (exact per-batch bound)
     std::vector<uint64_t> h_doff;
     bool has_delta = false;
+    bool has_ext = false;             // the batch holds rare records (op_scan_kernel): no fixed-capacity kernels
     DevBuf<int32_t> red;              // small reduction / query-result buffer
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
@@ -156,12 +157,22 @@ __global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_
 }
 
 // any op of the batch flagged MTR_F_DELTA (the host sizes delta buffers only when one is)
-__global__ void any_delta_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
+// bit 0: an op flagged MTR_F_DELTA (the host sizes delta buffers only then); bit 1: a rare record the
+// fixed-capacity kernels do not carry (Eng::X: relative positions, handle-table loads, combining
+// annotates, marker ordinals)
+__global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    bool any = false;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
-        any = any || (ops[i].flags & MTR_F_DELTA) != 0;
-    if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(out, 1);
+    bool any = false, ext = false;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const mtr_op op = ops[i];
+        any = any || (op.flags & MTR_F_DELTA) != 0;
+        ext = ext || op.type == MTR_OP_RELPOS || op.type == MTR_OP_HANDLES || (op.flags & MTR_F_REL) ||
+              (op.type == MTR_OP_ANNOTATE && op.payload2 != 0) ||
+              ((op.flags & MTR_F_MARKER) && op.payload2 != 0 &&
+               (op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT || op.type == MTR_OP_LOAD));
+    }
+    const int bits = (__ballot(any) ? 1 : 0) | (__ballot(ext) ? 2 : 0);
+    if (bits && (threadIdx.x & 63) == 0) atomicOr(out, bits);
 }
 
 // out[0] = max nseg, out[1] = max remaining ops, out[2] = max heapn
@@ -386,17 +397,19 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
     // per flagged set-cell, and per vector one per unlinked segment -- at most the segments present
     // at the batch start plus two per op (split + insert / load)
     e->has_delta = false;
+    e->has_ext = false;
     e->h_doff.assign(size_t(b->n_docs) + 1, 0);
     bool any = false;
     if (b->n_ops) {  // one pass over the uploaded ops on the device instead of the host
         HIPCHK(hipMemsetAsync(e->red.p, 0, sizeof(int32_t), e->stream));
         const uint64_t blocks = std::min<uint64_t>((b->n_ops + 255) / 256, 4096);
-        any_delta_kernel<<<uint32_t(blocks), 256, 0, e->stream>>>(e->ops.p, b->n_ops, e->red.p);
+        op_scan_kernel<<<uint32_t(blocks), 256, 0, e->stream>>>(e->ops.p, b->n_ops, e->red.p);
         HIPCHK(hipGetLastError());
         int32_t flag = 0;
         HIPCHK(hipMemcpyAsync(&flag, e->red.p, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
-        any = flag != 0;
+        any = (flag & 1) != 0;
+        e->has_ext = (flag & 2) != 0;
     }
     if (any) {
         std::vector<uint64_t> need(b->n_docs, 0);
@@ -659,9 +672,9 @@ static int run_impl(mtr_engine* e, int gen) {
             } else if (P.global_mode) {
                 apply_kernel<true><<<cnt, NT, lds, st>>>(P);
             } else {
-                if (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
+                if (e->has_ext || (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
                     !launch_fixed_cap_p1(cap, uint32_t(cnt), lds, st, P) &&
-                    !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P))
+                    !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P)))
                     apply_kernel<false><<<cnt, NT, lds, st>>>(P);
             }
             HIPCHK(hipGetLastError());

@@ -40,6 +40,10 @@ enum {
                                    (PermutationVector.adjustPosition, permutationvector.ts:232-247) and, when both
                                    are live, allocates row and col handles (getAllocatedHandle, :209-230).
                                    No updateSeqNumbers on either vector. */
+    MTR_OP_HANDLES = 16,        /* PermutationVector.load's HandleTable.load (permutationvector.ts:327-345,
+                                   handletable.ts:88), ahead of the vector's snapshot segments: pos1 = entry
+                                   count, payload = offset of the entries in the document's text (two UTF-16
+                                   units each, low half first).  Matrix documents only (MTR_F_COLS: cols). */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for
@@ -127,6 +131,11 @@ typedef struct mtr_delta {
  * insert (onDelta INSERT, permutationvector.ts:354-361).
  */
 #define MTR_HANDLE_UNALLOCATED ((int32_t)0x80000000) /* Handle.unallocated, handletable.ts:11 */
+/* Loading a matrix from its summary (SharedMatrix.loadCore, matrix.ts:611-631): per vector (rows, then cols
+ * with MTR_F_COLS) one MTR_OP_HANDLES record, its header segments as MTR_OP_LOAD records whose PermutationSegment
+ * spec [length, start] keeps its start (payload = start, payload2 = length), an MTR_OP_START_COLLAB with
+ * MTR_F_APPEND (that vector only, at its own header's minSeq / seq), then its body segments (MTR_F_APPEND
+ * inserts). */
 
 /*
  * Snapshot segments (MTR_OP_LOAD, and MTR_OP_INSERT with MTR_F_APPEND) carry their merge info

@@ -837,7 +837,9 @@ class Tree {
         if (permMode) {  // PermutationSegment.fromJSONObject + reset() on INSERT (permutationvector.ts:45-48, 354-361)
             s->perm = true;
             s->len = int(op.payload2);
-            s->start = MTR_HANDLE_UNALLOCATED;
+            // a snapshot segment keeps its start: loading fires no delta callback (mergeTree.ts:1410-1418)
+            const bool snap = op.type == MTR_OP_LOAD || (op.flags & MTR_F_APPEND);
+            s->start = snap ? int(op.payload) : MTR_HANDLE_UNALLOCATED;
             return s;
         }
         if (op.flags & MTR_F_MARKER) {
@@ -1035,6 +1037,13 @@ class Tree {
                 break;
             case MTR_OP_SEQ:
                 break;
+            case MTR_OP_HANDLES: {  // HandleTable.load (handletable.ts:88), PermutationVector.load (permutationvector.ts:327-345)
+                if (!permMode || collaborating || op.pos1 < 1) return MTR_ERR_BAD_OP;
+                const uint16_t* t = tabs.b->text + dd.text_base + op.payload;
+                handles.assign(size_t(op.pos1), 0);
+                for (int k = 0; k < op.pos1; k++) handles[size_t(k)] = int32_t(uint32_t(t[2 * k]) | (uint32_t(t[2 * k + 1]) << 16));
+                return status;
+            }
             case MTR_OP_LOCAL_INSERT: {
                 if (collaborating) return MTR_ERR_UNSUPPORTED;
                 Seg* s = segmentFromSpec(op, dd);
@@ -1337,10 +1346,10 @@ struct oracle_doc {
     Tree& view() { return sel ? cols : tree; }
     // SharedMatrix.processCore, remote branch (matrix.ts:636-693)
     int applyMatrix(const mtr_op& op, const mtr_doc_desc& dd) {
-        if (op.type == MTR_OP_START_COLLAB) {  // didAttach/onConnect start both vectors, matrix.ts:514-532
+        if (op.type == MTR_OP_START_COLLAB && !(op.flags & MTR_F_APPEND)) {  // didAttach/onConnect start both vectors, matrix.ts:514-532
             int st = tree.apply(op, dd);
             return st != MTR_OK ? st : cols.apply(op, dd);
-        }
+        }  // (with MTR_F_APPEND: one vector's SnapshotLoader start, routed by MTR_F_COLS below)
         if (op.type == MTR_OP_SETCELL) {
             if (!tree.pendingLoad.empty()) tree.reloadFromSegments();
             if (!cols.pendingLoad.empty()) cols.reloadFromSegments();

@@ -453,3 +453,118 @@ def test_matrix_cell_records_match_oracle():
         for w, name in ((0, "rows"), (1, "cols")):
             blobs = o.select(w).summarize(rb, 0)
             assert list(tree[name]["segments"].values()) + [tree[name]["handleTable"]] == blobs
+
+
+# ---------------------------------------------------------------- load from a summary (f3)
+def _vector_tree(blobs):
+    """PermutationVector.summarize's tree from [segment blobs..., handleTable] (permutationvector.ts:310-325)."""
+    return {"segments": {("header" if i == 0 else f"body_{i - 1}"): b for i, b in enumerate(blobs[:-1])},
+            "handleTable": blobs[-1]}
+
+
+def _oracle_matrix_tree(log, o, b):
+    return {"rows": _vector_tree(o.select(0).summarize(b, 0)), "cols": _vector_tree(o.select(1).summarize(b, 0)),
+            "cells": log.cells_blob()}
+
+
+def _oracle_continue(tree, loader, msgs, chunk):
+    """SharedMatrix.load from `tree` (the oracle), then the remaining messages in chunks."""
+    it = Interner()
+    lg = CellMatrixLog()
+    lg.load_summary(tree, loader, it)
+    o = OracleDoc(options(), matrix=True)
+    b = build_batch([lg], it)
+    assert o.apply(b, 0) == 0
+    lg.resolve(o.select(0).deltas(), o.select(1).deltas())
+    first = _oracle_matrix_tree(lg, o, b)
+    for k in range(0, len(msgs), chunk):
+        for m in msgs[k:k + chunk]:
+            lg.message(m, it)
+        b = build_batch([lg], it)
+        assert o.apply(b, 0) == 0
+        lg.resolve(o.select(0).deltas(), o.select(1).deltas())
+    return first, _oracle_matrix_tree(lg, o, b)
+
+
+@pytest.mark.parametrize("writers,lag", [(8, 16), (16, 64)])
+def test_matrix_load_round_trip_oracle(writers, lag):
+    """summarize -> load -> summarize is the identity (vectors' segments and handle tables, cells), and
+    replay continues from the loaded matrix (C4-mix documents, split at a third)."""
+    cfg = matrix_cfg(4, 1500, writers=writers, max_lag=lag)
+    gb, _, status = generate_matrix(cfg, tables(writers=writers), 0, 4, threads=4)
+    assert (status == 0).all()
+    for d in range(4):
+        observer, msgs = matrix_messages(gb, d, np.random.default_rng(d))
+        cut = len(msgs) // 3
+        log, o, b = _oracle_cells(observer, msgs[:cut], 211)
+        tree = _oracle_matrix_tree(log, o, b)
+        first, _ = _oracle_continue(tree, "loader", msgs[cut:], 173)
+        assert first == tree
+
+
+@pytest.mark.gpu
+def test_matrix_load_round_trip_engine_matches_oracle():
+    """Engine: summarize -> load -> continue for C4-mix matrices; the vectors' summaries and the cells
+    blob equal the oracle doing the same from the same summary."""
+    from fluidframework_amd.cells import matrix_summary
+    from fluidframework_amd.engine import Engine
+
+    n, nops = 8, 1800
+    cfg = matrix_cfg(n, nops, writers=8, max_lag=32)
+    gb, _, status = generate_matrix(cfg, tables(writers=8), 0, n, threads=8)
+    assert (status == 0).all()
+    feeds = [matrix_messages(gb, m, np.random.default_rng(m)) for m in range(n)]
+
+    eng = Engine(2 * n, max_segments=2 * nops + 128, heap_entries=2 * nops + 128, text_units=1 << 15,
+                 prop_words=1024, remover_cells=4096, ops_per_launch=64)
+    eng2 = Engine(2 * n, max_segments=2 * nops + 128, heap_entries=2 * nops + 128, text_units=1 << 15,
+                  prop_words=1024, remover_cells=4096, ops_per_launch=64)
+    for m in range(n):
+        eng.set_matrix(2 * m, 2 * m + 1)
+        eng2.set_matrix(2 * m, 2 * m + 1)
+    cuts = [len(f[1]) // 2 for f in feeds]
+    # first half on the engine
+    it = Interner()
+    logs = []
+    for observer, _ in feeds:
+        lg = CellMatrixLog()
+        lg.start_collab(observer)
+        logs.append(lg)
+    for k in range(0, max(cuts), 257):
+        for lg, (_, msgs), c in zip(logs, feeds, cuts):
+            for msg in msgs[k:min(k + 257, c)]:
+                lg.message(msg, it)
+        eng.apply(build_batch([x for lg in logs for x in (lg, lg.cols_log())], it))
+        for m, lg in enumerate(logs):
+            lg.resolve(eng.deltas(2 * m), eng.deltas(2 * m + 1))
+    eng.summarize()
+    trees = [matrix_summary(eng, 2 * m, 2 * m + 1, logs[m]) for m in range(n)]
+    # load into a second engine and continue
+    it2 = Interner()
+    logs2 = []
+    for m in range(n):
+        lg = CellMatrixLog()
+        lg.load_summary(trees[m], "loader-%d" % m, it2)
+        logs2.append(lg)
+    rest = [f[1][c:] for f, c in zip(feeds, cuts)]
+
+    def apply2():
+        eng2.apply(build_batch([x for lg in logs2 for x in (lg, lg.cols_log())], it2))
+        for m, lg in enumerate(logs2):
+            assert eng2.status(2 * m)[0] == 0 and eng2.status(2 * m + 1)[0] == 0
+            lg.resolve(eng2.deltas(2 * m), eng2.deltas(2 * m + 1))
+
+    apply2()  # the load alone: summarize reproduces the loaded tree
+    eng2.summarize()
+    for m in range(n):
+        assert matrix_summary(eng2, 2 * m, 2 * m + 1, logs2[m]) == trees[m]
+    for k in range(0, max(len(r) for r in rest), 311):
+        for lg, r in zip(logs2, rest):
+            for msg in r[k:k + 311]:
+                lg.message(msg, it2)
+        apply2()
+    eng2.summarize()
+    for m in range(n):
+        got = matrix_summary(eng2, 2 * m, 2 * m + 1, logs2[m])
+        _, exp = _oracle_continue(trees[m], "loader-%d" % m, rest[m], 311)
+        assert got == exp, f"matrix {m}: round trip differs from the oracle"
