@@ -69,10 +69,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=None,
-                    help="PMC summary of this config (default: profiles/traffic_r01.json, _c4 for C4)")
+                    help="PMC summary of this config (default: profiles/traffic_r02.json for C3, the r01 files else)")
     a = ap.parse_args()
     if a.traffic_file is None:
-        name = "traffic_r01.json" if a.config != "C4" else "traffic_r01_c4.json"
+        name = {"C3": "traffic_r02.json", "C4": "traffic_r01_c4.json"}.get(a.config, "traffic_r01.json")
         a.traffic_file = os.path.join(ROOT, "profiles", name)
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:

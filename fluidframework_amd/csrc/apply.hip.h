@@ -889,12 +889,8 @@ struct Eng {
         uint32_t dst;
         int propused, status;
     };
-    #ifdef MTR_SERIAL_INLINE
-    static MTR_DI
-#else
-    static __device__ __attribute__((noinline))
-#endif
-    PropRes props_apply_serial(const D& L, const KParams& P, int propused,
+        // (out of line: rare, and inlining it costs the replay kernels 2.5 % at C3)
+    static __device__ __attribute__((noinline)) PropRes props_apply_serial(const D& L, const KParams& P, int propused,
                                                                          uint32_t old, uint32_t pp,
                                              uint32_t comb) {
         PropRes r{old, propused, MTR_OK};
