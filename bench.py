@@ -44,7 +44,12 @@ PRESETS = {
     # SharedMatrix replay: docs = matrices (two PermutationVector documents each), 20 % row/col
     # splices (insert 12 : remove 8) and 80 % setCell
     "C4": dict(docs=1_000, ops=20_000, writers=8, max_lag=64),
+    # long context: documents pre-grown to 200,000 segments through a summary load (reloadFromSegments),
+    # then collaboration with 64 writers and lags up to 4,096 (a deep window); HBM-resident
+    # (1,000 documents x 20,000 messages; --docs / --ops select a part of it)
+    "C5": dict(docs=1_000, ops=20_000, writers=64, max_lag=4096),
 }
+GROW = {"C5": 200_000}
 MATRIX = {"C4"}
 
 
@@ -63,7 +68,8 @@ def parse():
     ap.add_argument("--ops", type=int, default=None, help="sequenced messages per document (preset)")
     ap.add_argument("--writers", type=int, default=None)
     ap.add_argument("--max-lag", type=int, default=None)
-    ap.add_argument("--ops-per-launch", type=int, default=48)
+    ap.add_argument("--ops-per-launch", type=int, default=None,
+                    help="ops per document per launch (48; 512 for the HBM-resident C5 documents)")
     ap.add_argument("--cpu-sample-docs", type=int, default=0,
                     help="default: about 60M messages of documents (~8 s on 16 host threads)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -77,6 +83,8 @@ def parse():
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
+    if a.ops_per_launch is None:
+        a.ops_per_launch = 512 if a.config in GROW else 48
     return a
 
 
@@ -165,6 +173,7 @@ def main():
 
     n, ops = a.docs, a.ops
     matrix = a.config in MATRIX
+    grow = GROW.get(a.config, 0)
     tabs = tables(writers=a.writers)
     if a.scaling == "strong" and a.config != "C1":
         doc_lo, doc_hi = shard.strong_range(rank, world, n)
@@ -198,6 +207,12 @@ def main():
         # handle tables live in the text arena of a vector document (<= positions ever inserted)
         eng = Engine(2 * n, device=local, max_segments=2 * ops + 128, heap_entries=2 * ops + 128,
                      text_units=2 * ops + 1024, prop_words=1024, remover_cells=8192, ops_per_launch=a.ops_per_launch)
+    elif grow:
+        cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=doc_lo,
+                       text_cap=2 * grow + 18 * ops + 16)
+        eng = Engine(n, device=local, max_segments=grow + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
+                     text_units=2 * int(cfg.text_cap) + 16384, prop_words=65536, remover_cells=65536,
+                     ops_per_launch=a.ops_per_launch)
     else:
         cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=doc_lo)
         text_units = 2 * int(cfg.text_cap) + 1024
@@ -211,7 +226,7 @@ def main():
     elif matrix:  # untimed: record the op logs on the device
         eng.generate_matrix(cfg, tabs)
     else:
-        eng.generate(cfg, tabs)
+        eng.generate(cfg, tabs, grow=grow)
     gen_s = time.time() - t0
     gen_stats = eng.stats()
     if gen_stats["bad_docs"]:
@@ -253,7 +268,7 @@ def main():
         if bad_text:
             raise SystemExit(f"{bad_text} fixture documents end with a text other than the reference's resultText")
     else:
-        want = n * (ops + 1)  # every document applied its whole log (START_COLLAB + messages)
+        want = n * (grow + ops + 1)  # every document applied its whole log (loads + START_COLLAB + messages)
     if st["ops"] != want:
         raise SystemExit(f"the step applied {st['ops']} op records, expected {want}")
     hashes = eng.hashes(2 * n if matrix else n)
@@ -336,9 +351,20 @@ def main():
         "model": "B_op = 16*S_d(t) + 32 + 2*L_ins (SURVEY.md 8d)" + (
             "; setCell: S_d = leaves of both vectors (two position resolutions)" if matrix else ""),
     }
+    if grow:  # SURVEY.md 8d's two-level model for C5, reported beside the flat-pass one
+        b2_step = 8.0 / 6.0 * st["sum_leaves_before_op"] + (16.0 * 14 + 32.0) * messages + 2.0 * st["text_units_inserted"]
+        roofline["two_level"] = {
+            "model": "B_op2 = 8*#blocks + 16*(leaf records in <= 2 touched leaf blocks) + 32 + 2*L_ins; "
+                     "#blocks ~ S/6 (reloadFromSegments' 7-per-block layout and its splits), 2 leaf blocks = 14 records",
+            "bytes_per_step": b2_step,
+            "achieved_span": round(b2_step / apply_s / 1e9, 3) if apply_s > 0 else 0.0,
+            "frac_span": round(b2_step / apply_s / 1e9 / HBM_PEAK_GBS, 5) if apply_s > 0 else 0.0,
+            "note": "the engine runs a flat pass (HBM-resident leaves, one scan and shift per op), so the "
+                    "two-level model prices work it does not avoid yet",
+        }
 
     e2e = None
-    if a.e2e_steps > 0 and world == 1 and fixture_text is None:
+    if a.e2e_steps > 0 and world == 1 and fixture_text is None and not grow:
         e2e = end_to_end(eng, n, a.e2e_steps, messages, matrix, hashes)
 
     cpu = None
@@ -346,8 +372,10 @@ def main():
     if not a.no_cpu_baseline and world == 1:
         from oracle.oracle import replay_batch, replay_matrix_batch
 
-        k = min(a.cpu_sample_docs or max(1, 60_000_000 // ops), n)
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        # (pre-grown documents: the oracle's block lengths are leaf sums, O(S) per op at 200k leaves --
+        # one document per host thread is the bounded sample)
+        k = min(a.cpu_sample_docs or (threads if grow else max(1, 60_000_000 // ops)), n)
         if fixture_text is not None:  # the whole fixture set, replayed 10 times (one pass is ~0.2 s)
             k = n
             secs = 0.0
@@ -371,7 +399,8 @@ def main():
             "unit": "ops/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"first {k} of the {n} {'matrices' if matrix else 'documents'} ({k * ops} messages), replay + V1 summary, one document "
+            "sample": f"first {k} of the {n} {'matrices' if matrix else 'documents'} ({k * ops} messages"
+                      f"{f' after {grow} loaded segments each' if grow else ''}), replay + V1 summary, one document "
                       f"per task on {threads} host threads (reference-algorithm C++ restatement, not Node)",
             "seconds": round(secs, 3),
         }
@@ -398,7 +427,8 @@ def main():
                          f"splices + 80% setCell, {a.writers} writers, lag<={a.max_lag}, V1 segments + handleTable"
                          if matrix else
                          f"{a.config}: {n} docs/GPU ({a.docs} {'per GPU' if a.scaling == 'weak' else 'in all'}) x {ops} ops, "
-                         f"{a.writers} writers, lag<={a.max_lag}, V1 summaries"),
+                         f"{a.writers} writers, lag<={a.max_lag}, V1 summaries"
+                         + (f", each pre-grown to {grow} segments by a summary load (HBM-resident)" if grow else "")),
             "docs_per_gpu": n,
             "docs_total": int(n * world) if a.scaling == "weak" or a.config == "C1" else int(a.docs),
             "ops_per_doc": ops,

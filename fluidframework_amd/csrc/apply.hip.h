@@ -172,6 +172,8 @@ struct KParams {
     // record mode (synthetic workloads): ops are drawn from include/mtr_synth.h with this
     // engine's own exact view lengths, written to gen_ops/gen_text, then applied
     int32_t gen;
+    int32_t gen_grow;  // record mode: the first gen_grow records (pre-grown snapshot segments) + START_COLLAB
+                       // are written before the run; messages are records gen_grow + 1 ...
     mtr_synth_cfg gen_cfg;
     mtr_synth_state* gen_state;  // [doc]
     mtr_op* gen_ops;             // == ops, writable
@@ -503,11 +505,38 @@ struct Eng {
     // length is E[i] - E[i-1] (masked), -1 if flagged.  Rounds of 64 leaves.
     static constexpr int EMASK = 0x7fffffff;
     static MTR_DI int ev(int e, int eprev) { return e < 0 ? -1 : e - (eprev & EMASK); }
+    // HBM-resident documents (G): the O(S) passes issue the loads of GK rounds of 64 leaves before
+    // using any of them, so a pass exposes HBM latency once per 64 * GK leaves (HBM bandwidth is not
+    // what bounds them: one wave per document walks its leaves in order)
+#ifndef MTR_GK
+#define MTR_GK 4
+#endif
+    static constexpr int GK = MTR_GK;
+
     static MTR_DI void prefix(D& L, const St& s, const View& v, int newlen) {
         PROF(P_PREFIX);
         const int S = s.nseg;
         const int ln = lane_id();
         int carry = 0;
+        if constexpr (G) {
+            for (int base = 0; base < S; base += 64 * GK) {
+                Hot hk[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) hk[q] = ld_hot(L, min(base + 64 * q + ln, S - 1));
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    if (base + 64 * q >= S) break;
+                    const int i = base + 64 * q + ln;
+                    const int x0 = vis_hot(L, hk[q], i, v, newlen, s.minseq, i < S);
+                    const int x = i < S ? x0 : 0;
+                    const int inc = wave_incl_scan(max(x, 0));
+                    if (i < S) L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
+                    carry += rdlane(inc, 63);
+                }
+            }
+            wsync();
+            return;
+        }
         Hot h = S > 0 ? ld_hot(L, ln) : Hot{};  // software-pipelined: loaded one round ahead
         for (int base = 0; base < S; base += 64) {
             // every lane evaluates (reads past the last leaf stay inside the LDS allocation);
@@ -650,6 +679,34 @@ struct Eng {
     static MTR_DI void shift_right1(D& L, const St& s, int at) {
         PROF(P_SHIFT);
         const int S = s.nseg;
+        if constexpr (G) {  // GK rounds per group: every load of the group before its stores (a round's
+                            // stores land above every slot the group's lower rounds read)
+            for (int hi = S; hi > at; hi -= 64 * GK) {
+                int a0[GK], a1[GK], a2[GK], a8[GK];
+                uint32_t a3[GK], a4[GK], a5[GK], a7[GK];
+                bool act[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int hq = hi - 64 * q;
+                    const int i = max(at, hq - 64) + lane_id();
+                    act[q] = hq > at && i < hq;
+                    const int ic = max(min(i, S - 1), 0);
+                    a0[q] = L.len[ic]; a1[q] = L.seq[ic]; a2[q] = L.rseq[ic]; a8[q] = L.E[ic];
+                    a3[q] = L.meta[ic]; a4[q] = L.text[ic]; a5[q] = L.props[ic]; a7[q] = L.uid[ic];
+                }
+                wsync();
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = max(at, hi - 64 * q - 64) + lane_id();
+                    if (act[q]) {
+                        L.len[i + 1] = a0[q]; L.seq[i + 1] = a1[q]; L.rseq[i + 1] = a2[q]; L.meta[i + 1] = a3[q];
+                        L.text[i + 1] = a4[q]; L.props[i + 1] = a5[q]; L.uid[i + 1] = a7[q]; L.E[i + 1] = a8[q];
+                    }
+                }
+                wsync();
+            }
+            return;
+        }
         for (int hi = S; hi > at; hi -= 64) {
             const int lo = max(at, hi - 64);
             const int i = lo + lane_id();
@@ -673,6 +730,35 @@ struct Eng {
         PROF_COUNT(P_NCOMPACT);
         const int S = s.nseg;
         int base = from;
+        if constexpr (G) {  // GK rounds per group, loads first (destinations never pass the group's sources)
+            for (int lo = from; lo < S; lo += 64 * GK) {
+                int a0[GK], a1[GK], a2[GK];
+                uint32_t a3[GK], a4[GK], a5[GK], a7[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int ic = min(lo + 64 * q + lane_id(), S - 1);
+                    a0[q] = L.len[ic]; a1[q] = L.seq[ic]; a2[q] = L.rseq[ic];
+                    a3[q] = L.meta[ic]; a4[q] = L.text[ic]; a5[q] = L.props[ic]; a7[q] = L.uid[ic];
+                }
+                wsync();
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = lo + 64 * q + lane_id();
+                    const bool keep = i < S && !(a3[q] & M_DEL);
+                    const uint64_t km = __ballot(keep);
+                    if (keep) {
+                        const int d = base + __popcll(km & lanes_below());
+                        L.len[d] = a0[q]; L.seq[d] = a1[q]; L.rseq[d] = a2[q]; L.meta[d] = a3[q];
+                        L.text[d] = a4[q]; L.props[d] = a5[q]; L.uid[d] = a7[q];
+                    }
+                    base += __popcll(km);
+                }
+                wsync();
+            }
+            s.nseg = base;
+            if (base == 0) s.height = 1;
+            return;
+        }
         for (int lo = from; lo < S; lo += 64) {
             const int i = lo + lane_id();
             const bool act = i < S;
@@ -698,6 +784,19 @@ struct Eng {
     static MTR_DI int find_uid(const D& L, const St& s, uint32_t u) {
         PROF(P_FINDUID);
         const int S = s.nseg;
+        if constexpr (G) {
+            for (int base = 0; base < S; base += 64 * GK) {
+                uint32_t uk[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) uk[q] = L.uid[min(base + 64 * q + lane_id(), S - 1)];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const uint64_t m = __ballot((base + 64 * q + lane_id() < S) & (uk[q] == u));
+                    if (m) return base + 64 * q + first_lane(m);
+                }
+            }
+            return -1;
+        }
         for (int base = 0; base < S; base += 64) {
             const int i = base + lane_id();
             const uint32_t ui = L.uid[min(i, S - 1)];  // unconditional (clamped) load: no divergent branch
@@ -2003,7 +2102,8 @@ struct Eng {
     // draw op `idx` of document d from the synthetic recipe using this engine's exact view length
     static MTR_DI void gen_op(D& L, const KParams& P, St& s, const mtr_doc_desc& dd, int idx) {
         const gptr<mtr_op> rec = gp(P.gen_ops) + dd.op_begin + idx;
-        if (idx == 0) {
+        if (idx < P.gen_grow) return;  // a pre-grown snapshot segment, written by synth_grow_kernel
+        if (idx == P.gen_grow) {
             if (threadIdx.x == 0) {
                 mtr_op z{};
                 z.type = MTR_OP_START_COLLAB;
@@ -2015,7 +2115,7 @@ struct Eng {
         if (threadIdx.x == 0) {
             mtr_op op;
             mtr_synth_state st = ld_struct<mtr_synth_state>(L.gst);
-            mtr_synth_begin(&P.gen_cfg, &st, idx, &op);
+            mtr_synth_begin(&P.gen_cfg, &st, idx - P.gen_grow, &op);
             st_struct(L.gst, st);
             L.sc->gen_ref = op.ref_seq;
             L.sc->gen_client = op.client;
@@ -2292,8 +2392,11 @@ struct Eng {
                 return false;
             }
         }
-        s.sum_s += (unsigned long long)s.nseg;
-        if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER) && !PM)
+        // (the B_op model's counters: snapshot-load appends and relative-position records are not flat passes)
+        if (op.type != MTR_OP_LOAD && op.type != MTR_OP_RELPOS && op.type != MTR_OP_HANDLES)
+            s.sum_s += (unsigned long long)s.nseg;
+        if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER) && !PM &&
+            !(op.flags & MTR_F_APPEND))
             s.sum_l += (unsigned long long)op.payload2;
         if (!PM) {  // text arena: keep room for this op's text plus zamboni merge copies
             const int need = int(op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT ? op.payload2 : 0) + 4096;

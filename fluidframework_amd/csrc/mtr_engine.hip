@@ -114,6 +114,7 @@ struct mtr_engine {
     DevBuf<uint32_t> dkind, dpart;
     std::vector<uint32_t> h_kind, h_part;
     mtr_synth_cfg gcfg{};
+    uint32_t ggrow = 0;  // pre-grown records of the record-mode run in progress
     // summaries
     DevBuf<int64_t> out_size, out_off;
     DevBuf<uint8_t> s_kind;                       // summary scratch (size pass -> write pass)
@@ -540,6 +541,7 @@ static int run_impl(mtr_engine* e, int gen) {
 #endif
     if (gen) {
         P.gen_cfg = e->gcfg;
+        P.gen_grow = int32_t(e->ggrow);
         P.gen_state = e->gstate.p;
         P.gen_ops = e->ops.p;
         P.gen_text = e->btext.p;
@@ -714,13 +716,42 @@ __global__ void synth_text_count_kernel(const mtr_synth_state* st, mtr_doc_desc*
     if (d < n) docs[d].text_count = st[d].text_used;
 }
 
+// the pre-grown documents' snapshot header segments (the oracle's generate_impl writes the same records):
+// segment k of every document is the two units ('a' + k % 26, 'A' + k / 26 % 26), NonCollabClient, no merge info
+__global__ void synth_grow_kernel(mtr_op* ops, uint16_t* text, mtr_synth_state* st, uint32_t n, uint32_t per,
+                                  uint32_t text_cap, uint32_t grow) {
+    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= uint64_t(n) * (grow + 1)) return;
+    const uint32_t d = uint32_t(t / (grow + 1)), k = uint32_t(t % (grow + 1));
+    mtr_op op{};
+    if (k < grow) {
+        op.type = MTR_OP_LOAD;
+        op.client = uint16_t(MTR_CLIENT_NONCOLLAB);
+        op.ref_seq = -1;
+        op.pos2 = -1;
+        op.payload = 2 * k;
+        op.payload2 = 2;
+        text[uint64_t(d) * text_cap + 2 * k] = uint16_t('a' + k % 26);
+        text[uint64_t(d) * text_cap + 2 * k + 1] = uint16_t('A' + (k / 26) % 26);
+    } else {
+        op.type = MTR_OP_START_COLLAB;
+        st[d].text_used = 2 * grow;
+    }
+    ops[uint64_t(d) * per + k] = op;
+}
+
 int mtr_generate(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch* tables) {
+    return mtr_generate_grown(e, cfg, tables, 0);
+}
+
+int mtr_generate_grown(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch* tables, uint32_t grow) {
     HIPCHK(hipSetDevice(e->device));
-    if (cfg->n_docs > e->max_docs || cfg->writers > MTR_SYNTH_MAX_WRITERS || cfg->writers + 1 > 0xfd) {
+    if (cfg->n_docs > e->max_docs || cfg->writers > MTR_SYNTH_MAX_WRITERS || cfg->writers + 1 > 0xfd ||
+        uint64_t(cfg->text_cap) < 2ull * grow) {
         set_err("mtr_generate: bad configuration");
         return MTR_ERR_BAD_OP;
     }
-    const uint32_t n = cfg->n_docs, per = cfg->ops_per_doc + 1;
+    const uint32_t n = cfg->n_docs, per = grow + cfg->ops_per_doc + 1;
     if (n == 0) return mtr_reset(e);
     std::vector<mtr_doc_desc> docs(n);
     for (uint32_t d = 0; d < n; d++) {
@@ -739,9 +770,18 @@ int mtr_generate(mtr_engine* e, const mtr_synth_cfg* cfg, const mtr_batch* table
     if (mtr_reset(e) != MTR_OK || mtr_submit(e, &b) != MTR_OK) return -1;
     if (e->ops.ensure(size_t(n) * per) || e->btext.ensure(size_t(n) * cfg->text_cap) || e->gstate.ensure(n)) return -1;
     e->gcfg = *cfg;
+    e->ggrow = grow;
     synth_init_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(*cfg, e->gstate.p, n);
     HIPCHK(hipGetLastError());
-    if (run_impl(e, 1) != MTR_OK) return -1;
+    if (grow) {
+        const uint64_t total = uint64_t(n) * (grow + 1);
+        synth_grow_kernel<<<uint32_t((total + 255) / 256), 256, 0, e->stream>>>(e->ops.p, e->btext.p, e->gstate.p, n,
+                                                                               per, cfg->text_cap, grow);
+        HIPCHK(hipGetLastError());
+    }
+    const int rc = run_impl(e, 1);
+    e->ggrow = 0;
+    if (rc != MTR_OK) return -1;
     synth_text_count_kernel<<<(n + 255) / 256, 256, 0, e->stream>>>(e->gstate.p, e->docs.p, n);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));

@@ -91,6 +91,8 @@ def lib():
         L.mtr_profile.restype = C.c_int
         L.mtr_generate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mtr_generate.restype = C.c_int
+        L.mtr_generate_grown.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+        L.mtr_generate_grown.restype = C.c_int
         L.mtr_generate_matrix.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.mtr_generate_matrix.restype = C.c_int
         L.mtr_download_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -181,18 +183,21 @@ class Engine:
         self.run()
         self.sync()
 
-    def generate(self, cfg, tabs):
+    def generate(self, cfg, tabs, grow=0):
         """Record mode: synthesize cfg.n_docs op logs (include/mtr_synth.h) with this engine's exact
-        view lengths and apply them; the recorded batch stays on the device for replays."""
+        view lengths and apply them; the recorded batch stays on the device for replays.  grow > 0:
+        every document first loads `grow` two-unit snapshot segments (config C5; mtr_generate_grown)."""
         self._tabs = tabs
         self._cfg = cfg
-        self._check(lib().mtr_generate(self.h, C.byref(cfg), C.addressof(tabs.c)), "mtr_generate")
+        self._grow = grow
+        self._check(lib().mtr_generate_grown(self.h, C.byref(cfg), C.addressof(tabs.c), grow), "mtr_generate")
 
     def generate_matrix(self, cfg, tabs):
         """Record mode for SharedMatrix logs (mtr_synth_matrix_finish): cfg.n_docs matrices, matrix m
         = engine documents (2m rows, 2m+1 cols); the recorded logs stay on the device for replays."""
         self._tabs = tabs
         self._cfg = cfg
+        self._grow = 0
         self._check(lib().mtr_generate_matrix(self.h, C.byref(cfg), C.addressof(tabs.c)), "mtr_generate_matrix")
 
     def download_matrix(self, lo, hi):
@@ -213,7 +218,7 @@ class Engine:
         pinned_memory the op and text arrays live in page-locked memory (full-rate uploads)."""
         from .synth import with_docs
         n = hi - lo
-        per = self._cfg.ops_per_doc + 1
+        per = getattr(self, "_grow", 0) + self._cfg.ops_per_doc + 1
         alloc = (lambda k, dt: pinned(k, dt)) if pinned_memory else (lambda k, dt: np.zeros(k, dtype=dt))
         docs = np.zeros(n, dtype=abi.DOC_DTYPE)
         ops = alloc(n * per, abi.OP_DTYPE)

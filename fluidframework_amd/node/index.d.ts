@@ -30,8 +30,35 @@ export class UnsupportedError extends Error {
 export class BatchReplayEngine {
 	constructor(maxDocs: number, options?: BatchReplayOptions);
 	createClient(): BatchReplayClient;
+	/** A SharedMatrix observer: its rows / cols PermutationVectors as two engine documents. */
+	createMatrix(): BatchMatrixClient;
 	/** Apply every queued message of every document (done implicitly before any read). */
 	flush(): void;
+	/** flush() on a libuv worker thread (napi_async_work); other calls on this engine throw until it settles. */
+	flushAsync(): Promise<void>;
+}
+
+/** getContainingSegment's answer (client.ts:1065-1078); both fields undefined when no segment covers pos. */
+export interface ContainingSegment {
+	segment?: {
+		text?: string;
+		marker?: { refType: number };
+		cachedLength: number;
+		seq: number;
+		clientId: string; // the long id ("original" for the non-collaborating client)
+		removedSeq?: number;
+		leafIndex: number;
+		propertySet?: number;
+	};
+	offset?: number;
+}
+
+/** SharedMatrix observer (matrix.ts:636-693, remote branch). */
+export class BatchMatrixClient {
+	startOrUpdateCollaboration(longClientId: string, minSeq?: number, currentSeq?: number): void;
+	applyMsg(msg: ISequencedDocumentMessage): void;
+	/** Each vector's PermutationVector.summarize blobs (V1 segments..., handleTable), permutationvector.ts:310-325. */
+	summarizeVectors(): { rows: string[]; cols: string[] };
 }
 
 /** Drop-in for the observer use of `Client` (client.ts:98). */
@@ -52,4 +79,16 @@ export class BatchReplayClient {
 		serializer: { stringify(value: unknown, bind: unknown): string } | undefined,
 		catchUpMsgs: ISequencedDocumentMessage[],
 	): ISummaryTreeWithStats; // client.ts:966
+	/** summarize with the GPU work on a worker thread. */
+	summarizeAsync(
+		runtime: { deltaManager: { minimumSequenceNumber: number; lastSequenceNumber: number } },
+		handle: unknown,
+		serializer: { stringify(value: unknown, bind: unknown): string } | undefined,
+		catchUpMsgs: ISequencedDocumentMessage[],
+	): Promise<ISummaryTreeWithStats>;
+	/** client.ts:1065: the segment holding pos at sequenceArgs' view (default: this client's current view). */
+	getContainingSegment(
+		pos: number,
+		sequenceArgs?: { referenceSequenceNumber: number; clientId: string },
+	): ContainingSegment;
 }

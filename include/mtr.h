@@ -160,6 +160,13 @@ int mtr_last_timing(mtr_engine* e, double* out, int32_t n);
 struct mtr_synth_cfg;
 int mtr_generate(mtr_engine* e, const struct mtr_synth_cfg* cfg, const mtr_batch* tables);
 
+/* Record mode with pre-grown documents (config C5): every document first loads `grow`
+ * two-unit snapshot header segments (MTR_OP_LOAD records, reloadFromSegments) and starts
+ * collaboration, then draws cfg->ops_per_doc messages as mtr_generate does; per document
+ * grow + 1 + ops_per_doc records and cfg->text_cap >= 2 * grow + the messages' text.  Draws the same
+ * logs as the oracle's oracle_generate_grown from the same seeds. */
+int mtr_generate_grown(mtr_engine* e, const struct mtr_synth_cfg* cfg, const mtr_batch* tables, uint32_t grow);
+
 /* Record mode for SharedMatrix workloads: cfg->n_docs matrices drawn from the
  * matrix recipe (mtr_synth_matrix_finish) with the engine's exact view lengths of both vectors.
  * Matrix m is the pair (rows = engine document 2m, cols = 2m + 1; paired as by mtr_set_matrix) and

@@ -285,3 +285,25 @@ def test_options_synthetic(newlen, v1, chunk):
         _compare_export(eng, d, orc)
         assert eng.summary(d) == orc.summarize(b, d)
     assert bad.size == 0
+
+
+def test_grown_record_mode_matches_oracle_generator():
+    """mtr_generate_grown (config C5's pre-grown documents drawn on the device) records the same logs
+    as the oracle's generator from the same seeds, and replays to the oracle's summaries."""
+    from fluidframework_amd.synth import make_cfg, tables
+    from oracle.oracle import generate
+
+    n, grow, ops = 4, 5000, 600
+    cfg = make_cfg(n, ops, writers=64, max_lag=512, text_cap=2 * grow + ops * 18 + 16)
+    tabs = tables(writers=64)
+    ob, ohash, ost = generate(cfg, tabs, 0, n, threads=4, grow=grow)
+    assert (ost == 0).all()
+    eng = _engine(n, max_segments=grow + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
+                  text_units=2 * (int(cfg.text_cap) + 8192), ops_per_launch=256)
+    eng.generate(cfg, tabs, grow=grow)
+    rec = eng.download(0, n)
+    assert rec.ops.tobytes() == ob.ops.tobytes()
+    eng.reset()
+    eng.run()
+    eng.summarize()
+    assert np.array_equal(eng.hashes(n), ohash)
