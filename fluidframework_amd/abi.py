@@ -17,6 +17,7 @@ OP_LOAD = 13
 OP_SETCELL = 14
 OP_RELPOS = 15
 OP_HANDLES = 16
+OP_ACK = 17
 REL_BEFORE = 1
 REL_OFFSET = 2
 COMB_NONE, COMB_REWRITE, COMB_INCR, COMB_CONSENSUS, COMB_KEEP = 0, 1, 2, 3, 4

@@ -313,7 +313,10 @@ class DocLog:
             return flags, int(ref), self._map_marker(props) if map_marker else 0, pp
         raise Unsupported("unrecognized segment spec")
 
-    # -- non-collaborating local edits (pre-attach SharedString / TestClient.insertTextLocal)
+    # -- local edits (Client.insertSegmentLocal / removeRangeLocal / annotateRangeLocal, client.ts:225-260):
+    # before collaboration they are final (pre-attach SharedString, TestClient.insertTextLocal); while
+    # collaborating each is a pending op the engine keeps in a SegmentGroup until this client's sequenced
+    # message for it arrives (message() turns that into MTR_OP_ACK records)
     def local_insert(self, pos: int, spec: Any, interner: Interner) -> None:
         flags, p1, p2, pp = self._seg(spec, interner)
         self.ops.append((abi.OP_LOCAL_INSERT, flags, 0, 0, 0, 0, pos, pp, p1, p2))
@@ -322,7 +325,23 @@ class DocLog:
         self.ops.append((abi.OP_LOCAL_REMOVE, 0, 0, 0, 0, 0, start, end, 0, 0))
 
     def local_annotate(self, start: int, end: int, props: dict, interner: Interner) -> None:
+        if isinstance(props, dict) and "markerId" in props:
+            self.marker_id_annotated = True
         self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, 0, 0, 0, start, end, interner.propop(props), 0))
+
+    def local_op(self, op: dict, interner: Interner) -> None:
+        """A local merge-tree op (the contents this client submits): insert / remove / annotate."""
+        t = op.get("type")
+        if t == 0:
+            self.local_insert(int(op["pos1"]), op["seg"], interner)
+        elif t == 1:
+            self.local_remove(int(op["pos1"]), int(op["pos2"]))
+        elif t == 2:
+            if js_truthy(op.get("combiningOp")):
+                raise Unsupported("local annotate with a combiningOp")
+            self.local_annotate(int(op["pos1"]), int(op["pos2"]), op.get("props") or {}, interner)
+        else:
+            raise Unsupported(f"local op type {t}")
 
     def start_collab(self, long_id: str | None, min_seq: int = 0, current_seq: int = 0) -> None:
         """Client.startOrUpdateCollaboration (client.ts:1133-1155): an undefined id keeps the client
@@ -413,14 +432,25 @@ class DocLog:
         if msg.get("type") != "op":
             self.ops.append((abi.OP_SEQ, abi.F_LAST, short, seq, ref, msn, 0, 0, 0, 0))
             return
-        if cid == self.observer_id:
-            raise Unsupported("message authored by the observer (local ack path)")
         contents = msg["contents"]
         if isinstance(contents, str):
             contents = parse(contents)
         members = contents["ops"] if contents.get("type") == 3 else [contents]
         if not members:
             self.ops.append((abi.OP_SEQ, abi.F_LAST, short, seq, ref, msn, 0, 0, 0, 0))
+            return
+        if cid == self.observer_id:  # this client's own op: ackPendingSegment per member (client.ts:641-663, 866-869)
+            for i, op in enumerate(members):
+                last = abi.F_LAST if i == len(members) - 1 else 0
+                t = op.get("type")
+                pp = 0
+                if t == 2:
+                    if js_truthy(op.get("combiningOp")):
+                        raise Unsupported("ack of a local annotate with a combiningOp")
+                    pp = interner.propop(op.get("props") or {})
+                elif t not in (0, 1):
+                    raise Unsupported(f"ack of op type {t}")
+                self.ops.append((abi.OP_ACK, last, short, seq, ref, msn, 0, 0, pp, t))
             return
         for i, op in enumerate(members):
             last = abi.F_LAST if i == len(members) - 1 else 0

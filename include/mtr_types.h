@@ -27,9 +27,13 @@ enum {
     MTR_OP_REMOVE = 1,          /* remote remove  (client.ts:430)  */
     MTR_OP_ANNOTATE = 2,        /* remote annotate(client.ts:457)  */
     MTR_OP_SEQ = 3,             /* non-"op" message: updateSeqNumbers only */
-    MTR_OP_LOCAL_INSERT = 8,    /* non-collaborating local insert (client.ts:237, seq=0, client=-1) */
-    MTR_OP_LOCAL_REMOVE = 9,    /* non-collaborating local remove */
-    MTR_OP_LOCAL_ANNOTATE = 10, /* non-collaborating local annotate */
+    MTR_OP_LOCAL_INSERT = 8,    /* local insert (Client.insertSegmentLocal, client.ts:237): before collaboration
+                                   seq = UniversalSequenceNumber, client = LocalClientId; while collaborating a
+                                   pending op (seq = UnassignedSequenceNumber, the local client's short id, a new
+                                   localSeq and SegmentGroup, mergeTree.ts:1397-1427, 1604-1637) until its ACK */
+    MTR_OP_LOCAL_REMOVE = 9,    /* local remove (client.ts:227; pending: mergeTree.ts:1955-2047) */
+    MTR_OP_LOCAL_ANNOTATE = 10, /* local annotate without a combiningOp (pending keys:
+                                   segmentPropertiesManager.ts:60-157) */
     MTR_OP_START_COLLAB = 12,   /* Client.startOrUpdateCollaboration (client.ts:1133): seq/min_seq = currentSeq/minSeq,
                                    client = the observer's short id */
     MTR_OP_LOAD = 13,           /* a snapshot header segment (SnapshotLoader.loadHeader, snapshotLoader.ts:130-167):
@@ -44,6 +48,11 @@ enum {
                                    handletable.ts:88), ahead of the vector's snapshot segments: pos1 = entry
                                    count, payload = offset of the entries in the document's text (two UTF-16
                                    units each, low half first).  Matrix documents only (MTR_F_COLS: cols). */
+    MTR_OP_ACK = 17,            /* one member op of a sequenced message this client authored (Client.applyMsg,
+                                   client.ts:866-869 -> ackPendingSegment, client.ts:641-663 and
+                                   mergeTree.ts:1283-1322): acks the oldest pending SegmentGroup; payload2 =
+                                   the member's MergeTreeDeltaType (segment.ack switches on it,
+                                   mergeTreeNodes.ts:439-479), payload = its prop-op for an annotate */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for

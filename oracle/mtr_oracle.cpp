@@ -89,6 +89,17 @@ struct Seg : Node {
     bool hasPropMgr = false;         // propertyManager !== undefined
     PropMap props;
     uint32_t markerOrdinal = 0;      // host marker ordinal + 1 of a Marker with a truthy markerId (0 = none)
+    // the local-op path: segmentGroups (segmentGroupCollection.ts), in enqueue order, and
+    // PropertiesManager.pendingKeyUpdateCount (segmentPropertiesManager.ts:25): key id -> count > 0
+    std::deque<struct SegGroup*> groups;
+    std::vector<std::pair<uint32_t, int>> pendingKeys;
+};
+
+// SegmentGroup (mergeTreeNodes.ts:57-62): the segments one pending local op touched, in the order they
+// joined it (walk order, then split-off halves as splitAt copies them, segmentGroupCollection.ts:47-62)
+struct SegGroup {
+    std::vector<Seg*> segments;
+    int localSeq = 0;
 };
 
 struct PSL;
@@ -217,6 +228,10 @@ class Tree {
     std::deque<Block> blockPool;
     Tables tabs;
     int status = MTR_OK;
+    // pending local ops: collabWindow.localSeq (mergeTreeNodes.ts:656) and MergeTree.pendingSegments
+    int localSeqCounter = 0;
+    std::deque<SegGroup*> pendingSegments;
+    std::deque<SegGroup> groupPool;
 
     Block* makeBlock() {
         blockPool.emplace_back();
@@ -389,6 +404,7 @@ class Tree {
             r->hasPropMgr = true;
             r->hasProps = true;
             r->props = s->props;
+            r->pendingKeys = s->pendingKeys;  // PropertiesManager.copyTo, segmentPropertiesManager.ts:160-184
         }
         r->parent = s->parent;
         r->removedClientIds = s->removedClientIds;
@@ -396,7 +412,82 @@ class Tree {
         r->removedSeq = s->removedSeq;
         r->seq = s->seq;
         r->clientId = s->clientId;
+        for (SegGroup* g : s->groups) {  // segmentGroups.copyTo -> enqueueOnCopy (segmentGroupCollection.ts:47-62)
+            r->groups.push_back(g);
+            g->segments.push_back(r);
+        }
         return r;
+    }
+
+    // addToPendingList, mergeTree.ts:1324-1357 (previousProps are kept only for rollback: not modelled)
+    SegGroup* addToPendingList(Seg* s, SegGroup* g, int localSeq) {
+        if (!g) {
+            groupPool.emplace_back();
+            g = &groupPool.back();
+            g->localSeq = localSeq;
+            pendingSegments.push_back(g);
+        }
+        s->groups.push_back(g);  // segment.segmentGroups.enqueue (segmentGroupCollection.ts:24-27)
+        g->segments.push_back(s);
+        return g;
+    }
+
+    static int* pendingCount(Seg* s, uint32_t key) {
+        for (auto& kc : s->pendingKeys)
+            if (kc.first == key) return &kc.second;
+        return nullptr;
+    }
+
+    // MergeTree.ackPendingSegment (mergeTree.ts:1283-1322) for one member op of this client's sequenced
+    // message; opType = that member's MergeTreeDeltaType, propop = its props (annotate)
+    void ackPendingSegment(int opType, uint32_t propop, int seq) {
+        if (!pendingSegments.empty()) {
+            SegGroup* g = pendingSegments.front();
+            pendingSegments.pop_front();
+            for (Seg* s : g->segments) {
+                // BaseSegment.ack, mergeTreeNodes.ts:439-479
+                if (s->groups.empty() || s->groups.front() != g) {
+                    status = MTR_ERR_ASSERT | 0x043;  // "On ack, unexpected segmentGroup!"
+                    return;
+                }
+                s->groups.pop_front();
+                if (opType == MTR_OP_ANNOTATE) {  // ackPendingProperties -> decrementPendingCounts (:32-58)
+                    const mtr_batch* b = tabs.b;
+                    for (uint32_t i = b->propop_off[propop]; i < b->propop_off[propop + 1]; i++) {
+                        const uint32_t k = b->propop_kv[2 * i];
+                        int* c = pendingCount(s, k);
+                        if (!c) continue;
+                        if (*c <= 0) {
+                            status = MTR_ERR_ASSERT | 0x05c;
+                            return;
+                        }
+                        if (--*c == 0)
+                            for (size_t j = 0; j < s->pendingKeys.size(); j++)
+                                if (s->pendingKeys[j].first == k) {
+                                    s->pendingKeys.erase(s->pendingKeys.begin() + j);
+                                    break;
+                                }
+                    }
+                } else if (opType == MTR_OP_INSERT) {
+                    if (s->seq != kUnassignedSeq) {
+                        status = MTR_ERR_ASSERT | 0x045;  // "On insert, seq number already assigned!"
+                        return;
+                    }
+                    s->seq = seq;
+                } else if (opType == MTR_OP_REMOVE) {
+                    if (!s->removed) {
+                        status = MTR_ERR_ASSERT | 0x046;  // "On remove ack, missing removal info!"
+                        return;
+                    }
+                    if (s->removedSeq == kUnassignedSeq) s->removedSeq = seq;
+                } else {
+                    status = MTR_ERR_BAD_OP;
+                    return;
+                }
+                addToLRUSet(s, seq);  // mergeTree.ts:1299-1301
+            }
+        }
+        zamboniSegments();  // mergeTree.ts:1318-1320
     }
 
     // ------------------------------------------------------------ walking
@@ -626,7 +717,10 @@ class Tree {
             Node* child = node->children[k];
             if (child->leaf) {
                 Seg* s = static_cast<Seg*>(child);
-                if (s->removed) {
+                if (!s->groups.empty()) {  // a segment of a pending local op is held (zamboni.ts:128, 185-188)
+                    hold.push_back(s);
+                    prev = nullptr;
+                } else if (s->removed) {
                     if (s->removedSeq > minSeq) {
                         hold.push_back(s);
                     } else {
@@ -782,12 +876,20 @@ class Tree {
     // properties: PropertiesManager.addProperties (segmentPropertiesManager.ts:60-157) for an observer
     // (no pending local keys: shouldModifyKey is always true), BaseSegment.addProperties
     // (mergeTreeNodes.ts:385-406).  comb = MTR_COMB_* | NaN value id << 3 (include/mtr_types.h).
-    void addProperties(Seg* s, uint32_t propop, uint32_t comb = 0) {
+    // seq: the op's seq (kUnassignedSeq for a pending local annotate); collab: collabWindow.collaborating as
+    // BaseSegment.addProperties passes it (false for a new segment's initial props, sequenceFactory.ts)
+    void addProperties(Seg* s, uint32_t propop, uint32_t comb = 0, int seq = kUniversalSeq, bool collab = false) {
         const mtr_batch* b = tabs.b;
         const uint32_t mode = comb & 7u, nanv = comb >> 3;
         s->hasPropMgr = true;
         s->hasProps = true;
         const uint32_t lo = b->propop_off[propop], hi = b->propop_off[propop + 1];
+        // shouldModifyKey (:94-104): a remote op leaves keys with pending local updates alone unless it
+        // has a (non-rewrite) combiningOp
+        const bool remote = seq != kUnassignedSeq && seq != kUniversalSeq;
+        auto modify = [&](uint32_t key) {
+            return !remote || mode >= MTR_COMB_INCR || pendingCount(s, key) == nullptr;
+        };
         if (mode == MTR_COMB_REWRITE) {  // delete old keys whose new value is falsy (:109-123)
             std::vector<std::pair<uint32_t, uint32_t>> kept;
             for (auto& kv : s->props.kv) {
@@ -798,12 +900,20 @@ class Tree {
                         truthy = v != MTR_NULL_VALUE && !(b->val_eq[v] & MTR_VEQ_FALSY);
                         break;
                     }
-                if (truthy) kept.push_back(kv);
+                if (truthy || !modify(kv.first)) kept.push_back(kv);
             }
             s->props.kv.swap(kept);
         }
         for (uint32_t i = lo; i < hi; i++) {
             uint32_t k = b->propop_kv[2 * i], v = b->propop_kv[2 * i + 1];
+            if (collab) {  // :126-138
+                if (seq == kUnassignedSeq) {
+                    if (int* c = pendingCount(s, k)) ++*c;
+                    else s->pendingKeys.push_back({k, 1});
+                } else if (!modify(k)) {
+                    continue;
+                }
+            }
             if (mode >= MTR_COMB_INCR) {  // newValue = combine(op, previousValue, undefined, seq), :145-147
                 const std::pair<uint32_t, uint32_t>* prev = nullptr;
                 for (auto& kv : s->props.kv)
@@ -871,6 +981,7 @@ class Tree {
     // insertSegments + blockInsert, mergeTree.ts:1397-1427,1594-1685
     void insertSegments(int pos, Seg* seg, int refSeq, int clientId, int seq) {
         ensureIntervalBoundary(pos, refSeq, clientId);
+        const int localSeq = seq == kUnassignedSeq ? ++localSeqCounter : 0;  // mergeTree.ts:1407-1408
         if (seg->len > 0) {
             seg->seq = seq;
             seg->clientId = clientId;
@@ -884,8 +995,8 @@ class Tree {
             updateRoot(splitNode);
             recordDeltas({seg}, MTR_OP_INSERT);  // mergeTree.ts:1414-1418
             if (collaborating) {  // saveIfLocal, mergeTree.ts:1618-1637
-                if (!(seg->seq == kUnassignedSeq && clientId == localClientId) && seg->seq > minSeq)
-                    addToLRUSet(seg, seg->seq);
+                if (seg->seq == kUnassignedSeq && clientId == localClientId) addToPendingList(seg, nullptr, localSeq);
+                else if (seg->seq > minSeq) addToLRUSet(seg, seg->seq);
             }
         }
         if (collaborating && seq != kUnassignedSeq) zamboniSegments();
@@ -897,6 +1008,8 @@ class Tree {
         ensureIntervalBoundary(end, refSeq, clientId);
         std::vector<Seg*> fresh;  // removedSegments (mergeTree.ts:1975-2000)
         bool overwrite = false;   // _overwrite: an overlapping remove rebuilds lengths (mergeTree.ts:1966,2012-2019)
+        const int localSeq = seq == kUnassignedSeq ? ++localSeqCounter : 0;  // mergeTree.ts:1970-1971
+        SegGroup* group = nullptr;
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
@@ -914,8 +1027,11 @@ class Tree {
                     s->removedSeq = seq;
                     fresh.push_back(s);
                 }
-                if (collaborating) {
-                    if (!(s->removedSeq == kUnassignedSeq && clientId == localClientId)) addToLRUSet(s, seq);
+                if (collaborating) {  // mergeTree.ts:2000-2010
+                    if (s->removedSeq == kUnassignedSeq && clientId == localClientId)
+                        group = addToPendingList(s, group, localSeq);
+                    else
+                        addToLRUSet(s, seq);
                 }
             },
             start, end,
@@ -932,12 +1048,17 @@ class Tree {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
         std::vector<Seg*> touched;
+        const int localSeq = seq == kUnassignedSeq ? ++localSeqCounter : 0;  // mergeTree.ts:1909-1910
+        SegGroup* group = nullptr;
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
-                addProperties(s, propop, comb);
+                addProperties(s, propop, comb, seq, collaborating);
                 touched.push_back(s);
-                if (collaborating && seq != kUnassignedSeq) addToLRUSet(s, seq);
+                if (collaborating) {  // mergeTree.ts:1921-1935
+                    if (seq == kUnassignedSeq) group = addToPendingList(s, group, localSeq);
+                    else addToLRUSet(s, seq);
+                }
             },
             start, end);
         recordDeltas(touched, MTR_OP_ANNOTATE);  // mergeTree.ts:1941-1946
@@ -1044,20 +1165,28 @@ class Tree {
                 for (int k = 0; k < op.pos1; k++) handles[size_t(k)] = int32_t(uint32_t(t[2 * k]) | (uint32_t(t[2 * k + 1]) << 16));
                 return status;
             }
+            // local ops (Client.insertSegmentLocal / removeRangeLocal / annotateRangeLocal -> applyInsertOp /
+            // applyRemoveRangeOp / applyAnnotateRangeOp without a sequenced message, client.ts:430-520):
+            // refSeq = currentSeq, the local client id, seq = UnassignedSequenceNumber while collaborating
+            // (a pending op until its ack), UniversalSequenceNumber before
             case MTR_OP_LOCAL_INSERT: {
-                if (collaborating) return MTR_ERR_UNSUPPORTED;
                 Seg* s = segmentFromSpec(op, dd);
-                insertSegments(op.pos1, s, currentSeq, localClientId, kUniversalSeq);
+                insertSegments(op.pos1, s, currentSeq, localClientId, collaborating ? kUnassignedSeq : kUniversalSeq);
                 return status;
             }
             case MTR_OP_LOCAL_REMOVE:
-                if (collaborating) return MTR_ERR_UNSUPPORTED;
-                markRangeRemoved(op.pos1, op.pos2, currentSeq, localClientId, kUniversalSeq);
+                markRangeRemoved(op.pos1, op.pos2, currentSeq, localClientId,
+                                 collaborating ? kUnassignedSeq : kUniversalSeq);
                 return status;
             case MTR_OP_LOCAL_ANNOTATE:
-                if (collaborating) return MTR_ERR_UNSUPPORTED;
-                annotateRange(op.pos1, op.pos2, op.payload, currentSeq, localClientId, kUniversalSeq);
+                if (op.payload2 != MTR_COMB_NONE) return MTR_ERR_UNSUPPORTED;  // pending combining ops
+                annotateRange(op.pos1, op.pos2, op.payload, currentSeq, localClientId,
+                              collaborating ? kUnassignedSeq : kUniversalSeq);
                 return status;
+            case MTR_OP_ACK:  // Client.applyMsg of this client's own message (client.ts:866-869)
+                if (!collaborating) return MTR_ERR_BAD_OP;
+                ackPendingSegment(int(op.payload2), op.payload, op.seq);
+                break;
             case MTR_OP_START_COLLAB:  // startOrUpdateCollaboration -> startCollaboration, client.ts:1133, mergeTree.ts:731
                 if (collaborating) return MTR_OK;
                 localClientId = opClient(op);

@@ -37,6 +37,64 @@ def replay_log(groups, interner: Interner) -> DocLog:
     return log
 
 
+def replay_writers(groups):
+    """The authoring clients of a replay log, in first-message order."""
+    seen = []
+    for g in groups:
+        for m in g["msgs"]:
+            if m["clientId"] not in seen:
+                seen.append(m["clientId"])
+    return seen
+
+
+def original_summary(groups):
+    """client.replay.spec.ts:27-29's original client ("A": initialText inserted locally, then
+    startOrUpdateCollaboration) as TestClient.createFromClientSnapshot summarizes it (SnapshotLegacy,
+    test/testClient.ts:70-87): {blob name: text}.  Computed with the CPU oracle (test infrastructure);
+    the legacy writer is pinned byte for byte by the snapshot fixtures."""
+    from oracle.oracle import OracleDoc, options
+
+    from fluidframework_amd.batch import build_batch
+
+    it = Interner()
+    log = replay_log(groups, it)
+    b = build_batch([log], it)
+    doc = OracleDoc(options(snapshot_v1=False))
+    if doc.apply(b, 0) != 0:
+        raise RuntimeError("original client failed to build")
+    blobs = doc.summarize(b, 0)
+    return {k: v.decode("utf-8") for k, v in zip(blob_names(len(blobs), False), blobs)}
+
+
+class Perspective:
+    """One writer client of client.replay.spec.ts:22-68 as its own document: created from the original
+    client's snapshot under its long id (createFromClientSnapshot), it applies its own op locally
+    (localTransaction -- a pending local op) right after catching up to the op's
+    referenceSequenceNumber with the messages queued for it, and every sequenced message in order
+    (its own become acks); at the end of a group it drains its queue and must read resultText."""
+
+    def __init__(self, writer: str, summary: dict, interner: Interner):
+        self.writer = writer
+        self.log = DocLog()
+        self.log.load_summary(summary, writer, interner)
+        self.queue = []
+        self.cur = 0
+
+    def _apply(self, m, interner):
+        self.log.message(m, interner)
+        self.cur = int(m["sequenceNumber"])
+
+    def feed(self, group, interner: Interner) -> None:
+        for m in group["msgs"]:
+            if m["clientId"] == self.writer:
+                while self.queue and m["referenceSequenceNumber"] > self.cur:
+                    self._apply(self.queue.pop(0), interner)
+                self.log.local_op(m["contents"], interner)
+            self.queue.append(m)
+        while self.queue:
+            self._apply(self.queue.pop(0), interner)
+
+
 def load_snapshots():
     with gzip.open(os.path.join(GOLDEN, "snapshots.json.gz"), "rt", encoding="utf-8") as fh:
         return json.load(fh)
