@@ -12,10 +12,12 @@ message handling the reference does on the JS thread:
 
 Property keys/values are interned into global tables (see include/mtr_types.h).  Remote annotates
 with a ``combiningOp`` are encoded per include/mtr_types.h (MTR_COMB_*); ``relativePos1/2`` become
-MTR_OP_RELPOS records resolved by the engine against the marker the id maps to.  Features outside the
-observer path (messages authored by the observer itself, combining results that are not plain JSON
-values, marker ids whose mapping depends on block-update order) make the document ``unsupported``
-(the reference-side shim keeps such documents on the TypeScript Client).
+MTR_OP_RELPOS records resolved by the engine against the marker the id maps to.  A client's own edits
+while collaborating are local ops (pending until acked) and its own sequenced messages become
+MTR_OP_ACK records (Client.applyMsg -> ackPendingSegment, client.ts:641-663, 866-869).  Features the
+engine does not build (local combining annotates, combining results that are not plain JSON values,
+marker ids whose mapping depends on block-update order) make the document ``unsupported`` (the
+reference-side shim keeps such documents on the TypeScript Client).
 """
 from __future__ import annotations
 
@@ -319,15 +321,19 @@ class DocLog:
     # message for it arrives (message() turns that into MTR_OP_ACK records)
     def local_insert(self, pos: int, spec: Any, interner: Interner) -> None:
         flags, p1, p2, pp = self._seg(spec, interner)
-        self.ops.append((abi.OP_LOCAL_INSERT, flags, 0, 0, 0, 0, pos, pp, p1, p2))
+        self.ops.append((abi.OP_LOCAL_INSERT, flags, 0, self._local_seq(), 0, 0, pos, pp, p1, p2))
+
+    def _local_seq(self) -> int:
+        """seq of a local op record: UnassignedSequenceNumber (-1) while collaborating (include/mtr_types.h)."""
+        return -1 if self.collaborating else 0
 
     def local_remove(self, start: int, end: int) -> None:
-        self.ops.append((abi.OP_LOCAL_REMOVE, 0, 0, 0, 0, 0, start, end, 0, 0))
+        self.ops.append((abi.OP_LOCAL_REMOVE, 0, 0, self._local_seq(), 0, 0, start, end, 0, 0))
 
     def local_annotate(self, start: int, end: int, props: dict, interner: Interner) -> None:
         if isinstance(props, dict) and "markerId" in props:
             self.marker_id_annotated = True
-        self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, 0, 0, 0, start, end, interner.propop(props), 0))
+        self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, self._local_seq(), 0, 0, start, end, interner.propop(props), 0))
 
     def local_op(self, op: dict, interner: Interner) -> None:
         """A local merge-tree op (the contents this client submits): insert / remove / annotate."""

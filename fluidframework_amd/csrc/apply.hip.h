@@ -59,7 +59,20 @@ constexpr uint32_t M_NL = 1u << 26;   // text leaf whose last unit is '\n' (Text
 constexpr uint32_t M_NLQ = 1u << 27;  // M_NL not known yet (left half of a split): read lazily by scour
 constexpr uint32_t M_NONL = 1u << 28; // the leaf's text holds no '\n' at all (so neither does any split half)
 constexpr uint32_t M_TOUCH = 1u << 29;  // transient: a delta segment of the current MTR_F_DELTA op
+constexpr uint32_t M_PEND = 1u << 30;   // the leaf belongs to pending local SegmentGroups (a list of cells by uid)
 constexpr uint32_t NS_UNDEF = 0, NS_FALSE = 1, NS_TRUE = 2;
+
+// The local-op path: a pending local insert keeps seq = LOCAL_BASE + localSeq and a pending
+// local remove removedSeq = LOCAL_BASE + localSeq -- above every sequence number (UnassignedSequenceNumber
+// is newer than anything sequenced: nodeLength / breakTie compare it that way, mergeTree.ts:935-1003,
+// 1719-1738), below RNONE.  Pending SegmentGroups live in a per-document ring of kPendRing entries
+// {localSeq, members so far, kind, prop-op}; a leaf's memberships are 2-word cells {next | kind << 24,
+// ring slot << 16 | ordinal in the group} in the remover arena, listed under key PEND_KEY | uid.
+constexpr int LOCAL_BASE = 0x40000000;
+constexpr int TIE_LOCAL = 0x7ffffffe;   // breakTie's newSeq of a local insert (Number.MAX_SAFE_INTEGER)
+constexpr int kPendRing = 256;
+constexpr uint32_t PEND_KEY = 0x40000000u;
+enum { PK_INSERT = 1, PK_REMOVE = 2, PK_ANNOTATE = 3 };
 
 constexpr uint32_t CL_LOCAL = 0xffu;      // LocalClientId (-1)
 constexpr uint32_t CL_NONCOLLAB = 0xfeu;  // NonCollabClient (-2)
@@ -124,7 +137,9 @@ struct DocHdr {
     int32_t op_cursor, fail_op, max_heap, texthalf;  // texthalf: active half of the text arena
     int32_t heap_need;  // LRU heap capacity the next launch must give this document (0 = none)
     int32_t dused;      // delta ranges recorded for the current batch
-    int32_t pad[2];
+    int32_t lseq;       // collabWindow.localSeq (mergeTreeNodes.ts:656)
+    int32_t phead, ptail;  // pending SegmentGroups: ring entries [phead, ptail) (MergeTree.pendingSegments)
+    int32_t pad[3];
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -179,6 +194,7 @@ struct KParams {
     mtr_op* gen_ops;             // == ops, writable
     uint16_t* gen_text;          // == btext, writable
     unsigned long long* prof;    // [P_COUNT] phase-timer sums (-DMTR_PROF builds)
+    uint32_t* pend;              // [doc][kPendRing][4] pending SegmentGroups (batches with local ops only)
 };
 
 // phase-timer slots (-DMTR_PROF builds)
@@ -190,7 +206,7 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
 // records, the batch's property tables), kept in LDS and read where used, so they never hold SGPRs
 // across the whole op loop (the loop's scalar state otherwise spills into VGPR lanes)
-enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_N };
+enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_HDR, CP_PEND, CP_N };
 
 // LDS-side scratch of one document: record-mode broadcast, cold pointers, phase timers
 struct Sc {
@@ -244,6 +260,8 @@ struct Doc {
     MTR_DI gptr<uint32_t> grt() const { return (gptr<uint32_t>)cold(CP_RT); }  // remover-head table
     MTR_DI gptr<uint32_t> gdelta() const { return (gptr<uint32_t>)cold(CP_DELTA); }  // mtr_delta records
     MTR_DI gptr<const uint32_t> tab(int k) const { return (gptr<const uint32_t>)cold(k); }
+    MTR_DI gptr<DocHdr> ghdr() const { return (gptr<DocHdr>)cold(CP_HDR); }      // this document's header
+    MTR_DI gptr<uint32_t> gpend() const { return (gptr<uint32_t>)cold(CP_PEND); }  // its pending-group ring
 };
 
 MTR_DI int bnd_of(uint32_t m) { return int((m & M_BND_MASK) >> M_BND_SHIFT); }
@@ -468,7 +486,8 @@ struct Eng {
         }
         // mergeTree.ts:967-1003
         const int seen = (removed & (inr != 0)) ? 0 : len;
-        const int r = vis ? seen : (removed ? -1 : 0);
+        // (a pending local remove is no removal here: removedSeq !== UnassignedSequenceNumber, :993-998)
+        const int r = vis ? seen : ((removed & (!X | (rseq < LOCAL_BASE))) ? -1 : 0);
         return (removed & (rseq <= v.ref)) ? -1 : r;
     }
     // 1 when client c is in leaf i's removedClientIds[1..] (the overlap list), for the lanes in `walk`
@@ -982,6 +1001,159 @@ struct Eng {
         }
     }
 
+    // ---- the local-op path (X instantiations only)
+    // head of leaf uid's pending-cell list (0xffffff = none); lane-parallel like rm_get / rm_set
+    static MTR_DI uint32_t pd_get(const D& L, uint32_t uid) { return rm_get(L, PEND_KEY | uid); }
+    static MTR_DI bool pd_set(const D& L, uint32_t uid, uint32_t head) { return rm_set(L, PEND_KEY | uid, head); }
+
+    // addToPendingList (mergeTree.ts:1324-1357) for leaf i (wave-uniform): a new SegmentGroup at the ring's
+    // tail when `slot` < 0, then the leaf joins it (segmentGroups.enqueue) with the group's next ordinal
+    static MTR_DI int pend_add(D& L, const KParams& P, St& s, int i, int slot, int kind, uint32_t pp, int lseq) {
+        const gptr<DocHdr> h = L.ghdr();
+        const gptr<uint32_t> ring = L.gpend();
+        if (!ring) {
+            s.status = MTR_ERR_CAPACITY;
+            return -1;
+        }
+        if (slot < 0) {
+            const int head = uni(h->phead), tail = uni(h->ptail);
+            if (tail - head >= kPendRing) {
+                s.status = MTR_ERR_CAPACITY;
+                return -1;
+            }
+            slot = tail % kPendRing;
+            if (lane_id() == 0) {
+                ring[4 * slot] = uint32_t(lseq);
+                ring[4 * slot + 1] = 0;
+                ring[4 * slot + 2] = uint32_t(kind);
+                ring[4 * slot + 3] = pp;
+                h->ptail = tail + 1;
+            }
+            wsync();
+        }
+        const int ord = int(uniu(ring[4 * slot + 1]));
+        if (s.rmused + 2 > P.rcap || ord > 0xffff) {
+            s.status = MTR_ERR_CAPACITY;
+            return slot;
+        }
+        const uint32_t u = uniu(L.uid[i]);
+        const uint32_t m = uniu(L.meta[i]);
+        const uint32_t c = uint32_t(s.rmused);
+        bool ok = true;
+        if (lane_id() == 0) {
+            const uint32_t nxt = (m & M_PEND) ? pd_get(L, u) : 0xffffffu;
+            L.grm()[c] = (nxt & 0xffffffu) | (uint32_t(kind) << 24);
+            L.grm()[c + 1] = (uint32_t(slot) << 16) | uint32_t(ord);
+            ring[4 * slot + 1] = uint32_t(ord + 1);
+            ok = pd_set(L, u, c);
+            L.meta[i] = m | M_PEND;
+        }
+        if (__ballot(!ok)) s.status = MTR_ERR_CAPACITY;
+        s.rmused += 2;
+        wsync();
+        return slot;
+    }
+
+    // the leaves a local remove / annotate touched (marked M_TOUCH by range_walk), in leaf (= walk)
+    // order, join one new group (none when no leaf was touched: no group is created)
+    static MTR_DI void pend_touched(D& L, const KParams& P, St& s, int kind, uint32_t pp, int lseq) {
+        int slot = -1;
+        for (int base = 0; base < s.nseg && s.status == MTR_OK; base += 64) {
+            const int i = base + lane_id();
+            const uint32_t m = L.meta[min(i, s.nseg - 1)];
+            const bool t = i < s.nseg && (m & M_TOUCH);
+            uint64_t tm = __ballot(t);
+            if (t) L.meta[i] = m & ~M_TOUCH;
+            wsync();
+            for (; tm && s.status == MTR_OK; tm &= tm - 1)
+                slot = pend_add(L, P, s, base + first_lane(tm), slot, kind, pp, lseq);
+        }
+    }
+
+    // splitAt's segmentGroups.copyTo (segmentGroupCollection.ts:47-62): the right half r (a copy of the
+    // left half's meta, M_PEND included) joins every group of the left half, each with its next ordinal
+    static MTR_DI void pend_copy(D& L, const KParams& P, St& s, uint32_t left_uid, int r) {
+        uint32_t c = uniu(lane_id() == 0 ? pd_get(L, left_uid) : 0u);
+        c = uniu(c);
+        if (lane_id() == 0) L.meta[r] = L.meta[r] & ~M_PEND;
+        wsync();
+        while (c != 0xffffffu && s.status == MTR_OK) {
+            const uint32_t w0 = uniu(L.grm()[c]), w1 = uniu(L.grm()[c + 1]);
+            pend_add(L, P, s, r, int(w1 >> 16), int(w0 >> 24), 0, 0);
+            c = w0 & 0xffffffu;
+        }
+    }
+
+    // one of a leaf's pending annotates holds `key` (PropertiesManager.pendingKeyUpdateCount[key] defined)
+    static MTR_DI bool key_pending(const D& L, uint32_t c, uint32_t key) {
+        const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV);
+        const gptr<uint32_t> ring = L.gpend();
+        while (c != 0xffffffu) {
+            const uint32_t w0 = L.grm()[c], w1 = L.grm()[c + 1];
+            if ((w0 >> 24) == PK_ANNOTATE) {
+                const uint32_t pp = ring[4 * (w1 >> 16) + 3];
+                for (uint32_t q = poff[pp]; q < poff[pp + 1]; q++)
+                    if (pkv[2 * q] == key) return true;
+            }
+            c = w0 & 0xffffffu;
+        }
+        return false;
+    }
+
+    // MergeTree.ackPendingSegment (mergeTree.ts:1283-1322) with BaseSegment.ack (mergeTreeNodes.ts:439-479)
+    // for one member op of this client's sequenced message (type: its MergeTreeDeltaType)
+    static MTR_DI void ack(D& L, St& s, int type, int seq) {
+        const gptr<DocHdr> h = L.ghdr();
+        const gptr<uint32_t> ring = L.gpend();
+        const int head = uni(h->phead), tail = uni(h->ptail);
+        if (head == tail || !ring) return;  // pendingSegments.shift() is undefined
+        const int slot = head % kPendRing;
+        const int cnt = int(uniu(ring[4 * slot + 1]));
+        if (lane_id() == 0) h->phead = head + 1;
+        // the group's members: each leaf holding a cell of this slot drops it; E[ordinal] = leaf
+        for (int base = 0; base < s.nseg; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, s.nseg - 1);
+            const uint32_t m = L.meta[ic];
+            if (i < s.nseg && (m & M_PEND)) {
+                const uint32_t u = L.uid[i];
+                uint32_t c = pd_get(L, u), prev = 0xffffffu, nlive = 0;
+                while (c != 0xffffffu) {
+                    const uint32_t w0 = L.grm()[c], w1 = L.grm()[c + 1];
+                    const uint32_t nx = w0 & 0xffffffu;
+                    if (int(w1 >> 16) == slot) {
+                        L.E[int(w1 & 0xffffu)] = i;
+                        if (prev == 0xffffffu) pd_set(L, u, nx);
+                        else L.grm()[prev] = (L.grm()[prev] & 0xff000000u) | nx;
+                    } else {
+                        prev = c;
+                        nlive++;
+                    }
+                    c = nx;
+                }
+                if (!nlive) L.meta[i] = m & ~M_PEND;
+            }
+        }
+        wsync();
+        for (int o = 0; o < cnt && s.status == MTR_OK; o++) {  // in group order
+            const int i = uni(L.E[o]);
+            if (type == MTR_OP_INSERT) {
+                if (uni(L.seq[i]) < LOCAL_BASE) s.status = MTR_ERR_ASSERT | 0x045;  // seq already assigned
+                else if (lane_id() == 0) L.seq[i] = seq;
+            } else if (type == MTR_OP_REMOVE) {
+                const int rs = uni(L.rseq[i]);
+                if (rs == RNONE) s.status = MTR_ERR_ASSERT | 0x046;  // missing removal info
+                else if (rs >= LOCAL_BASE && lane_id() == 0) L.rseq[i] = seq;
+            } else if (type != MTR_OP_ANNOTATE) {
+                s.status = MTR_ERR_BAD_OP;
+            }
+            wsync();
+            int bs, be;
+            block_bounds1(L, s, i, bs, be);
+            add_lru_block(L, s, bs, uniu(L.uid[i]), seq);  // mergeTree.ts:1299-1301
+        }
+    }
+
     // ---- properties (PropertiesManager.addProperties without combining ops,
     //      segmentPropertiesManager.ts:60-157; JS own-key order).  Entry: [n, k0, v0, k1, v1, ...]
     struct PropRes {
@@ -989,9 +1161,11 @@ struct Eng {
         int propused, status;
     };
         // (out of line: rare, and inlining it costs the replay kernels 2.5 % at C3)
+    // pl: the leaf's pending-cell list (0xffffff = none): keys a pending local annotate holds are left
+    // alone unless a combining op other than rewrite applies (shouldModifyKey, segmentPropertiesManager.ts:94-104)
     static __device__ __attribute__((noinline)) PropRes props_apply_serial(const D& L, const KParams& P, int propused,
                                                                          uint32_t old, uint32_t pp,
-                                             uint32_t comb) {
+                                             uint32_t comb, uint32_t pl = 0xffffffu) {
         PropRes r{old, propused, MTR_OK};
         const gptr<uint32_t> gprop = L.gprop();
         const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX),
@@ -1021,7 +1195,7 @@ struct Eng {
                         keep = nv != MTR_NULL_VALUE && !(uniu(veq[nv]) & MTR_VEQ_FALSY);
                         break;
                     }
-                if (keep) {
+                if (keep || (pl != 0xffffffu && key_pending(L, pl, key))) {
                     e[1 + 2 * w] = key;
                     e[2 + 2 * w] = val;
                     w++;
@@ -1032,6 +1206,7 @@ struct Eng {
         for (uint32_t q = lo; q < hi; q++) {
             const uint32_t key = uniu(pkv[2 * q]);
             uint32_t val = uniu(pkv[2 * q + 1]);
+            if (pl != 0xffffffu && mode < MTR_COMB_INCR && key_pending(L, pl, key)) continue;
             int at = -1;
             for (uint32_t k = 0; k < n; k++)
                 if (uniu(e[1 + 2 * k]) == key) {
@@ -1410,6 +1585,11 @@ struct Eng {
                 const uint32_t m = rdlane(vm, t);
                 if (k > cs && bnd_of(m) >= 1) prev = -1;  // next child block
                 if (m & M_DEL) continue;
+                if (X && (m & M_PEND)) {  // segmentGroups not empty: held (zamboni.ts:128, 185-188)
+                    kept++;
+                    prev = -1;
+                    continue;
+                }
                 const int rs = rdlane(vr, t);
                 if (rs != RNONE) {
                     if (rs > minseq) {
@@ -1480,7 +1660,8 @@ struct Eng {
         const int vr = in ? vr0 : RNONE, vl = in ? vl0 : 0;
         const bool pre = (vm & M_DEL) != 0;
         const bool removed = vr != RNONE;
-        const bool cand = !pre & !removed & (vs <= minseq) & (vl > 0);
+        const bool held = X && (vm & M_PEND) != 0;  // in a pending SegmentGroup: kept (zamboni.ts:128, 185-188)
+        const bool cand = !pre & !removed & !held & (vs <= minseq) & (vl > 0);
         {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
             const bool q = cand & !PM & ((vm & (M_NLQ | M_MARKER)) == M_NLQ);
             if (__ballot(q)) {
@@ -1520,7 +1701,7 @@ struct Eng {
         }
         link = link & !((vp == pp) & pset_never(vp));  // a shared set holding a never-equal value
         if (!PM && __ballot(link & (vl > kGranularity))) return -1;
-        const bool unlink = !pre & removed & (vr <= minseq);
+        const bool unlink = !pre & removed & !held & (vr <= minseq);
         const uint64_t lm = __ballot(link);
         if (unlink | link) L.meta[i] = vm | M_DEL;
         if (PM) {  // UNLINK frees the segment's handles, in leaf order
@@ -1721,7 +1902,7 @@ struct Eng {
     // ------------------------------------------------------------ boundary / insert
     // ensureIntervalBoundary (mergeTree.ts:1706-1716) on the current scan arrays: split the leaf
     // holding pos at an offset > 0; the two halves' scan entries are set in place.
-    static MTR_DI void split_at(D& L, St& s, int pos) {
+    static MTR_DI void split_at(D& L, const KParams& P, St& s, int pos) {
         PROF(P_SPLIT);
         const int S = s.nseg;
         const int i = lower_bound_E(L, s, pos);
@@ -1771,6 +1952,7 @@ struct Eng {
             L.E[j] = e - v + off;
             L.E[r] = e;
             wsync();
+            if (X && (m0 & M_PEND)) pend_copy(L, P, s, uniu(rdlane(uj, jl)), r);
             s.nseg++;
             overflow_fix(L, s, r);
         }
@@ -1779,8 +1961,10 @@ struct Eng {
     // insertSegments/blockInsert/insertingWalk with onLeaf (mergeTree.ts:1397-1427, 1594-1685),
     // on the current scan arrays.  `pre`: lane t holds unit t of the op's text in `pf`
     // (prefetched during the previous op).
+    // seq: breakTie's newSeq; sseq: the seq the new leaf keeps (LOCAL_BASE + localSeq for a pending local
+    // insert, which passes lseq > 0 and joins a new SegmentGroup)
     static MTR_DI int insert_at(D& L, const KParams& P, St& s, const View& v, const mtr_op& op, int pos, int seq,
-                                uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf) {
+                                uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf, int sseq, int lseq) {
         PROF(P_INSERT);
         const bool marker = (op.flags & MTR_F_MARKER) != 0;
         const int len = marker ? 1 : int(op.payload2);
@@ -1821,6 +2005,7 @@ struct Eng {
         }
         const int S = s.nseg;
         int slot = -1, inherit = 0;
+        bool nocand = false;  // no leaf of the block took the insert: it goes at the block's end
         uint32_t om = 0;  // meta of the leaf that starts the block when the new leaf takes its place
         bool om_known = false;
         int wbs = -1, wbe = -1;  // the leaf block around the slot, when the window saw both ends
@@ -1852,6 +2037,7 @@ struct Eng {
                         const uint64_t cm = __ballot((ln >= 31) & (w < be) & (vw >= 0) &
                                                      ((ew > pos) | ((vw == 0) & (seq > sw))));
                         slot = cm ? i - 31 + first_lane(cm) : be;
+                        nocand = !cm;
                         inherit = slot == bs ? 1 : 0;
                         wbs = bs;
                         wbe = be + 1;  // the block after the insert
@@ -1870,10 +2056,42 @@ struct Eng {
                         }
                         const uint64_t cm = __ballot(c);
                         slot = cm ? i + first_lane(cm) : be;
+                        nocand = !cm;
                         inherit = slot == bs ? 1 : 0;
                     }
                 }
             }
+        }
+        if (X && nocand && slot >= 0 && slot < S && s.collab && !v.local && uni(L.seq[slot]) >= LOCAL_BASE) {
+            // insertingWalk's continuePredicate (mergeTree.ts:1611-1615, 1815-1828): the first segment after
+            // the block is an unacked local one, so a remote insert walks on into the following leaf
+            // blocks at position 0 (pending segments are 0 long and lose breakTie to it)
+            int b0 = slot;
+            for (;;) {
+                const int b1 = block_end(L, s, b0, 1);
+                const int j = b0 + ln;
+                bool c = false;
+                if (j < b1) {
+                    const int ej = L.E[j];
+                    const int vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
+                    c = vj >= 0 && ((ej & EMASK) > pos || (vj == 0 && seq > L.seq[j]));
+                }
+                const uint64_t cm = __ballot(c);
+                if (cm) {
+                    slot = b0 + first_lane(cm);
+                    inherit = slot == b0 ? 1 : 0;
+                    break;
+                }
+                if (b1 < S && uni(L.seq[b1]) >= LOCAL_BASE && uni(L.seq[b1]) != RNONE) {
+                    b0 = b1;
+                    continue;
+                }
+                slot = b1;
+                inherit = 0;
+                break;
+            }
+            om_known = false;
+            wbs = wbe = -1;
         }
         if (slot < 0) return -1;
         shift_right1(L, s, slot);
@@ -1891,7 +2109,7 @@ struct Eng {
             L.meta[slot + 1] = set_ns(set_bnd(om, 0), NS_UNDEF);
         }
         L.len[slot] = len;
-        L.seq[slot] = seq;
+        L.seq[slot] = sseq;
         L.rseq[slot] = RNONE;
         L.meta[slot] = m;
         // PermutationSegment: start reset to unallocated on INSERT (permutationvector.ts:354-361) -- not for a
@@ -1914,6 +2132,7 @@ struct Eng {
         // saveIfLocal (mergeTree.ts:1618-1637): remote segments above minSeq go to the LRU
         if (op.flags & MTR_F_APPEND) set_merge_info(L, P, s, slot, op, dd);
         if (s.collab && !v.local && seq > s.minseq) add_lru_block(L, s, xbs, uint32_t(s.uidnext - 1), seq);
+        if (X && lseq > 0) pend_add(L, P, s, slot, -1, PK_INSERT, 0, lseq);  // saveIfLocal, mergeTree.ts:1618-1626
         return slot;
     }
 
@@ -2016,7 +2235,10 @@ struct Eng {
     // visible length > 0 inside [start, end), on the current scan arrays, 64 leaves per round.
     // The walk stops at the first leaf whose view start (E - max(V,0), nondecreasing) is >= end.
     static MTR_DI void range_walk(D& L, const KParams& P, St& s, const View& v, int start, int end, int seq,
-                                  uint32_t client, int is_remove, uint32_t pp, uint32_t comb, bool dl) {
+                                  uint32_t client, int is_remove, uint32_t pp, uint32_t comb, bool dl,
+                                  bool pending = false) {
+        // (pending: a local op while collaborating -- its leaves are marked M_TOUCH for pend_touched and
+        // every key applies; remote ops leave keys with pending local updates alone)
         PROF(P_RANGE);
         if (end == start) return;
         const int S = s.nseg;
@@ -2038,8 +2260,11 @@ struct Eng {
             if (am) {
                 if (is_remove) {
                     const int rs = act ? rj : RNONE;
-                    const bool ov = act && rs != RNONE;  // overlapping remove: removedClientIds.push
-                    const uint64_t om = __ballot(ov);
+                    // a pending local remove a remote remove overtakes: removedClientIds.unshift(client),
+                    // removedSeq = seq (mergeTree.ts:1976-1987)
+                    const bool pr = X && act && rs != RNONE && rs >= LOCAL_BASE;
+                    const bool ov = act && rs != RNONE && !pr;  // overlapping remove: removedClientIds.push
+                    const uint64_t om = __ballot(ov | pr);
                     const int nov = __popcll(om);
                     if (s.rmused + nov > P.rcap) {
                         s.status = MTR_ERR_CAPACITY;
@@ -2054,6 +2279,20 @@ struct Eng {
                         full = !rm_set(L, uj, cell);
                         mj |= M_OVERLAP;
                         L.meta[j] = mj;
+                    } else if (pr) {  // the old first remover becomes removedClientIds[1]: the oldest cell
+                        const uint32_t cell = uint32_t(s.rmused + __popcll(om & lanes_below()));
+                        const uint32_t uj = L.uid[j];
+                        L.grm()[cell] = (((mj >> M_FREM_SHIFT) & 0xffu) << 24) | 0xffffffu;
+                        uint32_t t = (mj & M_OVERLAP) ? rm_get(L, uj) : 0xffffffu;
+                        if (t == 0xffffffu) {
+                            full = !rm_set(L, uj, cell);
+                        } else {
+                            while ((L.grm()[t] & 0xffffffu) != 0xffffffu) t = L.grm()[t] & 0xffffffu;
+                            L.grm()[t] = (L.grm()[t] & 0xff000000u) | cell;
+                        }
+                        L.rseq[j] = seq;
+                        mj = (mj & ~(0xffu << M_FREM_SHIFT)) | (client << M_FREM_SHIFT) | M_OVERLAP;
+                        L.meta[j] = mj;
                     } else if (act) {
                         L.rseq[j] = seq;
                         mj = (mj & ~(0xffu << M_FREM_SHIFT) & ~M_OVERLAP) | (client << M_FREM_SHIFT);
@@ -2066,11 +2305,25 @@ struct Eng {
                     // one new property set per distinct old set in the round (memoized addProperties)
                     const uint32_t old = act ? L.props[j] : 0u;
                     uint64_t pend = am;
+                    if (X && !pending) {  // leaves with pending local annotates: one filtered set each
+                        uint64_t pm = __ballot(act && (mj & M_PEND));
+                        pend &= ~pm;
+                        for (; pm; pm &= pm - 1) {
+                            const int l = first_lane(pm);
+                            const uint32_t pl = uniu(pd_get(L, uniu(L.uid[base + l])));
+                            const PropRes r = props_apply_serial(L, P, s.propused, rdlane(old, l), pp, comb, pl);
+                            s.propused = uni(r.propused);
+                            if (uni(r.status) != MTR_OK) s.status = uni(r.status);
+                            if (ln == l) L.props[j] = uniu(r.dst);
+                            wsync();
+                        }
+                    }
                     while (pend) {
                         const uint32_t o = rdlane(old, first_lane(pend));
-                        const uint64_t sel = __ballot(act && old == o);
+                        const bool mine = act && old == o && (!X || ((pend >> ln) & 1));
+                        const uint64_t sel = __ballot(mine);
                         const uint32_t nw = props_apply(L, P, s, o, pp, comb);
-                        if (act && old == o) L.props[j] = nw;
+                        if (mine) L.props[j] = nw;
                         pend &= ~sel;
                     }
                     if (dl && act) {  // every annotated segment is a delta segment
@@ -2301,6 +2554,8 @@ struct Eng {
             L.sc->cp[CP_PKV] = (unsigned long long)P.propop_kv;
             L.sc->cp[CP_KIX] = (unsigned long long)P.key_index;
             L.sc->cp[CP_VEQ] = (unsigned long long)P.val_eq;
+            L.sc->cp[CP_HDR] = (unsigned long long)(P.hdr + d);
+            L.sc->cp[CP_PEND] = (unsigned long long)(P.pend ? P.pend + size_t(d) * kPendRing * 4 : nullptr);
         }
         wsync();
     }
@@ -2387,6 +2642,10 @@ struct Eng {
             int need = 0;
             if (op.type == MTR_OP_INSERT) need = 1;
             else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) need = min(max(pos2 - pos1, 0), s.nseg + 2);
+            else if (X && op.type == MTR_OP_ACK && L.gpend()) {  // one push per member at most
+                const int hd = uni(L.ghdr()->phead);
+                if (hd != uni(L.ghdr()->ptail)) need = min(int(uniu(L.gpend()[4 * (hd % kPendRing) + 1])), s.nseg + 2);
+            }
             if (need && s.heapn + need + 1 >= L.lhcap) {
                 s.heap_need = s.heapn + need + 2;
                 return false;
@@ -2424,18 +2683,28 @@ struct Eng {
         int zop = 0;
         View v;
         int seq = op.seq;
+        int sseq = 0, lseq = 0;  // the seq an inserted leaf keeps; localSeq of a pending local op
         uint32_t client = enc_client(int(int16_t(op.client)));
         if (local_op) {
-            if (s.collab) {
-                s.status = MTR_ERR_UNSUPPORTED;
-                s.fail_op = gidx;
-                return false;
-            }
             v.ref = s.curseq;
-            v.client = CL_LOCAL;
             v.local = 1;
-            seq = 0;
-            client = CL_LOCAL;
+            if (s.collab) {  // a pending local op (seq = UnassignedSequenceNumber, the local client)
+                if (!X || (op.type == MTR_OP_LOCAL_ANNOTATE && op.payload2 != 0)) {
+                    s.status = MTR_ERR_UNSUPPORTED;  // (pending combining annotates: not built)
+                    s.fail_op = gidx;
+                    return false;
+                }
+                lseq = uni(L.ghdr()->lseq) + 1;  // ++collabWindow.localSeq (mergeTree.ts:1407, 1909, 1970)
+                if (lane_id() == 0) L.ghdr()->lseq = lseq;
+                v.client = uint32_t(s.local);
+                client = uint32_t(s.local);
+                seq = TIE_LOCAL;
+                sseq = LOCAL_BASE + lseq;
+            } else {
+                v.client = CL_LOCAL;
+                seq = 0;
+                client = CL_LOCAL;
+            }
         } else {
             // a snapshot body append walks at (UniversalSequenceNumber, segment client)
             v.ref = (op.flags & MTR_F_APPEND) ? 0 : op.ref_seq;
@@ -2450,9 +2719,9 @@ struct Eng {
                 int pos = pos1;
                 if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
                 prefix(L, s, v, P.new_length_calc);
-                split_at(L, s, pos);
-                insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf);
-                zop = s.collab;
+                split_at(L, P, s, pos);
+                insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf, lseq ? sseq : seq, lseq);
+                zop = s.collab && !local_op;
                 break;
             }
             case MTR_OP_REMOVE:
@@ -2461,14 +2730,28 @@ struct Eng {
             case MTR_OP_LOCAL_ANNOTATE: {
                 const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
                 prefix(L, s, v, P.new_length_calc);
-                split_at(L, s, pos1);
-                split_at(L, s, pos2);
-                range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
-                           op.type == MTR_OP_ANNOTATE ? op.payload2 : 0u, DL && !PM && (op.flags & MTR_F_DELTA) != 0);
-                zop = s.collab;
+                split_at(L, P, s, pos1);
+                split_at(L, P, s, pos2);
+                if (X && lseq) {  // pending: removedSeq = LOCAL_BASE + localSeq; the touched leaves join a group
+                    range_walk(L, P, s, v, pos1, pos2, sseq, client, is_remove, op.payload, 0u, true, true);
+                    if (s.status == MTR_OK)
+                        pend_touched(L, P, s, is_remove ? PK_REMOVE : PK_ANNOTATE, is_remove ? 0u : op.payload, lseq);
+                } else {
+                    range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
+                               op.type == MTR_OP_ANNOTATE ? op.payload2 : 0u, DL && !PM && (op.flags & MTR_F_DELTA) != 0);
+                }
+                zop = s.collab && !local_op;
                 break;
             }
             case MTR_OP_SEQ:
+                break;
+            case MTR_OP_ACK:  // Client.applyMsg of this client's own message (client.ts:866-869)
+                if (!X || !s.collab) {
+                    s.status = MTR_ERR_BAD_OP;
+                    break;
+                }
+                ack(L, s, int(op.payload2), op.seq);
+                zop = 1;  // ackPendingSegment ends with zamboniSegments (mergeTree.ts:1318-1320)
                 break;
             case MTR_OP_HANDLES: {  // HandleTable.load (handletable.ts:88): handles = the summary's array
                 const int n = op.pos1;
@@ -2653,8 +2936,8 @@ struct Eng {
             if (t != uint32_t(MTR_HANDLE_UNALLOCATED))  // already has a handle: segment.start + offset
                 return int(t) + pos - (i > 0 ? (uni(L.E[i - 1]) & EMASK) : 0);
         }
-        if (pos) split_at(L, s, pos);
-        split_at(L, s, pos + 1);
+        if (pos) split_at(L, P, s, pos);
+        split_at(L, P, s, pos + 1);
         const int i = lower_bound_E(L, s, pos + 1);
         const int h = alloc_handle(L, P, s);
         if (s.status != MTR_OK) return -1;

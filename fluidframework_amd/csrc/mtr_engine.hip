@@ -102,6 +102,9 @@ struct mtr_engine {
     std::vector<uint64_t> h_doff;
     bool has_delta = false;
     bool has_ext = false;             // the batch holds rare records (op_scan_kernel): no fixed-capacity kernels
+    bool pend_seen = false;           // a batch since mtr_reset held local ops while collaborating or acks:
+                                      // documents may hold pending segments, so every launch is an X kernel
+    DevBuf<uint32_t> pend;            // [doc][kPendRing][4] pending SegmentGroups (allocated on first use)
     DevBuf<int32_t> red;              // small reduction / query-result buffer
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
@@ -160,19 +163,22 @@ __global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_
 // any op of the batch flagged MTR_F_DELTA (the host sizes delta buffers only when one is)
 // bit 0: an op flagged MTR_F_DELTA (the host sizes delta buffers only then); bit 1: a rare record the
 // fixed-capacity kernels do not carry (Eng::X: relative positions, handle-table loads, combining
-// annotates, marker ordinals)
+// annotates, marker ordinals); bit 2: the local-op path (MTR_OP_ACK, or a local op recorded while
+// collaborating: seq = UnassignedSequenceNumber)
 __global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    bool any = false, ext = false;
+    bool any = false, ext = false, pend = false;
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const mtr_op op = ops[i];
         any = any || (op.flags & MTR_F_DELTA) != 0;
+        pend = pend || op.type == MTR_OP_ACK ||
+               (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE && op.seq == -1);
         ext = ext || op.type == MTR_OP_RELPOS || op.type == MTR_OP_HANDLES || (op.flags & MTR_F_REL) ||
               (op.type == MTR_OP_ANNOTATE && op.payload2 != 0) ||
               ((op.flags & MTR_F_MARKER) && op.payload2 != 0 &&
                (op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT || op.type == MTR_OP_LOAD));
     }
-    const int bits = (__ballot(any) ? 1 : 0) | (__ballot(ext) ? 2 : 0);
+    const int bits = (__ballot(any) ? 1 : 0) | (__ballot(ext) ? 2 : 0) | (__ballot(pend) ? 4 : 0);
     if (bits && (threadIdx.x & 63) == 0) atomicOr(out, bits);
 }
 
@@ -312,6 +318,7 @@ int mtr_engine_destroy(mtr_engine* e) {
                     &e->val_off, &e->val_eq, &e->client_off})
         b->release();
     e->hdr.release();
+    e->pend.release();
     e->text.release();
     e->btext.release();
     e->docs.release();
@@ -363,6 +370,7 @@ int mtr_reset(mtr_engine* e) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync(e->stat.p, 0, e->stat.n * sizeof(unsigned long long), e->stream));
     e->summarized = false;
+    e->pend_seen = false;
     return MTR_OK;
 }
 
@@ -411,7 +419,14 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
         HIPCHK(hipStreamSynchronize(e->stream));
         any = (flag & 1) != 0;
         e->has_ext = (flag & 2) != 0;
+        if (flag & 4) {
+            if (!e->pend.p) {
+                if (e->pend.ensure(size_t(std::max<uint32_t>(e->max_docs, 1)) * kPendRing * 4)) return -1;
+            }
+            e->pend_seen = true;
+        }
     }
+    e->has_ext = e->has_ext || e->pend_seen;
     if (any) {
         std::vector<uint64_t> need(b->n_docs, 0);
         for (uint32_t d = 0; d < b->n_docs; d++) {
@@ -531,6 +546,7 @@ static int run_impl(mtr_engine* e, int gen) {
     P.doff = e->has_delta ? e->doff.p : nullptr;
     P.dkind = e->dkind.p;
     P.dpart = e->dpart.p;
+    P.pend = e->pend.p;
     P.gen = gen;
 #ifdef MTR_PROF
     if (!e->prof.p) {

@@ -234,7 +234,7 @@ MTR_DI int legacy_vis(const SDoc& D, int len, int rs, uint32_t m, int sq) {
     }
     if (rem && rs <= ref) return -1;
     if (cl == CL_NONCOLLAB || sq <= ref) return len;
-    if (rem) return -1;
+    if (rem && rs < LOCAL_BASE) return -1;  // a pending local remove: removedSeq === Unassigned (:993-998)
     return 0;
 }
 
@@ -242,7 +242,8 @@ MTR_DI int legacy_vis(const SDoc& D, int len, int rs, uint32_t m, int sq) {
 MTR_DI int leaf_kind(const SDoc& D, int v1, int len, int rs, uint32_t m, int sq) {
     const bool rem = rs != RNONE;
     if (v1) {  // snapshotV1.ts:180-298
-        if (rem && rs <= D.minseq) return 0;
+        // unacked inserts are elided, and so are pending removes (removedSeq -1 <= minSeq, :211)
+        if ((rem && (rs <= D.minseq || rs >= LOCAL_BASE)) || sq >= LOCAL_BASE) return 0;
         if (sq <= D.minseq && !rem) return 1;
         return 2;
     }

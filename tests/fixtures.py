@@ -84,14 +84,15 @@ class Perspective:
         self.log.message(m, interner)
         self.cur = int(m["sequenceNumber"])
 
-    def feed(self, group, interner: Interner) -> None:
-        for m in group["msgs"]:
+    def feed(self, group, interner: Interner, lo: int = 0, hi: int | None = None, drain: bool = True) -> None:
+        """Messages [lo, hi) of the group; drain = the group ends here (apply everything queued)."""
+        for m in group["msgs"][lo:hi]:
             if m["clientId"] == self.writer:
                 while self.queue and m["referenceSequenceNumber"] > self.cur:
                     self._apply(self.queue.pop(0), interner)
                 self.log.local_op(m["contents"], interner)
             self.queue.append(m)
-        while self.queue:
+        while drain and self.queue:
             self._apply(self.queue.pop(0), interner)
 
 
