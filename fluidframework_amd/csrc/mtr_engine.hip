@@ -1148,22 +1148,91 @@ static int fetch_doc(mtr_engine* e, uint32_t doc, HostDoc& hd) {
     return 0;
 }
 
-int64_t mtr_get_text(mtr_engine* e, uint32_t doc, uint16_t* out, int64_t cap) {
-    HostDoc hd;
-    if (doc >= e->max_docs || fetch_doc(e, doc, hd)) return -1;
-    const size_t sc = e->caps.max_segments;
-    int64_t n = 0;
-    for (int i = 0; i < hd.h.nseg; i++) {
-        const uint32_t m = hd.seg[F_META * sc + i];
-        const int32_t rs = int32_t(hd.seg[F_RSEQ * sc + i]);
-        if (rs != RNONE || (m & M_MARKER)) continue;  // local view: removed segments are not visible
-        const uint32_t len = hd.seg[F_LEN * sc + i], t = hd.seg[F_TEXT * sc + i];
-        for (uint32_t k = 0; k < len; k++) {
-            if (out && n < cap) out[n] = hd.text[t + k];
-            n++;
+// MergeTreeTextHelper.getText (MergeTreeTextHelper.ts:20-81) at the local view, on the device: one wave
+// per document [lo, lo + gridDim.x) walks its leaves 64 at a time (text segments that are not removed;
+// markers add nothing), an add-scan places each leaf's units, and the wave copies them leaf by leaf
+// (coalesced runs from the document's text arena).  Pass 1 (out == nullptr) writes the lengths to
+// lens[doc - lo]; pass 2 writes the units at off[doc - lo].
+__global__ void __launch_bounds__(NT) text_kernel(const DocHdr* hdr, const uint32_t* seg, const uint16_t* text,
+                                                  int segcap, int tcap, uint32_t lo, int64_t* lens,
+                                                  const int64_t* off, uint16_t* out) {
+    const uint32_t d = lo + blockIdx.x;
+    const int S = __builtin_amdgcn_readfirstlane(hdr[d].nseg);
+    const int ln = threadIdx.x;
+    const uint32_t* g = seg + size_t(d) * NF * segcap;
+    const uint16_t* tx = text + size_t(d) * tcap;
+    int64_t carry = out ? off[blockIdx.x] : 0;
+    for (int base = 0; base < S; base += 64) {
+        const int i = base + ln;
+        int len = 0;
+        uint32_t t = 0;
+        if (i < S && int(g[F_RSEQ * segcap + i]) == RNONE && !(g[F_META * segcap + i] & M_MARKER)) {
+            len = int(g[F_LEN * segcap + i]);
+            t = g[F_TEXT * segcap + i];
         }
+        const int inc = wave_incl_scan(len);
+        if (out) {
+            const int n = min(64, S - base);
+            for (int l = 0; l < n; l++) {
+                const int ll = __builtin_amdgcn_readlane(len, l);
+                const uint32_t tl = uint32_t(__builtin_amdgcn_readlane(int(t), l));
+                const int64_t o = carry + __builtin_amdgcn_readlane(inc, l) - ll;
+                for (int k = ln; k < ll; k += 64) out[o + k] = tx[tl + k];
+            }
+        }
+        carry += __builtin_amdgcn_readlane(inc, 63);
     }
-    return n;
+    if (!out && ln == 0) lens[blockIdx.x] = carry;
+}
+
+// texts of documents [lo, hi): out = the concatenated units, doc_off[i] = start of document lo + i
+// (doc_off[hi - lo] = total); returns the total (nothing written when out is NULL), -1 when cap is
+// too small or on error
+int64_t mtr_get_texts(mtr_engine* e, uint32_t lo, uint32_t hi, uint16_t* out, int64_t cap, int64_t* doc_off) {
+    HIPCHK(hipSetDevice(e->device));
+    if (hi > e->max_docs || lo > hi) {
+        set_err("mtr_get_texts: bad document range");
+        return -1;
+    }
+    const uint32_t n = hi - lo;
+    if (doc_off) doc_off[0] = 0;
+    if (n == 0) return 0;
+    DevBuf<int64_t> lens, offs;
+    if (lens.ensure(n) || offs.ensure(size_t(n) + 1)) return -1;
+    text_kernel<<<n, NT, 0, e->stream>>>(e->hdr.p, e->seg.p, e->text.p, int(e->caps.max_segments),
+                                         int(e->caps.text_units), lo, lens.p, nullptr, nullptr);
+    HIPCHK(hipGetLastError());
+    std::vector<int64_t> hl(n), ho(size_t(n) + 1, 0);
+    HIPCHK(hipMemcpyAsync(hl.data(), lens.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (uint32_t i = 0; i < n; i++) ho[i + 1] = ho[i] + hl[i];
+    const int64_t total = ho[n];
+    if (doc_off) std::copy(ho.begin(), ho.end(), doc_off);
+    if (!out || total == 0) return total;
+    if (total > cap) {
+        set_err("mtr_get_texts: output buffer too small");
+        return -1;
+    }
+    DevBuf<uint16_t> dev;
+    if (dev.ensure(size_t(total))) return -1;
+    HIPCHK(hipMemcpyAsync(offs.p, ho.data(), (size_t(n) + 1) * sizeof(int64_t), hipMemcpyHostToDevice, e->stream));
+    text_kernel<<<n, NT, 0, e->stream>>>(e->hdr.p, e->seg.p, e->text.p, int(e->caps.max_segments),
+                                         int(e->caps.text_units), lo, lens.p, offs.p, dev.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, dev.p, size_t(total) * sizeof(uint16_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return total;
+}
+
+int64_t mtr_get_text(mtr_engine* e, uint32_t doc, uint16_t* out, int64_t cap) {
+    if (doc >= e->max_docs) {
+        set_err("mtr_get_text: bad document");
+        return -1;
+    }
+    int64_t off[2];
+    const int64_t n = mtr_get_texts(e, doc, doc + 1, nullptr, 0, off);
+    if (n <= 0 || !out || n > cap) return n;
+    return mtr_get_texts(e, doc, doc + 1, out, cap, off);
 }
 
 int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,

@@ -71,6 +71,8 @@ def lib():
         L.mtr_summary_bytes.restype = C.c_int64
         L.mtr_get_text.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.mtr_get_text.restype = C.c_int64
+        L.mtr_get_texts.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p]
+        L.mtr_get_texts.restype = C.c_int64
         L.mtr_get_containing_segment.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
                                                  C.POINTER(SegmentInfo), C.c_void_p, C.c_int64]
         L.mtr_get_containing_segment.restype = C.c_int
@@ -293,6 +295,17 @@ class Engine:
         buf = np.zeros(max(n, 1), dtype="<u2")
         lib().mtr_get_text(self.h, doc, buf.ctypes.data, n)
         return buf[:n].tobytes().decode("utf-16-le", "surrogatepass")
+
+    def texts(self, lo, hi) -> list[str]:
+        """Local-view texts of documents [lo, hi): one device gather, one download (mtr_get_texts)."""
+        off = np.zeros(hi - lo + 1, dtype="<i8")
+        n = lib().mtr_get_texts(self.h, lo, hi, None, 0, off.ctypes.data)
+        if n < 0:
+            raise EngineError(_err())
+        buf = np.zeros(max(n, 1), dtype="<u2")
+        if n and lib().mtr_get_texts(self.h, lo, hi, buf.ctypes.data, n, off.ctypes.data) != n:
+            raise EngineError(f"mtr_get_texts failed: {_err()}")
+        return [buf[off[i]:off[i + 1]].tobytes().decode("utf-16-le", "surrogatepass") for i in range(hi - lo)]
 
     def deltas(self, doc) -> np.ndarray:
         """The delta ranges (abi.DELTA_DTYPE) of the MTR_F_DELTA ops of the last batch for one document."""

@@ -32,7 +32,7 @@ function native() {
 
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
-    START_COLLAB: 12, SETCELL: 14, RELPOS: 15 };
+    START_COLLAB: 12, SETCELL: 14, RELPOS: 15, ACK: 17 };
 const REL = { BEFORE: 1, OFFSET: 2 };
 const COMB = { NONE: 0, REWRITE: 1, INCR: 2, CONSENSUS: 3, KEEP: 4 };
 const VEQ = { NEVER: 0x80000000, FALSY: 0x40000000, INCR_STR: 0x20000000, CONS_MUT: 0x10000000 };
@@ -278,12 +278,26 @@ class DocLog {
     push(type, flags, client, seq, ref, msn, pos1, pos2, payload, payload2) {
         this.ops.push([type, flags, client, seq, ref, msn, pos1, pos2, payload, payload2]);
     }
+    // local edits (client.ts:225-260): final before collaboration; while collaborating a pending op
+    // (record seq = UnassignedSequenceNumber) until this client's sequenced message acks it
+    localSeq() { return this.collaborating ? -1 : 0; }
     localInsert(pos, spec, it) {
         const s = this._seg(spec, it);
-        this.push(OP.LOCAL_INSERT, s[0], 0, 0, 0, 0, pos, s[3], s[1], s[2]);
+        this.push(OP.LOCAL_INSERT, s[0], 0, this.localSeq(), 0, 0, pos, s[3], s[1], s[2]);
     }
-    localRemove(start, end) { this.push(OP.LOCAL_REMOVE, 0, 0, 0, 0, 0, start, end, 0, 0); }
-    localAnnotate(start, end, props, it) { this.push(OP.LOCAL_ANNOTATE, 0, 0, 0, 0, 0, start, end, it.propop(props), 0); }
+    localRemove(start, end) { this.push(OP.LOCAL_REMOVE, 0, 0, this.localSeq(), 0, 0, start, end, 0, 0); }
+    localAnnotate(start, end, props, it) {
+        if (props && typeof props === 'object' && 'markerId' in props) this.markerIdAnnotated = true;
+        this.push(OP.LOCAL_ANNOTATE, 0, 0, this.localSeq(), 0, 0, start, end, it.propop(props), 0);
+    }
+    localOp(op, it) {  // Client.localTransaction member (client.ts:1029-1048)
+        if (op.type === 0) this.localInsert(op.pos1, op.seg, it);
+        else if (op.type === 1) this.localRemove(op.pos1, op.pos2);
+        else if (op.type === 2) {
+            if (op.combiningOp) throw new UnsupportedError('local annotate with a combiningOp');
+            this.localAnnotate(op.pos1, op.pos2, op.props || {}, it);
+        } else throw new UnsupportedError('local op type ' + op.type);
+    }
     startCollab(longId, minSeq, currentSeq) {  // client.ts:1133-1155
         if (longId === undefined) return;  // detached: stay local until attached
         if (this.observerId === undefined) {
@@ -299,16 +313,29 @@ class DocLog {
         }
     }
     seqUpdate(min, seq) { this.push(OP.SEQ, F.LAST, 0, seq, seq, min, 0, 0, 0, 0); }
-    message(msg, it) {  // Client.applyMsg, client.ts:858-887
+    message(msg, it, local) {  // Client.applyMsg, client.ts:858-887
         const cid = msg.clientId === null || msg.clientId === undefined ? 'null' : String(msg.clientId);
         const short = this.shortId(cid);
         const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
         if (msg.type !== 'op') { this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
-        if (cid === this.observerId) throw new UnsupportedError('message authored by the observer (local ack path)');
         let contents = msg.contents;
         if (typeof contents === 'string') contents = JSON.parse(contents);
         const members = contents.type === 3 ? contents.ops : [contents];  // MergeTreeDeltaType.GROUP
         if (members.length === 0) { this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
+        if (cid === this.observerId || local) {  // ackPendingSegment per member (client.ts:641-663, 866-869)
+            members.forEach((op, i) => {
+                const last = i === members.length - 1 ? F.LAST : 0;
+                let pp = 0;
+                if (op.type === 2) {
+                    if (op.combiningOp) throw new UnsupportedError('ack of a local annotate with a combiningOp');
+                    pp = it.propop(op.props || {});
+                } else if (op.type !== 0 && op.type !== 1) {
+                    throw new UnsupportedError('ack of op type ' + op.type);
+                }
+                this.push(OP.ACK, last, short, seq, ref, msn, 0, 0, pp, op.type);
+            });
+            return;
+        }
         members.forEach((op, i) => {
             const last = i === members.length - 1 ? F.LAST : 0;
             if (op.type === 0) {
@@ -627,7 +654,10 @@ class BatchReplayClient {
         this.currentSeq = currentSeq || 0;
     }
     applyMsg(msg, local) {
-        if (local) throw new UnsupportedError('local (acked) ops are outside the observer path');
+        const own = local || (msg.type === 'op' && String(msg.clientId) === this.log.observerId);
+        if (own && !this.engine.options.snapshotV1) {
+            throw new UnsupportedError("this client's own message in the legacy catch-up format");
+        }
         this._queue(() => {
             if (!this.engine.options.snapshotV1 && msg.type === 'op' &&
                 msg.referenceSequenceNumber !== msg.sequenceNumber - 1) {
@@ -642,7 +672,7 @@ class BatchReplayClient {
                 }
             }
             const lo = this.log.ops.length;
-            this.log.message(msg, this.engine.interner);
+            this.log.message(msg, this.engine.interner, local);
             if (!this.engine.options.snapshotV1 && msg.type === 'op') this.engine.catchUps[this.doc].add(msg, this.log, lo);
         });
         this.currentSeq = msg.sequenceNumber;
@@ -659,6 +689,10 @@ class BatchReplayClient {
             this.engine.interner));
     }
     removeRangeLocal(start, end) { this._queue(() => this.log.localRemove(start, end)); }
+    /** Client.localTransaction (client.ts:1029-1048): every member op as a local (pending) op. */
+    localTransaction(groupOp) {
+        this._queue(() => { for (const op of groupOp.ops) this.log.localOp(op, this.engine.interner); });
+    }
     annotateRangeLocal(start, end, props) { this._queue(() => this.log.localAnnotate(start, end, props, this.engine.interner)); }
     getCurrentSeq() { return this.currentSeq; }
     getText() {

@@ -112,8 +112,15 @@ int mtr_summary_hashes(mtr_engine* e, uint64_t* out, uint32_t n_docs);
 /* Total summary bytes of all documents (after mtr_summarize). */
 int64_t mtr_summary_bytes(mtr_engine* e);
 
-/* Local-view text of one document (UTF-16 units); returns length (writes <= cap units). */
+/* Local-view text of one document (UTF-16 units), gathered on the device
+ * (MergeTreeTextHelper.getText, MergeTreeTextHelper.ts:20-81); returns the length (writes the text only
+ * when it fits in cap units), -1 on error. */
 int64_t mtr_get_text(mtr_engine* e, uint32_t doc, uint16_t* out, int64_t cap);
+
+/* Local-view texts of documents [lo, hi) in one device gather and one download: doc_off[i] = first unit
+ * of document lo + i in out, doc_off[hi - lo] = total.  Returns the total units (out NULL: a size query,
+ * nothing written; doc_off filled either way), -1 when cap is too small or on error. */
+int64_t mtr_get_texts(mtr_engine* e, uint32_t lo, uint32_t hi, uint16_t* out, int64_t cap, int64_t* doc_off);
 
 /* Client.getContainingSegment(pos, {referenceSequenceNumber, clientId}) (client.ts:1065-1078 ->
  * mergeTree.ts:787-813): the segment holding position pos in the (ref_seq, client) view, found on the

@@ -95,3 +95,27 @@ def test_writer_perspectives_engine(new_length):
     eng.summarize()
     for d, (name, _, v) in enumerate(views):
         assert eng.summary(d) == orcs[d].summarize(b, d), f"{name}/{v.writer} summary"
+
+
+@pytest.mark.gpu
+def test_bulk_device_texts():
+    """mtr_get_texts (one device gather for a document range) equals the per-document reads and the
+    oracle's getText, for writers holding pending local segments mid-group."""
+    from fluidframework_amd.engine import Engine
+
+    it, views = _all_perspectives()
+    views = views[:24]
+    eng = Engine(len(views), max_segments=8192, heap_entries=8192, text_units=1 << 18, prop_words=1 << 18,
+                 remover_cells=1 << 14, ops_per_launch=64)
+    orcs = [OracleDoc(options()) for _ in views]
+    for _, groups, v in views:
+        v.feed(groups[0], it)
+        v.feed(groups[1], it, 0, len(groups[1]["msgs"]) // 2, drain=False)
+    b = build_batch([v.log for _, _, v in views], it)
+    eng.apply(b)
+    for d in range(len(views)):
+        assert orcs[d].apply(b, d) == 0
+    bulk = eng.texts(0, len(views))
+    assert bulk == [eng.text(d) for d in range(len(views))]
+    assert bulk == [o.text() for o in orcs]
+    assert eng.texts(3, 3) == []

@@ -317,3 +317,57 @@ def test_async_host_and_containing_segment(tmp_path):
             assert got[3] in (-1, e[2])  # text segments carry their text
             n_hit += 1
     assert n_hit > 250
+
+
+def _writer_events(groups, writer):
+    """client.replay.spec.ts:41-68 from one writer's side: its op as a local op right after it caught
+    up to the op's referenceSequenceNumber, every sequenced message in order (its own are acks)."""
+    events, queue, cur = [], [], 0
+    for g in groups:
+        for m in g["msgs"]:
+            if m["clientId"] == writer:
+                while queue and m["referenceSequenceNumber"] > cur:
+                    x = queue.pop(0)
+                    events.append({"msg": x})
+                    cur = x["sequenceNumber"]
+                events.append({"local": m["contents"]})
+            queue.append(m)
+        while queue:
+            x = queue.pop(0)
+            events.append({"msg": x})
+            cur = x["sequenceNumber"]
+    return events
+
+
+def test_js_local_op_packer_matches_python_packer(tmp_path):
+    """Local ops while collaborating (seq = UnassignedSequenceNumber records) and acks of this client's
+    own messages: the Node packer's arrays equal the Python packer's."""
+    from fixtures import replay_writers
+
+    _addon()
+    feeds = []
+    for p in replay_files()[3:6]:
+        groups = load_replay(p)
+        for w in replay_writers(groups)[:2]:
+            feeds.append({"observer": w, "events": _writer_events(groups, w)})
+    path = tmp_path / "feeds.json"
+    path.write_text(json.dumps(feeds))
+    js = json.loads(_node([os.path.join(HERE, "node", "pack_events.js"), str(path)]))
+    raw = {k: base64.b64decode(v) for k, v in js.items()}
+    it = Interner()
+    logs = []
+    for f in feeds:
+        log = DocLog()
+        log.start_collab(f["observer"])
+        for ev in f["events"]:
+            if "local" in ev:
+                log.local_op(ev["local"], it)
+            else:
+                log.message(ev["msg"], it)
+        logs.append(log)
+    py = build_batch(logs, it)
+    assert int((py.ops["type"] == 17).sum()) > 0 and int((py.ops["seq"] == -1).sum()) > 0
+    assert raw["docs"] == py.docs.tobytes()
+    assert raw["ops"] == py.ops.tobytes()
+    n_kv = 2 * int(py.propop_off[-1])
+    assert np.array_equal(np.frombuffer(raw["propopKv"], "<u4")[:n_kv], py.propop_kv[:n_kv])
