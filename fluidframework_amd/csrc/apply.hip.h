@@ -71,6 +71,12 @@ constexpr uint32_t NS_UNDEF = 0, NS_FALSE = 1, NS_TRUE = 2;
 constexpr int LOCAL_BASE = 0x40000000;
 constexpr int TIE_LOCAL = 0x7ffffffe;   // breakTie's newSeq of a local insert (Number.MAX_SAFE_INTEGER)
 constexpr int kPendRing = 256;
+// HBM-resident documents of at least kGapMin leaves keep one hole slot per kGapEvery (Eng::spread), so a
+// split or an insert moves the leaves up to the next hole instead of the rest of the document; a shift
+// looks for a hole within kHoleWindow slots
+constexpr int kGapMin = 8192;
+constexpr int kGapEvery = 16;
+constexpr int kHoleWindow = 1024;
 constexpr uint32_t PEND_KEY = 0x40000000u;
 enum { PK_INSERT = 1, PK_REMOVE = 2, PK_ANNOTATE = 3 };
 
@@ -139,7 +145,8 @@ struct DocHdr {
     int32_t dused;      // delta ranges recorded for the current batch
     int32_t lseq;       // collabWindow.localSeq (mergeTreeNodes.ts:656)
     int32_t phead, ptail;  // pending SegmentGroups: ring entries [phead, ptail) (MergeTree.pendingSegments)
-    int32_t pad[3];
+    int32_t holes;         // HBM-resident documents: hole slots among the nseg leaf slots (see Eng::spread)
+    int32_t pad[2];
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -228,6 +235,7 @@ struct St {
     int htop;  // seq of the LRU heap's top entry (valid while heapn > 0)
     int heap_need;
     int dused;
+    int holes;   // hole slots (HBM-resident documents only)
     int cur_op;  // index of the op being applied (delta-reporting instantiations only)
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
@@ -460,6 +468,11 @@ struct Eng {
         return vis_hot(L, ld_hot(L, i), i, v, newlen, minseq, valid);
     }
     static MTR_DI int vis_hot(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
+        const int r = vis_leaf(L, h, i, v, newlen, minseq, valid);
+        if constexpr (G) return (h.meta & M_DEL) ? -1 : r;  // a hole slot is no leaf (Eng::spread)
+        return r;
+    }
+    static MTR_DI int vis_leaf(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
         const int len = h.len;
         const int rseq = h.rseq;
         const uint32_t m = h.meta;
@@ -614,12 +627,13 @@ struct Eng {
         v.local = (!s.collab || uint32_t(s.local) == v.client) ? 1 : 0;
         int i, before;
         find1(L, s, v, pos, i, before, P.new_length_calc);
+        const int li = (G && s.holes && i < s.nseg) ? count_live(L, 0, i) : i;  // the leaf's ordinal
         if (lane_id() == 0) {
             if (i >= s.nseg || pos < 0) {
                 out[0] = -1;
             } else {
                 const uint32_t m = L.meta[i];
-                out[0] = i;
+                out[0] = li;
                 out[1] = pos - before;
                 out[2] = L.len[i];
                 out[3] = L.seq[i];
@@ -694,12 +708,28 @@ struct Eng {
     }
 
     // ------------------------------------------------------------ data movement
-    // move leaves [at, S) (with their scan entries) to [at+1, S+1); rounds of 64 from the top
-    static MTR_DI void shift_right1(D& L, const St& s, int at) {
+    // move leaves [at, S) (with their scan entries) to [at+1, S+1); rounds of 64 from the top.
+    // HBM-resident documents with hole slots (Eng::spread) only move [at, h) into the first hole h at
+    // or after `at`.  Returns whether the slot count grew (no hole was taken).
+    static MTR_DI bool shift_right1(D& L, St& s, int at) {
         PROF(P_SHIFT);
-        const int S = s.nseg;
+        int S = s.nseg;
+        bool grew = true;
         if constexpr (G) {  // GK rounds per group: every load of the group before its stores (a round's
                             // stores land above every slot the group's lower rounds read)
+            if (s.holes > 0) {  // the first hole at or after `at`, within a bounded window
+                const int lim = min(S, at + kHoleWindow);
+                for (int base = at; base < lim; base += 64) {
+                    const int i = base + lane_id();
+                    const uint64_t hm = __ballot(i < lim && (L.meta[min(i, S - 1)] & M_DEL));
+                    if (hm) {
+                        S = base + first_lane(hm);  // move [at, hole) up into the hole
+                        grew = false;
+                        s.holes--;
+                        break;
+                    }
+                }
+            }
             for (int hi = S; hi > at; hi -= 64 * GK) {
                 int a0[GK], a1[GK], a2[GK], a8[GK];
                 uint32_t a3[GK], a4[GK], a5[GK], a7[GK];
@@ -724,7 +754,7 @@ struct Eng {
                 }
                 wsync();
             }
-            return;
+            return grew;
         }
         for (int hi = S; hi > at; hi -= 64) {
             const int lo = max(at, hi - 64);
@@ -740,6 +770,7 @@ struct Eng {
             }
             wsync();
         }
+        return grew;
     }
 
     // stream compaction of leaves without M_DEL (zamboni unlink / append); rounds of 64 from the
@@ -797,6 +828,70 @@ struct Eng {
         }
         s.nseg = base;
         if (base == 0) s.height = 1;
+    }
+
+    // ---- hole slots (HBM-resident documents of >= kGapMin leaves): a hole is a slot with M_DEL, no
+    // length, no uid and removedSeq 0 -- undefined in every view (vis_hot), skipped by every walk,
+    // scour and summary; shifts take the next hole (shift_right1), zamboni leaves its deleted leaves
+    // as holes (holeify) instead of compacting the rest of the document
+    static MTR_DI void hole_fields(D& L, int i) {
+        L.meta[i] = M_DEL;
+        L.len[i] = 0;
+        L.seq[i] = 0;
+        L.rseq[i] = 0;
+        L.uid[i] = NONE32;
+        L.props[i] = NONE32;
+        L.text[i] = uint32_t(MTR_HANDLE_UNALLOCATED);
+    }
+    static MTR_DI void holeify(D& L, St& s, int from, int to) {
+        int made = 0;
+        for (int base = from; base < to; base += 64) {
+            const int i = base + lane_id();
+            const bool in = i < to;
+            const uint32_t m = L.meta[min(i, to - 1)];
+            const bool h = in && (m & M_DEL) && L.uid[min(i, to - 1)] != NONE32;  // newly deleted
+            if (h) hole_fields(L, i);
+            made += __popcll(__ballot(h));
+        }
+        wsync();
+        s.holes += made;
+        if (s.holes >= s.nseg) {  // nothing left
+            s.nseg = 0;
+            s.holes = 0;
+            s.height = 1;
+        }
+    }
+    // Lay the leaves out with one hole per kGapEvery slots (all holes squeezed out first): leaf k goes
+    // to slot k + k / (kGapEvery - 1).  Moves run from the top down, so no leaf is overwritten before it
+    // is read.  Only between ops (no leaf index is held).
+    static MTR_DI void spread(D& L, St& s, int cap) {
+        if (s.holes) {
+            compact(L, s, 0);
+            s.holes = 0;
+        }
+        const int S = s.nseg;
+        const int n_new = S + (S - 1) / (kGapEvery - 1) + 1;
+        if (S < kGapMin || n_new > cap) return;
+        for (int top = S; top > 0; top -= 64) {
+            const int i = top - 64 + lane_id();
+            const bool in = i >= 0;
+            const int ic = max(i, 0);
+            const int a0 = L.len[ic], a1 = L.seq[ic], a2 = L.rseq[ic];
+            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = L.props[ic], a7 = L.uid[ic];
+            wsync();
+            if (in) {
+                const int d = i + i / (kGapEvery - 1);
+                L.len[d] = a0; L.seq[d] = a1; L.rseq[d] = a2; L.meta[d] = a3;
+                L.text[d] = a4; L.props[d] = a5; L.uid[d] = a7;
+            }
+            wsync();
+        }
+        const int last = (S - 1) + (S - 1) / (kGapEvery - 1);  // slot of the last leaf
+        for (int i = lane_id(); i <= last; i += 64)
+            if (i % kGapEvery == kGapEvery - 1) hole_fields(L, i);
+        wsync();
+        s.nseg = last + 1;
+        s.holes = s.nseg - S;
     }
 
     // index of the leaf with this uid, -1 if unlinked (uids are unique)
@@ -889,6 +984,27 @@ struct Eng {
         return -1;
     }
 
+    // leaves of [bs, be) that are not hole slots; the index of the n-th (0-based) of them
+    static MTR_DI int count_live(const D& L, int bs, int be) {
+        int c = 0;
+        for (int base = bs; base < be; base += 64) {
+            const int i = base + lane_id();
+            c += __popcll(__ballot((i < be) & !(L.meta[min(i, be - 1)] & M_DEL)));
+        }
+        return c;
+    }
+    static MTR_DI int nth_live(const D& L, int bs, int be, int n) {
+        for (int base = bs; base < be; base += 64) {
+            const int i = base + lane_id();
+            const bool t = (i < be) & !(L.meta[min(i, be - 1)] & M_DEL);
+            const uint64_t m = __ballot(t);
+            const int pc = __popcll(m);
+            if (n < pc) return base + first_lane(__ballot(t && __popcll(m & lanes_below()) == n));
+            n -= pc;
+        }
+        return -1;
+    }
+
     // [bs, be) = the leaf block holding leaf x, from one ballot over leaves x-31 .. x+32 (leaf
     // blocks hold at most 7 leaves); the loops above take over only if a bound lies outside
     static MTR_DI void block_bounds1(const D& L, const St& s, int x, int& bs, int& be) {
@@ -912,10 +1028,11 @@ struct Eng {
         int level = 1;
         int bs = hbs, be = hbe;
         if (bs < 0) block_bounds1(L, s, x, bs, be);
-        int cnt = be - bs;
+        int cnt = G && s.holes ? count_live(L, bs, be) : be - bs;  // (holes are no children)
         int xbs = bs;
         while (cnt >= kMaxNodesInBlock) {
             int c5 = bs + kMaxNodesInBlock / 2;
+            if (G && s.holes && level == 1) c5 = nth_live(L, bs, be, kMaxNodesInBlock / 2);
             if (level == 1 && x >= c5) xbs = c5;
             if (level > 1) c5 = nth_bnd(L, bs, be, level - 1, kMaxNodesInBlock / 2);
             uint32_t m = set_bnd(uniu(L.meta[c5]), level);
@@ -1772,7 +1889,7 @@ struct Eng {
     // zamboniSegments body for one popped LRU entry whose segment is leaf x
     // (zamboni.ts:33-58 + packParent zamboni.ts:63-120).  Returns the first leaf index at or
     // after which leaves may be marked for deletion (the caller compacts from there), or -1.
-    static MTR_DI int zamboni_block(D& L, const KParams& P, St& s, int x) {
+    static MTR_DI int zamboni_block(D& L, const KParams& P, St& s, int x, int& to) {
         PROF(P_ZBLOCK);
         PROF_COUNT(P_NZBLOCK);
         const int H = s.height;
@@ -1781,7 +1898,8 @@ struct Eng {
         const uint32_t m1 = uniu(L.meta[rs1]);
         if (ns_of(m1) == NS_FALSE) return -1;
         const int topb1 = bnd_of(m1);
-        const int before = re1 - rs1;
+        const int before = G && s.holes ? count_live(L, rs1, re1) : re1 - rs1;
+        to = re1;  // leaves marked for deletion lie in [from, to)
         int kept;
         {
             PROF(P_SCOUR1);
@@ -1819,6 +1937,7 @@ struct Eng {
                 ce = pe;
                 if (l == 2) {
                     from = ps;
+                    to = max(to, pe);
                     // packParent scours every child of P again -- including the block just
                     // scoured: scourNode is not idempotent (a dropped tombstone no longer resets
                     // the merge candidate), zamboni.ts:68-73,122-193.
@@ -1875,8 +1994,12 @@ struct Eng {
             const uint32_t u = heap_pop(L, s);
             const int x = find_uid(L, s, u);
             if (x < 0) continue;
-            const int from = zamboni_block(L, P, s, x);
-            if (from >= 0) compact(L, s, from);
+            int to = 0;
+            const int from = zamboni_block(L, P, s, x, to);
+            if (from >= 0) {
+                if (G && s.holes) holeify(L, s, from, to);  // deleted leaves stay as hole slots
+                else compact(L, s, from);
+            }
         }
     }
 
@@ -1928,7 +2051,7 @@ struct Eng {
         const uint32_t m0 = rdlane(mj, jl);
         const int off = pos - (e - v);
         if (!(off > 0 && !(m0 & M_MARKER))) return;
-        shift_right1(L, s, j + 1);
+        const bool grew = shift_right1(L, s, j + 1);
         {  // BaseSegment.splitAt, mergeTreeNodes.ts:481-510
             const int r = j + 1;
             L.len[r] = rdlane(lj, jl) - off;
@@ -1953,7 +2076,7 @@ struct Eng {
             L.E[r] = e;
             wsync();
             if (X && (m0 & M_PEND)) pend_copy(L, P, s, uniu(rdlane(uj, jl)), r);
-            s.nseg++;
+            if (grew) s.nseg++;
             overflow_fix(L, s, r);
         }
     }
@@ -2094,7 +2217,8 @@ struct Eng {
             wbs = wbe = -1;
         }
         if (slot < 0) return -1;
-        shift_right1(L, s, slot);
+        const bool grew = shift_right1(L, s, slot);
+        if (G && !grew) wbs = wbe = -1;  // a hole was taken: overflow_fix finds the block itself
         uint32_t m = client & M_CLIENT_MASK;
         if (marker) m |= M_MARKER;
         else m |= (nl ? M_NL : 0u) | (nonl ? M_NONL : 0u);
@@ -2127,7 +2251,7 @@ struct Eng {
             s.status = uni(s.status);
         }
         wsync();
-        s.nseg = S + 1;
+        s.nseg = S + (grew ? 1 : 0);
         const int xbs = S == 0 ? 0 : overflow_fix(L, s, slot, wbs, wbe);
         // saveIfLocal (mergeTree.ts:1618-1637): remote segments above minSeq go to the LRU
         if (op.flags & MTR_F_APPEND) set_merge_info(L, P, s, slot, op, dd);
@@ -2175,6 +2299,7 @@ struct Eng {
         if (s.height != 0) {  // reloadFromSegments replaces the whole tree
             s.nseg = 0;
             s.height = 0;
+            s.holes = 0;
         }
         const bool marker = !PM && (op.flags & MTR_F_MARKER) != 0;
         const int len = marker ? 1 : int(op.payload2);
@@ -2229,6 +2354,7 @@ struct Eng {
         }
         wsync();
         s.height = H;
+        if (G && !PM && S >= kGapMin) spread(L, s, L.cap);
     }
 
     // markRangeRemoved / annotateRange walk (mergeTree.ts:1955-2047, 1895-1953): leaves with
@@ -2404,6 +2530,7 @@ struct Eng {
             s.texthalf = h.texthalf;
             s.heap_need = 0;
             s.dused = h.dused;
+            s.holes = G ? h.holes : 0;
             s.ops_done = 0;
             s.sum_s = 0;
             s.sum_l = 0;
@@ -2477,6 +2604,7 @@ struct Eng {
             h.texthalf = s.texthalf;
             h.heap_need = s.heap_need;
             h.dused = s.dused;
+            if (G) h.holes = s.holes;
             st_struct(hp, h);
             if (GN) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
 #ifdef MTR_PROF
@@ -2679,6 +2807,9 @@ struct Eng {
             return true;
         }
         if (s.height == 0) finish_load(L, s);
+        // holes ran low, or the slots fill the slab while holes remain
+        if (G && !PM && s.nseg >= kGapMin && (s.holes * 64 < s.nseg || (s.holes && s.nseg + 2 >= L.cap)))
+            spread(L, s, L.cap);
         const bool local_op = op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE;
         int zop = 0;
         View v;

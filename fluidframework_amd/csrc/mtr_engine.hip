@@ -1298,9 +1298,11 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
     if (doc >= e->max_docs || fetch_doc(e, doc, hd)) return -1;
     const size_t sc = e->caps.max_segments;
     if (height) *height = hd.h.height;
-    if (hd.h.nseg > cap) return -int64_t(hd.h.nseg);
+    if (hd.h.nseg - hd.h.holes > cap) return -int64_t(hd.h.nseg - hd.h.holes);
+    int k = 0;  // leaf ordinal (hole slots of HBM-resident documents are skipped)
     for (int i = 0; i < hd.h.nseg; i++) {
         const uint32_t m = hd.seg[F_META * sc + i];
+        if (hd.h.holes && (m & M_DEL)) continue;
         const int32_t rs = int32_t(hd.seg[F_RSEQ * sc + i]);
         int nrem = 0;
         if (rs != RNONE) {
@@ -1323,7 +1325,7 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
                 h = (h ^ (v < e->h_val_eq.size() ? e->h_val_eq[v] : v)) * 16777619u;
             }
         }
-        int32_t* r = out + 8 * i;
+        int32_t* r = out + 8 * k++;
         r[0] = int32_t(hd.seg[F_LEN * sc + i]);
         r[1] = int32_t(hd.seg[F_SEQ * sc + i]);
         r[2] = dec_client(m & M_CLIENT_MASK);
@@ -1334,7 +1336,7 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
         r[6] = e->h_kind[doc] ? int32_t(hd.seg[F_TEXT * sc + i]) : ((m & M_MARKER) ? 1 : 0);
         r[7] = int32_t(h);
     }
-    return hd.h.nseg;
+    return k;
 }
 
 // debug: the scan arrays (E, V) an HBM-resident document's last op left in the scratch slab

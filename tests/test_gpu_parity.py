@@ -214,12 +214,14 @@ def test_c5_shaped_hbm_resident(n, grow, ops):
     tabs = tables(writers=64)
     b, _, status = generate(cfg, tabs, 0, n, threads=8, grow=grow)
     assert (status == 0).all()
-    eng = _engine(n, max_segments=grow + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
+    eng = _engine(n, max_segments=grow + grow // 14 + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
                   text_units=2 * (int(cfg.text_cap) + 8192), ops_per_launch=256)
     t0 = time.time()
     eng.apply(b)
     eng.summarize()
     print(f"C5-shaped: {n} docs x ({grow} loaded + {ops} ops) in {time.time() - t0:.2f} s", eng.timing())
+    # the documents run with hole slots (one per 16): more slots than leaves can exist
+    assert eng.stats()["max_leaves"] > grow + grow // 20
     for d in range(n):
         st, op = eng.status(d)
         assert st == 0, f"doc {d}: status {st:#x} at op {op}"
@@ -298,7 +300,7 @@ def test_grown_record_mode_matches_oracle_generator():
     tabs = tables(writers=64)
     ob, ohash, ost = generate(cfg, tabs, 0, n, threads=4, grow=grow)
     assert (ost == 0).all()
-    eng = _engine(n, max_segments=grow + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
+    eng = _engine(n, max_segments=grow + grow // 14 + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
                   text_units=2 * (int(cfg.text_cap) + 8192), ops_per_launch=256)
     eng.generate(cfg, tabs, grow=grow)
     rec = eng.download(0, n)
