@@ -146,7 +146,8 @@ struct DocHdr {
     int32_t lseq;       // collabWindow.localSeq (mergeTreeNodes.ts:656)
     int32_t phead, ptail;  // pending SegmentGroups: ring entries [phead, ptail) (MergeTree.pendingSegments)
     int32_t holes;         // HBM-resident documents: hole slots among the nseg leaf slots (see Eng::spread)
-    int32_t pad[2];
+    int32_t chunked;       // ... and their per-64-slot chunk summaries are valid (two-level view scan)
+    int32_t pad;
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -202,6 +203,7 @@ struct KParams {
     uint16_t* gen_text;          // == btext, writable
     unsigned long long* prof;    // [P_COUNT] phase-timer sums (-DMTR_PROF builds)
     uint32_t* pend;              // [doc][kPendRing][4] pending SegmentGroups (batches with local ops only)
+    int32_t* csum;               // [doc][2][segcap / 64 + 1] chunk summaries of HBM-resident documents
 };
 
 // phase-timer slots (-DMTR_PROF builds)
@@ -213,7 +215,7 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
 // records, the batch's property tables), kept in LDS and read where used, so they never hold SGPRs
 // across the whole op loop (the loop's scalar state otherwise spills into VGPR lanes)
-enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_HDR, CP_PEND, CP_N };
+enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_HDR, CP_PEND, CP_CSUM, CP_N };
 
 // LDS-side scratch of one document: record-mode broadcast, cold pointers, phase timers
 struct Sc {
@@ -236,6 +238,7 @@ struct St {
     int heap_need;
     int dused;
     int holes;   // hole slots (HBM-resident documents only)
+    int chunked; // chunk summaries valid (HBM-resident documents with holes)
     int cur_op;  // index of the op being applied (delta-reporting instantiations only)
     unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
 };
@@ -270,6 +273,10 @@ struct Doc {
     MTR_DI gptr<const uint32_t> tab(int k) const { return (gptr<const uint32_t>)cold(k); }
     MTR_DI gptr<DocHdr> ghdr() const { return (gptr<DocHdr>)cold(CP_HDR); }      // this document's header
     MTR_DI gptr<uint32_t> gpend() const { return (gptr<uint32_t>)cold(CP_PEND); }  // its pending-group ring
+    MTR_DI gptr<int> gcsum() const { return (gptr<int>)cold(CP_CSUM); }          // chunk summaries (len, then ev)
+    int rlo = 0, rhi = 0;  // the op's view-scan region (slots) when the scan was two-level (E valid there)
+    int shi = 0;           // end of the slots the last shift_right1 moved (chunk-summary upkeep)
+    int wlo = 0, whi = 0;  // slots the last range walk touched
 };
 
 MTR_DI int bnd_of(uint32_t m) { return int((m & M_BND_MASK) >> M_BND_SHIFT); }
@@ -586,6 +593,138 @@ struct Eng {
         wsync();
     }
 
+    // ---- two-level view scan (HBM-resident documents with hole slots, s.chunked)
+    // The slots form chunks of 64.  Per chunk the document keeps its local length (the leaves that are
+    // not removed) and its newest event (the largest seq, and removedSeq of a removed leaf, over its
+    // leaves).  A chunk whose newest event is <= the view's refSeq looks the same to every client at that
+    // refSeq -- each leaf was inserted by then, and removed by then or not at all -- so its view length
+    // is its local length; only the other chunks are scanned leaf by leaf.  This restates what
+    // PartialSequenceLengths does per block (partialLengths.ts:698-735) for chunks of the flat leaf order.
+    static MTR_DI gptr<int> cs_len(const D& L) { return L.gcsum(); }
+    static MTR_DI gptr<int> cs_ev(const D& L) { return L.gcsum() + (L.cap / 64 + 1); }
+    static MTR_DI A<int> cs_pre(const D& L) { return L.E + L.cap; }  // inclusive chunk prefix of a view
+    // recompute the summaries of the chunks covering slots [lo, hi)
+    static MTR_DI void csum_update(D& L, const St& s, int lo, int hi) {
+        if constexpr (G) {
+            if (!s.chunked) return;
+            hi = min(hi, s.nseg);
+            if (lo >= hi) return;
+            const gptr<int> cl = cs_len(L), ce = cs_ev(L);
+            for (int c = max(lo, 0) >> 6; c <= (hi - 1) >> 6; c++) {
+                const int i = c * 64 + lane_id();
+                const bool in = i < s.nseg;
+                const int ic = min(i, s.nseg - 1);
+                const uint32_t m = L.meta[ic];
+                const int len = L.len[ic], sq = L.seq[ic], rs = L.rseq[ic];
+                const bool live = in && !(m & M_DEL);
+                const bool rem = rs != RNONE;
+                int x = (live && !rem) ? len : 0;
+                int ev = live ? max(sq, rem ? rs : 0) : 0;
+                x = rdlane(wave_incl_scan(x), 63);
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
+                if (lane_id() == 0) {
+                    cl[c] = x;
+                    ce[c] = ev;
+                }
+            }
+            wsync();
+        }
+    }
+    // the view's chunk lengths, their inclusive prefix in cs_pre; returns the view's total length
+    static MTR_DI int prefix2(D& L, const St& s, const View& v, int newlen) {
+        PROF(P_PREFIX);
+        const int S = s.nseg, nch = (S + 63) >> 6;
+        const gptr<int> cl = cs_len(L), ce = cs_ev(L);
+        const A<int> cp = cs_pre(L);
+        const int ln = lane_id();
+        int carry = 0;
+        for (int cb = 0; cb < nch; cb += 64) {
+            const int c = cb + ln;
+            const bool in = c < nch;
+            int len = in ? cl[min(c, nch - 1)] : 0;
+            const int ev = in ? ce[min(c, nch - 1)] : 0;
+            uint64_t dm = __ballot(in && !v.local && ev > v.ref);
+            while (dm) {  // chunks with events after refSeq: their leaves' view lengths, GK chunks at a time
+                int lq[GK];
+                Hot hq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    lq[q] = dm ? first_lane(dm) : -1;
+                    dm &= dm - 1;
+                    const int i = (cb + max(lq[q], 0)) * 64 + ln;
+                    hq[q] = ld_hot(L, min(i, S - 1));
+                }
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    if (lq[q] < 0) break;
+                    const int i = (cb + lq[q]) * 64 + ln;
+                    const int x0 = vis_hot(L, hq[q], i, v, newlen, s.minseq, i < S);
+                    const int sum = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
+                    if (ln == lq[q]) len = sum;
+                }
+            }
+            const int inc = wave_incl_scan(len);
+            if (in) cp[c] = carry + inc;
+            carry += rdlane(inc, 63);
+        }
+        wsync();
+        return carry;
+    }
+    // the scan array E of chunks [c0, c1] from the chunk prefix
+    static MTR_DI void materialize(D& L, const St& s, const View& v, int newlen, int c0, int c1) {
+        const int S = s.nseg;
+        const A<int> cp = cs_pre(L);
+        for (int c = c0; c <= c1; c++) {
+            const int i = c * 64 + lane_id();
+            const int base = c > 0 ? uni(cp[c - 1]) : 0;
+            const Hot h = ld_hot(L, min(i, S - 1));
+            const int x0 = vis_hot(L, h, i, v, newlen, s.minseq, i < S);
+            const int x = i < S ? x0 : 0;
+            const int inc = wave_incl_scan(max(x, 0));
+            if (i < S) L.E[i] = (base + inc) | (x < 0 ? int(0x80000000u) : 0);
+        }
+        wsync();
+    }
+    // first chunk whose inclusive prefix reaches pos (the last chunk if none)
+    static MTR_DI int chunk_of(const D& L, int nch, int pos) {
+        const A<int> cp = cs_pre(L);
+        int lo = 0, hi = nch;
+        const int ln = lane_id();
+        while (hi - lo > 64) {
+            const int stride = (hi - lo + 64) >> 6;
+            const int idx = lo + (ln + 1) * stride - 1;
+            const uint64_t m = __ballot((idx >= hi) | (cp[min(idx, hi - 1)] >= pos));
+            const int k = first_lane(m);
+            const int nlo = lo + k * stride;
+            hi = min(hi, lo + (k + 1) * stride - 1);
+            lo = nlo;
+        }
+        const int i = lo + ln;
+        const uint64_t m = __ballot((i < hi) & (cp[min(i, max(hi - 1, 0))] >= pos));
+        return min(m ? lo + first_lane(m) : hi, nch - 1);
+    }
+    // The op's view scan: flat (prefix) or two-level, with E valid over the chunks around positions
+    // [p_lo, p_hi] (one chunk before, two after: the searches' windows and the walk's reach).  Returns
+    // the view's total length.
+    static MTR_DI int view_scan(D& L, St& s, const View& v, int newlen, int p_lo, int p_hi) {
+        if constexpr (G) {
+            L.rhi = 0;
+            if (s.chunked && s.nseg > 0) {
+                const int total = prefix2(L, s, v, newlen);
+                const int nch = (s.nseg + 63) >> 6;
+                const int c0 = max(0, chunk_of(L, nch, p_lo) - 1);
+                const int c1 = min(nch - 1, chunk_of(L, nch, p_hi) + 2);
+                materialize(L, s, v, newlen, c0, c1);
+                L.rlo = c0 * 64;
+                L.rhi = (c1 + 1) * 64;
+                return total;
+            }
+        }
+        prefix(L, s, v, newlen);
+        return s.nseg > 0 ? (uni(L.E[s.nseg - 1]) & EMASK) : 0;
+    }
+
     // getContainingSegment of one document (mergeTree.ts:787-813: nodeMap over [pos, pos + 1)): i = the
     // first leaf whose inclusive visible prefix exceeds pos (S if none), before = the visible length
     // ahead of it.  Writes no scan array.
@@ -730,6 +869,7 @@ struct Eng {
                     }
                 }
             }
+            L.shi = S + 1;  // slots [at, S + 1) changed
             for (int hi = S; hi > at; hi -= 64 * GK) {
                 int a0[GK], a1[GK], a2[GK], a8[GK];
                 uint32_t a3[GK], a4[GK], a5[GK], a7[GK];
@@ -859,12 +999,14 @@ struct Eng {
             s.nseg = 0;
             s.holes = 0;
             s.height = 1;
+            s.chunked = 0;
         }
     }
     // Lay the leaves out with one hole per kGapEvery slots (all holes squeezed out first): leaf k goes
     // to slot k + k / (kGapEvery - 1).  Moves run from the top down, so no leaf is overwritten before it
     // is read.  Only between ops (no leaf index is held).
     static MTR_DI void spread(D& L, St& s, int cap) {
+        s.chunked = 0;
         if (s.holes) {
             compact(L, s, 0);
             s.holes = 0;
@@ -892,19 +1034,22 @@ struct Eng {
         wsync();
         s.nseg = last + 1;
         s.holes = s.nseg - S;
+        s.chunked = L.gcsum() ? 1 : 0;  // chunk summaries for the two-level view scan
+        csum_update(L, s, 0, s.nseg);
     }
 
     // index of the leaf with this uid, -1 if unlinked (uids are unique)
     static MTR_DI int find_uid(const D& L, const St& s, uint32_t u) {
         PROF(P_FINDUID);
         const int S = s.nseg;
-        if constexpr (G) {
-            for (int base = 0; base < S; base += 64 * GK) {
-                uint32_t uk[GK];
+        if constexpr (G) {  // one word per leaf: 4 * GK rounds of loads in flight
+            constexpr int FK = 4 * GK;
+            for (int base = 0; base < S; base += 64 * FK) {
+                uint32_t uk[FK];
 #pragma unroll
-                for (int q = 0; q < GK; q++) uk[q] = L.uid[min(base + 64 * q + lane_id(), S - 1)];
+                for (int q = 0; q < FK; q++) uk[q] = L.uid[min(base + 64 * q + lane_id(), S - 1)];
 #pragma unroll
-                for (int q = 0; q < GK; q++) {
+                for (int q = 0; q < FK; q++) {
                     const uint64_t m = __ballot((base + 64 * q + lane_id() < S) & (uk[q] == u));
                     if (m) return base + 64 * q + first_lane(m);
                 }
@@ -943,6 +1088,10 @@ struct Eng {
     // first i with E[i] >= pos (S if none): 64-ary search
     static MTR_DI int lower_bound_E(const D& L, const St& s, int pos) {
         int lo = 0, hi = s.nseg;  // answer in [lo, hi]; hi qualifies (or is S)
+        if (G && L.rhi > 0) {  // a two-level scan: E holds only the op's region
+            lo = min(L.rlo, s.nseg);
+            hi = min(L.rhi, s.nseg);
+        }
         const int ln = lane_id();
         while (hi - lo > 64) {
             // the hi - lo + 1 candidates in 64 strides: lane 63's probe reaches hi, which qualifies
@@ -1265,6 +1414,7 @@ struct Eng {
                 s.status = MTR_ERR_BAD_OP;
             }
             wsync();
+            if (G) csum_update(L, s, i, i + 1);
             int bs, be;
             block_bounds1(L, s, i, bs, be);
             add_lru_block(L, s, bs, uniu(L.uid[i]), seq);  // mergeTree.ts:1299-1301
@@ -1997,8 +2147,13 @@ struct Eng {
             int to = 0;
             const int from = zamboni_block(L, P, s, x, to);
             if (from >= 0) {
-                if (G && s.holes) holeify(L, s, from, to);  // deleted leaves stay as hole slots
-                else compact(L, s, from);
+                if (G && s.holes) {  // deleted leaves stay as hole slots
+                    holeify(L, s, from, to);
+                    csum_update(L, s, from, to);
+                } else {
+                    compact(L, s, from);
+                    s.chunked = 0;
+                }
             }
         }
     }
@@ -2077,6 +2232,7 @@ struct Eng {
             wsync();
             if (X && (m0 & M_PEND)) pend_copy(L, P, s, uniu(rdlane(uj, jl)), r);
             if (grew) s.nseg++;
+            if (G) csum_update(L, s, j, max(L.shi, r + 1));
             overflow_fix(L, s, r);
         }
     }
@@ -2257,6 +2413,7 @@ struct Eng {
         if (op.flags & MTR_F_APPEND) set_merge_info(L, P, s, slot, op, dd);
         if (s.collab && !v.local && seq > s.minseq) add_lru_block(L, s, xbs, uint32_t(s.uidnext - 1), seq);
         if (X && lseq > 0) pend_add(L, P, s, slot, -1, PK_INSERT, 0, lseq);  // saveIfLocal, mergeTree.ts:1618-1626
+        if (G) csum_update(L, s, slot, max(L.shi, slot + 1));
         return slot;
     }
 
@@ -2371,7 +2528,10 @@ struct Eng {
         const int ln = lane_id();
         const bool lru = s.collab && !v.local;
         int last_blk = -1;  // leaf-block start of the last touched leaf
-        for (int base = lower_bound_E(L, s, start + 1); base < S; base += 64) {
+        L.wlo = lower_bound_E(L, s, start + 1);
+        L.whi = L.wlo;
+        for (int base = L.wlo; base < S; base += 64) {
+            L.whi = min(base + 64, S);
             const int j = base + ln;
             const bool in = j < S;
             const int jc = min(j, S - 1);  // unconditional (clamped) loads
@@ -2505,9 +2665,7 @@ struct Eng {
         v.ref = uni(L.sc->gen_ref);
         v.client = enc_client(uni(L.sc->gen_client));
         v.local = 0;
-        prefix(L, s, v, P.new_length_calc);
-        const int S = s.nseg;
-        const int len = S > 0 ? (uni(L.E[S - 1]) & EMASK) : 0;
+        const int len = view_scan(L, s, v, P.new_length_calc, 0, 0);
         if (threadIdx.x == 0) {
             mtr_op op = ld_struct<mtr_op>(rec);
             mtr_synth_state st = ld_struct<mtr_synth_state>(L.gst);
@@ -2531,6 +2689,7 @@ struct Eng {
             s.heap_need = 0;
             s.dused = h.dused;
             s.holes = G ? h.holes : 0;
+            s.chunked = G ? h.chunked : 0;
             s.ops_done = 0;
             s.sum_s = 0;
             s.sum_l = 0;
@@ -2604,7 +2763,10 @@ struct Eng {
             h.texthalf = s.texthalf;
             h.heap_need = s.heap_need;
             h.dused = s.dused;
-            if (G) h.holes = s.holes;
+            if (G) {
+                h.holes = s.holes;
+                h.chunked = s.chunked;
+            }
             st_struct(hp, h);
             if (GN) st_struct(gp(P.gen_state) + d, ld_struct<mtr_synth_state>(L.gst));
 #ifdef MTR_PROF
@@ -2684,6 +2846,7 @@ struct Eng {
             L.sc->cp[CP_VEQ] = (unsigned long long)P.val_eq;
             L.sc->cp[CP_HDR] = (unsigned long long)(P.hdr + d);
             L.sc->cp[CP_PEND] = (unsigned long long)(P.pend ? P.pend + size_t(d) * kPendRing * 4 : nullptr);
+            L.sc->cp[CP_CSUM] = (unsigned long long)(P.csum ? P.csum + size_t(d) * 2 * (P.segcap / 64 + 1) : nullptr);
         }
         wsync();
     }
@@ -2843,13 +3006,13 @@ struct Eng {
             v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
         }
         // (each op type calls the view scan itself: one hoisted call site measured 2.5 % slower at C3)
-        if (X && op.type == MTR_OP_RELPOS) prefix(L, s, v, P.new_length_calc);
+        if (X && op.type == MTR_OP_RELPOS) view_scan(L, s, v, P.new_length_calc, 0, 0);
         switch (op.type) {
             case MTR_OP_INSERT:
             case MTR_OP_LOCAL_INSERT: {
                 int pos = pos1;
                 if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
-                prefix(L, s, v, P.new_length_calc);
+                view_scan(L, s, v, P.new_length_calc, pos, pos);
                 split_at(L, P, s, pos);
                 insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf, lseq ? sseq : seq, lseq);
                 zop = s.collab && !local_op;
@@ -2860,7 +3023,7 @@ struct Eng {
             case MTR_OP_ANNOTATE:
             case MTR_OP_LOCAL_ANNOTATE: {
                 const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
-                prefix(L, s, v, P.new_length_calc);
+                view_scan(L, s, v, P.new_length_calc, min(pos1, pos2), max(pos1, pos2));
                 split_at(L, P, s, pos1);
                 split_at(L, P, s, pos2);
                 if (X && lseq) {  // pending: removedSeq = LOCAL_BASE + localSeq; the touched leaves join a group
@@ -2871,6 +3034,7 @@ struct Eng {
                     range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
                                op.type == MTR_OP_ANNOTATE ? op.payload2 : 0u, DL && !PM && (op.flags & MTR_F_DELTA) != 0);
                 }
+                if (G && is_remove) csum_update(L, s, L.wlo, L.whi);
                 zop = s.collab && !local_op;
                 break;
             }
@@ -2905,6 +3069,7 @@ struct Eng {
                 int p = -1;
                 if (mu >> 32) {
                     const int x = find_uid(L, s, uint32_t(mu));
+                    if (G && L.rhi > 0 && x > 0) materialize(L, s, v, P.new_length_calc, (x - 1) >> 6, (x - 1) >> 6);
                     p = x > 0 ? (uni(L.E[x - 1]) & EMASK) : 0;
                     const int off = (op.payload2 & MTR_REL_OFFSET) ? int(op.payload) : 0;
                     p = (op.payload2 & MTR_REL_BEFORE) ? p - off : p + 1 + off;

@@ -105,6 +105,7 @@ struct mtr_engine {
     bool pend_seen = false;           // a batch since mtr_reset held local ops while collaborating or acks:
                                       // documents may hold pending segments, so every launch is an X kernel
     DevBuf<uint32_t> pend;            // [doc][kPendRing][4] pending SegmentGroups (allocated on first use)
+    DevBuf<int32_t> csum;             // [doc][2][segcap / 64 + 1] chunk summaries (first HBM-resident launch)
     DevBuf<int32_t> red;              // small reduction / query-result buffer
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
@@ -319,6 +320,7 @@ int mtr_engine_destroy(mtr_engine* e) {
         b->release();
     e->hdr.release();
     e->pend.release();
+    e->csum.release();
     e->text.release();
     e->btext.release();
     e->docs.release();
@@ -645,6 +647,11 @@ static int run_impl(mtr_engine* e, int gen) {
             if (lds > lds_limit) {
                 // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
                 if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
+                if (!e->csum.p) {  // for every document the engine may hold: it must never move
+                    const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * (size_t(P.segcap) / 64 + 1);
+                    if (e->csum.ensure(n)) return -1;
+                }
+                P.csum = e->csum.p;
                 P.global_mode = 1;
                 P.scratch = e->scratch.p;
                 cap = P.segcap;
