@@ -204,6 +204,7 @@ struct KParams {
     unsigned long long* prof;    // [P_COUNT] phase-timer sums (-DMTR_PROF builds)
     uint32_t* pend;              // [doc][kPendRing][4] pending SegmentGroups (batches with local ops only)
     int32_t* csum;               // [doc][2][segcap / 64 + 1] chunk summaries of HBM-resident documents
+    int32_t* umap;               // [doc][2 * segcap] uid -> slot hints of HBM-resident documents
 };
 
 // phase-timer slots (-DMTR_PROF builds)
@@ -215,7 +216,8 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
 // records, the batch's property tables), kept in LDS and read where used, so they never hold SGPRs
 // across the whole op loop (the loop's scalar state otherwise spills into VGPR lanes)
-enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_HDR, CP_PEND, CP_CSUM, CP_N };
+enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_HDR, CP_PEND, CP_CSUM, CP_UMAP,
+       CP_N };
 
 // LDS-side scratch of one document: record-mode broadcast, cold pointers, phase timers
 struct Sc {
@@ -274,6 +276,7 @@ struct Doc {
     MTR_DI gptr<DocHdr> ghdr() const { return (gptr<DocHdr>)cold(CP_HDR); }      // this document's header
     MTR_DI gptr<uint32_t> gpend() const { return (gptr<uint32_t>)cold(CP_PEND); }  // its pending-group ring
     MTR_DI gptr<int> gcsum() const { return (gptr<int>)cold(CP_CSUM); }          // chunk summaries (len, then ev)
+    MTR_DI gptr<int> gumap() const { return (gptr<int>)cold(CP_UMAP); }          // uid -> slot hints
     int rlo = 0, rhi = 0;  // the op's view-scan region (slots) when the scan was two-level (E valid there)
     int shi = 0;           // end of the slots the last shift_right1 moved (chunk-summary upkeep)
     int wlo = 0, whi = 0;  // slots the last range walk touched
@@ -890,6 +893,7 @@ struct Eng {
                     if (act[q]) {
                         L.len[i + 1] = a0[q]; L.seq[i + 1] = a1[q]; L.rseq[i + 1] = a2[q]; L.meta[i + 1] = a3[q];
                         L.text[i + 1] = a4[q]; L.props[i + 1] = a5[q]; L.uid[i + 1] = a7[q]; L.E[i + 1] = a8[q];
+                        if (s.chunked) hint(L, a7[q], i + 1);
                     }
                 }
                 wsync();
@@ -970,6 +974,14 @@ struct Eng {
         if (base == 0) s.height = 1;
     }
 
+    // uid -> slot hint of a chunked document (find_uid checks it before scanning; a stale hint only costs
+    // the scan)
+    static MTR_DI void hint(const D& L, uint32_t u, int i) {
+        if constexpr (G) {
+            if (u < uint32_t(2 * L.cap)) L.gumap()[u] = i;
+        }
+    }
+
     // ---- hole slots (HBM-resident documents of >= kGapMin leaves): a hole is a slot with M_DEL, no
     // length, no uid and removedSeq 0 -- undefined in every view (vis_hot), skipped by every walk,
     // scour and summary; shifts take the next hole (shift_right1), zamboni leaves its deleted leaves
@@ -1025,6 +1037,7 @@ struct Eng {
                 const int d = i + i / (kGapEvery - 1);
                 L.len[d] = a0; L.seq[d] = a1; L.rseq[d] = a2; L.meta[d] = a3;
                 L.text[d] = a4; L.props[d] = a5; L.uid[d] = a7;
+                if (L.gumap()) hint(L, a7, d);
             }
             wsync();
         }
@@ -1043,6 +1056,10 @@ struct Eng {
         PROF(P_FINDUID);
         const int S = s.nseg;
         if constexpr (G) {  // one word per leaf: 4 * GK rounds of loads in flight
+            if (s.chunked && u < uint32_t(2 * L.cap)) {  // the slot hint, verified
+                const int h = uni(L.gumap()[u]);
+                if (h >= 0 && h < S && uniu(L.uid[h]) == u) return h;
+            }
             constexpr int FK = 4 * GK;
             for (int base = 0; base < S; base += 64 * FK) {
                 uint32_t uk[FK];
@@ -2222,6 +2239,7 @@ struct Eng {
             L.props[r] = rdlane(pj, jl);
             const uint32_t ur = uint32_t(s.uidnext++);
             L.uid[r] = ur;
+            if (G && s.chunked && lane_id() == 0) hint(L, ur, r);
             if (m0 & M_OVERLAP) {  // the right half shares the remover list
                 if (lane_id() == 0 && !rm_set(L, ur, rm_get(L, rdlane(uj, jl)))) s.status = MTR_ERR_CAPACITY;
                 s.status = uni(s.status);
@@ -2402,6 +2420,7 @@ struct Eng {
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
         L.props[slot] = pr;
         L.uid[slot] = uint32_t(s.uidnext++);
+        if (G && s.chunked && lane_id() == 0) hint(L, uint32_t(s.uidnext - 1), slot);
         if (X && marker && op.payload2 != 0) {  // mapIdToSegment (mergeTree.ts:1655-1662)
             if (lane_id() == 0 && !mk_set(L, op.payload2 - 1, uint32_t(s.uidnext - 1))) s.status = MTR_ERR_CAPACITY;
             s.status = uni(s.status);
@@ -2847,6 +2866,7 @@ struct Eng {
             L.sc->cp[CP_HDR] = (unsigned long long)(P.hdr + d);
             L.sc->cp[CP_PEND] = (unsigned long long)(P.pend ? P.pend + size_t(d) * kPendRing * 4 : nullptr);
             L.sc->cp[CP_CSUM] = (unsigned long long)(P.csum ? P.csum + size_t(d) * 2 * (P.segcap / 64 + 1) : nullptr);
+            L.sc->cp[CP_UMAP] = (unsigned long long)(P.umap ? P.umap + size_t(d) * 2 * P.segcap : nullptr);
         }
         wsync();
     }

@@ -106,6 +106,7 @@ struct mtr_engine {
                                       // documents may hold pending segments, so every launch is an X kernel
     DevBuf<uint32_t> pend;            // [doc][kPendRing][4] pending SegmentGroups (allocated on first use)
     DevBuf<int32_t> csum;             // [doc][2][segcap / 64 + 1] chunk summaries (first HBM-resident launch)
+    DevBuf<int32_t> umap;             // [doc][2 * segcap] uid -> slot hints (with csum)
     DevBuf<int32_t> red;              // small reduction / query-result buffer
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
@@ -321,6 +322,7 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->hdr.release();
     e->pend.release();
     e->csum.release();
+    e->umap.release();
     e->text.release();
     e->btext.release();
     e->docs.release();
@@ -650,8 +652,11 @@ static int run_impl(mtr_engine* e, int gen) {
                 if (!e->csum.p) {  // for every document the engine may hold: it must never move
                     const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * (size_t(P.segcap) / 64 + 1);
                     if (e->csum.ensure(n)) return -1;
+                    if (e->umap.ensure(size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * size_t(P.segcap))) return -1;
+                    HIPCHK(hipMemsetAsync(e->umap.p, 0xff, e->umap.n * sizeof(int32_t), e->stream));
                 }
                 P.csum = e->csum.p;
+                P.umap = e->umap.p;
                 P.global_mode = 1;
                 P.scratch = e->scratch.p;
                 cap = P.segcap;
