@@ -18,6 +18,7 @@ OP_SETCELL = 14
 OP_RELPOS = 15
 OP_HANDLES = 16
 OP_ACK = 17
+OP_ROLLBACK = 18
 REL_BEFORE = 1
 REL_OFFSET = 2
 COMB_NONE, COMB_REWRITE, COMB_INCR, COMB_CONSENSUS, COMB_KEEP = 0, 1, 2, 3, 4

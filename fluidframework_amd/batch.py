@@ -335,6 +335,19 @@ class DocLog:
             self.marker_id_annotated = True
         self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, self._local_seq(), 0, 0, start, end, interner.propop(props), 0))
 
+    def rollback(self, op: dict, interner: Interner) -> None:
+        """Client.rollback (client.ts:421-423 -> MergeTree.rollback, mergeTree.ts:2049-2159) of the newest
+        pending local op `op` (its contents)."""
+        t = op.get("type")
+        pp = 0
+        if t == 2:
+            if js_truthy(op.get("combiningOp")):
+                raise Unsupported("rollback of a combining annotate")
+            pp = interner.propop(op.get("props") or {})
+        elif t not in (0, 1):
+            raise Unsupported(f"rollback of op type {t}")
+        self.ops.append((abi.OP_ROLLBACK, 0, 0, -1, 0, 0, 0, 0, pp, t))
+
     def local_op(self, op: dict, interner: Interner) -> None:
         """A local merge-tree op (the contents this client submits): insert / remove / annotate."""
         t = op.get("type")

@@ -147,7 +147,7 @@ struct DocHdr {
     int32_t phead, ptail;  // pending SegmentGroups: ring entries [phead, ptail) (MergeTree.pendingSegments)
     int32_t holes;         // HBM-resident documents: hole slots among the nseg leaf slots (see Eng::spread)
     int32_t chunked;       // ... and their per-64-slot chunk summaries are valid (two-level view scan)
-    int32_t pad;
+    int32_t pfree;         // free list of pending-membership cells (first cell + 1, 0 = empty)
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -1291,7 +1291,8 @@ struct Eng {
 
     // addToPendingList (mergeTree.ts:1324-1357) for leaf i (wave-uniform): a new SegmentGroup at the ring's
     // tail when `slot` < 0, then the leaf joins it (segmentGroups.enqueue) with the group's next ordinal
-    static MTR_DI int pend_add(D& L, const KParams& P, St& s, int i, int slot, int kind, uint32_t pp, int lseq) {
+    static MTR_DI int pend_add(D& L, const KParams& P, St& s, int i, int slot, int kind, uint32_t pp, int lseq,
+                               uint32_t oldp = NONE32) {
         const gptr<DocHdr> h = L.ghdr();
         const gptr<uint32_t> ring = L.gpend();
         if (!ring) {
@@ -1315,26 +1316,63 @@ struct Eng {
             wsync();
         }
         const int ord = int(uniu(ring[4 * slot + 1]));
-        if (s.rmused + 2 > P.rcap || ord > 0xffff) {
+        const int fr = uni(h->pfree);  // a cell an ack or a rollback freed, else a new one
+        if ((!fr && s.rmused + 3 > P.rcap) || ord > 0xffff) {
             s.status = MTR_ERR_CAPACITY;
             return slot;
         }
         const uint32_t u = uniu(L.uid[i]);
         const uint32_t m = uniu(L.meta[i]);
-        const uint32_t c = uint32_t(s.rmused);
+        const uint32_t c = fr ? uint32_t(fr - 1) : uint32_t(s.rmused);
+        if (fr) {
+            const uint32_t nf = uniu(L.grm()[c]) & 0xffffffu;
+            if (lane_id() == 0) h->pfree = nf == 0xffffffu ? 0 : int(nf + 1);
+        }
         bool ok = true;
         if (lane_id() == 0) {
             const uint32_t nxt = (m & M_PEND) ? pd_get(L, u) : 0xffffffu;
             L.grm()[c] = (nxt & 0xffffffu) | (uint32_t(kind) << 24);
             L.grm()[c + 1] = (uint32_t(slot) << 16) | uint32_t(ord);
+            L.grm()[c + 2] = oldp;  // a local annotate's previousProps (the set before the op)
             ring[4 * slot + 1] = uint32_t(ord + 1);
             ok = pd_set(L, u, c);
             L.meta[i] = m | M_PEND;
         }
         if (__ballot(!ok)) s.status = MTR_ERR_CAPACITY;
-        s.rmused += 2;
+        if (!fr) s.rmused += 3;
         wsync();
         return slot;
+    }
+
+    // unlink the cell of ring slot `slot` from leaf i's membership list and put it on the free list
+    // (wave-uniform); returns the cell's previousProps word; clears M_PEND when no cell is left
+    static MTR_DI uint32_t pend_drop(D& L, int i, int slot) {
+        const gptr<DocHdr> h = L.ghdr();
+        const uint32_t u = uniu(L.uid[i]);
+        uint32_t c = uniu(pd_get(L, u)), prev = 0xffffffu, oldp = NONE32;
+        int left = 0;
+        while (c != 0xffffffu) {
+            const uint32_t w0 = uniu(L.grm()[c]), w1 = uniu(L.grm()[c + 1]);
+            const uint32_t nx = w0 & 0xffffffu;
+            if (int(w1 >> 16) == slot) {
+                oldp = uniu(L.grm()[c + 2]);
+                const int fr = uni(h->pfree);
+                if (lane_id() == 0) {
+                    if (prev == 0xffffffu) pd_set(L, u, nx);
+                    else L.grm()[prev] = (L.grm()[prev] & 0xff000000u) | nx;
+                    L.grm()[c] = fr ? uint32_t(fr - 1) : 0xffffffu;  // push on the free list
+                    h->pfree = int(c + 1);
+                }
+            } else {
+                prev = c;
+                left++;
+            }
+            wsync();
+            c = nx;
+        }
+        if (!left && lane_id() == 0) L.meta[i] = L.meta[i] & ~M_PEND;
+        wsync();
+        return oldp;
     }
 
     // the leaves a local remove / annotate touched (marked M_TOUCH by range_walk), in leaf (= walk)
@@ -1361,8 +1399,8 @@ struct Eng {
         if (lane_id() == 0) L.meta[r] = L.meta[r] & ~M_PEND;
         wsync();
         while (c != 0xffffffu && s.status == MTR_OK) {
-            const uint32_t w0 = uniu(L.grm()[c]), w1 = uniu(L.grm()[c + 1]);
-            pend_add(L, P, s, r, int(w1 >> 16), int(w0 >> 24), 0, 0);
+            const uint32_t w0 = uniu(L.grm()[c]), w1 = uniu(L.grm()[c + 1]), w2 = uniu(L.grm()[c + 2]);
+            pend_add(L, P, s, r, int(w1 >> 16), int(w0 >> 24), 0, 0, w2);  // (previousProps duplicated)
             c = w0 & 0xffffffu;
         }
     }
@@ -1393,33 +1431,22 @@ struct Eng {
         const int slot = head % kPendRing;
         const int cnt = int(uniu(ring[4 * slot + 1]));
         if (lane_id() == 0) h->phead = head + 1;
-        // the group's members: each leaf holding a cell of this slot drops it; E[ordinal] = leaf
+        // the group's members: E[ordinal] = leaf
         for (int base = 0; base < s.nseg; base += 64) {
             const int i = base + lane_id();
             const int ic = min(i, s.nseg - 1);
             const uint32_t m = L.meta[ic];
             if (i < s.nseg && (m & M_PEND)) {
-                const uint32_t u = L.uid[i];
-                uint32_t c = pd_get(L, u), prev = 0xffffffu, nlive = 0;
-                while (c != 0xffffffu) {
-                    const uint32_t w0 = L.grm()[c], w1 = L.grm()[c + 1];
-                    const uint32_t nx = w0 & 0xffffffu;
-                    if (int(w1 >> 16) == slot) {
-                        L.E[int(w1 & 0xffffu)] = i;
-                        if (prev == 0xffffffu) pd_set(L, u, nx);
-                        else L.grm()[prev] = (L.grm()[prev] & 0xff000000u) | nx;
-                    } else {
-                        prev = c;
-                        nlive++;
-                    }
-                    c = nx;
+                for (uint32_t c = pd_get(L, L.uid[i]); c != 0xffffffu; c = L.grm()[c] & 0xffffffu) {
+                    const uint32_t w1 = L.grm()[c + 1];
+                    if (int(w1 >> 16) == slot) L.E[int(w1 & 0xffffu)] = i;
                 }
-                if (!nlive) L.meta[i] = m & ~M_PEND;
             }
         }
         wsync();
-        for (int o = 0; o < cnt && s.status == MTR_OK; o++) {  // in group order
+        for (int o = 0; o < cnt && s.status == MTR_OK; o++) {  // in group order: drop the cell, then ack
             const int i = uni(L.E[o]);
+            pend_drop(L, i, slot);
             if (type == MTR_OP_INSERT) {
                 if (uni(L.seq[i]) < LOCAL_BASE) s.status = MTR_ERR_ASSERT | 0x045;  // seq already assigned
                 else if (lane_id() == 0) L.seq[i] = seq;
@@ -1435,6 +1462,137 @@ struct Eng {
             int bs, be;
             block_bounds1(L, s, i, bs, be);
             add_lru_block(L, s, bs, uniu(L.uid[i]), seq);  // mergeTree.ts:1299-1301
+        }
+    }
+
+    // a copy of set `cur` with each key of prop-op pp set to its value in set `old`, or deleted where
+    // `old` lacks it (annotate rollback: the op's previousProps, mergeTree.ts:2129-2152); out of line (rare)
+    static __device__ __attribute__((noinline)) uint32_t props_restore(const D& L, const KParams& P, St& s,
+                                                                      uint32_t cur, uint32_t old, uint32_t pp) {
+        const gptr<uint32_t> gprop = L.gprop();
+        const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX),
+                                   veq = L.tab(CP_VEQ);
+        cur = cur == NONE32 ? cur : (cur & PN_MASK);
+        old = old == NONE32 ? old : (old & PN_MASK);
+        const uint32_t n_cur = cur == NONE32 ? 0u : uniu(gprop[cur]);
+        const uint32_t n_old = old == NONE32 ? 0u : uniu(gprop[old]);
+        const uint32_t lo = uniu(poff[pp]), hi = uniu(poff[pp + 1]);
+        const uint32_t need = 1 + 2 * (n_cur + (hi - lo));
+        if (uint32_t(s.propused) + need > uint32_t(P.pcap)) {
+            s.status = MTR_ERR_CAPACITY;
+            return cur;
+        }
+        const uint32_t dst = uint32_t(s.propused);
+        const gptr<uint32_t> e = gprop + dst;
+        uint32_t n = n_cur;
+        for (uint32_t k = 0; k < 2 * n_cur; k++) e[1 + k] = uniu(gprop[cur + 1 + k]);
+        for (uint32_t q = lo; q < hi; q++) {
+            const uint32_t key = uniu(pkv[2 * q]);
+            uint32_t val = MTR_NULL_VALUE;
+            for (uint32_t k = 0; k < n_old; k++)
+                if (uniu(gprop[old + 1 + 2 * k]) == key) {
+                    val = uniu(gprop[old + 2 + 2 * k]);
+                    break;
+                }
+            int at = -1;
+            for (uint32_t k = 0; k < n; k++)
+                if (uniu(e[1 + 2 * k]) == key) {
+                    at = int(k);
+                    break;
+                }
+            if (val == MTR_NULL_VALUE) {
+                if (at >= 0) {
+                    for (uint32_t k = uint32_t(at); k + 1 < n; k++) {
+                        e[1 + 2 * k] = uniu(e[1 + 2 * (k + 1)]);
+                        e[2 + 2 * k] = uniu(e[2 + 2 * (k + 1)]);
+                    }
+                    n--;
+                }
+            } else if (at >= 0) {
+                e[2 + 2 * at] = val;
+            } else {  // a new key in JS own-key order
+                const uint32_t ix = uniu(kix[key]);
+                uint32_t pos = n;
+                if (ix != MTR_NOT_INDEX) {
+                    pos = 0;
+                    while (pos < n && uniu(kix[uniu(e[1 + 2 * pos])]) != MTR_NOT_INDEX &&
+                           uniu(kix[uniu(e[1 + 2 * pos])]) < ix)
+                        pos++;
+                    for (uint32_t k = n; k > pos; k--) {
+                        e[1 + 2 * k] = uniu(e[1 + 2 * (k - 1)]);
+                        e[2 + 2 * k] = uniu(e[2 + 2 * (k - 1)]);
+                    }
+                }
+                e[1 + 2 * pos] = key;
+                e[2 + 2 * pos] = val;
+                n++;
+            }
+        }
+        uint32_t never = 0;
+        for (uint32_t k = 0; k < n; k++)
+            if (uniu(veq[uniu(e[2 + 2 * k])]) & MTR_VEQ_NEVER) never = MTR_PROPS_NEVER;
+        e[0] = n;
+        s.propused += int(1 + 2 * n);
+        wsync();
+        return dst | never;
+    }
+
+    // MergeTree.rollback (mergeTree.ts:2049-2159): revert the newest pending local op (type: its
+    // MergeTreeDeltaType; pp: its prop-op for an annotate).  The group leaves the ring's tail; each member
+    // (in group order) drops its cell and is reverted: a remove is undone, an insert becomes a segment
+    // removed at UniversalSequenceNumber by this client (markRangeRemoved, :2117-2131), an annotate's keys
+    // get their previous values back
+    static MTR_DI void rollback(D& L, const KParams& P, St& s, int type, uint32_t pp) {
+        const gptr<DocHdr> h = L.ghdr();
+        const gptr<uint32_t> ring = L.gpend();
+        const int head = uni(h->phead), tail = uni(h->ptail);
+        if (head == tail || !ring) {  // "Rollback op doesn't match last edit"
+            s.status = MTR_ERR_BAD_OP;
+            return;
+        }
+        const int slot = (tail - 1) % kPendRing;
+        const int cnt = int(uniu(ring[4 * slot + 1]));
+        if (lane_id() == 0) h->ptail = tail - 1;
+        for (int base = 0; base < s.nseg; base += 64) {  // E[ordinal] = member leaf
+            const int i = base + lane_id();
+            const uint32_t m = L.meta[min(i, s.nseg - 1)];
+            if (i < s.nseg && (m & M_PEND)) {
+                for (uint32_t c = pd_get(L, L.uid[i]); c != 0xffffffu; c = L.grm()[c] & 0xffffffu) {
+                    const uint32_t w1 = L.grm()[c + 1];
+                    if (int(w1 >> 16) == slot) L.E[int(w1 & 0xffffu)] = i;
+                }
+            }
+        }
+        wsync();
+        for (int o = 0; o < cnt && s.status == MTR_OK; o++) {
+            const int i = uni(L.E[o]);
+            const uint32_t oldp = pend_drop(L, i, slot);  // segmentGroups.pop()
+            uint32_t m = uniu(L.meta[i]);
+            if (type == MTR_OP_REMOVE) {
+                const int rs = uni(L.rseq[i]);
+                if (rs == RNONE || rs < LOCAL_BASE || ((m >> M_FREM_SHIFT) & 0xffu) != uint32_t(s.local)) {
+                    s.status = MTR_ERR_ASSERT | 0x39d;  // the removal is not (only) this client's pending one
+                    break;
+                }
+                m &= ~((0xffu << M_FREM_SHIFT) | M_OVERLAP);
+                if (lane_id() == 0) L.rseq[i] = RNONE;
+            } else if (type == MTR_OP_INSERT) {
+                const bool live = uni(L.rseq[i]) == RNONE;  // (a removed one is not walked again)
+                if (live) m = (m & ~((0xffu << M_FREM_SHIFT) | M_OVERLAP)) | (uint32_t(s.local) << M_FREM_SHIFT);
+                if (lane_id() == 0) {
+                    L.seq[i] = 0;
+                    if (live) L.rseq[i] = 0;
+                }
+            } else if (type == MTR_OP_ANNOTATE) {
+                const uint32_t np = props_restore(L, P, s, uniu(L.props[i]), oldp, pp);
+                if (lane_id() == 0) L.props[i] = np;
+            } else {
+                s.status = MTR_ERR_BAD_OP;
+                break;
+            }
+            if (lane_id() == 0) L.meta[i] = m;
+            wsync();
+            if (G) csum_update(L, s, i, i + 1);
         }
     }
 
@@ -2538,7 +2696,7 @@ struct Eng {
     // The walk stops at the first leaf whose view start (E - max(V,0), nondecreasing) is >= end.
     static MTR_DI void range_walk(D& L, const KParams& P, St& s, const View& v, int start, int end, int seq,
                                   uint32_t client, int is_remove, uint32_t pp, uint32_t comb, bool dl,
-                                  bool pending = false) {
+                                  bool pending = false, int plseq = 0) {
         // (pending: a local op while collaborating -- its leaves are marked M_TOUCH for pend_touched and
         // every key applies; remote ops leave keys with pending local updates alone)
         PROF(P_RANGE);
@@ -2547,6 +2705,7 @@ struct Eng {
         const int ln = lane_id();
         const bool lru = s.collab && !v.local;
         int last_blk = -1;  // leaf-block start of the last touched leaf
+        int pslot = -1;     // the pending annotate's group (created with its first segment)
         L.wlo = lower_bound_E(L, s, start + 1);
         L.whi = L.wlo;
         for (int base = L.wlo; base < S; base += 64) {
@@ -2634,6 +2793,14 @@ struct Eng {
                     if (dl && act) {  // every annotated segment is a delta segment
                         mj |= M_TOUCH;
                         L.meta[j] = mj;
+                    }
+                    if (X && pending) {  // addToPendingList with previousProps, in walk order (mergeTree.ts:1921-1930)
+                        wsync();
+                        for (uint64_t t = am; t && s.status == MTR_OK; t &= t - 1) {
+                            const int l = first_lane(t);
+                            pslot = pend_add(L, P, s, base + l, pslot, PK_ANNOTATE, pp, plseq, rdlane(old, l));
+                        }
+                        mj = L.meta[jc];
                     }
                 }
                 wsync();
@@ -3047,9 +3214,9 @@ struct Eng {
                 split_at(L, P, s, pos1);
                 split_at(L, P, s, pos2);
                 if (X && lseq) {  // pending: removedSeq = LOCAL_BASE + localSeq; the touched leaves join a group
-                    range_walk(L, P, s, v, pos1, pos2, sseq, client, is_remove, op.payload, 0u, true, true);
-                    if (s.status == MTR_OK)
-                        pend_touched(L, P, s, is_remove ? PK_REMOVE : PK_ANNOTATE, is_remove ? 0u : op.payload, lseq);
+                    range_walk(L, P, s, v, pos1, pos2, sseq, client, is_remove, op.payload, 0u, is_remove != 0, true,
+                               lseq);
+                    if (s.status == MTR_OK && is_remove) pend_touched(L, P, s, PK_REMOVE, 0u, lseq);
                 } else {
                     range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
                                op.type == MTR_OP_ANNOTATE ? op.payload2 : 0u, DL && !PM && (op.flags & MTR_F_DELTA) != 0);
@@ -3059,6 +3226,13 @@ struct Eng {
                 break;
             }
             case MTR_OP_SEQ:
+                break;
+            case MTR_OP_ROLLBACK:  // Client.rollback (client.ts:421-423) of the newest pending local op
+                if (!X || !s.collab) {
+                    s.status = MTR_ERR_BAD_OP;
+                    break;
+                }
+                rollback(L, P, s, int(op.payload2), op.payload);
                 break;
             case MTR_OP_ACK:  // Client.applyMsg of this client's own message (client.ts:866-869)
                 if (!X || !s.collab) {

@@ -173,7 +173,7 @@ __global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const mtr_op op = ops[i];
         any = any || (op.flags & MTR_F_DELTA) != 0;
-        pend = pend || op.type == MTR_OP_ACK ||
+        pend = pend || op.type == MTR_OP_ACK || op.type == MTR_OP_ROLLBACK ||
                (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE && op.seq == -1);
         ext = ext || op.type == MTR_OP_RELPOS || op.type == MTR_OP_HANDLES || (op.flags & MTR_F_REL) ||
               (op.type == MTR_OP_ANNOTATE && op.payload2 != 0) ||

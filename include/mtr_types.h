@@ -53,6 +53,9 @@ enum {
                                    mergeTree.ts:1283-1322): acks the oldest pending SegmentGroup; payload2 =
                                    the member's MergeTreeDeltaType (segment.ack switches on it,
                                    mergeTreeNodes.ts:439-479), payload = its prop-op for an annotate */
+    MTR_OP_ROLLBACK = 18,       /* Client.rollback (client.ts:421 -> MergeTree.rollback, mergeTree.ts:2049-2159) of the
+                                   newest pending local op: payload2 = its MergeTreeDeltaType, payload = its
+                                   prop-op (annotate) */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for

@@ -100,6 +100,10 @@ struct Seg : Node {
 struct SegGroup {
     std::vector<Seg*> segments;
     int localSeq = 0;
+    // a local annotate's previousProps (mergeTree.ts:1330-1351): each member's properties before the op
+    // (the deltas of the op's keys derive from them), parallel to `segments`
+    bool hasPrevious = false;
+    std::vector<std::pair<bool, PropMap>> previousProps;
 };
 
 struct PSL;
@@ -413,6 +417,12 @@ class Tree {
         r->seq = s->seq;
         r->clientId = s->clientId;
         for (SegGroup* g : s->groups) {  // segmentGroups.copyTo -> enqueueOnCopy (segmentGroupCollection.ts:47-62)
+            if (g->hasPrevious)  // previousProps of the source segment, duplicated for the copy
+                for (size_t k = 0; k < g->segments.size(); k++)
+                    if (g->segments[k] == s) {
+                        g->previousProps.push_back(g->previousProps[k]);
+                        break;
+                    }
             r->groups.push_back(g);
             g->segments.push_back(r);
         }
@@ -436,6 +446,83 @@ class Tree {
         for (auto& kc : s->pendingKeys)
             if (kc.first == key) return &kc.second;
         return nullptr;
+    }
+
+    // findRollbackPosition (mergeTree.ts:2164-2181): the cachedLengths of the segments ahead that are not
+    // removed (a pending local remove counts as removed)
+    int findRollbackPosition(Seg* seg) {
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        int pos = 0;
+        for (Seg* x : lv) {
+            if (x == seg) break;
+            if (!x->removed) pos += x->len;
+        }
+        return pos;
+    }
+
+    // MergeTree.rollback (mergeTree.ts:2049-2159): revert the newest pending local op (type = its
+    // MergeTreeDeltaType; propop = its props for an annotate)
+    void rollback(int type, uint32_t propop) {
+        if (pendingSegments.empty()) {
+            status = MTR_ERR_BAD_OP;  // "Rollback op doesn't match last edit"
+            return;
+        }
+        SegGroup* g = pendingSegments.back();
+        if (type == MTR_OP_ANNOTATE && !g->hasPrevious) {
+            status = MTR_ERR_BAD_OP;
+            return;
+        }
+        pendingSegments.pop_back();
+        for (size_t k = 0; k < g->segments.size(); k++) {
+            Seg* s = g->segments[k];
+            if (s->groups.empty() || s->groups.back() != g) {  // segmentGroups.pop()
+                status = MTR_ERR_ASSERT | (type == MTR_OP_REMOVE ? 0x3ee : 0x3ef);
+                return;
+            }
+            s->groups.pop_back();
+            if (type == MTR_OP_REMOVE) {
+                if (!s->removed || s->removedClientIds.empty() || s->removedClientIds[0] != localClientId) {
+                    status = MTR_ERR_ASSERT | 0x39d;
+                    return;
+                }
+                s->removed = false;
+                s->removedSeq = 0;
+                s->removedClientIds.clear();
+            } else if (type == MTR_OP_INSERT) {
+                const int start = findRollbackPosition(s);
+                s->seq = kUniversalSeq;
+                markRangeRemoved(start, start + s->len, kUniversalSeq, localClientId, kUniversalSeq);
+            } else if (type == MTR_OP_ANNOTATE) {
+                // annotateRange(start, start + cachedLength, previousProps[k], ..., UniversalSequenceNumber,
+                // PropertiesRollback.Rollback): the walk at the segment's own local-view range reaches only
+                // it; addProperties then drops the op keys' pending counts and restores their values
+                const mtr_batch* b = tabs.b;
+                const auto& prev = g->previousProps[k];
+                s->hasPropMgr = true;
+                s->hasProps = true;
+                for (uint32_t q = b->propop_off[propop]; q < b->propop_off[propop + 1]; q++) {
+                    const uint32_t key = b->propop_kv[2 * q];
+                    if (int* c = pendingCount(s, key)) {  // decrementPendingCounts (:37-58)
+                        if (--*c == 0)
+                            for (size_t j = 0; j < s->pendingKeys.size(); j++)
+                                if (s->pendingKeys[j].first == key) {
+                                    s->pendingKeys.erase(s->pendingKeys.begin() + j);
+                                    break;
+                                }
+                    }
+                    const std::pair<uint32_t, uint32_t>* pv = nullptr;
+                    if (prev.first)
+                        for (auto& kv : prev.second.kv)
+                            if (kv.first == key) pv = &kv;
+                    if (pv) propSet(s->props, key, pv->second, tabs);
+                    else propDelete(s->props, key);
+                }
+            } else {
+                status = MTR_ERR_BAD_OP;
+                return;
+            }
+        }
     }
 
     // MergeTree.ackPendingSegment (mergeTree.ts:1283-1322) for one member op of this client's sequenced
@@ -1053,11 +1140,17 @@ class Tree {
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
+                const std::pair<bool, PropMap> before{s->hasProps, s->props};
                 addProperties(s, propop, comb, seq, collaborating);
                 touched.push_back(s);
                 if (collaborating) {  // mergeTree.ts:1921-1935
-                    if (seq == kUnassignedSeq) group = addToPendingList(s, group, localSeq);
-                    else addToLRUSet(s, seq);
+                    if (seq == kUnassignedSeq) {
+                        group = addToPendingList(s, group, localSeq);
+                        group->hasPrevious = true;  // addToPendingList's previousProps (:1330-1351)
+                        group->previousProps.push_back(before);
+                    } else {
+                        addToLRUSet(s, seq);
+                    }
                 }
             },
             start, end);
@@ -1182,6 +1275,10 @@ class Tree {
                 if (op.payload2 != MTR_COMB_NONE) return MTR_ERR_UNSUPPORTED;  // pending combining ops
                 annotateRange(op.pos1, op.pos2, op.payload, currentSeq, localClientId,
                               collaborating ? kUnassignedSeq : kUniversalSeq);
+                return status;
+            case MTR_OP_ROLLBACK:  // Client.rollback (client.ts:421-423) of the newest pending local op
+                if (!collaborating) return MTR_ERR_BAD_OP;
+                rollback(int(op.payload2), op.payload);
                 return status;
             case MTR_OP_ACK:  // Client.applyMsg of this client's own message (client.ts:866-869)
                 if (!collaborating) return MTR_ERR_BAD_OP;
