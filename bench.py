@@ -360,8 +360,9 @@ def main():
             "bytes_per_step": b2_step,
             "achieved_span": round(b2_step / apply_s / 1e9, 3) if apply_s > 0 else 0.0,
             "frac_span": round(b2_step / apply_s / 1e9 / HBM_PEAK_GBS, 5) if apply_s > 0 else 0.0,
-            "note": "the engine runs a flat pass (HBM-resident leaves, one scan and shift per op), so the "
-                    "two-level model prices work it does not avoid yet",
+            "note": "SURVEY 8d's model; the engine's own two-level pass reads 8 B of chunk summary per 64 slots "
+                    "and rescans only chunks with events after the op's refSeq (DESIGN.md 2), so the flat-pass "
+                    "frac prices leaf reads it no longer makes",
         }
 
     e2e = None
