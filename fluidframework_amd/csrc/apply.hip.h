@@ -2231,13 +2231,16 @@ struct Eng {
             kept = re1 - rs1 <= 64 ? scour_par(L, P, s, rs1, re1) : -1;
             if (kept < 0) kept = scour_range(L, P, s, rs1, re1);
         }
-        {  // block.needsScour = false, kept on the block's first surviving leaf
-            const int i = rs1 + lane_id();
+        // block.needsScour = false, kept on the block's first surviving leaf (a block of an HBM-resident
+        // document can span more than 64 slots: holes)
+        for (int b = rs1; b < re1; b += 64) {
+            const int i = b + lane_id();
             const uint64_t m = __ballot(i < re1 && !(L.meta[min(i, re1 - 1)] & M_DEL));
             if (m) {
-                const int first = rs1 + first_lane(m);
+                const int first = b + first_lane(m);
                 L.meta[first] = set_ns(set_bnd(uniu(L.meta[first]), topb1), NS_FALSE);
                 wsync();
+                break;
             }
         }
         if (kept >= before) return -1;
@@ -2500,18 +2503,25 @@ struct Eng {
                             om = uint32_t(rdlane(int(mw), bs - i + 31));
                             om_known = true;
                         }
-                    } else {  // a bound outside the window
+                    } else {  // a bound outside the window (a block can span more than 64 slots: holes)
                         const int bs = block_start(L, i, 1), be = block_end(L, s, i, 1);
-                        const int j = i + ln;
-                        bool c = false;
-                        if (j < be) {
-                            const int ej = L.E[j];
-                            const int vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
-                            c = vj >= 0 && ((ej & EMASK) > pos || (vj == 0 && seq > L.seq[j]));
+                        slot = be;
+                        nocand = true;
+                        for (int jb = i; jb < be; jb += 64) {
+                            const int j = jb + ln;
+                            bool c = false;
+                            if (j < be) {
+                                const int ej = L.E[j];
+                                const int vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
+                                c = vj >= 0 && ((ej & EMASK) > pos || (vj == 0 && seq > L.seq[j]));
+                            }
+                            const uint64_t cm = __ballot(c);
+                            if (cm) {
+                                slot = jb + first_lane(cm);
+                                nocand = false;
+                                break;
+                            }
                         }
-                        const uint64_t cm = __ballot(c);
-                        slot = cm ? i + first_lane(cm) : be;
-                        nocand = !cm;
                         inherit = slot == bs ? 1 : 0;
                     }
                 }
@@ -2524,16 +2534,20 @@ struct Eng {
             int b0 = slot;
             for (;;) {
                 const int b1 = block_end(L, s, b0, 1);
-                const int j = b0 + ln;
-                bool c = false;
-                if (j < b1) {
-                    const int ej = L.E[j];
-                    const int vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
-                    c = vj >= 0 && ((ej & EMASK) > pos || (vj == 0 && seq > L.seq[j]));
+                int found = -1;
+                for (int jb = b0; jb < b1 && found < 0; jb += 64) {
+                    const int j = jb + ln;
+                    bool c = false;
+                    if (j < b1) {
+                        const int ej = L.E[j];
+                        const int vj = ev(ej, j > 0 ? L.E[j - 1] : 0);
+                        c = vj >= 0 && ((ej & EMASK) > pos || (vj == 0 && seq > L.seq[j]));
+                    }
+                    const uint64_t cm = __ballot(c);
+                    if (cm) found = jb + first_lane(cm);
                 }
-                const uint64_t cm = __ballot(c);
-                if (cm) {
-                    slot = b0 + first_lane(cm);
+                if (found >= 0) {
+                    slot = found;
                     inherit = slot == b0 ? 1 : 0;
                     break;
                 }

@@ -198,7 +198,8 @@ def test_summarize_load_continue_on_device():
         assert eng.summary(n + d) == orcs[d].summarize(b, n + d)
 
 
-@pytest.mark.parametrize("n,grow,ops", [(8, 20000, 2000), (2, 200000, 300)], ids=["20k-segments", "200k-segments"])
+@pytest.mark.parametrize("n,grow,ops", [(8, 20000, 2000), (4, 20000, 12000), (2, 200000, 300)],
+                         ids=["20k-segments", "20k-segments-long", "200k-segments"])
 def test_c5_shaped_hbm_resident(n, grow, ops):
     """Config C5's shape: documents pre-grown through a summary load (20k, and C5's
     full 200k header segments, reloadFromSegments), then 64 writers with lags up to 4096 keeping the
