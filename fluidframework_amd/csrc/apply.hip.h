@@ -717,7 +717,9 @@ struct Eng {
                 const int total = prefix2(L, s, v, newlen);
                 const int nch = (s.nseg + 63) >> 6;
                 const int c0 = max(0, chunk_of(L, nch, p_lo) - 1);
-                const int c1 = min(nch - 1, chunk_of(L, nch, p_hi) + 2);
+                // (to the chunk of the first leaf past p_hi: chunks with no length in the view -- runs of
+                // holes, leaves removed for it -- may lie between, and breakTie's candidates reach that leaf)
+                const int c1 = min(nch - 1, chunk_of(L, nch, p_hi + 1) + 2);
                 materialize(L, s, v, newlen, c0, c1);
                 L.rlo = c0 * 64;
                 L.rhi = (c1 + 1) * 64;

@@ -32,7 +32,7 @@ def piece(lo, hi):
 
 
 def fresh():
-    eng = Engine(1, max_segments=grow + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
+    eng = Engine(1, max_segments=grow + grow // 14 + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
                  text_units=2 * (int(cfg.text_cap) + 8192), prop_words=1 << 16, remover_cells=1 << 14,
                  ops_per_launch=256)
     return eng, OracleDoc(options())

@@ -232,6 +232,29 @@ def test_c5_shaped_hbm_resident(n, grow, ops):
         assert eng.summary(d) == orc.summarize(b, d)
 
 
+@pytest.mark.timeout(600)
+def test_c5_full_documents():
+    """Two of config C5's documents at full size (200k loaded segments, 20k ops from 64 writers, lag
+    <= 4096): zamboni shrinks them to ~14k leaves in ~214k slots, so long runs of hole slots and
+    chunks with no length in a view appear (the regime of the two fixes in DESIGN.md §2).  Summary
+    digests equal the oracle's, which recorded the logs."""
+    from fluidframework_amd.synth import make_cfg, tables
+    from oracle.oracle import generate
+
+    n, grow, ops = 2, 200000, 20000
+    cfg = make_cfg(n, ops, writers=64, max_lag=4096, text_cap=2 * grow + ops * 18 + 16)
+    tabs = tables(writers=64)
+    b, ohash, status = generate(cfg, tabs, 0, n, threads=8, grow=grow)
+    assert (status == 0).all()
+    eng = _engine(n, max_segments=grow + grow // 14 + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
+                  text_units=2 * (int(cfg.text_cap) + 8192), ops_per_launch=256)
+    eng.apply(b)
+    eng.summarize()
+    for d in range(n):
+        assert eng.status(d)[0] == 0, f"doc {d}: {eng.status(d)}"
+    assert (eng.hashes(n) == ohash).all()
+
+
 def test_long_ranges_grow_the_lds_heap():
     """Removes/annotates over up to 120 units touch many leaf blocks, each an LRU push: documents
     whose LDS heap could overflow yield before the op and are relaunched with a larger heap
