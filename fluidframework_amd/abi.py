@@ -19,6 +19,9 @@ OP_RELPOS = 15
 OP_HANDLES = 16
 OP_ACK = 17
 OP_ROLLBACK = 18
+OP_REGENERATE = 19
+DELTA_REGEN = 64
+DELTA_REGEN_X = 72
 REL_BEFORE = 1
 REL_OFFSET = 2
 COMB_NONE, COMB_REWRITE, COMB_INCR, COMB_CONSENSUS, COMB_KEEP = 0, 1, 2, 3, 4

@@ -348,6 +348,20 @@ class DocLog:
             raise Unsupported(f"rollback of op type {t}")
         self.ops.append((abi.OP_ROLLBACK, 0, 0, -1, 0, 0, 0, 0, pp, t))
 
+    def regenerate(self, op: dict) -> int:
+        """Client.regeneratePendingOp (client.ts:917-960) of the oldest pending local op `op` (its contents;
+        a GROUP is one record per member, in order).  Returns the index of the first record in this batch's
+        op list: the MTR_DELTA_REGEN records of record k carry op = k (fluidframework_amd.regen builds the
+        new op from them)."""
+        members = op["ops"] if op.get("type") == 3 else [op]
+        first = len(self.ops)
+        for m in members:
+            t = m.get("type")
+            if t not in (0, 1, 2):
+                raise Unsupported(f"regenerate of op type {t}")
+            self.ops.append((abi.OP_REGENERATE, abi.F_DELTA, 0, -1, 0, 0, 0, 0, 0, t))
+        return first
+
     def local_op(self, op: dict, interner: Interner) -> None:
         """A local merge-tree op (the contents this client submits): insert / remove / annotate."""
         t = op.get("type")

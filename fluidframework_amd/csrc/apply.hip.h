@@ -148,6 +148,7 @@ struct DocHdr {
     int32_t holes;         // HBM-resident documents: hole slots among the nseg leaf slots (see Eng::spread)
     int32_t chunked;       // ... and their per-64-slot chunk summaries are valid (two-level view scan)
     int32_t pfree;         // free list of pending-membership cells (first cell + 1, 0 = empty)
+    int32_t lastnorm;      // Client.lastNormalizationRefSeq (client.ts:910): currentSeq of the last normalization
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -1595,6 +1596,227 @@ struct Eng {
             if (lane_id() == 0) L.meta[i] = m;
             wsync();
             if (G) csum_update(L, s, i, i + 1);
+        }
+    }
+
+    // ---- reconnect: Client.regeneratePendingOp (client.ts:917-960); X + DL instantiations only
+    struct LeafRec {
+        int len, seq, rseq;
+        uint32_t meta, text, props, uid;
+    };
+    static MTR_DI LeafRec leaf_ld(const D& L, int i) {
+        return LeafRec{L.len[i], L.seq[i], L.rseq[i], L.meta[i], L.text[i], L.props[i], L.uid[i]};
+    }
+    // a leaf's data into slot i; the slot keeps its tree-structure bits (leaf-block bounds, needsScour):
+    // assignChild puts the segment at the (parent, index) place (mergeTree.ts:2303-2308)
+    static MTR_DI void leaf_st(D& L, int i, const LeafRec& x) {
+        constexpr uint32_t kPlace = M_BND_MASK | M_NS_MASK;
+        L.len[i] = x.len;
+        L.seq[i] = x.seq;
+        L.rseq[i] = x.rseq;
+        L.meta[i] = (x.meta & ~kPlace) | (L.meta[i] & kPlace);
+        L.text[i] = x.text;
+        L.props[i] = x.props;
+        L.uid[i] = x.uid;
+    }
+    // normalizeAdjacentSegments (mergeTree.ts:2231-2331) on the run of leaves in slots [a, b) (holes
+    // skipped): removed-and-acked segments slide past every local one (keeping their order), each locally
+    // removed segment slides past the unacked inserts newer than its removal, and the run's leaves take
+    // the run's slots in the new order.  Serial (lane 0): runs are short and reconnects rare.
+    static __device__ __attribute__((noinline)) void normalize_run(D& L, const KParams& P, St& s, int a, int b) {
+        int n = 0;
+        for (int base = a; base < b; base += 64) {  // the run's slots -> E[0, n)
+            const int i = base + lane_id();
+            const bool in = i < b && !(L.meta[min(i, b - 1)] & M_DEL);
+            const uint64_t m = __ballot(in);
+            if (in) L.E[n + __popcll(m & lanes_below())] = i;
+            n += __popcll(m);
+        }
+        wsync();
+        if (s.rmused + n > P.rcap) {  // scratch for the order: the remover arena's free tail
+            s.status = MTR_ERR_CAPACITY;
+            return;
+        }
+        const gptr<uint32_t> T = L.grm() + s.rmused;
+        if (lane_id() == 0) {
+            auto acked = [&](int k) {
+                const int rs = L.rseq[L.E[k]];
+                return rs != RNONE && rs < LOCAL_BASE;
+            };
+            int last = -1;  // the last segment that is not removed-and-acked
+            for (int k = n - 1; k >= 0 && last < 0; k--)
+                if (!acked(k)) last = k;
+            if (last >= 0) {
+                // walking back from `last`: T[p, n) holds the other segments of (j, last] in their new order
+                // (the acked ones have all moved behind `last`)
+                int p = n;
+                for (int j = last; j >= 0; j--) {
+                    if (acked(j)) continue;
+                    const int rs = L.rseq[L.E[j]];
+                    int k = 0;
+                    if (rs != RNONE) {  // a local removal: past unacked inserts with localSeq > localRemovedSeq
+                        const int lr = rs - LOCAL_BASE;
+                        while (p + k < n) {
+                            const int sq = L.seq[L.E[int(T[p + k])]];
+                            if (!(sq >= LOCAL_BASE && sq - LOCAL_BASE > lr)) break;
+                            k++;
+                        }
+                    }
+                    for (int q = 0; q < k; q++) T[p - 1 + q] = T[p + q];
+                    T[p - 1 + k] = uint32_t(j);
+                    p--;
+                }
+                int w = 0;
+                for (int q = p; q < n; q++) T[w++] = T[q];
+                for (int k = 0; k < n; k++)
+                    if (acked(k)) T[w++] = uint32_t(k);
+                // slot E[k] takes the leaf of slot E[T[k]]: cycle by cycle, one leaf in registers
+                for (int k = 0; k < n; k++) {
+                    if (T[k] & 0x80000000u) continue;
+                    if (int(T[k]) == k) {
+                        T[k] |= 0x80000000u;
+                        continue;
+                    }
+                    const LeafRec tmp = leaf_ld(L, L.E[k]);
+                    int cur = k;
+                    for (;;) {
+                        const int src = int(T[cur] & 0x7fffffffu);
+                        T[cur] |= 0x80000000u;
+                        if (src == k) {
+                            leaf_st(L, L.E[cur], tmp);
+                            break;
+                        }
+                        leaf_st(L, L.E[cur], leaf_ld(L, L.E[src]));
+                        cur = src;
+                    }
+                }
+            }
+        }
+        wsync();
+        if (G) csum_update(L, s, a, b);
+    }
+    // normalizeSegmentsOnRebase (mergeTree.ts:2352-2381): runs of removed / unacked leaves that hold both an
+    // unacked insert and an acked removal are normalized
+    static __device__ __attribute__((noinline)) void normalize(D& L, const KParams& P, St& s) {
+        const int S = s.nseg;
+        int a = -1, end = 0, cnt = 0;
+        bool loc = false, ack = false;
+        for (int base = 0; base < S && s.status == MTR_OK; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, S - 1);
+            const uint32_t m = L.meta[ic];
+            const int sq = L.seq[ic], rs = L.rseq[ic];
+            const bool leaf = i < S && !(m & M_DEL);
+            const bool run = leaf && (rs != RNONE || sq >= LOCAL_BASE);
+            const uint64_t rm = __ballot(run), bm = __ballot(leaf && !run);
+            const uint64_t lm = __ballot(run && sq >= LOCAL_BASE), am = __ballot(run && rs != RNONE && rs < LOCAL_BASE);
+            if (!rm) {  // no run leaf here: at most the open run ends
+                if (bm && a >= 0) {
+                    if (loc && ack && cnt > 1) normalize_run(L, P, s, a, end);
+                    a = -1;
+                    cnt = 0;
+                    loc = ack = false;
+                }
+                continue;
+            }
+            for (uint64_t ev = rm | bm; ev && s.status == MTR_OK; ev &= ev - 1) {
+                const int l = first_lane(ev);
+                const uint64_t bit = 1ull << l;
+                if (rm & bit) {
+                    if (a < 0) a = base + l;
+                    cnt++;
+                    loc = loc || (lm & bit) != 0;
+                    ack = ack || (am & bit) != 0;
+                    end = base + l + 1;
+                } else if (a >= 0) {
+                    if (loc && ack && cnt > 1) normalize_run(L, P, s, a, end);
+                    a = -1;
+                    cnt = 0;
+                    loc = ack = false;
+                }
+            }
+        }
+        if (s.status == MTR_OK && a >= 0 && loc && ack && cnt > 1) normalize_run(L, P, s, a, end);
+    }
+    // regeneratePendingOp -> resetPendingDeltaToOps (client.ts:708-800) for the oldest pending group (type: the
+    // op's MergeTreeDeltaType); gidx: the record's index (the MTR_DELTA_REGEN records' op field)
+    static __device__ __attribute__((noinline)) void regenerate(D& L, const KParams& P, St& s, int type, int gidx) {
+        const gptr<DocHdr> h = L.ghdr();
+        const gptr<uint32_t> ring = L.gpend();
+        if (uni(h->lastnorm) != s.curseq) {  // client.ts:921-926
+            normalize(L, P, s);
+            if (lane_id() == 0) h->lastnorm = s.curseq;
+            wsync();
+            if (s.status != MTR_OK) return;
+        }
+        const int head = uni(h->phead), tail = uni(h->ptail);
+        if (head == tail || !ring) {
+            s.status = MTR_ERR_ASSERT | 0x034;  // "Segment group not at head of merge tree pending queue"
+            return;
+        }
+        const int slot = head % kPendRing;
+        const int lseq = int(uniu(ring[4 * slot])), cnt = int(uniu(ring[4 * slot + 1]));
+        const uint32_t ppo = uniu(ring[4 * slot + 3]);
+        if (lane_id() == 0) h->phead = head + 1;  // pendingSegments.shift()
+        wsync();
+        const int S = s.nseg;
+        // findReconnectionPosition (client.ts:699-706): getPosition at (currentSeq, this client, localSeq) --
+        // the inclusive prefix of localNetLength(leaf, currentSeq, localSeq) (mergeTree.ts:613-662) in E
+        int carry = 0;
+        for (int base = 0; base < S; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, S - 1);
+            const uint32_t m = L.meta[ic];
+            const int sq = L.seq[ic], rs = L.rseq[ic], ln = L.len[ic];
+            const bool lrem = rs != RNONE && rs >= LOCAL_BASE;  // localRemovedSeq = rs - LOCAL_BASE
+            bool zero = (m & M_DEL) || (lrem && rs - LOCAL_BASE <= lseq);
+            zero = zero || (sq >= LOCAL_BASE ? sq - LOCAL_BASE > lseq : (rs != RNONE && !lrem));
+            const int inc = wave_incl_scan(i < S && !zero ? ln : 0);
+            if (i < S) L.E[i] = carry + inc;
+            carry += rdlane(inc, 63);
+        }
+        wsync();
+        const int kind = type == MTR_OP_INSERT ? PK_INSERT : (type == MTR_OP_REMOVE ? PK_REMOVE : PK_ANNOTATE);
+        int off = 0, seen = 0;  // off: the member's offset in the inserted text (its pieces, in tree order)
+        for (int base = 0; base < S && seen < cnt && s.status == MTR_OK; base += 64) {
+            const int i = base + lane_id();
+            bool mem = false;
+            if (i < S && (L.meta[i] & M_PEND))
+                for (uint32_t c = pd_get(L, L.uid[i]); c != 0xffffffu; c = L.grm()[c] & 0xffffffu)
+                    mem = mem || int(L.grm()[c + 1] >> 16) == slot;
+            for (uint64_t mm = __ballot(mem); mm && s.status == MTR_OK; mm &= mm - 1) {  // ordinal order
+                const int j = base + first_lane(mm);
+                seen++;
+                const int sq = uni(L.seq[j]), rs = uni(L.rseq[j]), ln = uni(L.len[j]);
+                const int before = j > 0 ? uni(L.E[j - 1]) : 0;
+                bool emit = false;
+                if (type == MTR_OP_ANNOTATE) {  // not removed, or removed by a pending local op (client.ts:741-755)
+                    emit = rs == RNONE || rs >= LOCAL_BASE;
+                } else if (type == MTR_OP_INSERT) {
+                    if (sq < LOCAL_BASE) {
+                        s.status = MTR_ERR_ASSERT | 0x037;  // "Segment already has assigned sequence number"
+                        break;
+                    }
+                    emit = true;
+                } else if (type == MTR_OP_REMOVE) {  // still removed by this client only (client.ts:771-780)
+                    emit = rs != RNONE && rs >= LOCAL_BASE;
+                } else {
+                    s.status = MTR_ERR_BAD_OP;
+                    break;
+                }
+                pend_drop(L, j, slot);  // segment.segmentGroups.dequeue()
+                const int here = off;
+                off += ln;
+                if (!emit) continue;
+                if constexpr (DL) {
+                    const uint32_t pr = uniu(L.props[j]);
+                    const int ref = (type == MTR_OP_INSERT && pr != NONE32) ? int(pr & PN_MASK) : -1;
+                    put_record(L, s, gidx, before, ln, uint32_t(MTR_DELTA_REGEN + type));
+                    put_record(L, s, gidx, type == MTR_OP_INSERT ? here : 0, ref, MTR_DELTA_REGEN_X);
+                }
+                // a new group of its own at the tail, same localSeq (client.ts:787-795)
+                pend_add(L, P, s, j, -1, kind, type == MTR_OP_ANNOTATE ? ppo : 0u, lseq);
+            }
         }
     }
 
@@ -3249,6 +3471,13 @@ struct Eng {
                     break;
                 }
                 rollback(L, P, s, int(op.payload2), op.payload);
+                break;
+            case MTR_OP_REGENERATE:  // Client.regeneratePendingOp (client.ts:917-960) of the oldest pending op
+                if (!X || !DL || PM || !s.collab) {
+                    s.status = MTR_ERR_BAD_OP;
+                    break;
+                }
+                regenerate(L, P, s, int(op.payload2), gidx);
                 break;
             case MTR_OP_ACK:  // Client.applyMsg of this client's own message (client.ts:866-869)
                 if (!X || !s.collab) {

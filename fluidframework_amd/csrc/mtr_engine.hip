@@ -173,7 +173,7 @@ __global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const mtr_op op = ops[i];
         any = any || (op.flags & MTR_F_DELTA) != 0;
-        pend = pend || op.type == MTR_OP_ACK || op.type == MTR_OP_ROLLBACK ||
+        pend = pend || op.type == MTR_OP_ACK || op.type == MTR_OP_ROLLBACK || op.type == MTR_OP_REGENERATE ||
                (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE && op.seq == -1);
         ext = ext || op.type == MTR_OP_RELPOS || op.type == MTR_OP_HANDLES || (op.flags & MTR_F_REL) ||
               (op.type == MTR_OP_ANNOTATE && op.payload2 != 0) ||
@@ -451,6 +451,8 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
                 } else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) {
                     need[d] += uint64_t(std::min<int64_t>(std::max<int64_t>(int64_t(op.pos2) - op.pos1, 0),
                                                           int64_t(e->caps.max_segments)));
+                } else if (op.type == MTR_OP_REGENERATE) {  // two records per member of the group
+                    need[d] += 2 * uint64_t(e->caps.max_segments);
                 }
             }
             if (kind == 1 && flagged) {
@@ -495,6 +497,27 @@ int64_t mtr_get_deltas(mtr_engine* e, uint32_t doc, mtr_delta* out, int64_t cap)
         HIPCHK(hipMemcpy(out, e->delta.p + e->h_doff[doc] * 4, size_t(n) * sizeof(mtr_delta),
                          hipMemcpyDeviceToHost));
     return n;
+}
+
+int64_t mtr_get_props(mtr_engine* e, uint32_t doc, uint32_t ref, uint32_t* out, int64_t cap) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const uint64_t pw = e->caps.prop_words;
+    if (doc >= e->max_docs || ref >= pw) {
+        set_err("mtr_get_props: bad document or properties reference");
+        return -1;
+    }
+    const uint32_t* base = e->prop.p + size_t(doc) * pw;
+    uint32_t n = 0;
+    HIPCHK(hipMemcpy(&n, base + ref, 4, hipMemcpyDeviceToHost));
+    const int64_t words = 1 + 2 * int64_t(n);
+    if (uint64_t(ref) + uint64_t(words) > pw) {
+        set_err("mtr_get_props: reference outside the property arena");
+        return -1;
+    }
+    if (words > cap) return -words;
+    HIPCHK(hipMemcpy(out, base + ref, size_t(words) * 4, hipMemcpyDeviceToHost));
+    return words;
 }
 
 int mtr_set_matrix(mtr_engine* e, uint32_t rows_doc, uint32_t cols_doc) {

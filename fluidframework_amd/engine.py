@@ -86,6 +86,8 @@ def lib():
         L.mtr_set_matrix.restype = C.c_int
         L.mtr_get_deltas.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.mtr_get_deltas.restype = C.c_int64
+        L.mtr_get_props.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int64]
+        L.mtr_get_props.restype = C.c_int64
         L.mtr_last_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.mtr_last_timing.restype = C.c_int
         L.mtr_last_error.restype = C.c_char_p
@@ -306,6 +308,17 @@ class Engine:
         if n and lib().mtr_get_texts(self.h, lo, hi, buf.ctypes.data, n, off.ctypes.data) != n:
             raise EngineError(f"mtr_get_texts failed: {_err()}")
         return [buf[off[i]:off[i + 1]].tobytes().decode("utf-16-le", "surrogatepass") for i in range(hi - lo)]
+
+    def props(self, doc, ref) -> list:
+        """The properties an MTR_DELTA_REGEN_X record references (mtr_get_props): [(key id, value id)]."""
+        n = lib().mtr_get_props(self.h, doc, ref, None, 0)
+        if n == -1:
+            raise EngineError(_err())
+        n = -n if n < 0 else n
+        out = np.zeros(max(n, 1), dtype="<u4")
+        if lib().mtr_get_props(self.h, doc, ref, out.ctypes.data, n) != n:
+            raise EngineError(f"mtr_get_props failed: {_err()}")
+        return [(int(out[1 + 2 * k]), int(out[2 + 2 * k])) for k in range(int(out[0]))]
 
     def deltas(self, doc) -> np.ndarray:
         """The delta ranges (abi.DELTA_DTYPE) of the MTR_F_DELTA ops of the last batch for one document."""

@@ -56,6 +56,17 @@ enum {
     MTR_OP_ROLLBACK = 18,       /* Client.rollback (client.ts:421 -> MergeTree.rollback, mergeTree.ts:2049-2159) of the
                                    newest pending local op: payload2 = its MergeTreeDeltaType, payload = its
                                    prop-op (annotate) */
+    MTR_OP_REGENERATE = 19,     /* Client.regeneratePendingOp (client.ts:917-960) of the oldest pending local op, for
+                                   a resubmit after reconnect: normalizeSegmentsOnRebase first when currentSeq moved
+                                   since the last one (mergeTree.ts:2352-2381, 2231-2331), then
+                                   resetPendingDeltaToOps (client.ts:708-800): the group leaves the head of the
+                                   pending queue and each member, in tree order, is re-expressed at its
+                                   findReconnectionPosition (getPosition at (currentSeq, localSeq)); every member
+                                   that still needs its op joins a new group of its own at the tail.  payload2 =
+                                   the op's MergeTreeDeltaType.  Flag it MTR_F_DELTA: per regenerated member the
+                                   engine records two mtr_delta entries, {op, position, cachedLength,
+                                   MTR_DELTA_REGEN + type} then {op, offset of the member's text in the op's
+                                   inserted text, properties reference, MTR_DELTA_REGEN_X} (see below). */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for
@@ -125,6 +136,14 @@ enum {
  * len = count; onRowHandlesRecycled / onColHandlesRecycled, matrix.ts:722-734). */
 #define MTR_DELTA_CELL MTR_OP_SETCELL
 #define MTR_DELTA_RECYCLE 32
+/* MTR_OP_REGENERATE results: kind MTR_DELTA_REGEN + MergeTreeDeltaType (pos = reconnection position, len =
+ * cachedLength; the new op is insert(pos, segment), remove(pos, pos + len) or annotate(pos, pos + len, the op's
+ * props)), followed by kind MTR_DELTA_REGEN_X: pos = the member's offset in the inserted text of the op being
+ * regenerated (insert; the member's text is that text's [pos, pos + len)), len = a properties reference
+ * (insert: the segment's current properties, which createInsertSegmentOp serializes when the op's own seg
+ * has no props -- mtr_get_props; -1 = properties undefined). */
+#define MTR_DELTA_REGEN 64
+#define MTR_DELTA_REGEN_X 72
 
 typedef struct mtr_delta {
     uint32_t op;

@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <list>
 #include <map>
 #include <unordered_map>
 #include <memory>
@@ -93,6 +94,10 @@ struct Seg : Node {
     // PropertiesManager.pendingKeyUpdateCount (segmentPropertiesManager.ts:25): key id -> count > 0
     std::deque<struct SegGroup*> groups;
     std::vector<std::pair<uint32_t, int>> pendingKeys;
+    // BaseSegment.localSeq / localRemovedSeq (mergeTreeNodes.ts:382-383): the local op that inserted /
+    // removed it while unacked (-1 = undefined); cleared by the ack (:460, 469)
+    int localSeq = -1;
+    int localRemovedSeq = -1;
 };
 
 // SegmentGroup (mergeTreeNodes.ts:57-62): the segments one pending local op touched, in the order they
@@ -416,6 +421,8 @@ class Tree {
         r->removedSeq = s->removedSeq;
         r->seq = s->seq;
         r->clientId = s->clientId;
+        r->localSeq = s->localSeq;  // mergeTreeNodes.ts:495-497
+        r->localRemovedSeq = s->localRemovedSeq;
         for (SegGroup* g : s->groups) {  // segmentGroups.copyTo -> enqueueOnCopy (segmentGroupCollection.ts:47-62)
             if (g->hasPrevious)  // previousProps of the source segment, duplicated for the copy
                 for (size_t k = 0; k < g->segments.size(); k++)
@@ -489,9 +496,11 @@ class Tree {
                 s->removed = false;
                 s->removedSeq = 0;
                 s->removedClientIds.clear();
+                s->localRemovedSeq = -1;
             } else if (type == MTR_OP_INSERT) {
                 const int start = findRollbackPosition(s);
                 s->seq = kUniversalSeq;
+                s->localSeq = -1;
                 markRangeRemoved(start, start + s->len, kUniversalSeq, localClientId, kUniversalSeq);
             } else if (type == MTR_OP_ANNOTATE) {
                 // annotateRange(start, start + cachedLength, previousProps[k], ..., UniversalSequenceNumber,
@@ -561,11 +570,13 @@ class Tree {
                         return;
                     }
                     s->seq = seq;
+                    s->localSeq = -1;
                 } else if (opType == MTR_OP_REMOVE) {
                     if (!s->removed) {
                         status = MTR_ERR_ASSERT | 0x046;  // "On remove ack, missing removal info!"
                         return;
                     }
+                    s->localRemovedSeq = -1;
                     if (s->removedSeq == kUnassignedSeq) s->removedSeq = seq;
                 } else {
                     status = MTR_ERR_BAD_OP;
@@ -575,6 +586,171 @@ class Tree {
             }
         }
         zamboniSegments();  // mergeTree.ts:1318-1320
+    }
+
+    // ------------------------------------------------------------ reconnect
+    static bool removedAndAcked(const Seg* s) { return s->removed && s->removedSeq != kUnassignedSeq; }
+    // localNetLength(segment, refSeq, localSeq), mergeTree.ts:613-662: the local client's view at localSeq
+    static int localNetLengthAt(const Seg* s, int refSeq, int lseq) {
+        if (s->seq != kUnassignedSeq) {  // inserted remotely (or acked)
+            if (s->seq > refSeq || (removedAndAcked(s) && s->removedSeq <= refSeq) ||
+                (s->localRemovedSeq >= 0 && s->localRemovedSeq <= lseq))
+                return 0;
+            return s->len;
+        }
+        if (s->localSeq > lseq || (s->localRemovedSeq >= 0 && s->localRemovedSeq <= lseq)) return 0;
+        return s->len;
+    }
+
+    // normalizeAdjacentSegments, mergeTree.ts:2231-2331: within a run of removed / unacked segments, acked
+    // removed segments slide past the local ones, and each locally removed segment slides past the
+    // unacked inserts newer than its removal; the run's segments then take the run's (parent, index)
+    // places in the new order
+    void normalizeAdjacent(const std::vector<Seg*>& run) {
+        std::list<Seg*> lst(run.begin(), run.end());
+        std::vector<std::pair<Block*, int>> places;
+        for (Seg* x : run) places.push_back({x->parent, x->index});
+        auto last = lst.end();  // the last segment not removed-and-acked
+        for (auto it = lst.end(); it != lst.begin();) {
+            --it;
+            if (!removedAndAcked(*it)) {
+                last = it;
+                break;
+            }
+        }
+        if (last == lst.end()) return;
+        for (auto slide = last;;) {
+            const bool first = slide == lst.begin();
+            const auto nearer = first ? lst.end() : std::prev(slide);
+            Seg* x = *slide;
+            if (removedAndAcked(x)) {  // past every segment that is not also remotely removed
+                lst.erase(slide);
+                lst.insert(std::next(last), x);
+            } else if (x->removed) {
+                if (x->localRemovedSeq < 0) {
+                    status = MTR_ERR_ASSERT | 0x54d;
+                    return;
+                }
+                auto cur = slide;
+                for (auto scan = std::next(slide); scan != lst.end() && !removedAndAcked(*scan) &&
+                                                   (*scan)->localSeq >= 0 && (*scan)->localSeq > x->localRemovedSeq;
+                     ++scan)
+                    cur = scan;
+                if (cur != slide) {
+                    const auto after = std::next(cur);
+                    lst.erase(slide);
+                    lst.insert(after, x);
+                }
+            }
+            if (first) break;
+            slide = nearer;
+        }
+        size_t i = 0;
+        std::vector<std::pair<int, Block*>> touched;
+        for (Seg* x : lst) {
+            Block* p = places[i].first;
+            const int ix = places[i].second;
+            i++;
+            p->children[ix] = x;
+            x->parent = p;
+            x->index = ix;
+        }
+        // nodeUpdateLengthNewStructure on the ancestors, deepest first
+        for (auto& pl : places) {
+            int depth = 0;
+            for (Block* b = pl.first; b; b = b->parent) depth++;
+            for (Block* b = pl.first; b; b = b->parent) touched.push_back({depth--, b});
+        }
+        std::sort(touched.begin(), touched.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+        for (size_t k = 0; k < touched.size(); k++)
+            if (k == 0 || touched[k].second != touched[k - 1].second) nodeUpdateLengthNewStructure(touched[k].second);
+    }
+    // normalizeSegmentsOnRebase, mergeTree.ts:2352-2381
+    void normalizeSegmentsOnRebase() {
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        std::vector<Seg*> run;
+        bool local = false, acked = false;
+        auto flush = [&]() {
+            if (local && acked && run.size() > 1) normalizeAdjacent(run);
+            run.clear();
+            local = acked = false;
+        };
+        for (Seg* x : lv) {
+            if (x->removed || x->seq == kUnassignedSeq) {
+                if (removedAndAcked(x)) acked = true;
+                if (x->seq == kUnassignedSeq) local = true;
+                run.push_back(x);
+            } else {
+                flush();
+            }
+        }
+        flush();
+    }
+    // Client.regeneratePendingOp (client.ts:917-960) of the oldest pending op (type: its MergeTreeDeltaType)
+    // -> resetPendingDeltaToOps (client.ts:708-800); results as MTR_DELTA_REGEN / _X records
+    int lastNormalizationRefSeq = 0;
+    std::vector<std::pair<bool, PropMap>> regenProps;  // properties references of the MTR_DELTA_REGEN_X records
+    void regenerate(int type) {
+        if (currentSeq != lastNormalizationRefSeq) {
+            normalizeSegmentsOnRebase();
+            lastNormalizationRefSeq = currentSeq;
+            if (status != MTR_OK) return;
+        }
+        if (pendingSegments.empty()) {
+            status = MTR_ERR_ASSERT | 0x034;  // "Segment group not at head of merge tree pending queue"
+            return;
+        }
+        SegGroup* g = pendingSegments.front();
+        pendingSegments.pop_front();
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        // findReconnectionPosition (client.ts:699-706): getPosition at (currentSeq, local client, localSeq)
+        std::vector<int> before(lv.size() + 1, 0);
+        for (size_t k = 0; k < lv.size(); k++) before[k + 1] = before[k] + localNetLengthAt(lv[k], currentSeq, g->localSeq);
+        int off = 0;  // the member's offset in the inserted text: the members are its pieces, in order
+        size_t seen = 0;
+        for (size_t k = 0; k < lv.size() && seen < g->segments.size(); k++) {  // sorted by ordinal
+            Seg* s = lv[k];
+            if (std::find(g->segments.begin(), g->segments.end(), s) == g->segments.end()) continue;
+            seen++;
+            if (s->groups.empty() || s->groups.front() != g) {
+                status = MTR_ERR_ASSERT | 0x035;  // "Segment group not at head of segment pending queue"
+                return;
+            }
+            s->groups.pop_front();
+            bool emit = false;
+            if (type == MTR_OP_ANNOTATE) {
+                emit = !s->removed || (s->localRemovedSeq >= 0 && s->removedSeq == kUnassignedSeq);
+            } else if (type == MTR_OP_INSERT) {
+                if (s->seq != kUnassignedSeq) {
+                    status = MTR_ERR_ASSERT | 0x037;  // "Segment already has assigned sequence number"
+                    return;
+                }
+                emit = true;
+            } else if (type == MTR_OP_REMOVE) {
+                emit = s->localRemovedSeq >= 0 && s->removed && s->removedSeq == kUnassignedSeq;
+            } else {
+                status = MTR_ERR_BAD_OP;
+                return;
+            }
+            const int here = off;
+            off += s->len;
+            if (!emit) continue;
+            uint32_t ref = 0xffffffffu;
+            if (type == MTR_OP_INSERT && s->hasProps) {
+                ref = uint32_t(regenProps.size());
+                regenProps.push_back({true, s->props});
+            }
+            deltas.push_back({curOpIndex, before[k], s->len, uint32_t(MTR_DELTA_REGEN + type)});
+            deltas.push_back({curOpIndex, type == MTR_OP_INSERT ? here : 0, int32_t(ref), MTR_DELTA_REGEN_X});
+            groupPool.emplace_back();  // a group of its own, at the tail (client.ts:787-795)
+            SegGroup* ng = &groupPool.back();
+            ng->localSeq = g->localSeq;
+            pendingSegments.push_back(ng);
+            s->groups.push_back(ng);
+            ng->segments.push_back(s);
+        }
     }
 
     // ------------------------------------------------------------ walking
@@ -1072,6 +1248,7 @@ class Tree {
         if (seg->len > 0) {
             seg->seq = seq;
             seg->clientId = clientId;
+            seg->localSeq = seq == kUnassignedSeq ? localSeq : -1;  // blockInsert, mergeTree.ts:1656
             if (seg->markerOrdinal) idToSegment[seg->markerOrdinal - 1] = seg;  // blockInsert, mergeTree.ts:1655-1662
             InsertContext ctx{LeafMode::Insert, seg, true};
             Block* splitNode = insertingWalk(root, pos, refSeq, clientId, seq, ctx);
@@ -1112,6 +1289,7 @@ class Tree {
                     s->removed = true;
                     s->removedClientIds.assign(1, clientId);
                     s->removedSeq = seq;
+                    s->localRemovedSeq = seq == kUnassignedSeq ? localSeq : -1;  // mergeTree.ts:1994
                     fresh.push_back(s);
                 }
                 if (collaborating) {  // mergeTree.ts:2000-2010
@@ -1279,6 +1457,10 @@ class Tree {
             case MTR_OP_ROLLBACK:  // Client.rollback (client.ts:421-423) of the newest pending local op
                 if (!collaborating) return MTR_ERR_BAD_OP;
                 rollback(int(op.payload2), op.payload);
+                return status;
+            case MTR_OP_REGENERATE:  // Client.regeneratePendingOp (client.ts:917-960) of the oldest pending op
+                if (!collaborating) return MTR_ERR_BAD_OP;
+                regenerate(int(op.payload2));
                 return status;
             case MTR_OP_ACK:  // Client.applyMsg of this client's own message (client.ts:866-869)
                 if (!collaborating) return MTR_ERR_BAD_OP;
@@ -1665,6 +1847,21 @@ int oracle_doc_apply(oracle_doc* d, const mtr_batch* b, uint32_t doc_index, uint
         if (st != MTR_OK) return st;
     }
     return d->matrix ? (t.status != MTR_OK ? t.status : d->cols.status) : t.status;
+}
+
+// the properties of an MTR_DELTA_REGEN_X record's reference as [n, key, value, ...] (n = 2n + 1 words)
+int64_t oracle_doc_regen_props(oracle_doc* d, uint32_t ref, uint32_t* out, int64_t cap) {
+    Tree& t = d->view();
+    if (ref >= t.regenProps.size()) return -1;
+    const PropMap& m = t.regenProps[ref].second;
+    const int64_t n = 1 + 2 * int64_t(m.kv.size());
+    if (n > cap) return -n;
+    out[0] = uint32_t(m.kv.size());
+    for (size_t k = 0; k < m.kv.size(); k++) {
+        out[1 + 2 * k] = m.kv[k].first;
+        out[2 + 2 * k] = m.kv[k].second;
+    }
+    return n;
 }
 
 int64_t oracle_doc_deltas(oracle_doc* d, mtr_delta* out, int64_t cap) {

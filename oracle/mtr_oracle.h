@@ -51,6 +51,7 @@ int64_t oracle_doc_export(oracle_doc* d, int32_t* out, int64_t cap_leaves, int32
  * engine's mtr_get_deltas reports them: SequenceDeltaEvent ranges, or for a matrix the selected
  * vector's cell / recycle records.  Returns the count or -(count). */
 int64_t oracle_doc_deltas(oracle_doc* d, mtr_delta* out, int64_t cap);
+int64_t oracle_doc_regen_props(oracle_doc* d, uint32_t ref, uint32_t* out, int64_t cap);
 
 /* Collaboration window state: out[0]=minSeq out[1]=currentSeq out[2]=#heap entries out[3]=#leaves */
 void oracle_doc_state(oracle_doc* d, int64_t* out);

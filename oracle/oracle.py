@@ -40,6 +40,8 @@ def lib():
         L.oracle_doc_export.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
         L.oracle_doc_deltas.restype = C.c_int64
         L.oracle_doc_deltas.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_doc_regen_props.restype = C.c_int64
+        L.oracle_doc_regen_props.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.oracle_doc_state.argtypes = [C.c_void_p, C.c_void_p]
         L.oracle_set_trace.argtypes = [C.c_int]
         L.oracle_generate.restype = C.c_int
@@ -155,6 +157,16 @@ class OracleDoc:
         out = np.zeros(max(n, 1), dtype=abi.DELTA_DTYPE)
         lib().oracle_doc_deltas(self.h, out.ctypes.data, n)
         return out[:n]
+
+    def regen_props(self, ref: int) -> list:
+        """The properties an MTR_DELTA_REGEN_X record references: [(key id, value id), ...] in JS order."""
+        n = lib().oracle_doc_regen_props(self.h, ref, None, 0)
+        if n == -1:
+            raise ValueError(f"no properties reference {ref}")
+        n = -n if n < 0 else n
+        out = np.zeros(max(n, 1), dtype="<u4")
+        lib().oracle_doc_regen_props(self.h, ref, out.ctypes.data, n)
+        return [(int(out[1 + 2 * k]), int(out[2 + 2 * k])) for k in range(int(out[0]))]
 
     def state(self):
         out = np.zeros(4, dtype="<i8")
