@@ -32,7 +32,8 @@ function native() {
 
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
-    START_COLLAB: 12, SETCELL: 14, RELPOS: 15, ACK: 17 };
+    START_COLLAB: 12, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19 };
+const DELTA_REGEN = 64, DELTA_REGEN_X = 72;
 const REL = { BEFORE: 1, OFFSET: 2 };
 const COMB = { NONE: 0, REWRITE: 1, INCR: 2, CONSENSUS: 3, KEEP: 4 };
 const VEQ = { NEVER: 0x80000000, FALSY: 0x40000000, INCR_STR: 0x20000000, CONS_MUT: 0x10000000 };
@@ -289,6 +290,27 @@ class DocLog {
     localAnnotate(start, end, props, it) {
         if (props && typeof props === 'object' && 'markerId' in props) this.markerIdAnnotated = true;
         this.push(OP.LOCAL_ANNOTATE, 0, 0, this.localSeq(), 0, 0, start, end, it.propop(props), 0);
+    }
+    rollback(op, it) {  // Client.rollback (client.ts:421-423 -> MergeTree.rollback, mergeTree.ts:2049-2159)
+        let pp = 0;
+        if (op.type === 2) {
+            if (op.combiningOp) throw new UnsupportedError('rollback of a combining annotate');
+            pp = it.propop(op.props || {});
+        } else if (op.type !== 0 && op.type !== 1) {
+            throw new UnsupportedError('rollback of op type ' + op.type);
+        }
+        this.push(OP.ROLLBACK, 0, 0, -1, 0, 0, 0, 0, pp, op.type);
+    }
+    // Client.regeneratePendingOp (client.ts:917-960): one record per member op; returns the first record's
+    // index in this batch (the op field of its MTR_DELTA_REGEN records)
+    regenerate(op) {
+        const members = op.type === 3 ? op.ops : [op];
+        const first = this.ops.length;
+        for (const m of members) {
+            if (m.type !== 0 && m.type !== 1 && m.type !== 2) throw new UnsupportedError('regenerate of op type ' + m.type);
+            this.push(OP.REGENERATE, F.DELTA, 0, -1, 0, 0, 0, 0, 0, m.type);
+        }
+        return first;
     }
     localOp(op, it) {  // Client.localTransaction member (client.ts:1029-1048)
         if (op.type === 0) this.localInsert(op.pos1, op.seg, it);
@@ -574,6 +596,55 @@ class CatchUpLog {
 }
 
 /** The observer Clients of many documents on one GPU. */
+/*
+ * resetPendingDeltaToOps (client.ts:708-800) from the engine's MTR_DELTA_REGEN / _X record pairs
+ * (include/mtr_types.h): per member of the pending group, in tree order, the op to resubmit --
+ * createInsertSegmentOp (the member's piece of the text, the op's own seg.props or else the segment's
+ * current properties), createRemoveRangeOp, createAnnotateRangeOp -- and a GROUP unless exactly one.
+ * The Python mirror is fluidframework_amd/regen.py.
+ */
+function regenRecords(d) {  // Int32Array of [op, pos, len, kind] -> Map(record index -> [[type, pos, len, off, ref]])
+    const out = new Map();
+    for (let i = 0; i < d.length; i += 4) {
+        const kind = d[i + 3] >>> 0;
+        if (kind < DELTA_REGEN || kind >= DELTA_REGEN + 3) continue;
+        if (i + 4 >= d.length || (d[i + 7] >>> 0) !== DELTA_REGEN_X) throw new Error('MTR_DELTA_REGEN without its _X record');
+        const op = d[i] >>> 0;
+        if (!out.has(op)) out.set(op, []);
+        out.get(op).push([kind - DELTA_REGEN, d[i + 1], d[i + 2], d[i + 5], d[i + 6]]);
+        i += 4;
+    }
+    return out;
+}
+function regenMember(op, r, propsOf) {
+    const [t, pos, n, off, ref] = r;
+    if (t !== op.type) throw new Error('regenerate record does not match the op');
+    if (t === 1) return { pos1: pos, pos2: pos + n, type: 1 };
+    if (t === 2) {
+        const o = { pos1: pos, pos2: pos + n, props: op.props, type: 2 };
+        if (op.combiningOp !== undefined) o.combiningOp = op.combiningOp;
+        return o;
+    }
+    const seg = op.seg;
+    const own = seg !== null && typeof seg === 'object' && seg.props !== undefined;  // client.ts:763-767
+    const props = own ? seg.props : (ref >= 0 ? propsOf(ref) : undefined);
+    let spec;
+    if (seg !== null && typeof seg === 'object' && 'marker' in seg) {
+        spec = { marker: seg.marker };
+        if (props !== undefined && props !== null) spec.props = props;
+    } else {
+        const text = (typeof seg === 'string' ? seg : seg.text).substring(off, off + n);  // UTF-16 units
+        spec = props !== undefined && props !== null ? { text, props } : text;
+    }
+    return { pos1: pos, seg: spec, type: 0 };
+}
+function regeneratedOp(resetOp, recs, first, propsOf) {
+    const members = resetOp.type === 3 ? resetOp.ops : [resetOp];
+    const ops = [];
+    members.forEach((m, k) => { for (const r of recs.get(first + k) || []) ops.push(regenMember(m, r, propsOf)); });
+    return ops.length === 1 ? ops[0] : { ops, type: 3 };
+}
+
 class BatchReplayEngine {
     constructor(maxDocs, options) {
         this.options = Object.assign({ newLengthCalc: 0, snapshotV1: 1, chunkSize: 10000, device: 0 }, options || {});
@@ -694,6 +765,28 @@ class BatchReplayClient {
         this._queue(() => { for (const op of groupOp.ops) this.log.localOp(op, this.engine.interner); });
     }
     annotateRangeLocal(start, end, props) { this._queue(() => this.log.localAnnotate(start, end, props, this.engine.interner)); }
+    /** Client.rollback(op, localOpMetadata) (client.ts:421-423) of the newest pending local op `op`. */
+    rollback(op) { this._queue(() => this.log.rollback(op, this.engine.interner)); }
+    /**
+     * Client.regeneratePendingOp(resetOp, segmentGroup) (client.ts:917-960) for the oldest pending op
+     * (`resetOp`, the op that was submitted): flushes the engine and returns the op to resubmit.
+     */
+    regeneratePendingOp(resetOp) {
+        let first = 0;
+        this._queue(() => { first = this.log.regenerate(resetOp); });
+        this.engine.flush();
+        this._check();
+        const recs = regenRecords(native().getDeltas(this.engine.h, this.doc));
+        return regeneratedOp(resetOp, recs, first, (ref) => this._props(ref));
+    }
+    _props(ref) {  // a property set of this document's arena -> the properties object
+        const w = native().getProps(this.engine.h, this.doc, ref);
+        const it = this.engine.interner;
+        const names = Array.from(it.keys.keys());  // ids are insertion order
+        const out = {};
+        for (let k = 0; k < w[0]; k++) out[names[w[1 + 2 * k]]] = JSON.parse(it.valBytes[w[2 + 2 * k]].toString('utf8'));
+        return out;
+    }
     getCurrentSeq() { return this.currentSeq; }
     getText() {
         this.engine.flush();
@@ -800,4 +893,5 @@ class BatchMatrixClient {
 }
 
 module.exports = { BatchReplayEngine, BatchReplayClient, BatchMatrixClient, Interner, DocLog, MatrixDocLog, matrixLogs,
+    regenRecords, regeneratedOp,
     buildBatch, UnsupportedError, OP, F, SummaryType, native };

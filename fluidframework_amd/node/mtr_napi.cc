@@ -436,6 +436,26 @@ napi_value GetDeltas(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, size_t(n) * 4, ab, 0, &arr));
     return arr;
 }
+// getProps(engine, doc, ref) -> Uint32Array [n, key id, value id, ...] (mtr_get_props): the properties an
+// MTR_DELTA_REGEN_X record references
+napi_value GetProps(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0, ref = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &ref));
+    int64_t n = mtr_get_props(e, doc, ref, nullptr, 0);
+    if (n == -1) return throw_engine(env, "mtr_get_props");
+    n = n < 0 ? -n : n;
+    void* data = nullptr;
+    napi_value ab, arr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, size_t(n) * 4, &data, &ab));
+    if (mtr_get_props(e, doc, ref, static_cast<uint32_t*>(data), n) != n) return throw_engine(env, "mtr_get_props");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_uint32_array, size_t(n), ab, 0, &arr));
+    return arr;
+}
 napi_value SetMatrix(napi_env env, napi_callback_info info) {
     napi_value argv[3];
     if (!get_args(env, info, 3, argv)) return nullptr;
@@ -458,7 +478,8 @@ napi_value Init(napi_env env, napi_value exports) {
                {"getSummary", GetSummary},     {"getText", GetText},     {"docStatus", DocStatus},
                {"stats", Stats},               {"reset", Reset},         {"setMatrix", SetMatrix},
                {"getDeltas", GetDeltas},       {"submitRunAsync", SubmitRunAsync},
-               {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment}};
+               {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment},
+               {"getProps", GetProps}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||

@@ -49,6 +49,8 @@ class Writer:
         self.batches = []
         self.regens = []  # per batch: {record index: [(type, pos, len, offset, props dict or None)]}
         self.seq = 0
+        self.events = []     # what the writer did, for the Node shim replay
+        self.regen_out = []  # the regenerated ops of each reconnect
         self.flush()
 
     def flush(self):
@@ -63,22 +65,33 @@ class Writer:
         return self.doc.text()
 
     def local(self, op):
+        self.events.append({"local": op})
         self.log.local_op(op, self.it)
         self.flush()
         return op
+
+    def rollback(self, op):
+        """Client.rollback of the newest pending op."""
+        self.events.append({"rollback": op})
+        self.log.rollback(op, self.it)
+        self.flush()
 
     def regenerate(self, ops):
         """regeneratePendingOp of each op, oldest first (each takes the queue head) -> the new ops."""
         firsts = [self.log.regenerate(op) for op in ops]
         recs = self.flush()
-        return [regen.regenerated_op(op, recs, f, lambda r: regen.props_dict(self.doc.regen_props(r), self.it))
-                for op, f in zip(ops, firsts)]
+        out = [regen.regenerated_op(op, recs, f, lambda r: regen.props_dict(self.doc.regen_props(r), self.it))
+               for op, f in zip(ops, firsts)]
+        self.events.append({"regen": ops})
+        self.regen_out.append(out)
+        return out
 
     def message(self, contents, client=ME, ref=None, msn=0):
         self.seq += 1
         m = {"clientId": client, "sequenceNumber": self.seq,
              "referenceSequenceNumber": self.seq - 1 if ref is None else ref,
              "minimumSequenceNumber": msn, "type": "op", "contents": contents}
+        self.events.append({"msg": m})
         self.log.message(m, self.it)
         self.flush()
         return m
@@ -211,6 +224,8 @@ def _farm(seed, rounds=30, newlen=False):
             else:
                 op = ins(rnd.randint(0, len(t)), "".join(rnd.choice("ABCD") for _ in range(rnd.randint(1, 4))))
             pending.append(w.local(op))
+        if len(pending) > 1 and rnd.random() < 0.25:  # the newest edit is rolled back, never sent
+            w.rollback(pending.pop())
         reconnect = rnd.random() < 0.75
         if not reconnect:  # the original messages are sequenced first, at their refSeq
             for op in pending:
@@ -233,6 +248,7 @@ def _farm(seed, rounds=30, newlen=False):
             for op in w.regenerate(pending):
                 seen.append(w.message(op, ref=cur, msn=msn))
         assert w.text() == observer_text(seen, it, newlen), f"seed {seed} round {r}"
+        w.events.append({"check": w.text()})
     return w
 
 
@@ -281,3 +297,24 @@ def test_reset_pending_kats_engine():
 def test_reconnect_farm_engine(newlen):
     for seed in range(3):
         _replay_engine(_farm(seed, newlen=newlen), newlen)
+
+
+@pytest.mark.gpu
+def test_reconnect_through_node_shim(tmp_path):
+    """BatchReplayClient.regeneratePendingOp / applyMsg / localTransaction (fluidframework_amd/node) on the
+    farm's events: the regenerated ops and the texts at every round equal the oracle's."""
+    import json
+    import os
+    import subprocess
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    for seed, newlen in ((0, False), (1, True)):
+        w = _farm(seed, rounds=12, newlen=newlen)
+        f = tmp_path / f"events{seed}.json"
+        f.write_text(json.dumps({"me": ME, "newlen": newlen, "events": w.events}))
+        r = subprocess.run(["node", os.path.join(here, "node", "reconnect_engine.js"), str(f)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout)
+        assert res["regens"] == w.regen_out
+        assert res["texts"] == [e["check"] for e in w.events if "check" in e]
