@@ -60,6 +60,8 @@ constexpr uint32_t M_NLQ = 1u << 27;  // M_NL not known yet (left half of a spli
 constexpr uint32_t M_NONL = 1u << 28; // the leaf's text holds no '\n' at all (so neither does any split half)
 constexpr uint32_t M_TOUCH = 1u << 29;  // transient: a delta segment of the current MTR_F_DELTA op
 constexpr uint32_t M_PEND = 1u << 30;   // the leaf belongs to pending local SegmentGroups (a list of cells by uid)
+constexpr uint32_t M_ZOMB = 1u << 31;   // ... or its list holds key cells of an annotate regenerate did not re-send
+constexpr uint32_t ZOMBIE_SLOT = 0xffffu;  // ring-slot field of such a cell (its word 2 = the annotate's prop-op)
 constexpr uint32_t NS_UNDEF = 0, NS_FALSE = 1, NS_TRUE = 2;
 
 // The local-op path: a pending local insert keeps seq = LOCAL_BASE + localSeq and a pending
@@ -1333,7 +1335,7 @@ struct Eng {
         }
         bool ok = true;
         if (lane_id() == 0) {
-            const uint32_t nxt = (m & M_PEND) ? pd_get(L, u) : 0xffffffu;
+            const uint32_t nxt = (m & (M_PEND | M_ZOMB)) ? pd_get(L, u) : 0xffffffu;
             L.grm()[c] = (nxt & 0xffffffu) | (uint32_t(kind) << 24);
             L.grm()[c + 1] = (uint32_t(slot) << 16) | uint32_t(ord);
             L.grm()[c + 2] = oldp;  // a local annotate's previousProps (the set before the op)
@@ -1368,7 +1370,7 @@ struct Eng {
                 }
             } else {
                 prev = c;
-                left++;
+                left += int(w1 >> 16) != int(ZOMBIE_SLOT);
             }
             wsync();
             c = nx;
@@ -1399,13 +1401,44 @@ struct Eng {
     static MTR_DI void pend_copy(D& L, const KParams& P, St& s, uint32_t left_uid, int r) {
         uint32_t c = uniu(lane_id() == 0 ? pd_get(L, left_uid) : 0u);
         c = uniu(c);
-        if (lane_id() == 0) L.meta[r] = L.meta[r] & ~M_PEND;
+        if (lane_id() == 0) L.meta[r] = L.meta[r] & ~(M_PEND | M_ZOMB);
         wsync();
         while (c != 0xffffffu && s.status == MTR_OK) {
             const uint32_t w0 = uniu(L.grm()[c]), w1 = uniu(L.grm()[c + 1]), w2 = uniu(L.grm()[c + 2]);
-            pend_add(L, P, s, r, int(w1 >> 16), int(w0 >> 24), 0, 0, w2);  // (previousProps duplicated)
+            if ((w1 >> 16) == ZOMBIE_SLOT) zomb_add(L, P, s, r, w2);  // PropertiesManager.copyTo's counts
+            else pend_add(L, P, s, r, int(w1 >> 16), int(w0 >> 24), 0, 0, w2);  // (previousProps duplicated)
             c = w0 & 0xffffffu;
         }
+    }
+    // a key cell for leaf i (wave-uniform): the pending key counts of annotate prop-op pp outlive its group
+    // (pendingKeyUpdateCount, segmentPropertiesManager.ts:25, when resetPendingDeltaToOps does not re-send
+    // the annotate to a segment removed meanwhile, client.ts:741-755)
+    static MTR_DI void zomb_add(D& L, const KParams& P, St& s, int i, uint32_t pp) {
+        const gptr<DocHdr> h = L.ghdr();
+        const int fr = uni(h->pfree);
+        if (!fr && s.rmused + 3 > P.rcap) {
+            s.status = MTR_ERR_CAPACITY;
+            return;
+        }
+        const uint32_t u = uniu(L.uid[i]);
+        const uint32_t m = uniu(L.meta[i]);
+        const uint32_t c = fr ? uint32_t(fr - 1) : uint32_t(s.rmused);
+        if (fr) {
+            const uint32_t nf = uniu(L.grm()[c]) & 0xffffffu;
+            if (lane_id() == 0) h->pfree = nf == 0xffffffu ? 0 : int(nf + 1);
+        }
+        bool ok = true;
+        if (lane_id() == 0) {
+            const uint32_t nxt = (m & (M_PEND | M_ZOMB)) ? pd_get(L, u) : 0xffffffu;
+            L.grm()[c] = (nxt & 0xffffffu) | (uint32_t(PK_ANNOTATE) << 24);
+            L.grm()[c + 1] = ZOMBIE_SLOT << 16;
+            L.grm()[c + 2] = pp;
+            ok = pd_set(L, u, c);
+            L.meta[i] = m | M_ZOMB;
+        }
+        if (__ballot(!ok)) s.status = MTR_ERR_CAPACITY;
+        if (!fr) s.rmused += 3;
+        wsync();
     }
 
     // one of a leaf's pending annotates holds `key` (PropertiesManager.pendingKeyUpdateCount[key] defined)
@@ -1415,7 +1448,7 @@ struct Eng {
         while (c != 0xffffffu) {
             const uint32_t w0 = L.grm()[c], w1 = L.grm()[c + 1];
             if ((w0 >> 24) == PK_ANNOTATE) {
-                const uint32_t pp = ring[4 * (w1 >> 16) + 3];
+                const uint32_t pp = (w1 >> 16) == ZOMBIE_SLOT ? L.grm()[c + 2] : ring[4 * (w1 >> 16) + 3];
                 for (uint32_t q = poff[pp]; q < poff[pp + 1]; q++)
                     if (pkv[2 * q] == key) return true;
             }
@@ -1805,6 +1838,8 @@ struct Eng {
                     break;
                 }
                 pend_drop(L, j, slot);  // segment.segmentGroups.dequeue()
+                // an annotate not re-sent keeps its pending key counts on the segment (they are never acked)
+                if (type == MTR_OP_ANNOTATE && !emit) zomb_add(L, P, s, j, ppo);
                 const int here = off;
                 off += ln;
                 if (!emit) continue;
@@ -2346,8 +2381,9 @@ struct Eng {
         const uint64_t below = nd & lanes_below();
         const int p = below ? last_lane(below) : -1;
         const int ps = p < 0 ? 0 : p;
-        // the previous leaf's meta word with its candidacy in the spare top bit: one shuffle
-        const uint32_t pmc = uint32_t(__shfl(int(vm | (cand ? 0x80000000u : 0u)), ps));
+        // the previous leaf's meta word with its candidacy in the top bit (M_ZOMB's place: only the marker
+        // and newline bits are read from it): one shuffle
+        const uint32_t pmc = uint32_t(__shfl(int((vm & ~M_ZOMB) | (cand ? 0x80000000u : 0u)), ps));
         const bool pc = (pmc >> 31) != 0;
         const uint32_t pm = pmc & 0x7fffffffu;
         const uint32_t pp = uint32_t(__shfl(int(vp), ps));
@@ -2633,7 +2669,7 @@ struct Eng {
             L.E[j] = e - v + off;
             L.E[r] = e;
             wsync();
-            if (X && (m0 & M_PEND)) pend_copy(L, P, s, uniu(rdlane(uj, jl)), r);
+            if (X && (m0 & (M_PEND | M_ZOMB))) pend_copy(L, P, s, uniu(rdlane(uj, jl)), r);
             if (grew) s.nseg++;
             if (G) csum_update(L, s, j, max(L.shi, r + 1));
             overflow_fix(L, s, r);
@@ -3008,7 +3044,7 @@ struct Eng {
                     const uint32_t old = act ? L.props[j] : 0u;
                     uint64_t pend = am;
                     if (X && !pending) {  // leaves with pending local annotates: one filtered set each
-                        uint64_t pm = __ballot(act && (mj & M_PEND));
+                        uint64_t pm = __ballot(act && (mj & (M_PEND | M_ZOMB)));
                         pend &= ~pm;
                         for (; pm; pm &= pm - 1) {
                             const int l = first_lane(pm);

@@ -123,6 +123,32 @@ def test_synthetic_record_mode_matches_oracle(writers, max_lag):
     assert np.array_equal(rhash, ohash)
 
 
+def test_c2_full_documents():
+    """Config C2's documents at full length (5,000 messages, 16 writers, lag <= 64, up to
+    ~1,300 leaves): record mode on the device equals the oracle-driven recipe op for op, and every
+    summary digest equals the oracle's."""
+    from fluidframework_amd.synth import make_cfg, tables
+    from oracle.oracle import generate
+
+    n, ops, writers = 64, 5000, 16
+    tabs = tables(writers=writers)
+    cfg = make_cfg(n, ops, writers=writers, max_lag=64, seed=0xc2)
+    eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128,
+                  text_units=2 * (int(cfg.text_cap) + 8192), prop_words=1 << 16, remover_cells=8192,
+                  ops_per_launch=128)
+    eng.generate(cfg, tabs)
+    for d in range(n):
+        st, op = eng.status(d)
+        assert st == 0, f"doc {d}: status {st:#x} at op {op}"
+    gb = eng.download(0, n)
+    ob, ohash, ost = generate(cfg, tabs, 0, n, threads=16)
+    assert (ost == 0).all()
+    assert np.array_equal(gb.ops, ob.ops), "recorded op logs differ from the oracle-driven recipe"
+    eng.summarize()
+    assert np.array_equal(eng.hashes(n), ohash)
+    assert eng.stats()["max_leaves"] > 600  # C2-sized documents
+
+
 @pytest.mark.parametrize("v1", [True, False], ids=["v1", "legacy"])
 def test_load_snapshot_fixtures(v1):
     """Client.load of every reference snapshot fixture on the device (reloadFromSegments + body

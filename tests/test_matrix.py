@@ -159,11 +159,12 @@ def expand_pairs(batch, tabs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("writers,lag,ops", [(8, 16, 2000), (16, 64, 1500), (3, 0, 1000)])
-def test_matrix_engine_matches_oracle(writers, lag, ops):
+@pytest.mark.parametrize("writers,lag,ops,n", [(8, 16, 2000, 48), (16, 64, 1500, 48), (3, 0, 1000, 48), (8, 64, 20000, 16)],
+                         ids=["w8-lag16", "w16-lag64", "w3-lag0", "c4-size"])
+def test_matrix_engine_matches_oracle(writers, lag, ops, n):
+    """(c4-size: config C4's matrices at full length -- 20,000 messages, 8 writers, lag <= 64.)"""
     from fluidframework_amd.engine import Engine
 
-    n = 48
     cfg = matrix_cfg(n, ops, writers=writers, max_lag=lag)
     tabs = tables(writers=writers)
     gb, _, status = generate_matrix(cfg, tabs, 0, n, threads=8)

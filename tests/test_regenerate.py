@@ -191,6 +191,28 @@ def _props_kat(kind):
     return w, new
 
 
+def _zombie_kat():
+    """An annotate regenerate does not re-send (its segments were removed remotely meanwhile,
+    client.ts:741-755) keeps its pending key counts (pendingKeyUpdateCount is only decremented by an ack):
+    a later annotate of the key from a client that had not seen the removal leaves it alone
+    (segmentPropertiesManager.ts:94-104) while it still applies the other keys."""
+    it = Interner()
+    w = Writer(it)
+    w.message(ins(0, "abcdef"), client="A")  # seq 1
+    op = w.local(ann(1, 3, {"k": "w"}))
+    w.message(rem(0, 4), client="A", ref=1)  # seq 2: "abcd" removed, the annotated "bc" with it
+    new = w.regenerate([op])[0]
+    w.message(new)  # seq 3: an empty group
+    w.message(ann(2, 4, {"k": "b", "j": 1}), client="B", ref=1)  # seq 4: B never saw the removal
+    return w, new
+
+
+def test_regenerate_drops_removed_annotate_oracle():
+    w, new = _zombie_kat()
+    assert new == {"ops": [], "type": 3}
+    assert w.text() == "ef"
+
+
 def test_regenerated_insert_uses_original_properties_oracle():
     _, op = _props_kat("marker")
     assert op["seg"] == {"marker": {"refType": 0}, "props": {"markerId": "id", "prop1": "foo"}}
@@ -290,6 +312,7 @@ def test_reset_pending_kats_engine():
     for kind in ("marker", "text", "plain"):
         w, _ = _props_kat(kind)
         _replay_engine(w)
+    _replay_engine(_zombie_kat()[0])  # the removed segment's props (leaf hashes) equal the oracle's
 
 
 @pytest.mark.gpu
