@@ -80,6 +80,11 @@ constexpr int kGapMin = 8192;
 constexpr int kGapEvery = 16;
 constexpr int kHoleWindow = 1024;
 constexpr uint32_t PEND_KEY = 0x40000000u;
+// chunk summaries of HBM-resident documents (Eng::csum_update): per 64-slot chunk its local length, newest
+// event, the length of its leaves whose visibility no view in the collaboration window can change, and
+// the slots of the other leaves (up to kChunkList; more = the chunk is scanned whole)
+constexpr int kChunkList = 8;
+constexpr int kCsumRows = 4 + kChunkList;
 enum { PK_INSERT = 1, PK_REMOVE = 2, PK_ANNOTATE = 3 };
 
 constexpr uint32_t CL_LOCAL = 0xffu;      // LocalClientId (-1)
@@ -608,6 +613,9 @@ struct Eng {
     // PartialSequenceLengths does per block (partialLengths.ts:698-735) for chunks of the flat leaf order.
     static MTR_DI gptr<int> cs_len(const D& L) { return L.gcsum(); }
     static MTR_DI gptr<int> cs_ev(const D& L) { return L.gcsum() + (L.cap / 64 + 1); }
+    static MTR_DI gptr<int> cs_base(const D& L) { return L.gcsum() + 2 * (L.cap / 64 + 1); }
+    static MTR_DI gptr<int> cs_n(const D& L) { return L.gcsum() + 3 * (L.cap / 64 + 1); }
+    static MTR_DI gptr<int> cs_slot(const D& L, int q) { return L.gcsum() + (4 + q) * (L.cap / 64 + 1); }
     static MTR_DI A<int> cs_pre(const D& L) { return L.E + L.cap; }  // inclusive chunk prefix of a view
     // recompute the summaries of the chunks covering slots [lo, hi)
     static MTR_DI void csum_update(D& L, const St& s, int lo, int hi) {
@@ -615,7 +623,7 @@ struct Eng {
             if (!s.chunked) return;
             hi = min(hi, s.nseg);
             if (lo >= hi) return;
-            const gptr<int> cl = cs_len(L), ce = cs_ev(L);
+            const gptr<int> cl = cs_len(L), ce = cs_ev(L), cb = cs_base(L), cn = cs_n(L);
             for (int c = max(lo, 0) >> 6; c <= (hi - 1) >> 6; c++) {
                 const int i = c * 64 + lane_id();
                 const bool in = i < s.nseg;
@@ -624,14 +632,23 @@ struct Eng {
                 const int len = L.len[ic], sq = L.seq[ic], rs = L.rseq[ic];
                 const bool live = in && !(m & M_DEL);
                 const bool rem = rs != RNONE;
+                // in the window: an event after minSeq (a pending local one included), so views differ on it
+                const bool win = live && (sq > s.minseq || (rem && rs > s.minseq));
+                const uint64_t wm = __ballot(win);
+                const int nw = __popcll(wm);
                 int x = (live && !rem) ? len : 0;
+                int fx = (live && !rem && !win) ? len : 0;  // removed at or before minSeq: in no view
                 int ev = live ? max(sq, rem ? rs : 0) : 0;
                 x = rdlane(wave_incl_scan(x), 63);
+                fx = rdlane(wave_incl_scan(fx), 63);
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
+                if (win && nw <= kChunkList) cs_slot(L, __popcll(wm & lanes_below()))[c] = i;
                 if (lane_id() == 0) {
                     cl[c] = x;
                     ce[c] = ev;
+                    cb[c] = fx;
+                    cn[c] = min(nw, kChunkList + 1);
                 }
             }
             wsync();
@@ -641,16 +658,37 @@ struct Eng {
     static MTR_DI int prefix2(D& L, const St& s, const View& v, int newlen) {
         PROF(P_PREFIX);
         const int S = s.nseg, nch = (S + 63) >> 6;
-        const gptr<int> cl = cs_len(L), ce = cs_ev(L);
+        const gptr<int> cl = cs_len(L), ce = cs_ev(L), cbs = cs_base(L), cn = cs_n(L);
         const A<int> cp = cs_pre(L);
         const int ln = lane_id();
         int carry = 0;
         for (int cb = 0; cb < nch; cb += 64) {
             const int c = cb + ln;
             const bool in = c < nch;
-            int len = in ? cl[min(c, nch - 1)] : 0;
-            const int ev = in ? ce[min(c, nch - 1)] : 0;
-            uint64_t dm = __ballot(in && !v.local && ev > v.ref);
+            const int cc = min(c, nch - 1);
+            int len = in ? cl[cc] : 0;
+            const int ev = in ? ce[cc] : 0;
+            const bool dirty = in && !v.local && ev > v.ref;
+            // a chunk with events after refSeq: its fixed length plus its listed in-window leaves' view lengths
+            const int nl = dirty ? cn[cc] : 0;
+            const bool listed = dirty && nl <= kChunkList;
+            if (__ballot(listed)) {
+                int sl[kChunkList];
+#pragma unroll
+                for (int q = 0; q < kChunkList; q++) sl[q] = (listed && q < nl) ? cs_slot(L, q)[cc] : 0;
+                Hot hq[kChunkList];
+#pragma unroll
+                for (int q = 0; q < kChunkList; q++) hq[q] = ld_hot(L, min(sl[q], S - 1));
+                int sum = listed ? cbs[cc] : 0;
+#pragma unroll
+                for (int q = 0; q < kChunkList; q++) {
+                    const bool on = listed && q < nl;
+                    const int x0 = vis_hot(L, hq[q], sl[q], v, newlen, s.minseq, on);
+                    sum += on ? max(x0, 0) : 0;
+                }
+                if (listed) len = sum;
+            }
+            uint64_t dm = __ballot(dirty && !listed);
             while (dm) {  // chunks with events after refSeq: their leaves' view lengths, GK chunks at a time
                 int lq[GK];
                 Hot hq[GK];
@@ -3306,7 +3344,7 @@ struct Eng {
             L.sc->cp[CP_VEQ] = (unsigned long long)P.val_eq;
             L.sc->cp[CP_HDR] = (unsigned long long)(P.hdr + d);
             L.sc->cp[CP_PEND] = (unsigned long long)(P.pend ? P.pend + size_t(d) * kPendRing * 4 : nullptr);
-            L.sc->cp[CP_CSUM] = (unsigned long long)(P.csum ? P.csum + size_t(d) * 2 * (P.segcap / 64 + 1) : nullptr);
+            L.sc->cp[CP_CSUM] = (unsigned long long)(P.csum ? P.csum + size_t(d) * kCsumRows * (P.segcap / 64 + 1) : nullptr);
             L.sc->cp[CP_UMAP] = (unsigned long long)(P.umap ? P.umap + size_t(d) * 2 * P.segcap : nullptr);
         }
         wsync();

@@ -105,7 +105,7 @@ struct mtr_engine {
     bool pend_seen = false;           // a batch since mtr_reset held local ops while collaborating or acks:
                                       // documents may hold pending segments, so every launch is an X kernel
     DevBuf<uint32_t> pend;            // [doc][kPendRing][4] pending SegmentGroups (allocated on first use)
-    DevBuf<int32_t> csum;             // [doc][2][segcap / 64 + 1] chunk summaries (first HBM-resident launch)
+    DevBuf<int32_t> csum;             // [doc][kCsumRows][segcap / 64 + 1] chunk summaries (first HBM-resident launch)
     DevBuf<int32_t> umap;             // [doc][2 * segcap] uid -> slot hints (with csum)
     DevBuf<int32_t> red;              // small reduction / query-result buffer
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
@@ -673,7 +673,7 @@ static int run_impl(mtr_engine* e, int gen) {
                 // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
                 if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
                 if (!e->csum.p) {  // for every document the engine may hold: it must never move
-                    const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * (size_t(P.segcap) / 64 + 1);
+                    const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * kCsumRows * (size_t(P.segcap) / 64 + 1);
                     if (e->csum.ensure(n)) return -1;
                     if (e->umap.ensure(size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * size_t(P.segcap))) return -1;
                     HIPCHK(hipMemsetAsync(e->umap.p, 0xff, e->umap.n * sizeof(int32_t), e->stream));

@@ -17,6 +17,7 @@ ap.add_argument("--ops", type=int, default=1000)
 ap.add_argument("--writers", type=int, default=8)
 ap.add_argument("--max-lag", type=int, default=32)
 ap.add_argument("--ops-per-launch", type=int, default=256)
+ap.add_argument("--grow", type=int, default=0, help="C5-shaped: documents pre-grown to this many segments")
 ap.add_argument("--matrix", action="store_true",
                 help="C4-shaped SharedMatrix pairs (x1 = setCell messages, x2 = row/col splices)")
 a = ap.parse_args()
@@ -27,6 +28,13 @@ if a.matrix:
     eng = Engine(2 * n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * ops + 1024,
                  prop_words=1024, remover_cells=8192, ops_per_launch=a.ops_per_launch)
     eng.generate_matrix(cfg, tables(writers=a.writers))
+elif a.grow:
+    g = a.grow
+    cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, text_cap=2 * g + 18 * ops + 16)
+    eng = Engine(n, max_segments=g + g // 14 + 2 * ops + 128, heap_entries=g + 2 * ops + 128,
+                 text_units=2 * int(cfg.text_cap) + 16384, prop_words=65536, remover_cells=65536,
+                 ops_per_launch=a.ops_per_launch)
+    eng.generate(cfg, tables(writers=a.writers), grow=g)
 else:
     cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag)
     eng = Engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
