@@ -662,55 +662,81 @@ struct Eng {
         const A<int> cp = cs_pre(L);
         const int ln = lane_id();
         int carry = 0;
-        for (int cb = 0; cb < nch; cb += 64) {
-            const int c = cb + ln;
-            const bool in = c < nch;
-            const int cc = min(c, nch - 1);
-            int len = in ? cl[cc] : 0;
-            const int ev = in ? ce[cc] : 0;
-            const bool dirty = in && !v.local && ev > v.ref;
-            // a chunk with events after refSeq: its fixed length plus its listed in-window leaves' view lengths
-            const int nl = dirty ? cn[cc] : 0;
-            const bool listed = dirty && nl <= kChunkList;
-            if (__ballot(listed)) {
-                int sl[kChunkList];
+        // RR rounds of 64 chunks per iteration: their summary, list and leaf loads are issued together,
+        // so one wave keeps RR independent chains of loads in flight
+        constexpr int RR = 2;
+        for (int cb = 0; cb < nch; cb += 64 * RR) {
+            int cc[RR], len[RR], ev[RR], nl[RR], fx[RR];
+            bool in[RR], dirty[RR], listed[RR];
 #pragma unroll
-                for (int q = 0; q < kChunkList; q++) sl[q] = (listed && q < nl) ? cs_slot(L, q)[cc] : 0;
-                Hot hq[kChunkList];
-#pragma unroll
-                for (int q = 0; q < kChunkList; q++) hq[q] = ld_hot(L, min(sl[q], S - 1));
-                int sum = listed ? cbs[cc] : 0;
-#pragma unroll
-                for (int q = 0; q < kChunkList; q++) {
-                    const bool on = listed && q < nl;
-                    const int x0 = vis_hot(L, hq[q], sl[q], v, newlen, s.minseq, on);
-                    sum += on ? max(x0, 0) : 0;
-                }
-                if (listed) len = sum;
+            for (int h = 0; h < RR; h++) {  // unconditional (clamped) loads
+                const int c = cb + 64 * h + ln;
+                in[h] = c < nch;
+                cc[h] = min(c, nch - 1);
+                len[h] = cl[cc[h]];
+                ev[h] = ce[cc[h]];
+                nl[h] = cn[cc[h]];
+                fx[h] = cbs[cc[h]];
             }
-            uint64_t dm = __ballot(dirty && !listed);
-            while (dm) {  // chunks with events after refSeq: their leaves' view lengths, GK chunks at a time
-                int lq[GK];
-                Hot hq[GK];
+            bool any = false;
 #pragma unroll
-                for (int q = 0; q < GK; q++) {
-                    lq[q] = dm ? first_lane(dm) : -1;
-                    dm &= dm - 1;
-                    const int i = (cb + max(lq[q], 0)) * 64 + ln;
-                    hq[q] = ld_hot(L, min(i, S - 1));
-                }
+            for (int h = 0; h < RR; h++) {
+                if (!in[h]) len[h] = 0;
+                dirty[h] = in[h] && !v.local && ev[h] > v.ref;
+                // a chunk with events after refSeq: its fixed length plus its listed in-window leaves'
+                listed[h] = dirty[h] && nl[h] <= kChunkList;
+                any = any || listed[h];
+            }
+            if (__ballot(any)) {
+                int sl[RR][kChunkList];
 #pragma unroll
-                for (int q = 0; q < GK; q++) {
-                    if (lq[q] < 0) break;
-                    const int i = (cb + lq[q]) * 64 + ln;
-                    const int x0 = vis_hot(L, hq[q], i, v, newlen, s.minseq, i < S);
-                    const int sum = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
-                    if (ln == lq[q]) len = sum;
+                for (int h = 0; h < RR; h++)
+#pragma unroll
+                    for (int q = 0; q < kChunkList; q++) sl[h][q] = (listed[h] && q < nl[h]) ? cs_slot(L, q)[cc[h]] : 0;
+                Hot hq[RR][kChunkList];
+#pragma unroll
+                for (int h = 0; h < RR; h++)
+#pragma unroll
+                    for (int q = 0; q < kChunkList; q++) hq[h][q] = ld_hot(L, min(sl[h][q], S - 1));
+#pragma unroll
+                for (int h = 0; h < RR; h++) {
+                    int sum = fx[h];
+#pragma unroll
+                    for (int q = 0; q < kChunkList; q++) {
+                        const bool on = listed[h] && q < nl[h];
+                        const int x0 = vis_hot(L, hq[h][q], sl[h][q], v, newlen, s.minseq, on);
+                        sum += on ? max(x0, 0) : 0;
+                    }
+                    if (listed[h]) len[h] = sum;
                 }
             }
-            const int inc = wave_incl_scan(len);
-            if (in) cp[c] = carry + inc;
-            carry += rdlane(inc, 63);
+#pragma unroll
+            for (int h = 0; h < RR; h++) {
+                const int c0 = cb + 64 * h;
+                uint64_t dm = __ballot(dirty[h] && !listed[h]);
+                while (dm) {  // more than kChunkList leaves in the window: the chunk's leaves, GK chunks at a time
+                    int lq[GK];
+                    Hot hq[GK];
+#pragma unroll
+                    for (int q = 0; q < GK; q++) {
+                        lq[q] = dm ? first_lane(dm) : -1;
+                        dm &= dm - 1;
+                        const int i = (c0 + max(lq[q], 0)) * 64 + ln;
+                        hq[q] = ld_hot(L, min(i, S - 1));
+                    }
+#pragma unroll
+                    for (int q = 0; q < GK; q++) {
+                        if (lq[q] < 0) break;
+                        const int i = (c0 + lq[q]) * 64 + ln;
+                        const int x0 = vis_hot(L, hq[q], i, v, newlen, s.minseq, i < S);
+                        const int sum = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
+                        if (ln == lq[q]) len[h] = sum;
+                    }
+                }
+                const int inc = wave_incl_scan(len[h]);
+                if (in[h]) cp[c0 + ln] = carry + inc;
+                carry += rdlane(inc, 63);
+            }
         }
         wsync();
         return carry;
@@ -1044,7 +1070,9 @@ struct Eng {
             const int i = base + lane_id();
             const bool in = i < to;
             const uint32_t m = L.meta[min(i, to - 1)];
-            const bool h = in && (m & M_DEL) && L.uid[min(i, to - 1)] != NONE32;  // newly deleted
+            const uint32_t u = L.uid[min(i, to - 1)];
+            const bool h = in && (m & M_DEL) && u != NONE32;  // newly deleted
+            if (h && s.chunked && u < uint32_t(2 * L.cap)) L.gumap()[u] = -2;  // the uid is gone for good
             if (h) hole_fields(L, i);
             made += __popcll(__ballot(h));
         }
@@ -1101,6 +1129,7 @@ struct Eng {
         if constexpr (G) {  // one word per leaf: 4 * GK rounds of loads in flight
             if (s.chunked && u < uint32_t(2 * L.cap)) {  // the slot hint, verified
                 const int h = uni(L.gumap()[u]);
+                if (h == -2) return -1;  // merged away or unlinked (holeify): uids are never reused
                 if (h >= 0 && h < S && uniu(L.uid[h]) == u) return h;
             }
             constexpr int FK = 4 * GK;
