@@ -3498,8 +3498,11 @@ struct Eng {
             return true;
         }
         if (s.height == 0) finish_load(L, s);
-        // holes ran low, or the slots fill the slab while holes remain
-        if (G && !PM && s.nseg >= kGapMin && (s.holes * 64 < s.nseg || (s.holes && s.nseg + 2 >= L.cap)))
+        // holes ran low, or the slots fill the slab while holes remain, or zamboni shrank the document so
+        // far that holes outnumber its leaves threefold (every slot-order pass -- view scans, block bounds,
+        // scour -- would step over them: C5's documents keep ~14k of 200k leaves)
+        if (G && !PM && s.nseg >= kGapMin &&
+            (s.holes * 64 < s.nseg || (s.holes && s.nseg + 2 >= L.cap) || s.holes > 3 * (s.nseg - s.holes)))
             spread(L, s, L.cap);
         const bool local_op = op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE;
         int zop = 0;
