@@ -53,7 +53,24 @@ GROW = {"C5": 200_000}
 MATRIX = {"C4"}
 
 
-def parse():
+def host_cores() -> int:
+    """Host cores this process may use: its CPU affinity, capped by the cgroup CPU quota and by
+    OMP_NUM_THREADS when the environment sets it (the GPU box gives one GPU's job a 16-core share of
+    a much larger machine, which os.cpu_count() does not show)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", choices=sorted(PRESETS), default="C3",
                     help="workload preset (C3 = the headline metric's 100k-document run)")
@@ -72,11 +89,13 @@ def parse():
                     help="ops per document per launch (48; 512 for the HBM-resident C5 documents)")
     ap.add_argument("--cpu-sample-docs", type=int, default=0,
                     help="default: about 60M messages of documents (~8 s on 16 host threads)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="default: every host core this job may use")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="multi-rank runs: nccl (= RCCL over xGMI); gloo only for the CPU tests' stub engine")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=None,
                     help="PMC summary of this config (default: profiles/traffic_r02.json for C3, the r01 files else)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.traffic_file is None:
         name = {"C3": "traffic_r02.json", "C4": "traffic_r01_c4.json"}.get(a.config, "traffic_r01.json")
         a.traffic_file = os.path.join(ROOT, "profiles", name)
@@ -147,24 +166,91 @@ def end_to_end(eng, n, steps, messages, matrix, hashes):
     }
 
 
+def cpu_baseline(a, eng, n, ops, grow, matrix, hashes, fixture_batch, messages):
+    """The reference's algorithm on the host cores of the same box, rank 0 at N=1:
+    the oracle replays a bounded sample of the same recorded documents with one document per task on
+    every host core this job may use, answering each remote block length from the block's
+    PartialSequenceLengths (getPartialLength, partialLengths.ts:698-735) as the reference does.  The
+    leaf-sum variant (the tests' checker) is timed on part of the sample beside it.  Both must
+    reproduce the engine's summary digests."""
+    from oracle.oracle import psl_answer, replay_batch, replay_matrix_batch
+
+    threads = a.cpu_threads or host_cores()
+    # bounded sample: ~6e7 messages of C2/C3 documents; one pre-grown C5 document per host thread
+    k = min(a.cpu_sample_docs or (threads if grow else max(1, 60_000_000 // ops)), n)
+    if fixture_batch is not None:
+        k = n
+        sample = fixture_batch
+    elif matrix:
+        sample = eng.download_matrix(0, k)
+    else:
+        sample = eng.download(0, k)
+
+    def replay(kk, reps=1):
+        secs, oh = 0.0, None
+        for _ in range(reps):
+            if matrix:
+                dt, oh, ost = replay_matrix_batch(sample, 0, kk, threads)
+            else:
+                dt, oh, ost = replay_batch(sample, 0, kk, threads)
+            secs += dt / reps
+        if matrix:
+            eq = int((oh == hashes[:2 * kk]).reshape(kk, 2).all(axis=1).sum())
+        else:
+            eq = int((oh == hashes[:kk]).sum())
+        return secs, eq, int((ost != 0).sum())
+
+    reps = 10 if fixture_batch is not None else 1  # (the fixture set replays in ~0.2 s)
+    with psl_answer():
+        secs, eq, errs = replay(k, reps)
+    bit_exact = {"checked_docs": k, "equal": eq, "oracle_errors": errs}
+    if eq != k or errs:
+        raise SystemExit(f"summaries differ from the CPU oracle (PartialSequenceLengths): {bit_exact}")
+    k2 = k if fixture_batch is not None else max(1, k // 4)
+    secs2, eq2, errs2 = replay(k2, reps)
+    if eq2 != k2 or errs2:
+        raise SystemExit(f"summaries differ from the CPU oracle (leaf sums): {eq2}/{k2}, {errs2} errors")
+    per_doc = ops if fixture_batch is None else messages / n
+    cpu = {
+        "value": round(k * per_doc / secs, 1),
+        "unit": "ops/s",
+        "cores": threads,
+        "kind": "port",
+        "algorithm": "PartialSequenceLengths",
+        "sample": f"first {k} of the {n} {'matrices' if matrix else 'documents'} ({int(k * per_doc)} messages"
+                  f"{f' after {grow} loaded segments each' if grow else ''}), replay + V1 summary, one document per "
+                  f"task on {threads} host threads; block lengths from PartialSequenceLengths.getPartialLength "
+                  f"as in the reference (reference-algorithm C++ restatement, not Node)",
+        "seconds": round(secs, 3),
+        "leaf_sum": {"value": round(k2 * per_doc / secs2, 1), "docs": k2, "seconds": round(secs2, 3),
+                     "note": "the oracle's leaf-sum block lengths (the tests' checker), same threads"},
+        "host_cpus_visible": os.cpu_count(),
+    }
+    return cpu, bit_exact
+
+
 def _bulk_record(buf, off, d):
     from fluidframework_amd.engine import Engine
 
     return Engine.split_record(buf, int(off[d]), int(off[d + 1]))
 
 
-def main():
-    a = parse()
+def main(argv=None):
+    a = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    reduce_device = f"cuda:{local}"
     if world > 1:
         import torch
         import torch.distributed as dist_mod
 
-        torch.cuda.set_device(local)
-        dist_mod.init_process_group("nccl")
+        if a.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+        else:
+            reduce_device = "cpu"
+        dist_mod.init_process_group(a.dist_backend)
         dist = dist_mod
 
     from fluidframework_amd import shard
@@ -276,7 +362,7 @@ def main():
     messages = n * ops if fixture_text is None else fixture_msgs
     run_digest = shard.digest(hashes)
     if dist is not None:  # the only collective: counters + summary digests over RCCL/xGMI
-        r = shard.reduce_run(dist, f"cuda:{local}", elapsed, messages, int(st["bad_docs"]), run_digest)
+        r = shard.reduce_run(dist, reduce_device, elapsed, messages, int(st["bad_docs"]), run_digest)
         elapsed, total_messages, bad, run_digest = r["elapsed"], float(r["messages"]), float(r["bad_docs"]), r["digest"]
     else:
         total_messages = float(messages)
@@ -327,7 +413,8 @@ def main():
             else None,
         }
     roofline = {
-        "bound": "hbm",
+        "bound": "hbm",  # (the contract's vocabulary: the path's roofline is HBM; no MFMA)
+        "binding": "instruction issue" if not grow else "per-wave latency",
         "limiter": "per-wave issue latency: one wave per document applies its ops in order (a chain of "
                    "dependent LDS round trips, ballots and scalar control per op); waves per SIMD are "
                    "capped by VGPRs and LDS per document. HBM sees only stage-in/out and arenas "
@@ -372,40 +459,8 @@ def main():
     cpu = None
     bit_exact = {"checked_docs": 0, "equal": 0}
     if not a.no_cpu_baseline and world == 1:
-        from oracle.oracle import replay_batch, replay_matrix_batch
-
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        # (pre-grown documents: the oracle's block lengths are leaf sums, O(S) per op at 200k leaves --
-        # one document per host thread is the bounded sample)
-        k = min(a.cpu_sample_docs or (threads if grow else max(1, 60_000_000 // ops)), n)
-        if fixture_text is not None:  # the whole fixture set, replayed 10 times (one pass is ~0.2 s)
-            k = n
-            secs = 0.0
-            for _ in range(10):
-                dt, ohash, ost = replay_batch(fixture_batch, 0, k, threads)
-                secs += dt / 10
-            eq = int((ohash == hashes[:k]).sum())
-        elif matrix:  # a matrix is equal when both of its vectors' summaries are
-            sample = eng.download_matrix(0, k)
-            secs, ohash, ost = replay_matrix_batch(sample, 0, k, threads)
-            eq = int((ohash == hashes[:2 * k]).reshape(k, 2).all(axis=1).sum())
-        else:
-            sample = eng.download(0, k)
-            secs, ohash, ost = replay_batch(sample, 0, k, threads)
-            eq = int((ohash == hashes[:k]).sum())
-        bit_exact = {"checked_docs": k, "equal": eq, "oracle_errors": int((ost != 0).sum())}
-        if eq != k or bit_exact["oracle_errors"]:
-            raise SystemExit(f"summaries differ from the CPU oracle: {bit_exact}")
-        cpu = {
-            "value": round((messages if fixture_text is not None else k * ops) / secs, 1),
-            "unit": "ops/s",
-            "cores": threads,
-            "kind": "port",
-            "sample": f"first {k} of the {n} {'matrices' if matrix else 'documents'} ({k * ops} messages"
-                      f"{f' after {grow} loaded segments each' if grow else ''}), replay + V1 summary, one document "
-                      f"per task on {threads} host threads (reference-algorithm C++ restatement, not Node)",
-            "seconds": round(secs, 3),
-        }
+        cpu, bit_exact = cpu_baseline(a, eng, n, ops, grow, matrix, hashes, fixture_batch if fixture_text is not None
+                                      else None, messages)
     out = {
         "metric": METRIC,
         "value": round(value, 1),

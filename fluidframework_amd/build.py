@@ -15,8 +15,9 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 ENGINE_SRC = ["mtr_engine.hip"]
-ENGINE_DEPS = ["apply.hip.h", "summary.hip.h", "mtr_engine.hip", "apply_caps.hip"]
+ENGINE_DEPS = ["apply.hip.h", "summary.hip.h", "mtr_engine.hip", "apply_caps.hip", "apply_variants.hip"]
 CAP_PARTS = 3  # kCapParts in apply.hip.h
+VARIANT_PARTS = 5  # kVariantParts in apply.hip.h
 
 
 def _stale(target, deps):
@@ -42,6 +43,8 @@ def build_engine(force=False, verbose=False, prof=False, variant=None, extra=())
         units = [(os.path.join(CSRC, f), os.path.join(objdir, f + ".o"), []) for f in ENGINE_SRC]
         units += [(os.path.join(CSRC, "apply_caps.hip"), os.path.join(objdir, f"apply_caps_{q}.o"), [f"-DMTR_CAP_PART={q}"])
                   for q in range(CAP_PARTS)]
+        units += [(os.path.join(CSRC, "apply_variants.hip"), os.path.join(objdir, f"apply_variants_{q}.o"),
+                   [f"-DMTR_VARIANT_PART={q}"]) for q in range(VARIANT_PARTS)]
         procs = []
         for src, obj, extra in units:
             cmd = flags + extra + ["-c", "-o", obj, src]

@@ -72,7 +72,9 @@ constexpr uint32_t NS_UNDEF = 0, NS_FALSE = 1, NS_TRUE = 2;
 // ring slot << 16 | ordinal in the group} in the remover arena, listed under key PEND_KEY | uid.
 constexpr int LOCAL_BASE = 0x40000000;
 constexpr int TIE_LOCAL = 0x7ffffffe;   // breakTie's newSeq of a local insert (Number.MAX_SAFE_INTEGER)
-constexpr int kPendRing = 256;
+// (a regenerate re-sends each member of a wide pending remove / annotate as its own group,
+// resetPendingDeltaToOps: the ring must hold one group per segment such an op spans; 16-bit slot field)
+constexpr int kPendRing = 4096;
 // HBM-resident documents of at least kGapMin leaves keep one hole slot per kGapEvery (Eng::spread), so a
 // split or an insert moves the leaves up to the next hole instead of the rest of the document; a shift
 // looks for a hole within kHoleWindow slots
@@ -386,7 +388,9 @@ struct ProfScope {
 
 // G: leaves in HBM (documents larger than LDS); PM: PermutationVector documents (SharedMatrix
 // rows/cols, permutationvector.ts) -- a separate instantiation so the SharedString kernel carries
-// no permutation code; CAP: the launch's LDS leaf capacity as a compile-time constant (0 = runtime),
+// no permutation code; CAP: the launch's LDS leaf capacity as a compile-time constant (0 = runtime, with the
+// rare records compiled in; -1 = runtime, without them: the replay kernels of documents above the largest
+// fixed class and of HBM-resident documents),
 // which puts every leaf array at a constant LDS offset (ds_read/ds_write immediate offsets from one
 // per-lane address instead of a base register and an address add per array)
 template <bool G, bool PM = false, int CAP = 0, bool DL = false, bool GN = false>
@@ -3330,7 +3334,7 @@ struct Eng {
             L.sc = (lptr<Sc>)(smem);
             L.gst = (lptr<mtr_synth_state>)(smem + ((sizeof(Sc) + 15) & ~size_t(15)));
         } else {
-            const int cap = CAP ? CAP : P.cap, lhcap = P.lhcap;
+            const int cap = CAP > 0 ? CAP : P.cap, lhcap = P.lhcap;
             char* p = smem;
             auto take = [&](size_t n) {
                 char* r = p;
@@ -3915,7 +3919,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MTR_WPE
 }
 
 // leaf capacities with a compile-time LDS layout (apply_kernel<false, CAP>, instantiated in
-// apply_caps.hip, kCapParts translation units); other capacities use the runtime layout (CAP = 0)
+// apply_caps.hip, kCapParts translation units); other capacities use the runtime layout (CAP = -1, or 0 for a
+// batch with rare records)
 constexpr int kCapParts = 3;
 bool launch_fixed_cap_p0(int cap, uint32_t grid, size_t lds, hipStream_t st, const KParams& P);
 bool launch_fixed_cap_p1(int cap, uint32_t grid, size_t lds, hipStream_t st, const KParams& P);
@@ -3931,6 +3936,25 @@ __global__ void __launch_bounds__(NT) apply_pair_kernel(KParams P, uint32_t pair
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
     Eng<G, true, 0, DL, GN>::run_pair(smem, pair_region, P, d);
+}
+
+// the runtime-layout instantiations, launched by name from mtr_engine.hip and compiled in kVariantParts
+// translation units (apply_variants.hip): X = the rare records compiled in, LEAN = without them, DL = delta
+// reporting, GN = record mode; PAIR = SharedMatrix pairs
+enum ApplyVariant {
+    AV_LDS_X = 0, AV_HBM_X, AV_LDS_LEAN, AV_HBM_LEAN, AV_LDS_DL, AV_HBM_DL, AV_LDS_GN, AV_HBM_GN,
+    AV_PAIR_LDS, AV_PAIR_HBM, AV_PAIR_LDS_DL, AV_PAIR_HBM_DL, AV_PAIR_LDS_GN, AV_PAIR_HBM_GN, AV_COUNT
+};
+constexpr int kVariantParts = 5;
+bool launch_variant_p0(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p1(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p2(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p3(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p4(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+inline bool launch_variant(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region = 0) {
+    return launch_variant_p0(v, grid, lds, st, P, region) || launch_variant_p1(v, grid, lds, st, P, region) ||
+           launch_variant_p2(v, grid, lds, st, P, region) || launch_variant_p3(v, grid, lds, st, P, region) ||
+           launch_variant_p4(v, grid, lds, st, P, region);
 }
 
 }  // namespace mtr

@@ -591,33 +591,6 @@ static int run_impl(mtr_engine* e, int gen) {
     }
     int dev_lds = 0;
     HIPCHK(hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->device));
-    static std::once_flag once;
-    std::call_once(once, [&] {
-        (void)hipFuncSetAttribute((const void*)apply_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_kernel<false, 0, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_kernel<true, 0, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_kernel<false, 0, false, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_kernel<true, 0, false, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<false, false, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void*)apply_pair_kernel<true, false, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
     // documents whose class needs more LDS than this stay HBM-resident (MTR_LDS_LIMIT, bytes; tuning knob)
     static const size_t lds_limit = [] {
         const char* v = std::getenv("MTR_LDS_LIMIT");
@@ -703,32 +676,27 @@ static int run_impl(mtr_engine* e, int gen) {
                 e->kev.push_back(x);
             }
             HIPCHK(hipEventRecord(e->kev[2 * nl], st));
+            int av = -1;
             if (pair) {
-                const uint32_t region = uint32_t(lds / 2);
-                if (P.gen) {  // record mode (mtr_generate_matrix)
-                    if (P.global_mode) apply_pair_kernel<true, false, true><<<cnt, NT, lds, st>>>(P, region);
-                    else apply_pair_kernel<false, false, true><<<cnt, NT, lds, st>>>(P, region);
-                } else if (P.doff) {  // a matrix tracked for its cells
-                    if (P.global_mode) apply_pair_kernel<true, true><<<cnt, NT, lds, st>>>(P, region);
-                    else apply_pair_kernel<false, true><<<cnt, NT, lds, st>>>(P, region);
-                } else if (P.global_mode) {
-                    apply_pair_kernel<true><<<cnt, NT, lds, st>>>(P, region);
-                } else {
-                    apply_pair_kernel<false><<<cnt, NT, lds, st>>>(P, region);
-                }
+                av = P.gen ? (P.global_mode ? AV_PAIR_HBM_GN : AV_PAIR_LDS_GN)  // record mode (mtr_generate_matrix)
+                     : P.doff ? (P.global_mode ? AV_PAIR_HBM_DL : AV_PAIR_LDS_DL)  // a matrix tracked for its cells
+                     : (P.global_mode ? AV_PAIR_HBM : AV_PAIR_LDS);
             } else if (P.gen) {  // record mode: the generating instantiation
-                if (P.global_mode) apply_kernel<true, 0, false, true><<<cnt, NT, lds, st>>>(P);
-                else apply_kernel<false, 0, false, true><<<cnt, NT, lds, st>>>(P);
+                av = P.global_mode ? AV_HBM_GN : AV_LDS_GN;
             } else if (P.doff) {  // a batch with MTR_F_DELTA ops: the delta-reporting instantiation
-                if (P.global_mode) apply_kernel<true, 0, true><<<cnt, NT, lds, st>>>(P);
-                else apply_kernel<false, 0, true><<<cnt, NT, lds, st>>>(P);
-            } else if (P.global_mode) {
-                apply_kernel<true><<<cnt, NT, lds, st>>>(P);
-            } else {
-                if (e->has_ext || (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
-                    !launch_fixed_cap_p1(cap, uint32_t(cnt), lds, st, P) &&
-                    !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P)))
-                    apply_kernel<false><<<cnt, NT, lds, st>>>(P);
+                av = P.global_mode ? AV_HBM_DL : AV_LDS_DL;
+            } else if (P.global_mode) {  // HBM-resident: the lean instantiation unless the batch has rare records
+                av = e->has_ext ? AV_HBM_X : AV_HBM_LEAN;
+            } else if (e->has_ext) {
+                av = AV_LDS_X;
+            } else if (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
+                       !launch_fixed_cap_p1(cap, uint32_t(cnt), lds, st, P) &&
+                       !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P)) {
+                av = AV_LDS_LEAN;  // above the fixed classes: runtime layout, lean
+            }
+            if (av >= 0 && !launch_variant(av, uint32_t(cnt), lds, st, P, pair ? uint32_t(lds / 2) : 0u)) {
+                set_err("no apply kernel variant " + std::to_string(av));
+                return -1;
             }
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(e->kev[2 * nl + 1], st));
@@ -1303,9 +1271,14 @@ int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t
     if (r[0] < 0) return MTR_OK;
     info->offset = r[1];
     info->length = r[2];
-    info->seq = r[3];
+    // pending local values are kept above every sequence number (LOCAL_BASE + localSeq, apply.hip.h):
+    // report them as the reference holds them, UnassignedSequenceNumber plus the localSeq
+    info->seq = r[3] >= LOCAL_BASE ? -1 : r[3];
+    info->local_seq = r[3] >= LOCAL_BASE ? r[3] - LOCAL_BASE : -1;
     info->client = r[4];
-    info->removed_seq = r[5];
+    info->removed = r[5] != -1;
+    info->removed_seq = r[5] >= LOCAL_BASE ? -1 : r[5];
+    info->local_removed_seq = r[5] >= LOCAL_BASE ? r[5] - LOCAL_BASE : -1;
     info->marker = r[6];
     info->ref_type = r[7];
     info->props = r[8];

@@ -35,7 +35,8 @@ class MtrCaps(C.Structure):
 class SegmentInfo(C.Structure):
     """include/mtr.h: mtr_segment_info"""
     _fields_ = [(n, C.c_int32) for n in ("leaf", "offset", "length", "seq", "client", "removed_seq", "marker",
-                                         "ref_type", "props", "start")]
+                                         "ref_type", "props", "start", "removed", "local_seq",
+                                         "local_removed_seq")]
 
 
 def lib():
@@ -337,11 +338,15 @@ class Engine:
         """Client.getContainingSegment(pos, {referenceSequenceNumber, clientId}) on the device:
         None when no segment covers pos, else a dict of mtr_segment_info fields plus the text."""
         info = SegmentInfo()
-        text = np.zeros(1 << 16, dtype="<u2")
+        text = np.zeros(1 << 12, dtype="<u2")
         self._check(lib().mtr_get_containing_segment(self.h, doc, pos, ref_seq, client, C.byref(info),
                                                      text.ctypes.data, text.size), "mtr_get_containing_segment")
         if info.leaf < 0:
             return None
+        if not info.marker and info.length > text.size:  # the text did not fit: ask again with room for it
+            text = np.zeros(info.length, dtype="<u2")
+            self._check(lib().mtr_get_containing_segment(self.h, doc, pos, ref_seq, client, C.byref(info),
+                                                         text.ctypes.data, text.size), "mtr_get_containing_segment")
         r = {n: getattr(info, n) for n, _ in SegmentInfo._fields_}
         r["text"] = None if info.marker else text[:info.length].tobytes().decode("utf-16-le", "surrogatepass")
         return r

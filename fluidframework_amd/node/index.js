@@ -655,6 +655,10 @@ class BatchReplayEngine {
         this.catchUps = [];
         this.dirty = false;
         this.summarized = false;
+        this.inFlight = false;  // an async run / summarize holds the engine (its batch was taken from the logs)
+    }
+    _assertIdle() {
+        if (this.inFlight) throw new Error('engine busy: await the pending flushAsync / summarizeAllAsync first');
     }
     createClient() {
         if (this.logs.length >= this.maxDocs) throw new Error('engine is full');
@@ -683,23 +687,41 @@ class BatchReplayEngine {
         this.summarized = false;
     }
     flush() {  // apply every queued message of every document
+        this._assertIdle();
         if (!this.dirty) return;
         native().submitRun(this.h, this._batch());
         this._afterRun();
     }
     /**
      * The asynchronous flush: the batch is applied on a worker thread (N-API async work) and the
-     * returned promise settles when the GPU is done, so the event loop keeps serving meanwhile.  Other
-     * calls on this engine throw until it settles (await it).
+     * returned promise settles when the GPU is done, so the event loop keeps serving meanwhile.  Every
+     * other call on this engine or its clients throws until it settles (await it): the batch has already
+     * been taken from the logs, so nothing may be queued behind it.
      */
     async flushAsync() {
+        this._assertIdle();
         if (!this.dirty) return;
-        await native().submitRunAsync(this.h, this._batch());
+        const batch = this._batch();
+        this.inFlight = true;
+        try {
+            await native().submitRunAsync(this.h, batch);
+        } finally {
+            this.inFlight = false;
+        }
         this._afterRun();
     }
     async summarizeAllAsync() {  // every document's blobs, built on a worker thread
         await this.flushAsync();
-        if (!this.summarized) { await native().summarizeAsync(this.h); this.summarized = true; }
+        if (!this.summarized) {
+            this._assertIdle();
+            this.inFlight = true;
+            try {
+                await native().summarizeAsync(this.h);
+            } finally {
+                this.inFlight = false;
+            }
+            this.summarized = true;
+        }
     }
 }
 
@@ -709,7 +731,7 @@ class BatchReplayClient {
         this.engine = engine; this.doc = doc; this.log = engine.logs[doc];
         this.currentSeq = 0;
     }
-    _queue(fn) { fn(); this.engine.dirty = true; }
+    _queue(fn) { this.engine._assertIdle(); fn(); this.engine.dirty = true; }
     _check() {
         const st = native().docStatus(this.engine.h, this.doc);
         if (st[0] === STATUS.OK) return;
@@ -816,8 +838,12 @@ class BatchReplayClient {
         const r = native().getContainingSegment(this.engine.h, this.doc, pos, ref, client);
         if (r === null) return { segment: undefined, offset: undefined };
         const longId = (c) => (c >= 0 ? this.log.clients[c] : 'original');
+        // (a pending local segment: seq / removedSeq = UnassignedSequenceNumber with its localSeq, as
+        // mergeTree.ts:1397-1427 / 1955-2047 leave them)
         const segment = { cachedLength: r.length, seq: r.seq, clientId: longId(r.client), leafIndex: r.leaf,
-            removedSeq: r.removedSeq < 0 ? undefined : r.removedSeq, propertySet: r.props < 0 ? undefined : r.props };
+            removedSeq: r.removed ? r.removedSeq : undefined, propertySet: r.props < 0 ? undefined : r.props };
+        if (r.localSeq >= 0) segment.localSeq = r.localSeq;
+        if (r.localRemovedSeq >= 0) segment.localRemovedSeq = r.localRemovedSeq;
         if (r.marker) segment.marker = { refType: r.refType };
         else segment.text = r.text;
         return { segment, offset: r.offset };
@@ -876,10 +902,11 @@ class BatchReplayClient {
 class BatchMatrixClient {
     constructor(engine, rowsDoc) { this.engine = engine; this.doc = rowsDoc; this.log = engine.logs[rowsDoc]; }
     startOrUpdateCollaboration(longClientId, minSeq, currentSeq) {
+        this.engine._assertIdle();
         this.log.startCollab(longClientId, minSeq || 0, currentSeq || 0);
         this.engine.dirty = true;
     }
-    applyMsg(msg) { this.log.message(msg, this.engine.interner); this.engine.dirty = true; }
+    applyMsg(msg) { this.engine._assertIdle(); this.log.message(msg, this.engine.interner); this.engine.dirty = true; }
     summarizeVectors() {
         this.engine.flush();
         for (const d of [this.doc, this.doc + 1]) {

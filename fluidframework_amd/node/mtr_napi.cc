@@ -101,6 +101,7 @@ bool arr_prop(napi_env env, napi_value obj, const char* name, const T** p, size_
     return true;
 }
 
+// (an engine with a job in flight is never finalized: the job holds a reference to its handle)
 void finalize_engine(napi_env, void* data, void*) {
     if (data) mtr_engine_destroy(static_cast<mtr_engine*>(data));
 }
@@ -179,6 +180,7 @@ struct AsyncJob {
     napi_async_work work = nullptr;
     napi_deferred deferred = nullptr;
     napi_ref keep = nullptr;  // the batch object: its arrays must outlive the host->device copies
+    napi_ref eref = nullptr;  // the engine handle: its finalizer (mtr_engine_destroy) must not run mid-job
     mtr_engine* e = nullptr;
     mtr_batch b{};
     bool summarize = false;
@@ -208,6 +210,7 @@ void job_complete(napi_env env, napi_status, void* data) {  // JS thread
     AsyncJob* j = static_cast<AsyncJob*>(data);
     g_busy.erase(j->e);
     if (j->keep) napi_delete_reference(env, j->keep);
+    if (j->eref) napi_delete_reference(env, j->eref);
     napi_value v;
     if (j->rc == 0) {
         napi_get_undefined(env, &v);
@@ -229,6 +232,7 @@ napi_value queue_job(napi_env env, AsyncJob* j, const char* name) {
         napi_create_async_work(env, nullptr, res, job_execute, job_complete, j, &j->work) != napi_ok ||
         napi_queue_async_work(env, j->work) != napi_ok) {
         if (j->keep) napi_delete_reference(env, j->keep);
+        if (j->eref) napi_delete_reference(env, j->eref);
         delete j;
         napi_throw_error(env, nullptr, "cannot queue asynchronous engine work");
         return nullptr;
@@ -249,6 +253,11 @@ napi_value SubmitRunAsync(napi_env env, napi_callback_info info) {
         delete j;
         return nullptr;
     }
+    if (napi_create_reference(env, argv[0], 1, &j->eref) != napi_ok) {
+        napi_delete_reference(env, j->keep);
+        delete j;
+        return nullptr;
+    }
     return queue_job(env, j, "mtr_submit_run");
 }
 
@@ -261,6 +270,10 @@ napi_value SummarizeAsync(napi_env env, napi_callback_info info) {
     AsyncJob* j = new AsyncJob();
     j->e = e;
     j->summarize = true;
+    if (napi_create_reference(env, argv[0], 1, &j->eref) != napi_ok) {
+        delete j;
+        return nullptr;
+    }
     return queue_job(env, j, "mtr_summarize");
 }
 
@@ -281,6 +294,11 @@ napi_value GetContainingSegment(napi_env env, napi_callback_info info) {
     std::vector<uint16_t> text(1 << 16);
     if (mtr_get_containing_segment(e, doc, pos, ref, client, &si, text.data(), int64_t(text.size())) != MTR_OK)
         return throw_engine(env, "mtr_get_containing_segment");
+    if (si.leaf >= 0 && !si.marker && si.length > int32_t(text.size())) {  // a longer text: ask again with room
+        text.resize(size_t(si.length));
+        if (mtr_get_containing_segment(e, doc, pos, ref, client, &si, text.data(), int64_t(text.size())) != MTR_OK)
+            return throw_engine(env, "mtr_get_containing_segment");
+    }
     napi_value r;
     if (si.leaf < 0) {
         NAPI_CALL(env, napi_get_null(env, &r));
@@ -292,7 +310,8 @@ napi_value GetContainingSegment(napi_env env, napi_callback_info info) {
         int32_t v;
     } f[] = {{"leaf", si.leaf},   {"offset", si.offset},         {"length", si.length}, {"seq", si.seq},
              {"client", si.client}, {"removedSeq", si.removed_seq}, {"marker", si.marker}, {"refType", si.ref_type},
-             {"props", si.props}, {"start", si.start}};
+             {"props", si.props}, {"start", si.start}, {"removed", si.removed}, {"localSeq", si.local_seq},
+             {"localRemovedSeq", si.local_removed_seq}};
     for (const auto& x : f) {
         napi_value v;
         NAPI_CALL(env, napi_create_int32(env, x.v, &v));

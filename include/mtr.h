@@ -140,11 +140,15 @@ typedef struct mtr_segment_info {
     int32_t length;      /* cachedLength */
     int32_t seq;         /* segment.seq */
     int32_t client;      /* segment.clientId: short id, -1 LocalClientId, -2 NonCollabClient */
-    int32_t removed_seq; /* removedSeq, -1 = not removed */
+    int32_t removed_seq; /* removedSeq; -1 = UnassignedSequenceNumber (a pending local remove) when removed,
+                            else not removed (undefined) */
     int32_t marker;      /* 1 = Marker (text holds nothing; ref_type holds its refType) */
     int32_t ref_type;    /* marker refType / PermutationSegment start handle / text arena offset */
     int32_t props;       /* property-set index in the document's arena, -1 = none */
     int32_t start;       /* the segment's position in the view */
+    int32_t removed;     /* 1 = the segment carries removal info (acked or pending) */
+    int32_t local_seq;   /* localSeq of a pending local insert (then seq = -1), else -1 */
+    int32_t local_removed_seq; /* localSeq of a pending local remove (then removed_seq = -1), else -1 */
 } mtr_segment_info;
 int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
                                mtr_segment_info* info, uint16_t* text, int64_t text_cap);

@@ -51,7 +51,8 @@ constexpr int kUndef = -1;                   // "undefined" node length
 constexpr int64_t kMaxSafe = 9007199254740991LL;
 int g_trace = 0;
 int g_trace_seq = -1;
-// PartialSequenceLengths cross-check (psl.h): off unless a test turns it on
+// PartialSequenceLengths (psl.h): 0 off; 1 maintained and cross-checked against leaf sums (tests);
+// 2 maintained and answering every remote block length, as the reference does (bench.py's CPU baseline)
 int g_psl = 0;
 std::atomic<long long> g_psl_checks{0}, g_psl_mismatch{0}, g_psl_rootlag{0};
 std::mutex g_psl_mu;
@@ -327,8 +328,14 @@ class Tree {
             return blockLocalLength(static_cast<const Block*>(n));
         }
         if (!n->leaf) {
-            const int l = blockRemoteLength(static_cast<const Block*>(n), refSeq, clientId);
-            if (pslOn) pslCheck(static_cast<const Block*>(n), refSeq, clientId, l);
+            const Block* b = static_cast<const Block*>(n);
+            // the reference's answer, partialLengths.getPartialLength (mergeTree.ts:928-931): O(log W) per
+            // block instead of the leaf sum (a leaf-level root keeps the leaf sum: its own partial length
+            // can read stale-high, see pslCheck; it has at most 7 leaves)
+            if (pslAnswer && b->pl && !(b == root && b->childCount > 0 && b->children[0]->leaf))
+                return int(b->pl->getPartialLength(refSeq, clientId));
+            const int l = blockRemoteLength(b, refSeq, clientId);
+            if (pslOn && !pslAnswer) pslCheck(b, refSeq, clientId, l);
             return l;
         }
         return leafRemoteLength(static_cast<const Seg*>(n), refSeq, clientId);
@@ -340,6 +347,7 @@ class Tree {
     // block keeps its PartialSequenceLengths, updated where mergeTree.ts / zamboni.ts update it, and
     // every remote block-length query compares the two (test/testUtils.ts:209-248).
     bool pslOn = g_psl != 0;
+    bool pslAnswer = g_psl == 2;
     //
     // One reference quirk is modelled, not flagged: a root whose children are leaves never receives
     // markRangeRemoved's post-order update (depthFirstNodeWalk's first block result is undefined,

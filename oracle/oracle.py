@@ -95,6 +95,17 @@ class psl_check:
         return False
 
 
+class psl_answer(psl_check):
+    """Context manager: oracle documents created inside answer every remote block length from their
+    PartialSequenceLengths (getPartialLength, partialLengths.ts:698-735, O(log W) per block), as the
+    reference does, instead of summing the block's leaves -- the reference's algorithm for bench.py's
+    CPU baseline.  (No cross-check: the leaf-sum path stays the tests' checker.)"""
+
+    def __enter__(self):
+        lib().oracle_set_psl_check(2)
+        return self
+
+
 def options(new_length_calc=False, snapshot_v1=True, chunk_size=10000):
     return abi.MtrOptions(int(new_length_calc), int(snapshot_v1), int(chunk_size), 0)
 

@@ -222,6 +222,27 @@ def test_regenerated_insert_uses_original_properties_oracle():
     assert op["seg"] == {"text": "abc", "props": {"prop2": "bar"}}
 
 
+def _wide_kat(n=300):
+    """A pending remove over more segments than 256 (the engine's former pending-group ring): remote inserts
+    at MSN 0 stay separate segments, the writer removes everything locally, regenerates it (one group per
+    segment, resetPendingDeltaToOps) and the regenerated removes are acked."""
+    it = Interner()
+    w = Writer(it)
+    for k in range(n):
+        w.message(ins(k, "ab"[k % 2]), client="A")
+    op = w.local(rem(0, n))
+    w.message(ins(0, "z"), client="A", ref=w.seq)  # the writer was disconnected: a remote op first
+    new = w.regenerate([op])[0]
+    w.message(new)
+    return w, new
+
+
+def test_regenerate_wide_remove_oracle():
+    w, new = _wide_kat()
+    assert new["type"] == 3 and len(new["ops"]) == 300
+    assert w.text() == "z"
+
+
 def _farm(seed, rounds=30, newlen=False):
     """client.reconnectFarm.spec.ts's shape with one reconnecting writer: per round the writer makes local
     edits; a remote writer's messages are sequenced first (the writer was disconnected); then the writer
@@ -313,6 +334,7 @@ def test_reset_pending_kats_engine():
         w, _ = _props_kat(kind)
         _replay_engine(w)
     _replay_engine(_zombie_kat()[0])  # the removed segment's props (leaf hashes) equal the oracle's
+    _replay_engine(_wide_kat()[0])    # 300 regenerated groups (more than 256 pending at once)
 
 
 @pytest.mark.gpu
