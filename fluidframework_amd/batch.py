@@ -190,6 +190,16 @@ def combine_absent(co: dict, seq: int) -> Any:
     return cur
 
 
+def _local_comb(co: Any) -> int:
+    """A local annotate's combiningOp: none, or "rewrite" (PropertiesManager.pendingRewriteCount,
+    segmentPropertiesManager.ts:72-80, 109-112); its ack / rollback records carry the same code (pos1)."""
+    if not js_truthy(co):
+        return abi.COMB_NONE
+    if isinstance(co, dict) and co.get("name") == "rewrite":
+        return abi.COMB_REWRITE
+    raise Unsupported("local annotate with a combiningOp other than rewrite")
+
+
 @dataclass
 class DocLog:
     """Per-document host state: client registry plus the ops/text of the batch being built."""
@@ -330,23 +340,23 @@ class DocLog:
     def local_remove(self, start: int, end: int) -> None:
         self.ops.append((abi.OP_LOCAL_REMOVE, 0, 0, self._local_seq(), 0, 0, start, end, 0, 0))
 
-    def local_annotate(self, start: int, end: int, props: dict, interner: Interner) -> None:
+    def local_annotate(self, start: int, end: int, props: dict, interner: Interner, combining_op: Any = None) -> None:
         if isinstance(props, dict) and "markerId" in props:
             self.marker_id_annotated = True
-        self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, self._local_seq(), 0, 0, start, end, interner.propop(props), 0))
+        comb = _local_comb(combining_op)
+        self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, self._local_seq(), 0, 0, start, end, interner.propop(props), comb))
 
     def rollback(self, op: dict, interner: Interner) -> None:
         """Client.rollback (client.ts:421-423 -> MergeTree.rollback, mergeTree.ts:2049-2159) of the newest
         pending local op `op` (its contents)."""
         t = op.get("type")
-        pp = 0
+        pp = comb = 0
         if t == 2:
-            if js_truthy(op.get("combiningOp")):
-                raise Unsupported("rollback of a combining annotate")
+            comb = _local_comb(op.get("combiningOp"))
             pp = interner.propop(op.get("props") or {})
         elif t not in (0, 1):
             raise Unsupported(f"rollback of op type {t}")
-        self.ops.append((abi.OP_ROLLBACK, 0, 0, -1, 0, 0, 0, 0, pp, t))
+        self.ops.append((abi.OP_ROLLBACK, 0, 0, -1, 0, 0, comb, 0, pp, t))
 
     def regenerate(self, op: dict) -> int:
         """Client.regeneratePendingOp (client.ts:917-960) of the oldest pending local op `op` (its contents;
@@ -370,9 +380,7 @@ class DocLog:
         elif t == 1:
             self.local_remove(int(op["pos1"]), int(op["pos2"]))
         elif t == 2:
-            if js_truthy(op.get("combiningOp")):
-                raise Unsupported("local annotate with a combiningOp")
-            self.local_annotate(int(op["pos1"]), int(op["pos2"]), op.get("props") or {}, interner)
+            self.local_annotate(int(op["pos1"]), int(op["pos2"]), op.get("props") or {}, interner, op.get("combiningOp"))
         else:
             raise Unsupported(f"local op type {t}")
 
@@ -476,14 +484,13 @@ class DocLog:
             for i, op in enumerate(members):
                 last = abi.F_LAST if i == len(members) - 1 else 0
                 t = op.get("type")
-                pp = 0
+                pp = comb = 0
                 if t == 2:
-                    if js_truthy(op.get("combiningOp")):
-                        raise Unsupported("ack of a local annotate with a combiningOp")
+                    comb = _local_comb(op.get("combiningOp"))
                     pp = interner.propop(op.get("props") or {})
                 elif t not in (0, 1):
                     raise Unsupported(f"ack of op type {t}")
-                self.ops.append((abi.OP_ACK, last, short, seq, ref, msn, 0, 0, pp, t))
+                self.ops.append((abi.OP_ACK, last, short, seq, ref, msn, comb, 0, pp, t))
             return
         for i, op in enumerate(members):
             last = abi.F_LAST if i == len(members) - 1 else 0

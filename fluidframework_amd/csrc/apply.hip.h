@@ -88,6 +88,10 @@ constexpr uint32_t PEND_KEY = 0x40000000u;
 constexpr int kChunkList = 8;
 constexpr int kCsumRows = 4 + kChunkList;
 enum { PK_INSERT = 1, PK_REMOVE = 2, PK_ANNOTATE = 3 };
+// a pending local "rewrite" annotate's cells and ring entry carry PK_REWRITE beside PK_ANNOTATE: while one is
+// pending, remote changes to the segment are blocked (pendingRewriteCount, segmentPropertiesManager.ts:72-80)
+constexpr int PK_REWRITE = 0x80;
+constexpr int PK_KIND = 0x7f;
 
 constexpr uint32_t CL_LOCAL = 0xffu;      // LocalClientId (-1)
 constexpr uint32_t CL_NONCOLLAB = 0xfeu;  // NonCollabClient (-2)
@@ -858,6 +862,11 @@ struct Eng {
                 out[7] = int(L.text[i]);
                 out[8] = L.props[i] == NONE32 ? -1 : int(L.props[i] & PN_MASK);
                 out[9] = before;
+                int groups = 0;  // segmentGroups.size: the leaf's pending cells (key cells are no group)
+                if (m & M_PEND)
+                    for (uint32_t c = pd_get(L, L.uid[i]); c != 0xffffffu; c = L.grm()[c] & 0xffffffu)
+                        groups += (L.grm()[c + 1] >> 16) != ZOMBIE_SLOT;
+                out[10] = groups;
             }
         }
     }
@@ -1476,7 +1485,7 @@ struct Eng {
         wsync();
         while (c != 0xffffffu && s.status == MTR_OK) {
             const uint32_t w0 = uniu(L.grm()[c]), w1 = uniu(L.grm()[c + 1]), w2 = uniu(L.grm()[c + 2]);
-            if ((w1 >> 16) == ZOMBIE_SLOT) zomb_add(L, P, s, r, w2);  // PropertiesManager.copyTo's counts
+            if ((w1 >> 16) == ZOMBIE_SLOT) zomb_add(L, P, s, r, w2, int(w0 >> 24) & PK_REWRITE);  // copyTo's counts
             else pend_add(L, P, s, r, int(w1 >> 16), int(w0 >> 24), 0, 0, w2);  // (previousProps duplicated)
             c = w0 & 0xffffffu;
         }
@@ -1484,7 +1493,7 @@ struct Eng {
     // a key cell for leaf i (wave-uniform): the pending key counts of annotate prop-op pp outlive its group
     // (pendingKeyUpdateCount, segmentPropertiesManager.ts:25, when resetPendingDeltaToOps does not re-send
     // the annotate to a segment removed meanwhile, client.ts:741-755)
-    static MTR_DI void zomb_add(D& L, const KParams& P, St& s, int i, uint32_t pp) {
+    static MTR_DI void zomb_add(D& L, const KParams& P, St& s, int i, uint32_t pp, int rw = 0) {
         const gptr<DocHdr> h = L.ghdr();
         const int fr = uni(h->pfree);
         if (!fr && s.rmused + 3 > P.rcap) {
@@ -1501,7 +1510,7 @@ struct Eng {
         bool ok = true;
         if (lane_id() == 0) {
             const uint32_t nxt = (m & (M_PEND | M_ZOMB)) ? pd_get(L, u) : 0xffffffu;
-            L.grm()[c] = (nxt & 0xffffffu) | (uint32_t(PK_ANNOTATE) << 24);
+            L.grm()[c] = (nxt & 0xffffffu) | (uint32_t(PK_ANNOTATE | rw) << 24);
             L.grm()[c + 1] = ZOMBIE_SLOT << 16;
             L.grm()[c + 2] = pp;
             ok = pd_set(L, u, c);
@@ -1512,17 +1521,28 @@ struct Eng {
         wsync();
     }
 
-    // one of a leaf's pending annotates holds `key` (PropertiesManager.pendingKeyUpdateCount[key] defined)
+    // one of a leaf's pending annotates holds `key` (PropertiesManager.pendingKeyUpdateCount[key] defined); a
+    // rewrite's null keys are not counted (segmentPropertiesManager.ts:127-131)
     static MTR_DI bool key_pending(const D& L, uint32_t c, uint32_t key) {
         const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV);
         const gptr<uint32_t> ring = L.gpend();
         while (c != 0xffffffu) {
             const uint32_t w0 = L.grm()[c], w1 = L.grm()[c + 1];
-            if ((w0 >> 24) == PK_ANNOTATE) {
+            if (((w0 >> 24) & PK_KIND) == PK_ANNOTATE) {
+                const bool rw = ((w0 >> 24) & PK_REWRITE) != 0;
                 const uint32_t pp = (w1 >> 16) == ZOMBIE_SLOT ? L.grm()[c + 2] : ring[4 * (w1 >> 16) + 3];
                 for (uint32_t q = poff[pp]; q < poff[pp + 1]; q++)
-                    if (pkv[2 * q] == key) return true;
+                    if (pkv[2 * q] == key && !(rw && pkv[2 * q + 1] == MTR_NULL_VALUE)) return true;
             }
+            c = w0 & 0xffffffu;
+        }
+        return false;
+    }
+    // a pending local rewrite on the leaf (pendingRewriteCount > 0): remote annotates leave it alone
+    static MTR_DI bool rewrite_pending(const D& L, uint32_t c) {
+        while (c != 0xffffffu) {
+            const uint32_t w0 = L.grm()[c];
+            if ((w0 >> 24) == uint32_t(PK_ANNOTATE | PK_REWRITE)) return true;
             c = w0 & 0xffffffu;
         }
         return false;
@@ -1574,8 +1594,12 @@ struct Eng {
 
     // a copy of set `cur` with each key of prop-op pp set to its value in set `old`, or deleted where
     // `old` lacks it (annotate rollback: the op's previousProps, mergeTree.ts:2129-2152); out of line (rare)
+    // rw: a rewrite's rollback (PropertiesRollback.Rewrite): its deltas are the old keys it deleted (old values,
+    // old order), then its non-null keys (old value or null), applied as a plain annotate (segmentPropertiesManager.ts
+    // :106-147; the pending counts go with the op's cells)
     static __device__ __attribute__((noinline)) uint32_t props_restore(const D& L, const KParams& P, St& s,
-                                                                      uint32_t cur, uint32_t old, uint32_t pp) {
+                                                                      uint32_t cur, uint32_t old, uint32_t pp,
+                                                                      bool rw = false) {
         const gptr<uint32_t> gprop = L.gprop();
         const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX),
                                    veq = L.tab(CP_VEQ);
@@ -1584,7 +1608,7 @@ struct Eng {
         const uint32_t n_cur = cur == NONE32 ? 0u : uniu(gprop[cur]);
         const uint32_t n_old = old == NONE32 ? 0u : uniu(gprop[old]);
         const uint32_t lo = uniu(poff[pp]), hi = uniu(poff[pp + 1]);
-        const uint32_t need = 1 + 2 * (n_cur + (hi - lo));
+        const uint32_t need = 1 + 2 * (n_cur + (hi - lo) + n_old);
         if (uint32_t(s.propused) + need > uint32_t(P.pcap)) {
             s.status = MTR_ERR_CAPACITY;
             return cur;
@@ -1593,14 +1617,30 @@ struct Eng {
         const gptr<uint32_t> e = gprop + dst;
         uint32_t n = n_cur;
         for (uint32_t k = 0; k < 2 * n_cur; k++) e[1 + k] = uniu(gprop[cur + 1 + k]);
-        for (uint32_t q = lo; q < hi; q++) {
-            const uint32_t key = uniu(pkv[2 * q]);
-            uint32_t val = MTR_NULL_VALUE;
-            for (uint32_t k = 0; k < n_old; k++)
-                if (uniu(gprop[old + 1 + 2 * k]) == key) {
-                    val = uniu(gprop[old + 2 + 2 * k]);
-                    break;
-                }
+        // delta steps: (rw) the old keys whose new value is absent or falsy, then the op's keys
+        const uint32_t n_del = rw ? n_old : 0u;
+        for (uint32_t q = 0; q < n_del + (hi - lo); q++) {
+            uint32_t key, val = MTR_NULL_VALUE;
+            if (q < n_del) {
+                key = uniu(gprop[old + 1 + 2 * q]);
+                bool truthy = false;
+                for (uint32_t j = lo; j < hi; j++)
+                    if (uniu(pkv[2 * j]) == key) {
+                        const uint32_t nv = uniu(pkv[2 * j + 1]);
+                        truthy = nv != MTR_NULL_VALUE && !(uniu(veq[nv]) & MTR_VEQ_FALSY);
+                        break;
+                    }
+                if (truthy) continue;
+                val = uniu(gprop[old + 2 + 2 * q]);
+            } else {
+                key = uniu(pkv[2 * (lo + q - n_del)]);
+                if (rw && uniu(pkv[2 * (lo + q - n_del) + 1]) == MTR_NULL_VALUE) continue;  // (the delete pass's)
+                for (uint32_t k = 0; k < n_old; k++)
+                    if (uniu(gprop[old + 1 + 2 * k]) == key) {
+                        val = uniu(gprop[old + 2 + 2 * k]);
+                        break;
+                    }
+            }
             int at = -1;
             for (uint32_t k = 0; k < n; k++)
                 if (uniu(e[1 + 2 * k]) == key) {
@@ -1649,7 +1689,7 @@ struct Eng {
     // (in group order) drops its cell and is reverted: a remove is undone, an insert becomes a segment
     // removed at UniversalSequenceNumber by this client (markRangeRemoved, :2117-2131), an annotate's keys
     // get their previous values back
-    static MTR_DI void rollback(D& L, const KParams& P, St& s, int type, uint32_t pp) {
+    static MTR_DI void rollback(D& L, const KParams& P, St& s, int type, uint32_t pp, uint32_t comb = 0) {
         const gptr<DocHdr> h = L.ghdr();
         const gptr<uint32_t> ring = L.gpend();
         const int head = uni(h->phead), tail = uni(h->ptail);
@@ -1691,7 +1731,7 @@ struct Eng {
                     if (live) L.rseq[i] = 0;
                 }
             } else if (type == MTR_OP_ANNOTATE) {
-                const uint32_t np = props_restore(L, P, s, uniu(L.props[i]), oldp, pp);
+                const uint32_t np = props_restore(L, P, s, uniu(L.props[i]), oldp, pp, (comb & 7u) == MTR_COMB_REWRITE);
                 if (lane_id() == 0) L.props[i] = np;
             } else {
                 s.status = MTR_ERR_BAD_OP;
@@ -1861,6 +1901,7 @@ struct Eng {
         const int slot = head % kPendRing;
         const int lseq = int(uniu(ring[4 * slot])), cnt = int(uniu(ring[4 * slot + 1]));
         const uint32_t ppo = uniu(ring[4 * slot + 3]);
+        const int rw = int(uniu(ring[4 * slot + 2])) & PK_REWRITE;
         if (lane_id() == 0) h->phead = head + 1;  // pendingSegments.shift()
         wsync();
         const int S = s.nseg;
@@ -1910,7 +1951,7 @@ struct Eng {
                 }
                 pend_drop(L, j, slot);  // segment.segmentGroups.dequeue()
                 // an annotate not re-sent keeps its pending key counts on the segment (they are never acked)
-                if (type == MTR_OP_ANNOTATE && !emit) zomb_add(L, P, s, j, ppo);
+                if (type == MTR_OP_ANNOTATE && !emit) zomb_add(L, P, s, j, ppo, rw);
                 const int here = off;
                 off += ln;
                 if (!emit) continue;
@@ -1921,7 +1962,8 @@ struct Eng {
                     put_record(L, s, gidx, type == MTR_OP_INSERT ? here : 0, ref, MTR_DELTA_REGEN_X);
                 }
                 // a new group of its own at the tail, same localSeq (client.ts:787-795)
-                pend_add(L, P, s, j, -1, kind, type == MTR_OP_ANNOTATE ? ppo : 0u, lseq);
+                pend_add(L, P, s, j, -1, kind | (type == MTR_OP_ANNOTATE ? rw : 0), type == MTR_OP_ANNOTATE ? ppo : 0u,
+                         lseq);
             }
         }
     }
@@ -1939,6 +1981,7 @@ struct Eng {
                                                                          uint32_t old, uint32_t pp,
                                              uint32_t comb, uint32_t pl = 0xffffffu) {
         PropRes r{old, propused, MTR_OK};
+        if (pl != 0xffffffu && rewrite_pending(L, pl)) return r;  // outstanding local rewrites block remote changes
         const gptr<uint32_t> gprop = L.gprop();
         const gptr<const uint32_t> poff = L.tab(CP_POFF), pkv = L.tab(CP_PKV), kix = L.tab(CP_KIX),
                                    veq = L.tab(CP_VEQ);
@@ -3143,7 +3186,9 @@ struct Eng {
                         wsync();
                         for (uint64_t t = am; t && s.status == MTR_OK; t &= t - 1) {
                             const int l = first_lane(t);
-                            pslot = pend_add(L, P, s, base + l, pslot, PK_ANNOTATE, pp, plseq, rdlane(old, l));
+                            pslot = pend_add(L, P, s, base + l, pslot,
+                                             PK_ANNOTATE | ((comb & 7u) == MTR_COMB_REWRITE ? PK_REWRITE : 0), pp,
+                                             plseq, rdlane(old, l));
                         }
                         mj = L.meta[jc];
                     }
@@ -3518,8 +3563,8 @@ struct Eng {
             v.ref = s.curseq;
             v.local = 1;
             if (s.collab) {  // a pending local op (seq = UnassignedSequenceNumber, the local client)
-                if (!X || (op.type == MTR_OP_LOCAL_ANNOTATE && op.payload2 != 0)) {
-                    s.status = MTR_ERR_UNSUPPORTED;  // (pending combining annotates: not built)
+                if (!X || (op.type == MTR_OP_LOCAL_ANNOTATE && op.payload2 != 0 && op.payload2 != MTR_COMB_REWRITE)) {
+                    s.status = MTR_ERR_UNSUPPORTED;  // (pending combining annotates other than rewrite: not built)
                     s.fail_op = gidx;
                     return false;
                 }
@@ -3562,12 +3607,13 @@ struct Eng {
                 split_at(L, P, s, pos1);
                 split_at(L, P, s, pos2);
                 if (X && lseq) {  // pending: removedSeq = LOCAL_BASE + localSeq; the touched leaves join a group
-                    range_walk(L, P, s, v, pos1, pos2, sseq, client, is_remove, op.payload, 0u, is_remove != 0, true,
-                               lseq);
+                    range_walk(L, P, s, v, pos1, pos2, sseq, client, is_remove, op.payload, is_remove ? 0u : op.payload2,
+                               is_remove != 0, true, lseq);
                     if (s.status == MTR_OK && is_remove) pend_touched(L, P, s, PK_REMOVE, 0u, lseq);
                 } else {
                     range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
-                               op.type == MTR_OP_ANNOTATE ? op.payload2 : 0u, DL && !PM && (op.flags & MTR_F_DELTA) != 0);
+                               (op.type == MTR_OP_ANNOTATE || (X && op.type == MTR_OP_LOCAL_ANNOTATE)) ? op.payload2 : 0u,
+                               DL && !PM && (op.flags & MTR_F_DELTA) != 0);
                 }
                 if (G && is_remove) csum_update(L, s, L.wlo, L.whi);
                 zop = s.collab && !local_op;
@@ -3580,7 +3626,7 @@ struct Eng {
                     s.status = MTR_ERR_BAD_OP;
                     break;
                 }
-                rollback(L, P, s, int(op.payload2), op.payload);
+                rollback(L, P, s, int(op.payload2), op.payload, uint32_t(op.pos1));
                 break;
             case MTR_OP_REGENERATE:  // Client.regeneratePendingOp (client.ts:917-960) of the oldest pending op
                 if (!X || !DL || PM || !s.collab) {

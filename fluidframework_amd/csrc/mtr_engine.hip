@@ -1263,7 +1263,7 @@ int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t
     if (e->red.ensure(16)) return -1;
     containing_kernel<<<1, NT, lds_bytes_global_mode(), e->stream>>>(P, doc, pos, ref_seq, client, e->red.p);
     HIPCHK(hipGetLastError());
-    int32_t r[10];
+    int32_t r[11];
     HIPCHK(hipMemcpyAsync(r, e->red.p, sizeof(r), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     std::memset(info, 0, sizeof(*info));
@@ -1283,6 +1283,7 @@ int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t
     info->ref_type = r[7];
     info->props = r[8];
     info->start = r[9];
+    info->groups = r[10];
     const bool has_text = !info->marker && e->h_kind[doc] == 0;
     if (text && has_text && info->length > 0 && text_cap >= info->length)
         HIPCHK(hipMemcpy(text, e->text.p + size_t(doc) * e->caps.text_units + uint32_t(r[7]),

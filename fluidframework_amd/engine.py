@@ -36,7 +36,7 @@ class SegmentInfo(C.Structure):
     """include/mtr.h: mtr_segment_info"""
     _fields_ = [(n, C.c_int32) for n in ("leaf", "offset", "length", "seq", "client", "removed_seq", "marker",
                                          "ref_type", "props", "start", "removed", "local_seq",
-                                         "local_removed_seq")]
+                                         "local_removed_seq", "groups")]
 
 
 def lib():

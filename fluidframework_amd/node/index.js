@@ -287,19 +287,19 @@ class DocLog {
         this.push(OP.LOCAL_INSERT, s[0], 0, this.localSeq(), 0, 0, pos, s[3], s[1], s[2]);
     }
     localRemove(start, end) { this.push(OP.LOCAL_REMOVE, 0, 0, this.localSeq(), 0, 0, start, end, 0, 0); }
-    localAnnotate(start, end, props, it) {
+    localAnnotate(start, end, props, it, combiningOp) {
         if (props && typeof props === 'object' && 'markerId' in props) this.markerIdAnnotated = true;
-        this.push(OP.LOCAL_ANNOTATE, 0, 0, this.localSeq(), 0, 0, start, end, it.propop(props), 0);
+        this.push(OP.LOCAL_ANNOTATE, 0, 0, this.localSeq(), 0, 0, start, end, it.propop(props), localComb(combiningOp));
     }
     rollback(op, it) {  // Client.rollback (client.ts:421-423 -> MergeTree.rollback, mergeTree.ts:2049-2159)
-        let pp = 0;
+        let pp = 0, comb = 0;
         if (op.type === 2) {
-            if (op.combiningOp) throw new UnsupportedError('rollback of a combining annotate');
+            comb = localComb(op.combiningOp);
             pp = it.propop(op.props || {});
         } else if (op.type !== 0 && op.type !== 1) {
             throw new UnsupportedError('rollback of op type ' + op.type);
         }
-        this.push(OP.ROLLBACK, 0, 0, -1, 0, 0, 0, 0, pp, op.type);
+        this.push(OP.ROLLBACK, 0, 0, -1, 0, 0, comb, 0, pp, op.type);
     }
     // Client.regeneratePendingOp (client.ts:917-960): one record per member op; returns the first record's
     // index in this batch (the op field of its MTR_DELTA_REGEN records)
@@ -315,10 +315,8 @@ class DocLog {
     localOp(op, it) {  // Client.localTransaction member (client.ts:1029-1048)
         if (op.type === 0) this.localInsert(op.pos1, op.seg, it);
         else if (op.type === 1) this.localRemove(op.pos1, op.pos2);
-        else if (op.type === 2) {
-            if (op.combiningOp) throw new UnsupportedError('local annotate with a combiningOp');
-            this.localAnnotate(op.pos1, op.pos2, op.props || {}, it);
-        } else throw new UnsupportedError('local op type ' + op.type);
+        else if (op.type === 2) this.localAnnotate(op.pos1, op.pos2, op.props || {}, it, op.combiningOp);
+        else throw new UnsupportedError('local op type ' + op.type);
     }
     startCollab(longId, minSeq, currentSeq) {  // client.ts:1133-1155
         if (longId === undefined) return;  // detached: stay local until attached
@@ -347,14 +345,14 @@ class DocLog {
         if (cid === this.observerId || local) {  // ackPendingSegment per member (client.ts:641-663, 866-869)
             members.forEach((op, i) => {
                 const last = i === members.length - 1 ? F.LAST : 0;
-                let pp = 0;
+                let pp = 0, comb = 0;
                 if (op.type === 2) {
-                    if (op.combiningOp) throw new UnsupportedError('ack of a local annotate with a combiningOp');
+                    comb = localComb(op.combiningOp);
                     pp = it.propop(op.props || {});
                 } else if (op.type !== 0 && op.type !== 1) {
                     throw new UnsupportedError('ack of op type ' + op.type);
                 }
-                this.push(OP.ACK, last, short, seq, ref, msn, 0, 0, pp, op.type);
+                this.push(OP.ACK, last, short, seq, ref, msn, comb, 0, pp, op.type);
             });
             return;
         }
@@ -645,6 +643,14 @@ function regeneratedOp(resetOp, recs, first, propsOf) {
     return ops.length === 1 ? ops[0] : { ops, type: 3 };
 }
 
+// a local annotate's combiningOp: none or "rewrite" (pendingRewriteCount, segmentPropertiesManager.ts:72-80); its
+// ack and rollback records carry the same code (pos1)
+function localComb(co) {
+    if (!co) return COMB.NONE;
+    if (typeof co === 'object' && co.name === 'rewrite') return COMB.REWRITE;
+    throw new UnsupportedError('local annotate with a combiningOp other than rewrite');
+}
+
 class BatchReplayEngine {
     constructor(maxDocs, options) {
         this.options = Object.assign({ newLengthCalc: 0, snapshotV1: 1, chunkSize: 10000, device: 0 }, options || {});
@@ -786,7 +792,9 @@ class BatchReplayClient {
     localTransaction(groupOp) {
         this._queue(() => { for (const op of groupOp.ops) this.log.localOp(op, this.engine.interner); });
     }
-    annotateRangeLocal(start, end, props) { this._queue(() => this.log.localAnnotate(start, end, props, this.engine.interner)); }
+    annotateRangeLocal(start, end, props, combiningOp) {  // client.ts:245-260
+        this._queue(() => this.log.localAnnotate(start, end, props, this.engine.interner, combiningOp));
+    }
     /** Client.rollback(op, localOpMetadata) (client.ts:421-423) of the newest pending local op `op`. */
     rollback(op) { this._queue(() => this.log.rollback(op, this.engine.interner)); }
     /**

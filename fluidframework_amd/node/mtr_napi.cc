@@ -311,7 +311,7 @@ napi_value GetContainingSegment(napi_env env, napi_callback_info info) {
     } f[] = {{"leaf", si.leaf},   {"offset", si.offset},         {"length", si.length}, {"seq", si.seq},
              {"client", si.client}, {"removedSeq", si.removed_seq}, {"marker", si.marker}, {"refType", si.ref_type},
              {"props", si.props}, {"start", si.start}, {"removed", si.removed}, {"localSeq", si.local_seq},
-             {"localRemovedSeq", si.local_removed_seq}};
+             {"localRemovedSeq", si.local_removed_seq}, {"groups", si.groups}};
     for (const auto& x : f) {
         napi_value v;
         NAPI_CALL(env, napi_create_int32(env, x.v, &v));

@@ -149,6 +149,7 @@ typedef struct mtr_segment_info {
     int32_t removed;     /* 1 = the segment carries removal info (acked or pending) */
     int32_t local_seq;   /* localSeq of a pending local insert (then seq = -1), else -1 */
     int32_t local_removed_seq; /* localSeq of a pending local remove (then removed_seq = -1), else -1 */
+    int32_t groups;      /* segmentGroups.size: the pending local ops the segment belongs to */
 } mtr_segment_info;
 int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
                                mtr_segment_info* info, uint16_t* text, int64_t text_cap);

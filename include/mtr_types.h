@@ -32,8 +32,9 @@ enum {
                                    pending op (seq = UnassignedSequenceNumber, the local client's short id, a new
                                    localSeq and SegmentGroup, mergeTree.ts:1397-1427, 1604-1637) until its ACK */
     MTR_OP_LOCAL_REMOVE = 9,    /* local remove (client.ts:227; pending: mergeTree.ts:1955-2047) */
-    MTR_OP_LOCAL_ANNOTATE = 10, /* local annotate without a combiningOp (pending keys:
-                                   segmentPropertiesManager.ts:60-157) */
+    MTR_OP_LOCAL_ANNOTATE = 10, /* local annotate (pending keys: segmentPropertiesManager.ts:60-157); payload2 =
+                                   MTR_COMB_NONE or MTR_COMB_REWRITE (a pending rewrite blocks remote changes to
+                                   the segment, :72-80) */
     MTR_OP_START_COLLAB = 12,   /* Client.startOrUpdateCollaboration (client.ts:1133): seq/min_seq = currentSeq/minSeq,
                                    client = the observer's short id */
     MTR_OP_LOAD = 13,           /* a snapshot header segment (SnapshotLoader.loadHeader, snapshotLoader.ts:130-167):
@@ -52,10 +53,11 @@ enum {
                                    client.ts:866-869 -> ackPendingSegment, client.ts:641-663 and
                                    mergeTree.ts:1283-1322): acks the oldest pending SegmentGroup; payload2 =
                                    the member's MergeTreeDeltaType (segment.ack switches on it,
-                                   mergeTreeNodes.ts:439-479), payload = its prop-op for an annotate */
+                                   mergeTreeNodes.ts:439-479), payload = its prop-op for an annotate, pos1 = its
+                                   MTR_COMB_* (a local "rewrite" annotate: pendingRewriteCount) */
     MTR_OP_ROLLBACK = 18,       /* Client.rollback (client.ts:421 -> MergeTree.rollback, mergeTree.ts:2049-2159) of the
                                    newest pending local op: payload2 = its MergeTreeDeltaType, payload = its
-                                   prop-op (annotate) */
+                                   prop-op (annotate), pos1 = its MTR_COMB_* (PropertiesRollback.Rewrite) */
     MTR_OP_REGENERATE = 19,     /* Client.regeneratePendingOp (client.ts:917-960) of the oldest pending local op, for
                                    a resubmit after reconnect: normalizeSegmentsOnRebase first when currentSeq moved
                                    since the last one (mergeTree.ts:2352-2381, 2231-2331), then

@@ -95,6 +95,7 @@ struct Seg : Node {
     // PropertiesManager.pendingKeyUpdateCount (segmentPropertiesManager.ts:25): key id -> count > 0
     std::deque<struct SegGroup*> groups;
     std::vector<std::pair<uint32_t, int>> pendingKeys;
+    int pendingRewrite = 0;  // PropertiesManager.pendingRewriteCount (segmentPropertiesManager.ts:26)
     // BaseSegment.localSeq / localRemovedSeq (mergeTreeNodes.ts:382-383): the local op that inserted /
     // removed it while unacked (-1 = undefined); cleared by the ack (:460, 469)
     int localSeq = -1;
@@ -422,6 +423,7 @@ class Tree {
             r->hasProps = true;
             r->props = s->props;
             r->pendingKeys = s->pendingKeys;  // PropertiesManager.copyTo, segmentPropertiesManager.ts:160-184
+            r->pendingRewrite = s->pendingRewrite;
         }
         r->parent = s->parent;
         r->removedClientIds = s->removedClientIds;
@@ -478,7 +480,7 @@ class Tree {
 
     // MergeTree.rollback (mergeTree.ts:2049-2159): revert the newest pending local op (type = its
     // MergeTreeDeltaType; propop = its props for an annotate)
-    void rollback(int type, uint32_t propop) {
+    void rollback(int type, uint32_t propop, uint32_t comb = 0) {
         if (pendingSegments.empty()) {
             status = MTR_ERR_BAD_OP;  // "Rollback op doesn't match last edit"
             return;
@@ -518,6 +520,10 @@ class Tree {
                 const auto& prev = g->previousProps[k];
                 s->hasPropMgr = true;
                 s->hasProps = true;
+                if ((comb & 7u) == MTR_COMB_REWRITE) {  // PropertiesRollback.Rewrite
+                    rollbackRewrite(s, propop, prev);
+                    continue;
+                }
                 for (uint32_t q = b->propop_off[propop]; q < b->propop_off[propop + 1]; q++) {
                     const uint32_t key = b->propop_kv[2 * q];
                     if (int* c = pendingCount(s, key)) {  // decrementPendingCounts (:37-58)
@@ -542,9 +548,59 @@ class Tree {
         }
     }
 
+    // The rollback of a local rewrite annotate on segment s (mergeTree.ts:2129-2152 with
+    // PropertiesRollback.Rewrite): decrementPendingCounts(true, oldProps) runs over the segment's *current*
+    // keys (segmentPropertiesManager.ts:84-89), then the op's deltas -- the previousProps addProperties
+    // returned (:106-147): the old keys the rewrite deleted (old values, old order), then its non-null keys
+    // (old value, or null) -- are applied as a plain annotate: null deletes, a value sets (appended when new)
+    void rollbackRewrite(Seg* s, uint32_t propop, const std::pair<bool, PropMap>& prev) {
+        const mtr_batch* b = tabs.b;
+        const uint32_t lo = b->propop_off[propop], hi = b->propop_off[propop + 1];
+        s->pendingRewrite--;
+        for (auto& kv : std::vector<std::pair<uint32_t, uint32_t>>(s->props.kv))
+            if (int* c = pendingCount(s, kv.first))
+                if (--*c == 0)
+                    for (size_t j = 0; j < s->pendingKeys.size(); j++)
+                        if (s->pendingKeys[j].first == kv.first) {
+                            s->pendingKeys.erase(s->pendingKeys.begin() + j);
+                            break;
+                        }
+        const PropMap old = prev.first ? prev.second : PropMap{};
+        auto oldVal = [&](uint32_t key) -> uint32_t {
+            for (auto& kv : old.kv)
+                if (kv.first == key) return kv.second;
+            return MTR_NULL_VALUE;
+        };
+        std::vector<std::pair<uint32_t, uint32_t>> deltas;
+        auto put = [&](uint32_t key, uint32_t v) {
+            for (auto& d : deltas)
+                if (d.first == key) {
+                    d.second = v;
+                    return;
+                }
+            deltas.push_back({key, v});
+        };
+        for (auto& kv : old.kv) {  // the delete pass: old keys whose new value is absent or falsy
+            bool truthy = false;
+            for (uint32_t i = lo; i < hi; i++)
+                if (b->propop_kv[2 * i] == kv.first) {
+                    const uint32_t v = b->propop_kv[2 * i + 1];
+                    truthy = v != MTR_NULL_VALUE && !(b->val_eq[v] & MTR_VEQ_FALSY);
+                    break;
+                }
+            if (!truthy) put(kv.first, kv.second);
+        }
+        for (uint32_t i = lo; i < hi; i++)  // the op's keys (a null one was handled by the delete pass)
+            if (b->propop_kv[2 * i + 1] != MTR_NULL_VALUE) put(b->propop_kv[2 * i], oldVal(b->propop_kv[2 * i]));
+        for (auto& d : deltas) {
+            if (d.second == MTR_NULL_VALUE) propDelete(s->props, d.first);
+            else propSet(s->props, d.first, d.second, tabs);
+        }
+    }
+
     // MergeTree.ackPendingSegment (mergeTree.ts:1283-1322) for one member op of this client's sequenced
     // message; opType = that member's MergeTreeDeltaType, propop = its props (annotate)
-    void ackPendingSegment(int opType, uint32_t propop, int seq) {
+    void ackPendingSegment(int opType, uint32_t propop, int seq, uint32_t comb = 0) {
         if (!pendingSegments.empty()) {
             SegGroup* g = pendingSegments.front();
             pendingSegments.pop_front();
@@ -557,10 +613,13 @@ class Tree {
                 s->groups.pop_front();
                 if (opType == MTR_OP_ANNOTATE) {  // ackPendingProperties -> decrementPendingCounts (:32-58)
                     const mtr_batch* b = tabs.b;
+                    const bool rewrite = (comb & 7u) == MTR_COMB_REWRITE;
+                    if (rewrite) s->pendingRewrite--;
                     for (uint32_t i = b->propop_off[propop]; i < b->propop_off[propop + 1]; i++) {
                         const uint32_t k = b->propop_kv[2 * i];
                         int* c = pendingCount(s, k);
                         if (!c) continue;
+                        if (rewrite && b->propop_kv[2 * i + 1] == MTR_NULL_VALUE) continue;  // not tracked
                         if (*c <= 0) {
                             status = MTR_ERR_ASSERT | 0x05c;
                             return;
@@ -1158,10 +1217,13 @@ class Tree {
         // shouldModifyKey (:94-104): a remote op leaves keys with pending local updates alone unless it
         // has a (non-rewrite) combiningOp
         const bool remote = seq != kUnassignedSeq && seq != kUniversalSeq;
+        // outstanding local rewrites block every remote change (:72-80)
+        if (s->pendingRewrite > 0 && remote && collab) return;
         auto modify = [&](uint32_t key) {
             return !remote || mode >= MTR_COMB_INCR || pendingCount(s, key) == nullptr;
         };
         if (mode == MTR_COMB_REWRITE) {  // delete old keys whose new value is falsy (:109-123)
+            if (collab && seq == kUnassignedSeq) s->pendingRewrite++;
             std::vector<std::pair<uint32_t, uint32_t>> kept;
             for (auto& kv : s->props.kv) {
                 bool truthy = false;
@@ -1179,6 +1241,7 @@ class Tree {
             uint32_t k = b->propop_kv[2 * i], v = b->propop_kv[2 * i + 1];
             if (collab) {  // :126-138
                 if (seq == kUnassignedSeq) {
+                    if (mode == MTR_COMB_REWRITE && v == MTR_NULL_VALUE) continue;  // (handled by the delete pass)
                     if (int* c = pendingCount(s, k)) ++*c;
                     else s->pendingKeys.push_back({k, 1});
                 } else if (!modify(k)) {
@@ -1458,13 +1521,14 @@ class Tree {
                                  collaborating ? kUnassignedSeq : kUniversalSeq);
                 return status;
             case MTR_OP_LOCAL_ANNOTATE:
-                if (op.payload2 != MTR_COMB_NONE) return MTR_ERR_UNSUPPORTED;  // pending combining ops
+                // (pending combining ops other than rewrite: not built)
+                if (op.payload2 != MTR_COMB_NONE && !(op.payload2 == MTR_COMB_REWRITE)) return MTR_ERR_UNSUPPORTED;
                 annotateRange(op.pos1, op.pos2, op.payload, currentSeq, localClientId,
-                              collaborating ? kUnassignedSeq : kUniversalSeq);
+                              collaborating ? kUnassignedSeq : kUniversalSeq, op.payload2);
                 return status;
             case MTR_OP_ROLLBACK:  // Client.rollback (client.ts:421-423) of the newest pending local op
                 if (!collaborating) return MTR_ERR_BAD_OP;
-                rollback(int(op.payload2), op.payload);
+                rollback(int(op.payload2), op.payload, uint32_t(op.pos1));
                 return status;
             case MTR_OP_REGENERATE:  // Client.regeneratePendingOp (client.ts:917-960) of the oldest pending op
                 if (!collaborating) return MTR_ERR_BAD_OP;
@@ -1472,7 +1536,7 @@ class Tree {
                 return status;
             case MTR_OP_ACK:  // Client.applyMsg of this client's own message (client.ts:866-869)
                 if (!collaborating) return MTR_ERR_BAD_OP;
-                ackPendingSegment(int(op.payload2), op.payload, op.seq);
+                ackPendingSegment(int(op.payload2), op.payload, op.seq, uint32_t(op.pos1));
                 break;
             case MTR_OP_START_COLLAB:  // startOrUpdateCollaboration -> startCollaboration, client.ts:1133, mergeTree.ts:731
                 if (collaborating) return MTR_OK;
@@ -1903,6 +1967,24 @@ int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32
     out[2] = s->len;
     out[3] = pos - off;
     return out[0];
+}
+
+int64_t oracle_doc_containing_props(oracle_doc* d, int32_t pos, int32_t ref_seq, int32_t client, uint32_t* out,
+                                    int64_t cap) {
+    Tree& t = d->view();
+    int off = 0;
+    Seg* s = t.containingSegment(pos, ref_seq, client, off);
+    if (!s) return -1;
+    const int64_t n = 3 + 2 * int64_t(s->props.kv.size());
+    if (n > cap) return -n;
+    out[0] = uint32_t(s->groups.size());
+    out[1] = s->hasProps ? 1u : 0u;
+    out[2] = uint32_t(s->props.kv.size());
+    for (size_t k = 0; k < s->props.kv.size(); k++) {
+        out[3 + 2 * k] = s->props.kv[k].first;
+        out[4 + 2 * k] = s->props.kv[k].second;
+    }
+    return n;
 }
 
 int32_t oracle_doc_marker_position(oracle_doc* d, uint32_t ordinal, int32_t ref_seq, int32_t client) {

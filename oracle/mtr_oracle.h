@@ -101,6 +101,10 @@ void oracle_set_trace(int on);
 /* getContainingSegment (mergeTree.ts:787-813) at (ref_seq, client): out[0] = leaf index in tree order
  * (-1 = none, also returned), out[1] = offset, out[2] = cachedLength, out[3] = segment start. */
 int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32_t client, int32_t* out);
+/* getContainingSegment's segment: out = [segmentGroups.size, properties !== undefined, n, key id, value id, ...];
+ * returns the word count, -needed when cap is short, -1 when no segment covers pos */
+int64_t oracle_doc_containing_props(oracle_doc* d, int32_t pos, int32_t ref_seq, int32_t client, uint32_t* out,
+                                    int64_t cap);
 
 /* Length of the doc in the (ref_seq, client) view (MergeTree.getLength, mergeTree.ts:757) */
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client);

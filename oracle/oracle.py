@@ -67,6 +67,8 @@ def lib():
         L.oracle_doc_containing.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
         L.oracle_doc_marker_position.restype = C.c_int32
         L.oracle_doc_marker_position.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32]
+        L.oracle_doc_containing_props.restype = C.c_int64
+        L.oracle_doc_containing_props.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int64]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         _LIB = L
@@ -189,6 +191,19 @@ class OracleDoc:
         out = np.zeros(4, dtype="<i4")
         lib().oracle_doc_containing(self.h, pos, ref_seq, client, out.ctypes.data)
         return tuple(int(x) for x in out) if out[0] >= 0 else (-1, 0, 0, 0)
+
+    def containing_props(self, pos, ref_seq, client):
+        """getContainingSegment's segment -> (segmentGroups.size, [(key id, value id)] or None when its
+        properties are undefined); None when no segment covers pos."""
+        out = np.zeros(256, dtype="<u4")
+        n = lib().oracle_doc_containing_props(self.h, pos, ref_seq, client, out.ctypes.data, out.size)
+        if n == -1:
+            return None
+        if n < -1:
+            out = np.zeros(-n, dtype="<u4")
+            lib().oracle_doc_containing_props(self.h, pos, ref_seq, client, out.ctypes.data, out.size)
+        pairs = [(int(out[3 + 2 * k]), int(out[4 + 2 * k])) for k in range(int(out[2]))]
+        return int(out[0]), (pairs if out[1] else None)
 
     def marker_position(self, ordinal, ref_seq, client):
         """getPosition of the marker mapped to a host marker ordinal at (refSeq, clientId); -1 if none."""
