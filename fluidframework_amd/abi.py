@@ -20,6 +20,21 @@ OP_HANDLES = 16
 OP_ACK = 17
 OP_ROLLBACK = 18
 OP_REGENERATE = 19
+OP_REF_CREATE = 20
+OP_REF_REMOVE = 21
+REF_SLIDE = 1
+REF_LOCALVIEW = 2
+# ReferenceType (ops.ts:9-36)
+REFTYPE_SIMPLE = 0x0
+REFTYPE_TILE = 0x1
+REFTYPE_NEST_BEGIN = 0x2
+REFTYPE_NEST_END = 0x4
+REFTYPE_RANGE_BEGIN = 0x10
+REFTYPE_RANGE_END = 0x20
+REFTYPE_SLIDE_ON_REMOVE = 0x40
+REFTYPE_STAY_ON_REMOVE = 0x80
+REFTYPE_TRANSIENT = 0x100
+DETACHED_POSITION = -1
 DELTA_REGEN = 64
 DELTA_REGEN_X = 72
 REL_BEFORE = 1

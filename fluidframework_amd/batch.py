@@ -216,6 +216,7 @@ class DocLog:
     marker_ids: dict = field(default_factory=dict)
     marker_dup: set = field(default_factory=set)  # ids mapped to two markers: block-update order decides
     marker_id_annotated: bool = False              # an annotate touched "markerId": remapped by blockUpdate
+    n_refs: int = 0                                # local references created (MTR_OP_REF_CREATE ids)
 
     def short_id(self, long_id: str) -> int:
         """Client.getOrAddShortClientId (client.ts:673-677)."""
@@ -371,6 +372,28 @@ class DocLog:
                 raise Unsupported(f"regenerate of op type {t}")
             self.ops.append((abi.OP_REGENERATE, abi.F_DELTA, 0, -1, 0, 0, 0, 0, 0, t))
         return first
+
+    # -- local references (localReference.ts)
+    def create_ref(self, pos: int, ref_type: int, view: tuple | None = None, slide: bool = False) -> int:
+        """createPositionReference (sequence/src/intervalCollection.ts:697-724): Client.getContainingSegment(pos,
+        view) (client.ts:1065-1078; view = (referenceSequenceNumber, long client id), None = the local view),
+        Client.getSlideToSegment when `slide` (client.ts:1085-1099), then createLocalReferencePosition
+        (client.ts:377-389) -- a detached reference when no segment holds pos.  Returns the reference id."""
+        if view is None:
+            short, ref, flags = 0, 0, abi.REF_LOCALVIEW
+        else:
+            short, ref, flags = self.short_id(str(view[1])), int(view[0]), 0
+        if slide:
+            flags |= abi.REF_SLIDE
+        self.ops.append((abi.OP_REF_CREATE, 0, short, 0, ref, 0, int(pos), 0, int(ref_type), flags))
+        self.n_refs += 1
+        return self.n_refs - 1
+
+    def remove_ref(self, ref_id: int) -> None:
+        """Client.removeLocalReferencePosition (client.ts:394-396)."""
+        if not 0 <= ref_id < self.n_refs:
+            raise ValueError(f"no local reference {ref_id}")
+        self.ops.append((abi.OP_REF_REMOVE, 0, 0, 0, 0, 0, 0, 0, int(ref_id), 0))
 
     def local_op(self, op: dict, interner: Interner) -> None:
         """A local merge-tree op (the contents this client submits): insert / remove / annotate."""

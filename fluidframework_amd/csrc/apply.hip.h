@@ -162,6 +162,7 @@ struct DocHdr {
     int32_t chunked;       // ... and their per-64-slot chunk summaries are valid (two-level view scan)
     int32_t pfree;         // free list of pending-membership cells (first cell + 1, 0 = empty)
     int32_t lastnorm;      // Client.lastNormalizationRefSeq (client.ts:910): currentSeq of the last normalization
+    int32_t nrefs;         // local references created (Eng::ref_create): ids 0 .. nrefs - 1
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -219,6 +220,8 @@ struct KParams {
     uint32_t* pend;              // [doc][kPendRing][4] pending SegmentGroups (batches with local ops only)
     int32_t* csum;               // [doc][2][segcap / 64 + 1] chunk summaries of HBM-resident documents
     int32_t* umap;               // [doc][2 * segcap] uid -> slot hints of HBM-resident documents
+    uint32_t* refs;              // [doc][3][refcap] local references (batches with reference records only)
+    int32_t refcap;
 };
 
 // phase-timer slots (-DMTR_PROF builds)
@@ -231,7 +234,7 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
 // records, the batch's property tables), kept in LDS and read where used, so they never hold SGPRs
 // across the whole op loop (the loop's scalar state otherwise spills into VGPR lanes)
 enum { CP_TEXT = 0, CP_PROP, CP_RM, CP_RT, CP_DELTA, CP_POFF, CP_PKV, CP_KIX, CP_VEQ, CP_HDR, CP_PEND, CP_CSUM, CP_UMAP,
-       CP_N };
+       CP_REFS, CP_N };
 
 // LDS-side scratch of one document: record-mode broadcast, cold pointers, phase timers
 struct Sc {
@@ -239,6 +242,7 @@ struct Sc {
     int gen_ref, gen_client;
     int rel[2];   // positions resolved by MTR_OP_RELPOS records for the next (MTR_F_REL) op
     int relmask;  // which of rel[] are pending: bit 0 pos1, bit 1 pos2
+    int nrefs, refcap;  // local references of the document (DocHdr.nrefs) and the table's capacity
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];
 #endif
@@ -868,6 +872,64 @@ struct Eng {
                         groups += (L.grm()[c + 1] >> 16) != ZOMBIE_SLOT;
                 out[10] = groups;
             }
+        }
+    }
+
+    // Client.localReferencePositionToPosition (client.ts:398-403 -> mergeTree.ts:1046-1062) of every local
+    // reference of a document on its HBM state: out[r] = DetachedReferencePosition when the reference has no
+    // segment, its segment is gone (unlinked, merged away) or no longer holds it (a Transient one is never held),
+    // else its offset (0 on a removed segment) plus the segment's local-view position.  info_id >= 0: out =
+    // {leaf ordinal of its segment (-1: none or gone), offset, ReferenceType, held} of that reference instead.
+    static MTR_DI void ref_query(char* smem, const KParams& P, uint32_t d, int32_t* out, int info_id) {
+        D L;
+        carve(L, smem, P, d);
+        St s;
+        load_doc(L, P, s, d);
+        const int n = rf_uid(L) ? nrefs(L) : 0;
+        const int S = s.nseg;
+        if (info_id >= 0) {
+            int o4[4] = {-1, 0, 0, 0};
+            if (info_id < n) {
+                const uint32_t u = uniu(rf_uid(L)[info_id]), t = uniu(rf_ty(L)[info_id]);
+                const int x = u == NONE32 ? -1 : find_uid(L, s, u);
+                o4[0] = (x >= 0 && G && s.holes) ? count_live(L, 0, x) : x;
+                o4[1] = int(uniu(rf_off(L)[info_id]));
+                o4[2] = int(t & ~RF_HELD);
+                o4[3] = (t & RF_HELD) ? 1 : 0;
+            }
+            if (lane_id() == 0)
+                for (int q = 0; q < 4; q++) out[q] = o4[q];
+            return;
+        }
+        for (int rb = 0; rb < n; rb += 64) {
+            const int r = rb + lane_id();
+            const int rc = min(r, n - 1);
+            const uint32_t u = rf_uid(L)[rc], o = rf_off(L)[rc], t = rf_ty(L)[rc];
+            const bool live = (r < n) & (u != NONE32) & ((t & (RF_HELD | RT_TRANSIENT)) != 0);
+            int res = MTR_DETACHED_POSITION;
+            bool found = false;
+            int carry = 0;
+            for (int base = 0; base < S && __ballot(live & !found); base += 64) {
+                const int i = base + lane_id();
+                const int ic = min(i, S - 1);
+                const uint32_t m = L.meta[ic];
+                const int rs = L.rseq[ic];
+                const bool leaf = (i < S) & !(m & M_DEL);
+                const int x = (leaf & (rs == RNONE)) ? L.len[ic] : 0;  // local view: removed leaves count 0
+                const int inc = wave_incl_scan(x);
+                const int excl = carry + inc - x;
+                const uint32_t ui = leaf ? L.uid[ic] : NONE32;
+                const int rm = rs != RNONE ? 1 : 0;  // isRemoved: acked or pending
+                for (int l = 0; l < 64; l++) {  // every reference lane looks for its leaf in this round
+                    const uint32_t ul = rdlane(ui, l);
+                    const int el = rdlane(excl, l), rl = rdlane(rm, l);
+                    const bool hit = live & !found & (ul == u);
+                    res = hit ? (rl ? 0 : int(o)) + el : res;
+                    found = found | hit;
+                }
+                carry += rdlane(inc, 63);
+            }
+            if (r < n) out[r] = res;
         }
     }
 
@@ -1548,6 +1610,195 @@ struct Eng {
         return false;
     }
 
+    // ---- local references (X instantiations, documents with references only)
+    // A per-document table of refcap entries, ids by creation (DocHdr.nrefs, kept in Sc during a launch):
+    // {uid of the reference's segment (NONE32: none -- a detached reference), offset, ReferenceType | RF_HELD}.
+    // RF_HELD: the segment's LocalReferenceCollection holds it (has(), localReference.ts:357-384).  Keyed by
+    // uid, a reference follows its leaf through shifts, compactions, spreads and normalization; splits
+    // (ref_split), scour's appends (ref_append) and acked removals (ref_slide) move it as the collection does.
+    static constexpr uint32_t RF_HELD = 0x80000000u;
+    static constexpr uint32_t RT_SLIDE = MTR_REFTYPE_SLIDE_ON_REMOVE, RT_STAY = MTR_REFTYPE_STAY_ON_REMOVE,
+                              RT_TRANSIENT = MTR_REFTYPE_TRANSIENT;
+    static MTR_DI int nrefs(const D& L) { return uni(L.sc->nrefs); }
+    static MTR_DI gptr<uint32_t> rf_uid(const D& L) { return (gptr<uint32_t>)L.cold(CP_REFS); }
+    static MTR_DI gptr<uint32_t> rf_off(const D& L) { return rf_uid(L) + uni(L.sc->refcap); }
+    static MTR_DI gptr<uint32_t> rf_ty(const D& L) { return rf_uid(L) + 2 * uni(L.sc->refcap); }
+    static MTR_DI bool removed_acked(int rs) { return rs != RNONE && rs < LOCAL_BASE; }
+
+    // LocalReferenceCollection.split (localReference.ts:398-420): the references held at offsets >= off of the
+    // leaf with uid ul go to the split-off leaf ur, at offset - off
+    static MTR_DI void ref_split(const D& L, uint32_t ul, int off, uint32_t ur) {
+        const int n = nrefs(L);
+        const gptr<uint32_t> U = rf_uid(L), O = rf_off(L), T = rf_ty(L);
+        for (int b = 0; b < n; b += 64) {
+            const int r = b + lane_id();
+            const int rc = min(r, n - 1);
+            const uint32_t u = U[rc], o = O[rc], t = T[rc];
+            if (r < n && u == ul && (t & RF_HELD) && int(o) >= off) {
+                U[r] = ur;
+                O[r] = o - uint32_t(off);
+            }
+        }
+        wsync();
+    }
+    // LocalReferenceCollection.append (localReference.ts:143-158, 332-350): the references held by the leaf with
+    // uid um go to the chain head uh, behind its `shift` units (its refsByOffset before the append)
+    static MTR_DI void ref_append(const D& L, uint32_t um, uint32_t uh, int shift) {
+        const int n = nrefs(L);
+        const gptr<uint32_t> U = rf_uid(L), O = rf_off(L), T = rf_ty(L);
+        for (int b = 0; b < n; b += 64) {
+            const int r = b + lane_id();
+            const int rc = min(r, n - 1);
+            const uint32_t u = U[rc], o = O[rc], t = T[rc];
+            if (r < n && u == um && (t & RF_HELD)) {
+                U[r] = uh;
+                O[r] = o + uint32_t(shift);
+            }
+        }
+        wsync();
+    }
+    // _getSlideToSegment's leaf predicate (mergeTree.ts:827-832): acked (seq is not UnassignedSequenceNumber) and
+    // not removed-and-acked; hole slots are no leaves
+    static MTR_DI bool slide_ok(uint32_t m, int sq, int rs) {
+        return !(m & M_DEL) && sq < LOCAL_BASE && !removed_acked(rs);
+    }
+    // MergeTree._getSlideToSegment (mergeTree.ts:821-840) of leaf x: the first such leaf after it
+    // (forwardExcursion), else the last before it (backwardExcursion); -1 if none
+    static MTR_DI int slide_target(const D& L, const St& s, int x) {
+        const int S = s.nseg;
+        for (int base = x + 1; base < S; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, S - 1);
+            const uint64_t m = __ballot((i < S) & slide_ok(L.meta[ic], L.seq[ic], L.rseq[ic]));
+            if (m) return base + first_lane(m);
+        }
+        for (int top = x - 1; top >= 0; top -= 64) {
+            const int i = top - lane_id();
+            const int ic = max(i, 0);
+            const uint64_t m = __ballot((i >= 0) & slide_ok(L.meta[ic], L.seq[ic], L.rseq[ic]));
+            if (m) return top - first_lane(m);
+        }
+        return -1;
+    }
+    // MergeTree.slideAckedRemovedSegmentReferences (mergeTree.ts:849-884) of leaf x, removed and acked
+    // (wave-uniform): held SlideOnRemove references go to the slide-to leaf -- offset 0 when it follows x
+    // (addBeforeTombstones), its last unit when it precedes x (addAfterTombstones, localReference.ts:426-490);
+    // other held references leave the collection (and their segment, when there is a slide-to leaf);
+    // StayOnRemove references stay
+    static MTR_DI void ref_slide(const D& L, const St& s, int x) {
+        const int n = nrefs(L);
+        if (!n) return;
+        const gptr<uint32_t> U = rf_uid(L), O = rf_off(L), T = rf_ty(L);
+        const uint32_t ux = uniu(L.uid[x]);
+        bool any = false;
+        for (int b = 0; b < n; b += 64) {
+            const int r = b + lane_id();
+            const int rc = min(r, n - 1);
+            const uint32_t t = T[rc];
+            any = any || ((r < n) & (U[rc] == ux) & ((t & RF_HELD) != 0) & !(t & RT_STAY));
+        }
+        if (!__ballot(any)) return;
+        const int tg = slide_target(L, s, x);
+        const uint32_t ut = tg >= 0 ? uniu(L.uid[tg]) : NONE32;
+        const uint32_t toff = (tg >= 0 && tg < x) ? uint32_t(uni(L.len[tg]) - 1) : 0u;
+        for (int b = 0; b < n; b += 64) {
+            const int r = b + lane_id();
+            const int rc = min(r, n - 1);
+            const uint32_t u = U[rc], t = T[rc];
+            if ((r < n) & (u == ux) & ((t & RF_HELD) != 0) & !(t & RT_STAY)) {
+                if (tg < 0) {
+                    T[r] = t & ~RF_HELD;  // removeLocalRef: the reference keeps its (removed) segment
+                } else if (t & RT_SLIDE) {
+                    U[r] = ut;
+                    O[r] = toff;
+                } else {  // lref.link(undefined, 0, undefined)
+                    U[r] = NONE32;
+                    O[r] = 0;
+                    T[r] = t & ~RF_HELD;
+                }
+            }
+        }
+        wsync();
+    }
+    // createPositionReference (sequence/src/intervalCollection.ts:697-724): getContainingSegment(pos1) at the
+    // record's view (client.ts:1065-1078), getSlideToSegment (client.ts:1085-1099), then
+    // createLocalReferencePosition (mergeTree.ts:2209-2226, localReference.ts:260-298) -- a detached reference
+    // when no segment holds the position
+    static MTR_DI void ref_create(D& L, const KParams& P, St& s, const mtr_op& op) {
+        const int n = nrefs(L);
+        if (!rf_uid(L) || n >= uni(L.sc->refcap)) {
+            s.status = MTR_ERR_CAPACITY;
+            return;
+        }
+        const uint32_t ty = op.payload;
+        if (int((ty & RT_SLIDE) != 0) + int((ty & RT_STAY) != 0) + int((ty & RT_TRANSIENT) != 0) > 1) {
+            s.status = MTR_ERR_BAD_OP;  // _validateReferenceType's UsageError (localReference.ts:23-39)
+            return;
+        }
+        View v;
+        if (op.payload2 & MTR_REF_LOCALVIEW) {
+            v.ref = s.curseq;
+            v.client = s.collab ? uint32_t(s.local) : CL_LOCAL;
+            v.local = 1;
+        } else {
+            v.ref = op.ref_seq;
+            v.client = enc_client(int(int16_t(op.client)));
+            v.local = (!s.collab || uint32_t(s.local) == v.client) ? 1 : 0;
+        }
+        int i = 0, before = 0;
+        find1(L, s, v, op.pos1, i, before, P.new_length_calc);
+        int off = op.pos1 - before;
+        if (i >= s.nseg || op.pos1 < 0) i = -1;
+        if (i >= 0 && (op.payload2 & MTR_REF_SLIDE) && removed_acked(uni(L.rseq[i]))) {
+            const int tg = slide_target(L, s, i);
+            off = (tg >= 0 && tg < i) ? uni(L.len[tg]) - 1 : 0;
+            i = tg;
+        }
+        uint32_t u = NONE32, tw = ty;
+        if (i >= 0) {
+            if (removed_acked(uni(L.rseq[i])) && !(ty & (RT_SLIDE | RT_TRANSIENT))) {
+                s.status = MTR_ERR_BAD_OP;  // "Can only create SlideOnRemove or Transient ... on a removed segment"
+                return;
+            }
+            u = uniu(L.uid[i]);
+            if (!(ty & RT_TRANSIENT)) {
+                if (off >= uni(L.len[i])) {
+                    s.status = MTR_ERR_ASSERT | 0x348;  // "offset cannot be beyond segment length"
+                    return;
+                }
+                tw |= RF_HELD;
+            }
+        }
+        if (lane_id() == 0) {
+            rf_uid(L)[n] = u;
+            rf_off(L)[n] = uint32_t(off);
+            rf_ty(L)[n] = tw;
+            L.sc->nrefs = n + 1;
+        }
+        wsync();
+    }
+    // MergeTree.removeLocalReferencePosition (mergeTree.ts:2190-2207) of reference r
+    static MTR_DI void ref_remove(D& L, St& s, uint32_t r) {
+        if (!rf_uid(L) || int(r) >= nrefs(L)) {
+            s.status = MTR_ERR_BAD_OP;
+            return;
+        }
+        if (lane_id() == 0) rf_ty(L)[r] = rf_ty(L)[r] & ~RF_HELD;
+        wsync();
+    }
+    // after a remove walk that was no pending local op: every leaf this op removed first, or whose pending local
+    // remove it overtook, is now removed and acked (removedSeq = this seq) and slides its references
+    // (mergeTree.ts:2023-2040).  Leaves an earlier member of the same GROUP removed hold only StayOnRemove
+    // references by now, so sliding them again changes nothing.
+    static MTR_DI void ref_slide_walk(const D& L, const St& s, int seq) {
+        for (int base = L.wlo; base < L.whi; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, L.whi - 1);
+            for (uint64_t m = __ballot((i < L.whi) & (L.rseq[ic] == seq)); m; m &= m - 1)
+                ref_slide(L, s, base + first_lane(m));
+        }
+    }
+
     // MergeTree.ackPendingSegment (mergeTree.ts:1283-1322) with BaseSegment.ack (mergeTreeNodes.ts:439-479)
     // for one member op of this client's sequenced message (type: its MergeTreeDeltaType)
     static MTR_DI void ack(D& L, St& s, int type, int seq) {
@@ -1574,6 +1825,7 @@ struct Eng {
         for (int o = 0; o < cnt && s.status == MTR_OK; o++) {  // in group order: drop the cell, then ack
             const int i = uni(L.E[o]);
             pend_drop(L, i, slot);
+            bool slid = false;
             if (type == MTR_OP_INSERT) {
                 if (uni(L.seq[i]) < LOCAL_BASE) s.status = MTR_ERR_ASSERT | 0x045;  // seq already assigned
                 else if (lane_id() == 0) L.seq[i] = seq;
@@ -1581,10 +1833,12 @@ struct Eng {
                 const int rs = uni(L.rseq[i]);
                 if (rs == RNONE) s.status = MTR_ERR_ASSERT | 0x046;  // missing removal info
                 else if (rs >= LOCAL_BASE && lane_id() == 0) L.rseq[i] = seq;
+                slid = rs != RNONE && rs >= LOCAL_BASE;  // ack() is true: no overlapping remove
             } else if (type != MTR_OP_ANNOTATE) {
                 s.status = MTR_ERR_BAD_OP;
             }
             wsync();
+            if (slid) ref_slide(L, s, i);  // mergeTree.ts:1294-1296
             if (G) csum_update(L, s, i, i + 1);
             int bs, be;
             block_bounds1(L, s, i, bs, be);
@@ -2422,6 +2676,9 @@ struct Eng {
                     const uint32_t tk = rdlane(vt, t);
                     const bool ca = PM ? perm_contig(ptext, plen, tk) : can_append(pmeta, plen, m, lk);
                     if (prev >= 0 && lk > 0 && ca && props_match_w(L, P, pprops, pk)) {
+                        if constexpr (X && !PM) {  // BaseSegment.append (mergeTreeNodes.ts:527-530)
+                            if (nrefs(L)) ref_append(L, uniu(L.uid[k]), uniu(L.uid[prev]), plen);
+                        }
                         if (PM) {
                             L.len[prev] = plen + lk;
                             wsync();
@@ -2471,6 +2728,7 @@ struct Eng {
         const int ic = min(i, ce - 1);
         const uint32_t vm0 = L.meta[ic], vp = L.props[ic], vt = L.text[ic];
         const int vr0 = L.rseq[ic], vs = L.seq[ic], vl0 = L.len[ic];
+        const uint32_t vu = X ? L.uid[ic] : 0u;  // (local references follow appends)
         uint32_t vm = in ? vm0 : M_DEL;
         const int vr = in ? vr0 : RNONE, vl = in ? vl0 : 0;
         const bool pre = (vm & M_DEL) != 0;
@@ -2545,6 +2803,13 @@ struct Eng {
                 todo &= ~mem;
                 const int e = last_lane(mem);
                 const int total = rdlane(incl, e) - rdlane(incl - vl, h);
+                if constexpr (X && !PM) {  // BaseSegment.append (mergeTreeNodes.ts:527-530), member by member
+                    if (nrefs(L))
+                        for (uint64_t mm = mem; mm; mm &= mm - 1) {
+                            const int l = first_lane(mm);
+                            ref_append(L, rdlane(vu, l), rdlane(vu, h), rdlane(off, l));
+                        }
+                }
                 if (PM) {  // BaseSegment.append: lengths only
                     if (ln == 0) L.len[cs + h] = total;
                     PROF_COUNT(P_NMERGE);
@@ -2775,6 +3040,12 @@ struct Eng {
             const uint32_t ur = uint32_t(s.uidnext++);
             L.uid[r] = ur;
             if (G && s.chunked && lane_id() == 0) hint(L, ur, r);
+            if constexpr (X) {  // mergeTreeNodes.ts:501-503
+                if (nrefs(L)) {
+                    wsync();
+                    ref_split(L, uniu(rdlane(uj, jl)), off, ur);
+                }
+            }
             if (m0 & M_OVERLAP) {  // the right half shares the remover list
                 if (lane_id() == 0 && !rm_set(L, ur, rm_get(L, rdlane(uj, jl)))) s.status = MTR_ERR_CAPACITY;
                 s.status = uni(s.status);
@@ -3276,6 +3547,7 @@ struct Eng {
         }
         if (threadIdx.x == 0) {
             L.sc->relmask = 0;
+            L.sc->nrefs = gp((const DocHdr*)P.hdr)[d].nrefs;
 #ifdef MTR_PROF
             for (int q = 0; q < P_COUNT; q++) L.sc->prof[q] = 0;
 #endif
@@ -3339,6 +3611,7 @@ struct Eng {
             h.texthalf = s.texthalf;
             h.heap_need = s.heap_need;
             h.dused = s.dused;
+            h.nrefs = L.sc->nrefs;
             if (G) {
                 h.holes = s.holes;
                 h.chunked = s.chunked;
@@ -3424,6 +3697,8 @@ struct Eng {
             L.sc->cp[CP_PEND] = (unsigned long long)(P.pend ? P.pend + size_t(d) * kPendRing * 4 : nullptr);
             L.sc->cp[CP_CSUM] = (unsigned long long)(P.csum ? P.csum + size_t(d) * kCsumRows * (P.segcap / 64 + 1) : nullptr);
             L.sc->cp[CP_UMAP] = (unsigned long long)(P.umap ? P.umap + size_t(d) * 2 * P.segcap : nullptr);
+            L.sc->cp[CP_REFS] = (unsigned long long)(P.refs ? P.refs + size_t(d) * 3 * size_t(P.refcap) : nullptr);
+            L.sc->refcap = P.refs ? P.refcap : 0;
         }
         wsync();
     }
@@ -3615,6 +3890,7 @@ struct Eng {
                                (op.type == MTR_OP_ANNOTATE || (X && op.type == MTR_OP_LOCAL_ANNOTATE)) ? op.payload2 : 0u,
                                DL && !PM && (op.flags & MTR_F_DELTA) != 0);
                 }
+                if (X && is_remove && !lseq && s.status == MTR_OK && nrefs(L)) ref_slide_walk(L, s, seq);
                 if (G && is_remove) csum_update(L, s, L.wlo, L.whi);
                 zop = s.collab && !local_op;
                 break;
@@ -3681,6 +3957,14 @@ struct Eng {
                 }
                 break;
             }
+            case MTR_OP_REF_CREATE:  // a local reference
+                if (!X || PM) s.status = MTR_ERR_BAD_OP;
+                else ref_create(L, P, s, op);
+                break;
+            case MTR_OP_REF_REMOVE:
+                if (!X || PM) s.status = MTR_ERR_BAD_OP;
+                else ref_remove(L, s, op.payload);
+                break;
             case MTR_OP_START_COLLAB:
                 if (!s.collab) {
                     s.collab = 1;

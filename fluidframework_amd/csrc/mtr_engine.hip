@@ -105,6 +105,10 @@ struct mtr_engine {
     bool pend_seen = false;           // a batch since mtr_reset held local ops while collaborating or acks:
                                       // documents may hold pending segments, so every launch is an X kernel
     DevBuf<uint32_t> pend;            // [doc][kPendRing][4] pending SegmentGroups (allocated on first use)
+    bool refs_seen = false;           // a batch since mtr_reset created local references: they follow splits,
+                                      // appends and removals in the X kernels only, so every launch is one
+    DevBuf<uint32_t> refs;            // [doc][3][ref_slots] local references (allocated on first use)
+    DevBuf<int32_t> qbuf;             // query results (reference positions)
     DevBuf<int32_t> csum;             // [doc][kCsumRows][segcap / 64 + 1] chunk summaries (first HBM-resident launch)
     DevBuf<int32_t> umap;             // [doc][2 * segcap] uid -> slot hints (with csum)
     DevBuf<int32_t> red;              // small reduction / query-result buffer
@@ -162,17 +166,18 @@ __global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_
     }
 }
 
-// any op of the batch flagged MTR_F_DELTA (the host sizes delta buffers only when one is)
+// bit 3: local-reference records (MTR_OP_REF_*)
 // bit 0: an op flagged MTR_F_DELTA (the host sizes delta buffers only then); bit 1: a rare record the
 // fixed-capacity kernels do not carry (Eng::X: relative positions, handle-table loads, combining
 // annotates, marker ordinals); bit 2: the local-op path (MTR_OP_ACK, or a local op recorded while
 // collaborating: seq = UnassignedSequenceNumber)
 __global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    bool any = false, ext = false, pend = false;
+    bool any = false, ext = false, pend = false, refs = false;
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const mtr_op op = ops[i];
         any = any || (op.flags & MTR_F_DELTA) != 0;
+        refs = refs || op.type == MTR_OP_REF_CREATE || op.type == MTR_OP_REF_REMOVE;
         pend = pend || op.type == MTR_OP_ACK || op.type == MTR_OP_ROLLBACK || op.type == MTR_OP_REGENERATE ||
                (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE && op.seq == -1);
         ext = ext || op.type == MTR_OP_RELPOS || op.type == MTR_OP_HANDLES || (op.flags & MTR_F_REL) ||
@@ -180,7 +185,8 @@ __global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
               ((op.flags & MTR_F_MARKER) && op.payload2 != 0 &&
                (op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT || op.type == MTR_OP_LOAD));
     }
-    const int bits = (__ballot(any) ? 1 : 0) | (__ballot(ext) ? 2 : 0) | (__ballot(pend) ? 4 : 0);
+    const int bits = (__ballot(any) ? 1 : 0) | (__ballot(ext) ? 2 : 0) | (__ballot(pend) ? 4 : 0) |
+                     (__ballot(refs) ? 8 : 0);
     if (bits && (threadIdx.x & 63) == 0) atomicOr(out, bits);
 }
 
@@ -244,6 +250,12 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
     if (c >= 0) list[size_t(c) * n + lbase[c] + rank] = d;
 }
 
+// local-reference positions (or one reference's info) of a document's HBM state (mtr_get_ref_positions / _info)
+__global__ void __launch_bounds__(NT) refs_kernel(KParams P, uint32_t d, int32_t* out, int info_id) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    Eng<true>::ref_query(smem, P, d, out, info_id);
+}
+
 // one getContainingSegment query on a document's HBM state (mtr_get_containing_segment)
 __global__ void __launch_bounds__(NT) containing_kernel(KParams P, uint32_t d, int pos, int ref, int client,
                                                         int32_t* out) {
@@ -266,7 +278,7 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
     auto* e = new mtr_engine();
     e->opt = opt ? *opt : mtr_options{0, 1, 10000, 0};
     if (e->opt.chunk_size <= 0) e->opt.chunk_size = 10000;
-    mtr_caps c{4096, 2048, 65536, 16384, 4096, 256};
+    mtr_caps c{4096, 2048, 65536, 16384, 4096, 256, 1024};
     if (caps) {
         if (caps->max_segments) c.max_segments = caps->max_segments;
         if (caps->heap_entries) c.heap_entries = caps->heap_entries;
@@ -274,6 +286,7 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
         if (caps->prop_words) c.prop_words = caps->prop_words;
         if (caps->remover_cells) c.remover_cells = caps->remover_cells;
         if (caps->ops_per_launch) c.ops_per_launch = caps->ops_per_launch;
+        if (caps->ref_slots) c.ref_slots = caps->ref_slots;
     }
     c.max_segments = (c.max_segments + 63) & ~63u;
     c.heap_entries = (c.heap_entries + 63) & ~63u;
@@ -321,6 +334,8 @@ int mtr_engine_destroy(mtr_engine* e) {
         b->release();
     e->hdr.release();
     e->pend.release();
+    e->refs.release();
+    e->qbuf.release();
     e->csum.release();
     e->umap.release();
     e->text.release();
@@ -375,6 +390,7 @@ int mtr_reset(mtr_engine* e) {
     HIPCHK(hipMemsetAsync(e->stat.p, 0, e->stat.n * sizeof(unsigned long long), e->stream));
     e->summarized = false;
     e->pend_seen = false;
+    e->refs_seen = false;
     return MTR_OK;
 }
 
@@ -429,8 +445,14 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
             }
             e->pend_seen = true;
         }
+        if (flag & 8) {
+            if (!e->refs.p &&
+                e->refs.ensure(size_t(std::max<uint32_t>(e->max_docs, 1)) * 3 * size_t(e->caps.ref_slots)))
+                return -1;
+            e->refs_seen = true;
+        }
     }
-    e->has_ext = e->has_ext || e->pend_seen;
+    e->has_ext = e->has_ext || e->pend_seen || e->refs_seen;
     if (any) {
         std::vector<uint64_t> need(b->n_docs, 0);
         for (uint32_t d = 0; d < b->n_docs; d++) {
@@ -574,6 +596,8 @@ static int run_impl(mtr_engine* e, int gen) {
     P.dkind = e->dkind.p;
     P.dpart = e->dpart.p;
     P.pend = e->pend.p;
+    P.refs = e->refs.p;
+    P.refcap = int(e->caps.ref_slots);
     P.gen = gen;
 #ifdef MTR_PROF
     if (!e->prof.p) {
@@ -1289,6 +1313,55 @@ int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t
         HIPCHK(hipMemcpy(text, e->text.p + size_t(doc) * e->caps.text_units + uint32_t(r[7]),
                          size_t(info->length) * sizeof(uint16_t), hipMemcpyDeviceToHost));
     return MTR_OK;
+}
+
+static int ref_query(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int info_id) {
+    HIPCHK(hipSetDevice(e->device));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (doc >= e->max_docs) {
+        set_err("local references: bad document");
+        return -1;
+    }
+    DocHdr h;
+    HIPCHK(hipMemcpy(&h, e->hdr.p + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
+    const int64_t n = e->refs.p ? h.nrefs : 0;
+    const int64_t words = info_id >= 0 ? 4 : n;
+    if (info_id < 0 && (n > cap || n == 0 || !out)) return int(n);
+    KParams P{};
+    P.hdr = e->hdr.p;
+    P.seg = e->seg.p;
+    P.heap = e->heap.p;
+    P.text = e->text.p;
+    P.prop = e->prop.p;
+    P.rm = e->rm.p;
+    P.segcap = int(e->caps.max_segments);
+    P.hcap = int(e->caps.heap_entries);
+    P.tcap = int(e->caps.text_units);
+    P.pcap = int(e->caps.prop_words);
+    P.rcap = int(e->caps.remover_cells);
+    P.rtab = e->rtab;
+    P.new_length_calc = e->opt.new_length_calc;
+    P.n_docs = e->n_docs;
+    P.refs = e->refs.p;
+    P.refcap = int(e->caps.ref_slots);
+    if (e->qbuf.ensure(size_t(std::max<int64_t>(words, 4)))) return -1;
+    refs_kernel<<<1, NT, lds_bytes_global_mode(), e->stream>>>(P, doc, e->qbuf.p, info_id);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, e->qbuf.p, size_t(words) * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return int(n);
+}
+
+int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap) {
+    return ref_query(e, doc, out, cap, -1);
+}
+
+int32_t mtr_get_ref_info(mtr_engine* e, uint32_t doc, uint32_t id, int32_t* out) {
+    if (!out) return -2;
+    out[0] = -1;
+    out[1] = out[2] = out[3] = 0;
+    if (ref_query(e, doc, out, 4, int(id)) < 0) return -2;
+    return out[0];
 }
 
 int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index) {

@@ -29,6 +29,7 @@ class MtrCaps(C.Structure):
         ("prop_words", C.c_uint32),
         ("remover_cells", C.c_uint32),
         ("ops_per_launch", C.c_uint32),
+        ("ref_slots", C.c_uint32),
     ]
 
 
@@ -103,6 +104,10 @@ def lib():
         L.mtr_download_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_uint64]
         L.mtr_download_batch.restype = C.c_int
+        L.mtr_get_ref_positions.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
+        L.mtr_get_ref_positions.restype = C.c_int64
+        L.mtr_get_ref_info.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+        L.mtr_get_ref_info.restype = C.c_int32
         _LIB = L
     return _LIB
 
@@ -141,9 +146,11 @@ class Engine:
     """One engine = the observer Clients of up to ``max_docs`` documents on one GPU."""
 
     def __init__(self, max_docs, *, device=0, new_length_calc=False, snapshot_v1=True, chunk_size=10000,
-                 max_segments=0, heap_entries=0, text_units=0, prop_words=0, remover_cells=0, ops_per_launch=0):
+                 max_segments=0, heap_entries=0, text_units=0, prop_words=0, remover_cells=0, ops_per_launch=0,
+                 ref_slots=0):
         self.opts = abi.MtrOptions(int(new_length_calc), int(snapshot_v1), int(chunk_size), 0)
-        self.caps = MtrCaps(max_segments, heap_entries, text_units, prop_words, remover_cells, ops_per_launch)
+        self.caps = MtrCaps(max_segments, heap_entries, text_units, prop_words, remover_cells, ops_per_launch,
+                            ref_slots)
         self.max_docs = int(max_docs)
         h = lib().mtr_engine_create(C.byref(self.opts), int(device), self.max_docs, C.byref(self.caps))
         if not h:
@@ -350,6 +357,25 @@ class Engine:
         r = {n: getattr(info, n) for n, _ in SegmentInfo._fields_}
         r["text"] = None if info.marker else text[:info.length].tobytes().decode("utf-16-le", "surrogatepass")
         return r
+
+    def ref_positions(self, doc) -> list:
+        """Client.localReferencePositionToPosition of every local reference of `doc`, by id
+        (abi.DETACHED_POSITION = -1 when it has none)."""
+        n = lib().mtr_get_ref_positions(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"mtr_get_ref_positions: {_err()}")
+        if n == 0:
+            return []
+        out = np.zeros(n, dtype="<i4")
+        self._check(int(lib().mtr_get_ref_positions(self.h, doc, out.ctypes.data, n) != n), "mtr_get_ref_positions")
+        return [int(x) for x in out]
+
+    def ref_info(self, doc, ref_id):
+        """(leaf index of the reference's segment or -1, offset, refType, held by the segment's collection)"""
+        out = np.zeros(4, dtype="<i4")
+        if lib().mtr_get_ref_info(self.h, doc, ref_id, out.ctypes.data) == -2:
+            raise EngineError(f"mtr_get_ref_info: {_err()}")
+        return int(out[0]), int(out[1]), int(out[2]), bool(out[3])
 
     def status(self, doc):
         op = C.c_int32(-1)

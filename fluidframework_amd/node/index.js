@@ -32,7 +32,9 @@ function native() {
 
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
-    START_COLLAB: 12, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19 };
+    START_COLLAB: 12, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19, REF_CREATE: 20, REF_REMOVE: 21 };
+const REF = { SLIDE: 1, LOCALVIEW: 2 };  // MTR_OP_REF_CREATE payload2
+const DetachedReferencePosition = -1;   // referencePositions.ts:103
 const DELTA_REGEN = 64, DELTA_REGEN_X = 72;
 const REL = { BEFORE: 1, OFFSET: 2 };
 const COMB = { NONE: 0, REWRITE: 1, INCR: 2, CONSENSUS: 3, KEEP: 4 };
@@ -200,6 +202,7 @@ class DocLog {
         this.ops = []; this.text = []; this.collaborating = false;
         // MergeTree.idToSegment (mergeTree.ts:549,668) as the host sees it: id key -> marker ordinal
         this.nMarkers = 0; this.markerIds = new Map(); this.markerDup = new Set(); this.markerIdAnnotated = false;
+        this.nRefs = 0;  // local references created (MTR_OP_REF_CREATE ids)
     }
     static _idKey(v) {  // SameValueZero keys; objects only match themselves (never from JSON)
         if (typeof v === 'boolean') return 'b' + v;
@@ -278,6 +281,7 @@ class DocLog {
     }
     push(type, flags, client, seq, ref, msn, pos1, pos2, payload, payload2) {
         this.ops.push([type, flags, client, seq, ref, msn, pos1, pos2, payload, payload2]);
+        this.nPushed = (this.nPushed || 0) + 1;  // (a stamp: getContainingSegment -> createLocalReferencePosition)
     }
     // local edits (client.ts:225-260): final before collaboration; while collaborating a pending op
     // (record seq = UnassignedSequenceNumber) until this client's sequenced message acks it
@@ -287,6 +291,21 @@ class DocLog {
         this.push(OP.LOCAL_INSERT, s[0], 0, this.localSeq(), 0, 0, pos, s[3], s[1], s[2]);
     }
     localRemove(start, end) { this.push(OP.LOCAL_REMOVE, 0, 0, this.localSeq(), 0, 0, start, end, 0, 0); }
+    // a local reference (localReference.ts): getContainingSegment(pos, view) [+ getSlideToSegment], then
+    // createLocalReferencePosition -- view = {referenceSequenceNumber, clientId} or undefined (the local view)
+    createRef(pos, refType, view, slide) {
+        let short = 0, ref = 0, flags = REF.LOCALVIEW;
+        if (view !== undefined) {
+            const cid = view.clientId === null || view.clientId === undefined ? 'null' : String(view.clientId);
+            short = this.shortId(cid);
+            ref = view.referenceSequenceNumber;
+            flags = 0;
+        }
+        if (slide) flags |= REF.SLIDE;
+        this.push(OP.REF_CREATE, 0, short, 0, ref, 0, pos, 0, refType, flags);
+        return this.nRefs++;
+    }
+    removeRef(id) { this.push(OP.REF_REMOVE, 0, 0, 0, 0, 0, 0, 0, id, 0); }
     localAnnotate(start, end, props, it, combiningOp) {
         if (props && typeof props === 'object' && 'markerId' in props) this.markerIdAnnotated = true;
         this.push(OP.LOCAL_ANNOTATE, 0, 0, this.localSeq(), 0, 0, start, end, it.propop(props), localComb(combiningOp));
@@ -817,6 +836,43 @@ class BatchReplayClient {
         for (let k = 0; k < w[0]; k++) out[names[w[1 + 2 * k]]] = JSON.parse(it.valBytes[w[2 + 2 * k]].toString('utf8'));
         return out;
     }
+    /**
+     * createPositionReference (sequence/src/intervalCollection.ts:697-724): a local reference at pos of the view
+     * sequenceArgs = {referenceSequenceNumber, clientId} (default: this client's local view), slid off a
+     * removed-and-acked segment when `slide` (Client.getSlideToSegment, client.ts:1085-1099), then
+     * createLocalReferencePosition (client.ts:377-389).  -> a reference handle for the calls below.
+     */
+    createPositionReference(pos, refType, sequenceArgs, slide) {
+        let id = 0;
+        this._queue(() => { id = this.log.createRef(pos, refType, sequenceArgs, !!slide); });
+        return { id, refType, client: this };
+    }
+    /**
+     * Client.createLocalReferencePosition(segment, offset, refType) (client.ts:377-389) for a segment this
+     * client's getContainingSegment returned, before any later edit: the same view and position.
+     */
+    createLocalReferencePosition(segment, offset, refType) {
+        if (!segment || segment._at === undefined || segment._at.stamp !== this.log.nPushed) {
+            throw new UnsupportedError('createLocalReferencePosition on a segment from before the last edit');
+        }
+        return this.createPositionReference(segment._at.start + (offset || 0), refType, segment._at.view, false);
+    }
+    /** Client.removeLocalReferencePosition (client.ts:394-396). */
+    removeLocalReferencePosition(lref) { this._queue(() => this.log.removeRef(lref.id)); return lref; }
+    /** Client.localReferencePositionToPosition (client.ts:398-403), on the device. */
+    localReferencePositionToPosition(lref) {
+        this.engine.flush();
+        this._check();
+        const p = native().getRefPositions(this.engine.h, this.doc);
+        return lref.id < p.length ? p[lref.id] : DetachedReferencePosition;
+    }
+    /** LocalReference.getOffset (localReference.ts:110) and its segment's leaf index (-1: none / gone). */
+    localReferenceSegment(lref) {
+        this.engine.flush();
+        this._check();
+        const r = native().getRefInfo(this.engine.h, this.doc, lref.id);
+        return { leafIndex: r[0], offset: r[1], held: r[3] === 1 };
+    }
     getCurrentSeq() { return this.currentSeq; }
     getText() {
         this.engine.flush();
@@ -850,6 +906,9 @@ class BatchReplayClient {
         // mergeTree.ts:1397-1427 / 1955-2047 leave them)
         const segment = { cachedLength: r.length, seq: r.seq, clientId: longId(r.client), leafIndex: r.leaf,
             removedSeq: r.removed ? r.removedSeq : undefined, propertySet: r.props < 0 ? undefined : r.props };
+        // (where createLocalReferencePosition finds it again while no edit intervened)
+        Object.defineProperty(segment, '_at', { value: { start: r.start, view: sequenceArgs,
+            stamp: this.log.nPushed }, enumerable: false });
         if (r.localSeq >= 0) segment.localSeq = r.localSeq;
         if (r.localRemovedSeq >= 0) segment.localRemovedSeq = r.localRemovedSeq;
         if (r.marker) segment.marker = { refType: r.refType };

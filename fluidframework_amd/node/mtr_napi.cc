@@ -327,6 +327,47 @@ napi_value GetContainingSegment(napi_env env, napi_callback_info info) {
     return r;
 }
 
+// getRefPositions(h, doc) -> Int32Array: localReferencePositionToPosition of every local reference
+// (client.ts:398-403, on the device; -1 = DetachedReferencePosition)
+napi_value GetRefPositions(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    const int64_t n = mtr_get_ref_positions(e, doc, nullptr, 0);
+    if (n < 0) return throw_engine(env, "mtr_get_ref_positions");
+    void* data = nullptr;
+    napi_value ab, r;
+    NAPI_CALL(env, napi_create_arraybuffer(env, size_t(n) * 4, &data, &ab));
+    if (n > 0 && mtr_get_ref_positions(e, doc, static_cast<int32_t*>(data), n) != n)
+        return throw_engine(env, "mtr_get_ref_positions");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, size_t(n), ab, 0, &r));
+    return r;
+}
+
+// getRefInfo(h, doc, id) -> [leaf, offset, refType, held] (LocalReference.getSegment/getOffset, localReference.ts:106-112)
+napi_value GetRefInfo(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0, id = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &id));
+    int32_t out[4];
+    if (mtr_get_ref_info(e, doc, id, out) == -2) return throw_engine(env, "mtr_get_ref_info");
+    napi_value r;
+    NAPI_CALL(env, napi_create_array_with_length(env, 4, &r));
+    for (uint32_t k = 0; k < 4; k++) {
+        napi_value v;
+        NAPI_CALL(env, napi_create_int32(env, out[k], &v));
+        NAPI_CALL(env, napi_set_element(env, r, k, v));
+    }
+    return r;
+}
+
 // summarize(h): every document's blobs on the device (Client.summarize, client.ts:966)
 napi_value Summarize(napi_env env, napi_callback_info info) {
     napi_value argv[1];
@@ -498,7 +539,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"stats", Stats},               {"reset", Reset},         {"setMatrix", SetMatrix},
                {"getDeltas", GetDeltas},       {"submitRunAsync", SubmitRunAsync},
                {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment},
-               {"getProps", GetProps}};
+               {"getProps", GetProps}, {"getRefPositions", GetRefPositions}, {"getRefInfo", GetRefInfo}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||

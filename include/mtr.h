@@ -43,6 +43,7 @@ typedef struct mtr_caps {
     uint32_t prop_words;     /* property-set arena per document (u32 words) */
     uint32_t remover_cells;  /* overlapping-remove list cells per document */
     uint32_t ops_per_launch; /* ops applied per document per kernel launch (0 = all) */
+    uint32_t ref_slots;      /* local references per document (allocated with the first batch that creates one) */
 } mtr_caps;
 
 /* Create an engine for up to max_docs documents on HIP device `device`. */
@@ -153,6 +154,17 @@ typedef struct mtr_segment_info {
 } mtr_segment_info;
 int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t ref_seq, int32_t client,
                                mtr_segment_info* info, uint16_t* text, int64_t text_cap);
+
+/* Local references (MTR_OP_REF_CREATE / MTR_OP_REF_REMOVE records, localReference.ts): out[r] =
+ * Client.localReferencePositionToPosition of reference r (client.ts:398-403 -> mergeTree.ts:1046-1062),
+ * MTR_DETACHED_POSITION (-1) when it has no position.  Returns the document's reference count (out written
+ * only when it fits in cap), -1 on error. */
+int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap);
+/* Reference `id` of document doc: out[0] = index (tree order) of the leaf of its segment (LocalReference.
+ * getSegment, localReference.ts:106; -1 = none, or the segment is no longer in the tree), out[1] = getOffset,
+ * out[2] = refType, out[3] = 1 when the segment's LocalReferenceCollection holds it (has(), :357-384).
+ * Returns out[0], or -2 on error. */
+int32_t mtr_get_ref_info(mtr_engine* e, uint32_t doc, uint32_t id, int32_t* out);
 
 /* Per-document status: MTR_OK or an MTR_ERR_* code; *op_index = op that failed (or -1). */
 int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index);

@@ -69,6 +69,16 @@ enum {
                                    engine records two mtr_delta entries, {op, position, cachedLength,
                                    MTR_DELTA_REGEN + type} then {op, offset of the member's text in the op's
                                    inserted text, properties reference, MTR_DELTA_REGEN_X} (see below). */
+    MTR_OP_REF_CREATE = 20,     /* a local reference: Client.getContainingSegment(pos1, {ref_seq, client})
+                                   (client.ts:1065-1078; payload2 & MTR_REF_LOCALVIEW: the local view, refSeq =
+                                   currentSeq, the local client), then Client.getSlideToSegment when payload2 &
+                                   MTR_REF_SLIDE (client.ts:1085-1099), then createLocalReferencePosition(segment,
+                                   offset, payload = ReferenceType, client.ts:377-389 -> mergeTree.ts:2209-2226), as
+                                   sequence/src/intervalCollection.ts:668-724 createPositionReference does; no
+                                   segment = a detached reference (createDetachedLocalReferencePosition).  The
+                                   document's references are numbered by creation, from 0. */
+    MTR_OP_REF_REMOVE = 21,     /* Client.removeLocalReferencePosition (client.ts:394-396 -> mergeTree.ts:2190-2207) of
+                                   reference payload */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for
@@ -82,6 +92,22 @@ enum {
 
 /* MTR_OP_RELPOS payload2 */
 enum { MTR_REL_BEFORE = 1, MTR_REL_OFFSET = 2 };
+
+/* MTR_OP_REF_CREATE payload2, and the ReferenceType bits (ops.ts:9-36) its payload carries */
+enum { MTR_REF_SLIDE = 1, MTR_REF_LOCALVIEW = 2 };
+enum {
+    MTR_REFTYPE_SIMPLE = 0x0,
+    MTR_REFTYPE_TILE = 0x1,
+    MTR_REFTYPE_NEST_BEGIN = 0x2,
+    MTR_REFTYPE_NEST_END = 0x4,
+    MTR_REFTYPE_RANGE_BEGIN = 0x10,
+    MTR_REFTYPE_RANGE_END = 0x20,
+    MTR_REFTYPE_SLIDE_ON_REMOVE = 0x40,
+    MTR_REFTYPE_STAY_ON_REMOVE = 0x80,
+    MTR_REFTYPE_TRANSIENT = 0x100
+};
+/* localReferencePositionToPosition of a reference with no position (referencePositions.ts:103) */
+#define MTR_DETACHED_POSITION (-1)
 
 /*
  * Marker ordinals (MergeTree.idToSegment, mergeTree.ts:549,668): an insert / load record of a Marker whose

@@ -13,9 +13,10 @@
 //    query (tests/test_partial_lengths.py: all golden logs and seeded sets agree;
 //    the one modelled quirk, a leaf-level root's stale own length, is documented
 //    at Tree::pslCheck).
-//  * Ordinals, tiles/range stacks, local references, attribution, pending
-//    segment groups and delta/maintenance events are not modelled: none of them
-//    change the observer's text, segment boundaries or summary bytes.
+//  * Ordinals, tiles/range stacks, attribution and maintenance events are not
+//    modelled: none of them change the observer's text, segment boundaries or
+//    summary bytes.  Local references (localReference.ts) are restated with their
+//    per-offset lists, since they are what localReferencePositionToPosition reads.
 #include "mtr_oracle.h"
 #include "../include/mtr_synth.h"
 #include "../include/mtr_digest.h"
@@ -100,6 +101,27 @@ struct Seg : Node {
     // removed it while unacked (-1 = undefined); cleared by the ack (:460, 469)
     int localSeq = -1;
     int localRemovedSeq = -1;
+    struct LocalRefs* localRefs = nullptr;  // BaseSegment.localRefs (mergeTreeNodes.ts:380)
+};
+
+// LocalReferenceCollection (localReference.ts:142-571): per offset of its segment the before / at / after
+// lists of reference ids (IRefsAtOffset, :129-133; an absent entry or list is a null pointer / has = false)
+struct RefsAtOffset {
+    std::list<int> lst[3];  // 0 before, 1 at, 2 after
+    bool has[3] = {false, false, false};
+};
+struct LocalRefs {
+    Seg* segment = nullptr;
+    std::vector<std::unique_ptr<RefsAtOffset>> byOffset;  // refsByOffset (its length tracks cachedLength)
+    int refCount = 0;
+};
+// LocalReference (localReference.ts:54-121): its ReferenceType, the segment and offset it is linked to, and
+// the list of that offset holding it (its listNode; -1 = undefined)
+struct LRef {
+    int refType = 0;
+    Seg* segment = nullptr;
+    int offset = 0;
+    int list = -1;
 };
 
 // SegmentGroup (mergeTreeNodes.ts:57-62): the segments one pending local op touched, in the order they
@@ -433,6 +455,7 @@ class Tree {
         r->clientId = s->clientId;
         r->localSeq = s->localSeq;  // mergeTreeNodes.ts:495-497
         r->localRemovedSeq = s->localRemovedSeq;
+        if (s->localRefs) refsSplit(s->localRefs, pos, r);  // mergeTreeNodes.ts:501-503
         for (SegGroup* g : s->groups) {  // segmentGroups.copyTo -> enqueueOnCopy (segmentGroupCollection.ts:47-62)
             if (g->hasPrevious)  // previousProps of the source segment, duplicated for the copy
                 for (size_t k = 0; k < g->segments.size(); k++)
@@ -644,7 +667,10 @@ class Tree {
                         return;
                     }
                     s->localRemovedSeq = -1;
-                    if (s->removedSeq == kUnassignedSeq) s->removedSeq = seq;
+                    if (s->removedSeq == kUnassignedSeq) {  // ack() is true: no overlapping remove
+                        s->removedSeq = seq;
+                        slideAckedRemovedSegmentReferences(s);  // mergeTree.ts:1294-1296
+                    }
                 } else {
                     status = MTR_ERR_BAD_OP;
                     return;
@@ -653,6 +679,175 @@ class Tree {
             }
         }
         zamboniSegments();  // mergeTree.ts:1318-1320
+    }
+
+    // ------------------------------------------------------------ local references
+    std::vector<LRef> refs;  // every reference by creation (the host's reference ids)
+    std::deque<LocalRefs> refPool;
+    static constexpr int kSlide = MTR_REFTYPE_SLIDE_ON_REMOVE, kStay = MTR_REFTYPE_STAY_ON_REMOVE,
+                         kTransient = MTR_REFTYPE_TRANSIENT;
+    LocalRefs* newLocalRefs(Seg* s, size_t len) {  // new LocalReferenceCollection(segment), localReference.ts:172-181
+        refPool.emplace_back();
+        LocalRefs* c = &refPool.back();
+        c->segment = s;
+        c->byOffset.resize(len);
+        return c;
+    }
+    RefsAtOffset& refSlot(LocalRefs* c, int offset) {  // refsByOffset[offset] ??= {} (a JS array grows on assignment)
+        if (size_t(offset) >= c->byOffset.size()) c->byOffset.resize(size_t(offset) + 1);
+        if (!c->byOffset[size_t(offset)]) c->byOffset[size_t(offset)].reset(new RefsAtOffset());
+        return *c->byOffset[size_t(offset)];
+    }
+    // LocalReferenceCollection.has (localReference.ts:357-384)
+    bool refsHas(const LocalRefs* c, int id) const {
+        const LRef& r = refs[size_t(id)];
+        return !(r.refType & kTransient) && r.segment == c->segment && r.list >= 0;
+    }
+    // removeLocalRef (localReference.ts:304-318)
+    void refsRemove(LocalRefs* c, int id) {
+        if (!c || !refsHas(c, id)) return;
+        LRef& r = refs[size_t(id)];
+        refSlot(c, r.offset).lst[r.list].remove(id);
+        r.list = -1;
+        c->refCount--;
+    }
+    // the collection's references in iteration order ([Symbol.iterator], localReference.ts:187-221): by offset,
+    // then before / at / after
+    static std::vector<int> refsOf(const LocalRefs* c) {
+        std::vector<int> out;
+        for (const auto& slot : c->byOffset)
+            if (slot)
+                for (int k = 0; k < 3; k++)
+                    if (slot->has[k]) out.insert(out.end(), slot->lst[k].begin(), slot->lst[k].end());
+        return out;
+    }
+    // MergeTree.createLocalReferencePosition (mergeTree.ts:2209-2226) -> createLocalRef / addLocalRef
+    // (localReference.ts:260-298); a null segment is createDetachedLocalReferencePosition (:123-127)
+    int createRef(Seg* seg, int offset, int refType) {
+        const int excl = !!(refType & kTransient) + !!(refType & kSlide) + !!(refType & kStay);
+        if (excl > 1) return MTR_ERR_BAD_OP;  // _validateReferenceType's UsageError (:23-39)
+        LRef r;
+        r.refType = refType;
+        const int id = int(refs.size());
+        if (!seg) {
+            refs.push_back(r);
+            return status;
+        }
+        if (removedAndAcked(seg) && !(refType & (kSlide | kTransient))) return MTR_ERR_BAD_OP;  // UsageError
+        if (!seg->localRefs) seg->localRefs = newLocalRefs(seg, size_t(seg->len));
+        r.segment = seg;
+        r.offset = offset;
+        refs.push_back(r);
+        if (!(refType & kTransient)) {
+            if (offset >= seg->len) return MTR_ERR_ASSERT | 0x348;  // "offset cannot be beyond segment length"
+            RefsAtOffset& slot = refSlot(seg->localRefs, offset);
+            slot.has[1] = true;
+            slot.lst[1].push_back(id);
+            refs[size_t(id)].list = 1;
+            seg->localRefs->refCount++;
+        }
+        return status;
+    }
+    // LocalReferenceCollection.split (localReference.ts:398-420): the references at offsets >= pos go to the
+    // split-off segment r
+    void refsSplit(LocalRefs* c, int pos, Seg* r) {
+        if (c->refCount) {
+            LocalRefs* rc = newLocalRefs(r, 0);
+            for (size_t k = size_t(pos); k < c->byOffset.size(); k++) rc->byOffset.push_back(std::move(c->byOffset[k]));
+            if (size_t(pos) < c->byOffset.size()) c->byOffset.resize(size_t(pos));
+            r->localRefs = rc;
+            for (int id : refsOf(rc)) {
+                refs[size_t(id)].segment = r;
+                refs[size_t(id)].offset -= pos;
+                c->refCount--;
+                rc->refCount++;
+            }
+        } else {
+            c->byOffset.resize(size_t(pos));  // refsByOffset.length = offset
+        }
+    }
+    // LocalReferenceCollection.append (static :143-158, instance :332-350): b's references move to a behind
+    // a's refsByOffset (called before a's cachedLength grows)
+    void refsAppend(Seg* a, Seg* b) {
+        if (b->localRefs && b->localRefs->refCount) {
+            if (!a->localRefs) a->localRefs = newLocalRefs(a, size_t(a->len));
+            LocalRefs* c = a->localRefs;
+            LocalRefs* o = b->localRefs;
+            if (int(c->byOffset.size()) != a->len) status = MTR_ERR_ASSERT | 0x2be;  // "contains a gap"
+            c->refCount += o->refCount;
+            o->refCount = 0;
+            const int base = int(c->byOffset.size());
+            for (int id : refsOf(o)) {
+                refs[size_t(id)].segment = a;
+                refs[size_t(id)].offset += base;
+            }
+            for (auto& p : o->byOffset) c->byOffset.push_back(std::move(p));
+            o->byOffset.clear();
+        } else if (a->localRefs) {
+            a->localRefs->byOffset.resize(a->localRefs->byOffset.size() + size_t(b->len));
+        }
+    }
+    // MergeTree._getSlideToSegment (mergeTree.ts:821-840): the first segment after s (forwardExcursion) that is
+    // acked and not removed-and-acked, else the last such before it (backwardExcursion), else none
+    Seg* getSlideToSegment(Seg* s) {
+        if (!s || !removedAndAcked(s)) return s;
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        const auto it = std::find(lv.begin(), lv.end(), s);
+        if (it == lv.end()) return nullptr;  // unlinked: the excursions visit nothing
+        auto ok = [](const Seg* x) { return x->seq != kUnassignedSeq && !removedAndAcked(x); };
+        for (auto j = it + 1; j != lv.end(); ++j)
+            if (ok(*j)) return *j;
+        for (auto j = it; j != lv.begin();)
+            if (ok(*--j)) return *j;
+        return nullptr;
+    }
+    // MergeTree.slideAckedRemovedSegmentReferences (mergeTree.ts:849-884) with addBeforeTombstones /
+    // addAfterTombstones (localReference.ts:426-490)
+    void slideAckedRemovedSegmentReferences(Seg* s) {
+        if (!s->localRefs || s->localRefs->refCount == 0) return;
+        Seg* ns = getSlideToSegment(s);
+        const std::vector<int> ids = refsOf(s->localRefs);
+        if (!ns) {
+            for (int id : ids)
+                if (!(refs[size_t(id)].refType & kStay)) refsRemove(s->localRefs, id);
+            return;
+        }
+        if (!ns->localRefs) ns->localRefs = newLocalRefs(ns, size_t(ns->len));
+        LocalRefs* c = ns->localRefs;
+        const bool after = leafIndex(ns) < leafIndex(s);  // newSegment.ordinal < segment.ordinal
+        const int off = after ? ns->len - 1 : 0;
+        RefsAtOffset& slot = refSlot(c, off);
+        const int k = after ? 2 : 0;
+        slot.has[k] = true;
+        std::list<int>& dst = slot.lst[k];
+        auto at = dst.begin();  // before-tombstones: in order at the front of the `before` list
+        for (int id : ids) {
+            LRef& r = refs[size_t(id)];
+            if (r.refType & kStay) continue;
+            refsRemove(r.segment->localRefs, id);  // link() with a new list node leaves the old collection
+            if (r.refType & kSlide) {
+                if (after) dst.push_back(id);
+                else at = std::next(dst.insert(at, id));
+                r.segment = ns;
+                r.offset = off;
+                r.list = k;
+                c->refCount++;
+            } else {
+                r.segment = nullptr;  // lref.link(undefined, 0, undefined)
+                r.offset = 0;
+            }
+        }
+    }
+    // MergeTree.referencePositionToLocalPosition (mergeTree.ts:1046-1062) at the local view
+    // (Client.localReferencePositionToPosition, client.ts:398-403)
+    int refPosition(int id) {
+        const LRef& r = refs[size_t(id)];
+        Seg* s = r.segment;
+        if (!s || !s->parent) return MTR_DETACHED_POSITION;
+        if ((r.refType & kTransient) || (s->localRefs && refsHas(s->localRefs, id)))
+            return (s->removed ? 0 : r.offset) + getPosition(s, currentSeq, localClientId);
+        return MTR_DETACHED_POSITION;
     }
 
     // ------------------------------------------------------------ reconnect
@@ -1069,6 +1264,7 @@ class Tree {
                         int ln = localNetLength(s);
                         bool ok = prev && canAppend(prev, s) && matchProperties(prev, s, tabs.b) && (ln > 0);
                         if (ok) {
+                            refsAppend(prev, s);    // BaseSegment.append, mergeTreeNodes.ts:527-530 (before lengths)
                             prev->text += s->text;  // TextSegment.append textSegment.ts:99-103 (BaseSegment.append for perm)
                             prev->len += s->len;
                             s->parent = nullptr;
@@ -1345,6 +1541,7 @@ class Tree {
         bool overwrite = false;   // _overwrite: an overlapping remove rebuilds lengths (mergeTree.ts:1966,2012-2019)
         const int localSeq = seq == kUnassignedSeq ? ++localSeqCounter : 0;  // mergeTree.ts:1970-1971
         SegGroup* group = nullptr;
+        std::vector<Seg*> localOverlapWithRefs;  // mergeTree.ts:1965, 1984-1986
         nodeMap(
             refSeq, clientId,
             [&](Seg* s) {
@@ -1353,6 +1550,7 @@ class Tree {
                     if (s->removedSeq == kUnassignedSeq) {
                         s->removedClientIds.insert(s->removedClientIds.begin(), clientId);
                         s->removedSeq = seq;
+                        if (s->localRefs && s->localRefs->refCount) localOverlapWithRefs.push_back(s);
                     } else {
                         s->removedClientIds.push_back(clientId);
                     }
@@ -1375,7 +1573,12 @@ class Tree {
                 if (overwrite) nodeUpdateLengthNewStructure(b);
                 else blockUpdateLength(b, seq, clientId);
             });
+        // already removed locally, so no event: their sliding references slide now (mergeTree.ts:2023-2025)
+        for (Seg* s : localOverlapWithRefs) slideAckedRemovedSegmentReferences(s);
         recordDeltas(fresh, MTR_OP_REMOVE);  // mergeTree.ts:2026-2031
+        // newly removed by someone else (or before collaboration): slide after the event (mergeTree.ts:2032-2040)
+        if (!collaborating || clientId != localClientId)
+            for (Seg* s : fresh) slideAckedRemovedSegmentReferences(s);
         if (collaborating && seq != kUnassignedSeq) zamboniSegments();
     }
 
@@ -1538,6 +1741,25 @@ class Tree {
                 if (!collaborating) return MTR_ERR_BAD_OP;
                 ackPendingSegment(int(op.payload2), op.payload, op.seq, uint32_t(op.pos1));
                 break;
+            case MTR_OP_REF_CREATE: {  // createPositionReference, sequence/src/intervalCollection.ts:697-724
+                const bool lv = (op.payload2 & MTR_REF_LOCALVIEW) != 0;
+                int off = 0;
+                Seg* s = containingSegment(op.pos1, lv ? currentSeq : op.ref_seq, lv ? localClientId : int(op.client), off);
+                if (s && (op.payload2 & MTR_REF_SLIDE)) {  // Client.getSlideToSegment, client.ts:1085-1099
+                    Seg* t = getSlideToSegment(s);
+                    if (t != s) {
+                        off = (t && leafIndex(t) < leafIndex(s)) ? t->len - 1 : 0;
+                        s = t;
+                    }
+                }
+                return createRef(s, off, int(op.payload));
+            }
+            case MTR_OP_REF_REMOVE: {  // MergeTree.removeLocalReferencePosition, mergeTree.ts:2190-2207
+                if (op.payload >= refs.size()) return MTR_ERR_BAD_OP;
+                Seg* s = refs[op.payload].segment;
+                if (s) refsRemove(s->localRefs, int(op.payload));
+                return status;
+            }
             case MTR_OP_START_COLLAB:  // startOrUpdateCollaboration -> startCollaboration, client.ts:1133, mergeTree.ts:731
                 if (collaborating) return MTR_OK;
                 localClientId = opClient(op);
@@ -1985,6 +2207,27 @@ int64_t oracle_doc_containing_props(oracle_doc* d, int32_t pos, int32_t ref_seq,
         out[4 + 2 * k] = s->props.kv[k].second;
     }
     return n;
+}
+
+int64_t oracle_doc_ref_positions(oracle_doc* d, int32_t* out, int64_t cap) {
+    Tree& t = d->view();
+    if (!t.pendingLoad.empty()) t.reloadFromSegments();
+    const int64_t n = int64_t(t.refs.size());
+    if (n > cap) return -n;
+    for (int64_t i = 0; i < n; i++) out[i] = t.refPosition(int(i));
+    return n;
+}
+
+int32_t oracle_doc_ref_info(oracle_doc* d, uint32_t id, int32_t* out) {
+    Tree& t = d->view();
+    if (id >= t.refs.size()) return -1;
+    const LRef& r = t.refs[id];
+    Seg* s = r.segment;
+    out[0] = s && s->parent ? t.leafIndex(s) : -1;
+    out[1] = r.offset;
+    out[2] = r.refType;
+    out[3] = (s && s->localRefs && t.refsHas(s->localRefs, int(id))) ? 1 : 0;
+    return out[0];
 }
 
 int32_t oracle_doc_marker_position(oracle_doc* d, uint32_t ordinal, int32_t ref_seq, int32_t client) {

@@ -106,6 +106,13 @@ int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32
 int64_t oracle_doc_containing_props(oracle_doc* d, int32_t pos, int32_t ref_seq, int32_t client, uint32_t* out,
                                     int64_t cap);
 
+/* Local references (MTR_OP_REF_CREATE records, localReference.ts): out[i] = localReferencePositionToPosition of
+ * reference i (client.ts:398-403; MTR_DETACHED_POSITION = -1).  Returns the count, -count when cap is short. */
+int64_t oracle_doc_ref_positions(oracle_doc* d, int32_t* out, int64_t cap);
+/* reference id: out = [leaf index of its segment (-1: none or unlinked, also returned), offset, refType,
+ * held by its segment's LocalReferenceCollection] */
+int32_t oracle_doc_ref_info(oracle_doc* d, uint32_t id, int32_t* out);
+
 /* Length of the doc in the (ref_seq, client) view (MergeTree.getLength, mergeTree.ts:757) */
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client);
 /* MergeTree.getPosition (mergeTree.ts:768-785) of the marker mapped to a host marker ordinal, -1 if none */

@@ -71,6 +71,10 @@ def lib():
         L.oracle_doc_containing_props.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_int64]
         L.oracle_doc_length.restype = C.c_int64
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        L.oracle_doc_ref_positions.restype = C.c_int64
+        L.oracle_doc_ref_positions.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_doc_ref_info.restype = C.c_int32
+        L.oracle_doc_ref_info.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -211,6 +215,20 @@ class OracleDoc:
 
     def length(self, ref_seq, client):
         return lib().oracle_doc_length(self.h, ref_seq, client)
+
+    def ref_positions(self) -> list:
+        """localReferencePositionToPosition of every local reference, by id (-1 = detached)."""
+        n = lib().oracle_doc_ref_positions(self.h, None, 0)
+        n = -n if n < 0 else n
+        out = np.zeros(max(n, 1), dtype="<i4")
+        lib().oracle_doc_ref_positions(self.h, out.ctypes.data, n)
+        return [int(x) for x in out[:n]]
+
+    def ref_info(self, ref_id: int):
+        """(leaf index of the reference's segment or -1, offset, refType, held by the segment's collection)"""
+        out = np.zeros(4, dtype="<i4")
+        lib().oracle_doc_ref_info(self.h, ref_id, out.ctypes.data)
+        return tuple(int(x) for x in out[:3]) + (bool(out[3]),)
 
 
 def replay_batch(batch, lo, hi, threads, opts=None):

@@ -1,0 +1,429 @@
+"""Local references: LocalReferenceCollection (merge-tree/src/localReference.ts:142-571) on
+segment splits and appends, slideAckedRemovedSegmentReferences (mergeTree.ts:849-884) on acked removals,
+and localReferencePositionToPosition (client.ts:398-403 -> mergeTree.ts:1046-1062).
+
+Known answers transcribed from packages/dds/merge-tree/src/test/client.localReference.spec.ts, as
+TestClient sessions: local edits, makeOpMessage messages applied to each client (a client's own message
+acks its pending op), references created from getContainingSegment (+ getSlideToSegment) and their
+positions asserted where the reference test asserts them.  A seeded farm shaped like
+client.localReferenceFarm.spec.ts puts a SlideOnRemove reference at every position on three clients and
+checks that every client resolves reference r to the same position after concurrent removes and zamboni.
+CPU: the oracle; -m gpu: the HIP engine must give the oracle's positions at every check.
+"""
+import random
+
+import pytest
+
+from fluidframework_amd import abi
+from fluidframework_amd.batch import DocLog, Interner, build_batch
+from oracle.oracle import OracleDoc, options
+
+SIMPLE, SLIDE, STAY, TRANSIENT = (abi.REFTYPE_SIMPLE, abi.REFTYPE_SLIDE_ON_REMOVE, abi.REFTYPE_STAY_ON_REMOVE,
+                                  abi.REFTYPE_TRANSIENT)
+DETACHED = abi.DETACHED_POSITION
+
+
+def ins(pos, text):
+    return {"type": 0, "pos1": pos, "seg": text}
+
+
+def rem(a, b):
+    return {"type": 1, "pos1": a, "pos2": b}
+
+
+class Session:
+    """TestClients (one DocLog each) on the oracle, and with `engine` also as documents of one HIP engine
+    whose reference positions must equal the oracle's at every query."""
+
+    def __init__(self, names, engine=False, new_length_calc=False):
+        self.it = Interner()
+        self.names = list(names)
+        self.logs = {n: DocLog() for n in self.names}
+        for n in self.names:
+            self.logs[n].start_collab(n)
+        self.cur = {n: 0 for n in self.names}
+        self.opts = options(new_length_calc=new_length_calc)
+        self.docs = {n: OracleDoc(self.opts) for n in self.names}
+        self.eng = None
+        if engine:
+            from fluidframework_amd.engine import Engine
+            self.eng = Engine(len(self.names), max_segments=4096, heap_entries=4096, text_units=1 << 16,
+                              prop_words=1 << 12, remover_cells=1 << 12, ops_per_launch=64,
+                              new_length_calc=new_length_calc, ref_slots=4096)
+        self.checks = 0
+
+    def local(self, c, op):
+        self.logs[c].local_op(op, self.it)
+        return op
+
+    def make(self, c, op, seq=-1, ref=None, msn=0):
+        """TestClient.makeOpMessage (testClient.ts:286-310): refSeq defaults to the client's currentSeq."""
+        return {"clientId": c, "sequenceNumber": seq, "referenceSequenceNumber": self.cur[c] if ref is None else ref,
+                "minimumSequenceNumber": msn, "type": "op", "contents": op}
+
+    def apply(self, c, m):
+        self.logs[c].message(m, self.it)
+        self.cur[c] = m["sequenceNumber"]
+
+    def update_min_seq(self, c, msn):
+        self.logs[c].seq_update(msn, self.cur[c])
+
+    def ref(self, c, pos, ref_type, view=None, slide=False):
+        return self.logs[c].create_ref(pos, ref_type, view, slide)
+
+    def remove_ref(self, c, r):
+        self.logs[c].remove_ref(r)
+
+    def flush(self):
+        b = build_batch([self.logs[n] for n in self.names], self.it)
+        for d, n in enumerate(self.names):
+            assert self.docs[n].apply(b, d) == 0, n
+        if self.eng is not None:
+            self.eng.apply(b)
+            for d, n in enumerate(self.names):
+                st, op = self.eng.status(d)
+                assert st == 0, f"{n}: engine status {st:#x} at op {op}"
+
+    def positions(self, c):
+        self.flush()
+        p = self.docs[c].ref_positions()
+        if self.eng is not None:
+            g = self.eng.ref_positions(self.names.index(c))
+            assert g == p, f"{c}: engine {g} oracle {p}"
+            self.checks += 1
+        return p
+
+    def pos(self, c, r):
+        return self.positions(c)[r]
+
+    def info(self, c, r):
+        self.flush()
+        i = self.docs[c].ref_info(r)
+        if self.eng is not None:
+            assert self.eng.ref_info(self.names.index(c), r) == i, c
+        return i
+
+    def text(self, c):
+        self.flush()
+        t = self.docs[c].text()
+        if self.eng is not None:
+            assert self.eng.text(self.names.index(c)) == t, c
+        return t
+
+
+def _inserts(s, seq, n):
+    """client1 appends str(i) and sends it with minimumSequenceNumber = seq - 1 (both clients apply it)."""
+    for i in range(n):
+        op = s.local("1", ins(len(s.text("1")), str(i)))
+        seq[0] += 1
+        m = s.make("1", op, seq[0], msn=seq[0] - 1)
+        s.apply("1", m)
+        s.apply("2", m)
+
+
+def kat_remove_non_sliding(s):  # client.localReference.spec.ts:32-86
+    seq = [0]
+    _inserts(s, seq, 5)
+    r = s.ref("1", 2, SIMPLE)
+    assert s.pos("1", r) == 2, "create position"
+    seq[0] += 1
+    m = s.make("2", s.local("2", rem(2, 3)), seq[0], msn=seq[0] - 1)
+    s.apply("1", m)
+    s.apply("2", m)
+    assert s.pos("1", r) == DETACHED, "after remove"
+    _inserts(s, seq, 5)
+    assert s.pos("1", r) == DETACHED, "after zamboni"
+
+
+def kat_remove_sliding(s):  # :88-133
+    seq = [0]
+    _inserts(s, seq, 5)
+    r = s.ref("1", 2, SLIDE)
+    assert s.pos("1", r) == 2
+    seq[0] += 1
+    m = s.make("2", s.local("2", rem(2, 3)), seq[0], msn=seq[0] - 1)
+    s.apply("1", m)
+    s.apply("2", m)
+    assert s.pos("1", r) == 2
+    _inserts(s, seq, 5)
+    assert s.pos("1", r) == 2
+
+
+def kat_remove_to_end_sliding(s):  # :135-171
+    seq = [0]
+    _inserts(s, seq, 5)
+    r = s.ref("1", 2, SLIDE)
+    assert s.pos("1", r) == 2
+    seq[0] += 1
+    m = s.make("2", s.local("2", rem(2, len(s.text("2")))), seq[0], msn=seq[0] - 1)
+    s.apply("1", m)
+    s.apply("2", m)
+    assert s.pos("1", r) == len(s.text("2")) - 1
+
+
+def kat_remove_from_end_sliding(s):  # :173-208
+    m = s.make("1", s.local("1", ins(0, "ABCD")), 1, msn=0)
+    s.apply("1", m)
+    r = s.ref("1", 3, SLIDE)
+    assert s.pos("1", r) == 3, "ref created"
+    remove1 = s.make("1", s.local("1", rem(3, 4)), 2, msn=1)
+    assert s.pos("1", r) == 3, "after remove"
+    remove2 = s.make("1", s.local("1", rem(1, 3)), 3, msn=2)
+    assert s.pos("1", r) == 1, "after second remove"
+    s.apply("1", remove1)
+    s.apply("1", remove2)
+    assert s.pos("1", r) == 0, "ops applied"
+
+
+def kat_slide_to_segment(s):  # getSlideOnRemoveReferencePosition, :210-275
+    insert1 = s.make("1", s.local("1", ins(0, "XYZ")), 1)
+    s.apply("1", insert1)
+    insert2 = s.make("1", s.local("1", ins(0, "ABC")), 2)
+    s.apply("1", insert2)
+
+    def slide_ref(pos, ref_seq):  # a reference at getSlideToSegment(getContainingSegment(pos, {refSeq, "2"}))
+        r = s.ref("1", pos, SLIDE, view=(ref_seq, "2"), slide=True)
+        leaf, off, _, _ = s.info("1", r)
+        return leaf, off, s.pos("1", r)
+
+    # on XYZ at offset 1; XYZ starts at 3 (position = 3 + 1)
+    assert slide_ref(1, 1)[1:] == (1, 4)
+    # on ABC at offset 2; ABC starts at 0
+    assert slide_ref(2, 2)[1:] == (2, 2)
+    remove = s.make("1", s.local("1", rem(2, 5)), 5)
+    # on the removed, unacked "XY" at offset 0: it starts at 2 (a removed segment's references read offset 0)
+    assert slide_ref(3, 2)[1:] == (0, 2)
+    s.apply("1", remove)
+    # slid from the removed, acked "XY" to "Z" (offset 0), which starts at 2
+    assert slide_ref(3, 2)[1:] == (0, 2)
+    remove = s.make("1", s.local("1", rem(2, 3)), 6)
+    # on the removed, unacked "Z", end of string
+    assert slide_ref(3, 2)[1:] == (0, 2)
+    s.apply("1", remove)
+    # slid from the removed, acked "XY" back to "AB", offset 1 (its last unit)
+    assert slide_ref(3, 2)[1:] == (1, 1)
+
+
+def kat_remove_all_sliding(s):  # :277-317
+    seq = [0]
+    _inserts(s, seq, 5)
+    r = s.ref("1", 2, SLIDE)
+    assert s.pos("1", r) == 2
+    seq[0] += 1
+    m = s.make("2", s.local("2", rem(0, len(s.text("2")))), seq[0], msn=seq[0] - 1)
+    s.apply("1", m)
+    s.apply("2", m)
+    assert s.pos("1", r) == DETACHED
+    leaf, _, _, held = s.info("1", r)
+    assert leaf >= 0 and not held  # getSegment() is still the removed segment; the collection let it go
+
+
+def kat_offsets_on_removed_segment(s):  # :319-389
+    insert1 = s.make("1", s.local("1", ins(0, "ABCD")), 1)
+    s.apply("1", insert1)
+    s.apply("2", insert1)
+    r1 = s.ref("1", 1, SLIDE)
+    r2 = s.ref("1", 3, SLIDE)
+    insert2 = s.make("1", s.local("1", ins(2, "XY")), 2)
+    assert (s.pos("1", r1), s.pos("1", r2)) == (1, 5)
+    remove = s.make("2", s.local("2", rem(0, 4)), 3)
+    # the segments client 2 found before its remove (ABCD at offsets 1 and 3): a view that still sees them
+    c1 = s.ref("2", 1, SLIDE, view=(1, "1"))
+    c2 = s.ref("2", 3, SLIDE, view=(1, "1"))
+    assert (s.pos("2", c1), s.pos("2", c2)) == (0, 0)
+    s.apply("1", insert2)
+    s.apply("2", insert2)
+    assert (s.pos("1", r1), s.pos("1", r2)) == (1, 5)
+    assert (s.pos("2", c1), s.pos("2", c2)) == (0, 2)
+    s.apply("1", remove)
+    s.apply("2", remove)
+    assert (s.pos("1", r1), s.pos("1", r2)) == (0, 1)
+    assert (s.pos("2", c1), s.pos("2", c2)) == (0, 1)
+
+
+def kat_transient_on_removed(s):  # :391-418
+    m = s.make("1", s.local("1", ins(0, "ABCD")), 1)
+    s.apply("1", m)
+    s.apply("2", m)
+    s.local("1", rem(0, 2))
+    other = s.make("2", s.local("2", ins(3, "X")))  # an op from before client 1's remove
+    r = s.ref("1", 0, TRANSIENT, view=(other["referenceSequenceNumber"], "2"))
+    leaf, off, _, _ = s.info("1", r)
+    assert (leaf, off) == (0, 0)  # the removed "AB", offset 0
+    assert s.pos("1", r) == 0
+
+
+def kat_offsets_slid_to_local_removed(s):  # :420-479
+    insert1 = s.make("1", s.local("1", ins(0, "ABCDE")), 1)
+    s.apply("1", insert1)
+    s.apply("2", insert1)
+    r = s.ref("1", 4, SLIDE)
+    remove1 = s.make("2", s.local("2", rem(4, 5)), 3)
+    insert2 = s.make("1", s.local("1", ins(2, "XY")), 4)
+    remove2 = s.make("2", s.local("2", rem(1, 4)), 5)
+    c2 = s.ref("2", 4, SLIDE, view=(1, "1"), slide=True)  # createReference1: refSeq insert1, client 1
+    assert s.pos("1", r) == 6
+    assert s.pos("2", c2) == 1
+    s.apply("1", remove1)
+    s.apply("2", remove1)
+    assert s.pos("1", r) == 5
+    assert s.pos("2", c2) == 1
+    s.apply("1", insert2)
+    s.apply("2", insert2)
+    assert s.pos("1", r) == 5
+    assert s.text("2") == "AXY"
+    assert s.pos("2", c2) == 3
+    s.apply("1", remove2)
+    s.apply("2", remove2)
+    assert s.pos("1", r) == 2
+    assert s.pos("2", c2) == 2
+
+
+def kat_split_empty_then_append(s):  # :481-525 (regression: 0x2be on zamboni's append)
+    msgs = [s.make("A", s.local("A", ins(0, "0123456789")), 1)]
+    t = s.ref("A", 9, SIMPLE)
+    s.remove_ref("A", t)
+    msgs.append(s.make("A", s.local("A", ins(5, "ABCD")), 2))
+    r = s.ref("A", 6, SIMPLE)
+    for m in msgs:
+        for c in ("A", "B"):
+            s.apply(c, m)
+    for c in ("A", "B"):
+        s.update_min_seq(c, 2)
+    assert s.text("A") == "01234ABCD56789"
+    assert s.pos("A", r) == 6
+    assert s.pos("A", t) == DETACHED
+
+
+def _stay_setup(s):  # :527-558 beforeEach
+    s.apply("1", s.make("1", s.local("1", ins(0, "B")), 1))
+    s.apply("1", s.make("1", s.local("1", ins(0, "A")), 2))
+    assert s.text("1") == "AB"
+    a = s.ref("1", 0, STAY)
+    b = s.ref("1", 1, STAY)
+    return a, b
+
+
+def _stay_case(lo, hi, which):
+    def kat(s):
+        a, b = _stay_setup(s)
+        r = a if which == "a" else b
+        before = s.info("1", r)
+        s.local("1", rem(lo, hi))
+        s.apply("1", s.make("2", rem(lo, hi), 3, ref=2))  # removeRangeRemote(lo, hi, 3, 2, "2")
+        after = s.info("1", r)
+        assert after[0] == before[0] and after[3], "ref was removed"
+        assert s.pos("1", r) == lo  # a removed segment: offset 0 at its position
+    return kat
+
+
+KATS = [
+    ("Remove segment of non-sliding local reference", ["1", "2"], kat_remove_non_sliding),
+    ("Remove segment of sliding local reference", ["1", "2"], kat_remove_sliding),
+    ("Remove segments to end with sliding local reference", ["1", "2"], kat_remove_to_end_sliding),
+    ("Remove segments from end with sliding local reference", ["1"], kat_remove_from_end_sliding),
+    ("getSlideOnRemoveReferencePosition", ["1", "2"], kat_slide_to_segment),
+    ("Remove all segments with sliding local reference", ["1", "2"], kat_remove_all_sliding),
+    ("References can have offsets on removed segment", ["1", "2"], kat_offsets_on_removed_segment),
+    ("Transient references can be created on removed segments", ["1", "2"], kat_transient_on_removed),
+    ("References can have offsets when slid to locally removed segment", ["1", "2"],
+     kat_offsets_slid_to_local_removed),
+    ("Split segment with no references and append to segment with references", ["A", "B"],
+     kat_split_empty_then_append),
+    ("StayOnRemove: when references would slide forward", ["1"], _stay_case(0, 1, "a")),
+    ("StayOnRemove: when references would slide backward", ["1"], _stay_case(1, 2, "b")),
+    ("StayOnRemove: when references would slide off the string", ["1"], _stay_case(0, 2, "a")),
+]
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k[0] for k in KATS])
+def test_local_reference_kats_oracle(kat):
+    name, clients, fn = kat
+    fn(Session(clients))
+
+
+# ---------------------------------------------------------------- farm
+def farm(seed, s, rounds=6, ops_per_round=10):
+    """client.localReferenceFarm.spec.ts:36-101 on three clients: random inserts, then a SlideOnRemove
+    reference at every position of every client, then rounds of concurrent removes (each op made at its
+    writer's local view, the round's messages sequenced after every op was made), zamboni by raising the
+    minimum sequence number step by step, and more rounds.  After each stage reference r resolves to the
+    same position on every client.  Returns the number of references."""
+    rnd = random.Random(seed)
+    names = s.names
+    seq = [0]
+    low = [0]  # the clients' minSeq
+
+    def rounds_of(kind, n):
+        for _ in range(n):
+            start = seq[0]  # the round's minimumSequenceNumber (mergeTreeOperationRunner.ts:262, 297)
+            msgs = []
+            for _ in range(ops_per_round):
+                w = rnd.choice(names)
+                t = s.text(w)
+                if kind == "insert" or not t:
+                    op = ins(rnd.randint(0, len(t)), "".join(rnd.choice("abcdef") for _ in range(rnd.randint(1, 4))))
+                else:
+                    a = rnd.randrange(len(t))
+                    op = rem(a, min(len(t), a + rnd.randint(1, 3)))
+                msgs.append((w, s.make(w, s.local(w, op), 0)))
+            for w, m in msgs:  # sequenced in the order they were made
+                seq[0] += 1
+                m["sequenceNumber"] = seq[0]
+                m["minimumSequenceNumber"] = start
+                low[0] = start
+                for c in names:
+                    s.apply(c, m)
+
+    def agree(stage):
+        ps = [s.positions(c) for c in names]
+        for c, p in zip(names[1:], ps[1:]):
+            assert p == ps[0], f"seed {seed} {stage}: client {c} {p} vs {ps[0]}"
+
+    rounds_of("insert", 2)
+    n = len(s.text(names[0]))
+    for c in names:
+        for t in range(n):
+            s.ref(c, t, SLIDE)
+    agree("initialize")
+    def zamboni():  # updateMinSeq from minSeq to every later sequence number: zamboni is incremental
+        for c in names:
+            for i in range(low[0], seq[0] + 1):
+                s.update_min_seq(c, i)
+        low[0] = seq[0]
+
+    zamboni()
+    agree("after init zamboni")
+    rounds_of("remove", rounds)
+    agree("after more ops")
+    zamboni()
+    agree("after final zamboni")
+    return n
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_local_reference_farm_oracle(seed):
+    s = Session(["a", "b", "c"])
+    n = farm(seed, s)
+    assert n > 0
+    ps = s.positions("a")
+    assert any(p == DETACHED for p in ps) or len(set(ps)) < len(ps)  # removes slid or detached some
+
+
+# ---------------------------------------------------------------- the HIP engine
+@pytest.mark.gpu
+@pytest.mark.parametrize("kat", KATS, ids=[k[0] for k in KATS])
+def test_local_reference_kats_engine(kat):
+    name, clients, fn = kat
+    s = Session(clients, engine=True)
+    fn(s)
+    assert s.checks > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("new_length", [False, True], ids=["oldlen", "newlen"])
+def test_local_reference_farm_engine(new_length):
+    for seed in range(4):
+        s = Session(["a", "b", "c"], engine=True, new_length_calc=new_length)
+        farm(seed, s)
+        assert s.checks > 0

@@ -48,7 +48,8 @@ def test_addon_loads_and_fails_loudly_without_a_gpu():
     lines = out.strip().splitlines()
     assert json.loads(lines[0]) == sorted(["createEngine", "submitRun", "summarize", "getSummary", "getText",
                                            "docStatus", "stats", "reset", "setMatrix", "getDeltas",
-                                           "submitRunAsync", "summarizeAsync", "getContainingSegment", "getProps"])
+                                           "submitRunAsync", "summarizeAsync", "getContainingSegment", "getProps",
+                                           "getRefPositions", "getRefInfo"])
     if lines[1] != "ENGINE":  # no HIP device here: construction must throw, never fall back
         assert lines[1].startswith("ERR mtr_engine_create")
 
