@@ -343,7 +343,7 @@ def test_local_reference_kats_oracle(kat):
 
 
 # ---------------------------------------------------------------- farm
-def farm(seed, s, rounds=6, ops_per_round=10):
+def farm(seed, s, rounds=6, ops_per_round=10, kind="remove"):
     """client.localReferenceFarm.spec.ts:36-101 on three clients: random inserts, then a SlideOnRemove
     reference at every position of every client, then rounds of concurrent removes (each op made at its
     writer's local view, the round's messages sequenced after every op was made), zamboni by raising the
@@ -361,7 +361,7 @@ def farm(seed, s, rounds=6, ops_per_round=10):
             for _ in range(ops_per_round):
                 w = rnd.choice(names)
                 t = s.text(w)
-                if kind == "insert" or not t:
+                if kind == "insert" or not t or (kind == "mixed" and rnd.random() < 0.4):
                     op = ins(rnd.randint(0, len(t)), "".join(rnd.choice("abcdef") for _ in range(rnd.randint(1, 4))))
                 else:
                     a = rnd.randrange(len(t))
@@ -394,7 +394,7 @@ def farm(seed, s, rounds=6, ops_per_round=10):
 
     zamboni()
     agree("after init zamboni")
-    rounds_of("remove", rounds)
+    rounds_of(kind, rounds)
     agree("after more ops")
     zamboni()
     agree("after final zamboni")
@@ -402,9 +402,10 @@ def farm(seed, s, rounds=6, ops_per_round=10):
 
 
 @pytest.mark.parametrize("seed", range(8))
-def test_local_reference_farm_oracle(seed):
+@pytest.mark.parametrize("kind", ["remove", "mixed"])
+def test_local_reference_farm_oracle(seed, kind):
     s = Session(["a", "b", "c"])
-    n = farm(seed, s)
+    n = farm(seed, s, kind=kind)
     assert n > 0
     ps = s.positions("a")
     assert any(p == DETACHED for p in ps) or len(set(ps)) < len(ps)  # removes slid or detached some
@@ -424,6 +425,7 @@ def test_local_reference_kats_engine(kat):
 @pytest.mark.parametrize("new_length", [False, True], ids=["oldlen", "newlen"])
 def test_local_reference_farm_engine(new_length):
     for seed in range(4):
-        s = Session(["a", "b", "c"], engine=True, new_length_calc=new_length)
-        farm(seed, s)
-        assert s.checks > 0
+        for kind in ("remove", "mixed"):
+            s = Session(["a", "b", "c"], engine=True, new_length_calc=new_length)
+            farm(seed, s, rounds=8, kind=kind)
+            assert s.checks > 0
