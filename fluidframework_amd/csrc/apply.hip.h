@@ -243,6 +243,8 @@ struct Sc {
     int rel[2];   // positions resolved by MTR_OP_RELPOS records for the next (MTR_F_REL) op
     int relmask;  // which of rel[] are pending: bit 0 pos1, bit 1 pos2
     int nrefs, refcap;  // local references of the document (DocHdr.nrefs) and the table's capacity
+    int fail_op, max_heap, heap_need;  // DocHdr's, for this launch
+    unsigned long long sum_s, sum_l;   // B_op counters: leaves before each op, inserted units
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];
 #endif
@@ -253,14 +255,14 @@ struct St {
     int nseg, height, minseq, curseq;
     int collab, local, heapn, uidnext;
     int textused, propused, rmused, status;  // textused: handle-table length for permutation vectors
-    int fail_op, max_heap, ops_done, texthalf;
+    int texthalf;
     int htop;  // seq of the LRU heap's top entry (valid while heapn > 0)
-    int heap_need;
-    int dused;
+    int dused;   // (delta-reporting instantiations only)
     int holes;   // hole slots (HBM-resident documents only)
     int chunked; // chunk summaries valid (HBM-resident documents with holes)
     int cur_op;  // index of the op being applied (delta-reporting instantiations only)
-    unsigned long long sum_s, sum_l;  // sum over ops of the leaf count before the op / inserted units
+    // (the failing op, the heap-size high-water mark, the heap a yield asks for and the B_op counters live in
+    // Sc: they change rarely, and every field here is an SGPR held across the whole op loop)
 };
 
 struct View {
@@ -307,6 +309,7 @@ MTR_DI uint32_t set_ns(uint32_t m, uint32_t ns) { return (m & ~M_NS_MASK) | (ns 
 
 // ------------------------------------------------------------------ wave primitives
 MTR_DI int lane_id() { return int(threadIdx.x); }  // blockDim.x == 64
+constexpr uint64_t LO32 = 0x00000000ffffffffull, HI32 = 0xffffffff00000000ull;  // lanes 0-31, 32-63
 MTR_DI uint64_t lanes_below() { return (uint64_t(1) << lane_id()) - 1; }
 MTR_DI int first_lane(uint64_t m) { return __ffsll((long long)m) - 1; }
 MTR_DI int last_lane(uint64_t m) { return 63 - __clzll((long long)m); }
@@ -1327,8 +1330,8 @@ struct Eng {
         const bool in = (i >= 0) & (i < S);
         const uint32_t mi = L.meta[in ? i : 0];
         const bool b = in & (bnd_of(mi) >= 1);
-        const uint64_t sm = __ballot((ln <= 31) & ((i <= 0) | b));
-        const uint64_t em = __ballot((ln > 31) & ((i >= S) | b));
+        const uint64_t sm = __ballot((i <= 0) | b) & LO32;
+        const uint64_t em = __ballot((i >= S) | b) & HI32;
         bs = sm ? max(0, x - 31 + last_lane(sm)) : block_start(L, x - 32, 1);
         be = em ? x - 31 + first_lane(em) : block_end(L, s, x + 32, 1);
     }
@@ -1385,7 +1388,10 @@ struct Eng {
         L.huid[k] = u;
         wsync();
         if (k == 1) s.htop = sq;
-        if (s.heapn > s.max_heap) s.max_heap = s.heapn;
+        {
+            const int mh = L.sc->max_heap;  // (every lane: the same value to the same word)
+            L.sc->max_heap = max(mh, s.heapn);
+        }
     }
     static MTR_DI uint32_t heap_pop(D& L, St& s) {
         PROF(P_HEAP);
@@ -3013,7 +3019,7 @@ struct Eng {
         const int lj = L.len[jc], sqj = L.seq[jc], rsj = L.rseq[jc];
         const int vj = ev(ej0, jc > 0 ? ep : 0);
         const int ej = ej0 & EMASK;
-        const uint64_t em = __ballot(!in | ((ln > 0) & (bnd_of(mj) >= 1)));
+        const uint64_t em = __ballot(!in | (bnd_of(mj) >= 1)) & ~uint64_t(1);
         const int be = em ? i + first_lane(em) : block_end(L, s, i + 63, 1);
         const uint64_t cm = __ballot((jj < be) & (vj >= 0) & (pos < ej));
         if (!cm) return;
@@ -3132,12 +3138,12 @@ struct Eng {
                     const int vw = ev(ew0, wc > 0 ? ewp : 0);
                     const int ew = ew0 & EMASK;
                     const bool bw = inw & (bnd_of(mw) >= 1);
-                    const uint64_t sm = __ballot((ln <= 31) & ((w <= 0) | bw));
-                    const uint64_t em = __ballot((ln > 31) & ((w >= S) | bw));
+                    const uint64_t sm = __ballot((w <= 0) | bw) & LO32;
+                    const uint64_t em = __ballot((w >= S) | bw) & HI32;
                     if (sm && em) {
                         const int bs = max(0, i - 31 + last_lane(sm));
                         const int be = i - 31 + first_lane(em);
-                        const uint64_t cm = __ballot((ln >= 31) & (w < be) & (vw >= 0) &
+                        const uint64_t cm = (HI32 | (uint64_t(1) << 31)) & __ballot((w < be) & (vw >= 0) &
                                                      ((ew > pos) | ((vw == 0) & (seq > sw))));
                         slot = cm ? i - 31 + first_lane(cm) : be;
                         nocand = !cm;
@@ -3531,15 +3537,11 @@ struct Eng {
             s.nseg = h.nseg; s.height = h.height; s.minseq = h.minseq; s.curseq = h.curseq;
             s.collab = h.collab; s.local = h.local; s.heapn = h.heapn; s.uidnext = h.uidnext;
             s.textused = h.textused; s.propused = h.propused; s.rmused = h.rmused;
-            s.status = h.status; s.fail_op = h.fail_op; s.max_heap = h.max_heap;
+            s.status = h.status;
             s.texthalf = h.texthalf;
-            s.heap_need = 0;
-            s.dused = h.dused;
+            s.dused = DL ? h.dused : 0;
             s.holes = G ? h.holes : 0;
             s.chunked = G ? h.chunked : 0;
-            s.ops_done = 0;
-            s.sum_s = 0;
-            s.sum_l = 0;
         }
         if (PM && s.textused == 0) {  // new HandleTable: handles = [1] (handletable.ts:24)
             if (threadIdx.x == 0) handles(L)[0] = 1;
@@ -3548,6 +3550,11 @@ struct Eng {
         if (threadIdx.x == 0) {
             L.sc->relmask = 0;
             L.sc->nrefs = gp((const DocHdr*)P.hdr)[d].nrefs;
+            L.sc->fail_op = gp((const DocHdr*)P.hdr)[d].fail_op;
+            L.sc->max_heap = gp((const DocHdr*)P.hdr)[d].max_heap;
+            L.sc->heap_need = 0;
+            L.sc->sum_s = 0;
+            L.sc->sum_l = 0;
 #ifdef MTR_PROF
             for (int q = 0; q < P_COUNT; q++) L.sc->prof[q] = 0;
 #endif
@@ -3577,7 +3584,7 @@ struct Eng {
         s.htop = s.heapn > 0 ? uni(L.hseq[1]) : 0;
     }
 
-    static MTR_DI void store_doc(D& L, const KParams& P, const St& s, uint32_t d) {
+    static MTR_DI void store_doc(D& L, const KParams& P, const St& s, uint32_t d, int ops_done) {
         wsync();
         if (!G) {
             const int S = s.nseg;
@@ -3605,12 +3612,12 @@ struct Eng {
             h.nseg = s.nseg; h.height = s.height; h.minseq = s.minseq; h.curseq = s.curseq;
             h.collab = s.collab; h.local = s.local; h.heapn = s.heapn; h.uidnext = s.uidnext;
             h.textused = s.textused; h.propused = s.propused; h.rmused = s.rmused; h.status = s.status;
-            h.op_cursor += s.ops_done;
-            h.fail_op = s.fail_op;
-            h.max_heap = s.max_heap;
+            h.op_cursor += ops_done;
+            h.fail_op = L.sc->fail_op;
+            h.max_heap = L.sc->max_heap;
             h.texthalf = s.texthalf;
-            h.heap_need = s.heap_need;
-            h.dused = s.dused;
+            h.heap_need = L.sc->heap_need;
+            if (DL) h.dused = s.dused;
             h.nrefs = L.sc->nrefs;
             if (G) {
                 h.holes = s.holes;
@@ -3623,11 +3630,11 @@ struct Eng {
             if (P.prof)
                 for (int q = 0; q < P_COUNT; q++) atomicAdd(&P.prof[q], L.sc->prof[q]);
 #endif
-            if (s.ops_done) {  // this document's counters (no cross-document atomics)
+            if (ops_done) {  // this document's counters (no cross-document atomics)
                 const gptr<unsigned long long> st = gp(P.stat_ops) + size_t(d) * 4;
-                st[0] += (unsigned long long)s.ops_done;
-                st[1] += s.sum_s;
-                st[2] += s.sum_l;
+                st[0] += (unsigned long long)ops_done;
+                st[1] += L.sc->sum_s;
+                st[2] += L.sc->sum_l;
             }
         }
     }
@@ -3763,6 +3770,19 @@ struct Eng {
     }
 
     // ------------------------------------------------------------ one op
+    // the B_op model's counters: every op but snapshot-load appends and relative-position /
+    // handle-table records is a flat pass over the leaves present before it; text inserts add their units
+    static MTR_DI bool counts_s(const mtr_op& op) {
+        return op.type != MTR_OP_LOAD && op.type != MTR_OP_RELPOS && op.type != MTR_OP_HANDLES;
+    }
+    static MTR_DI bool counts_l(const mtr_op& op) {
+        return (op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER) && !PM &&
+               !(op.flags & MTR_F_APPEND);
+    }
+    // the document stops at op gidx (DocHdr.fail_op)
+    static MTR_DI void set_fail(D& L, int gidx) {
+        if (lane_id() == 0) L.sc->fail_op = gidx;
+    }
     // Client.applyMsg for one member op (client.ts:858-887): dispatch, zamboni after the op, then
     // updateSeqNumbers on the message's last member op.  Returns false when the document stops
     // (s.status != MTR_OK; s.fail_op = gidx).
@@ -3790,23 +3810,17 @@ struct Eng {
                 if (hd != uni(L.ghdr()->ptail)) need = min(int(uniu(L.gpend()[4 * (hd % kPendRing) + 1])), s.nseg + 2);
             }
             if (need && s.heapn + need + 1 >= L.lhcap) {
-                s.heap_need = s.heapn + need + 2;
+                L.sc->heap_need = s.heapn + need + 2;
                 return false;
             }
         }
-        // (the B_op model's counters: snapshot-load appends and relative-position records are not flat passes)
-        if (op.type != MTR_OP_LOAD && op.type != MTR_OP_RELPOS && op.type != MTR_OP_HANDLES)
-            s.sum_s += (unsigned long long)s.nseg;
-        if ((op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT) && !(op.flags & MTR_F_MARKER) && !PM &&
-            !(op.flags & MTR_F_APPEND))
-            s.sum_l += (unsigned long long)op.payload2;
         if (!PM) {  // text arena: keep room for this op's text plus zamboni merge copies
             const int need = int(op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT ? op.payload2 : 0) + 4096;
             if (s.textused + need > text_end(s, P)) text_gc(L, P, s);
         }
         if (s.nseg + 2 >= L.cap) s.status = MTR_ERR_CAPACITY;  // every op adds at most two leaves
         if (s.status != MTR_OK) {
-            s.fail_op = gidx;
+            set_fail(L, gidx);
             return false;
         }
         if (X && (op.flags & MTR_F_REL)) {  // consumed
@@ -3816,7 +3830,7 @@ struct Eng {
         if (op.type == MTR_OP_LOAD) {  // SnapshotLoader.loadHeader segment
             load_leaf(L, P, s, op, dd);
             if (s.status != MTR_OK) {
-                s.fail_op = gidx;
+                set_fail(L, gidx);
                 return false;
             }
             return true;
@@ -3840,7 +3854,7 @@ struct Eng {
             if (s.collab) {  // a pending local op (seq = UnassignedSequenceNumber, the local client)
                 if (!X || (op.type == MTR_OP_LOCAL_ANNOTATE && op.payload2 != 0 && op.payload2 != MTR_COMB_REWRITE)) {
                     s.status = MTR_ERR_UNSUPPORTED;  // (pending combining annotates other than rewrite: not built)
-                    s.fail_op = gidx;
+                    set_fail(L, gidx);
                     return false;
                 }
                 lseq = uni(L.ghdr()->lseq) + 1;  // ++collabWindow.localSeq (mergeTree.ts:1407, 1909, 1970)
@@ -3995,7 +4009,7 @@ struct Eng {
             if (zrun) zamboni(L, P, s);
         }
         if (s.status != MTR_OK) {
-            s.fail_op = gidx;
+            set_fail(L, gidx);
             return false;
         }
         return true;
@@ -4024,20 +4038,23 @@ struct Eng {
         // lane t holds the 8 words of op (chunk + t); the next op's text is prefetched into `pf`
         uint32_t ow[8];
         uint32_t pf = 0, npf = 0;
-        bool pre = false, npre = false;
+        int pre = 0, npre = 0;  // (ints, not bools: a bool live across the loop is a 64-bit lane mask)
+        // the B_op counters accumulate in VGPRs (the scalar unit is the bottleneck), Sc at the end
+        uint32_t acc_s = 0, acc_l = 0;
+        int done = 0;
         for (int k = 0; k < n_ops; k++) {
             PROF(P_OP);
             mtr_op op;
             if (GN) {
                 gen_op(L, P, s, dd, cursor + k);
                 op = uni_struct(ld_struct<mtr_op>(ops + k));
-                pre = false;
+                pre = 0;
             } else {
-                if ((k & 63) == 0) {
-                    const gptr<const uint32_t> w = (gptr<const uint32_t>)(ops + k + ln);
+                if ((k & 63) == 0) {  // (unconditional, clamped loads: no exec-mask blocks around them)
+                    const gptr<const uint32_t> w = (gptr<const uint32_t>)(ops + min(k + ln, n_ops - 1));
 #pragma unroll
-                    for (int q = 0; q < 8; q++) ow[q] = k + ln < n_ops ? w[q] : 0u;
-                    npre = false;
+                    for (int q = 0; q < 8; q++) ow[q] = w[q];
+                    npre = 0;
                 }
                 uint32_t wv[8];
 #pragma unroll
@@ -4045,25 +4062,34 @@ struct Eng {
                 __builtin_memcpy(&op, wv, sizeof(op));
                 pre = npre;
                 pf = npf;
-                npre = false;
+                npre = 0;
                 const int t1 = (k + 1) & 63;
                 if (t1 != 0 && k + 1 < n_ops) {  // issue the next insert's text loads now
                     const uint32_t w0 = rdlane(ow[0], t1), len1 = rdlane(ow[7], t1), off1 = rdlane(ow[6], t1);
                     const uint32_t ty = w0 & 0xffu, fl = (w0 >> 8) & 0xffu;
                     if ((ty == MTR_OP_INSERT || ty == MTR_OP_LOCAL_INSERT) && !(fl & MTR_F_MARKER) && len1 <= 64) {
-                        npre = true;
+                        npre = 1;
                         npf = uint32_t(ln) < len1 ? uint32_t(btext[off1 + ln]) : 0u;
                     }
                 }
             }
-            if (!apply_op(L, P, s, op, dd, pre, pf, cursor + k)) break;
-            s.ops_done = k + 1;
+            const uint32_t nseg0 = uint32_t(s.nseg);
+            if (!apply_op(L, P, s, op, dd, pre != 0, pf, cursor + k)) break;
+            done = k + 1;
+            const uint32_t cs = counts_s(op) ? nseg0 : 0u, cl = counts_l(op) ? op.payload2 : 0u;
+            acc_s += cs;
+            acc_l += cl;
+            asm("" : "+v"(acc_s), "+v"(acc_l));
+        }
+        if (lane_id() == 0) {
+            L.sc->sum_s += acc_s;
+            L.sc->sum_l += acc_l;
         }
         // a launch never ends between MTR_OP_RELPOS records and their op: the next one re-runs them
-        if (X) s.ops_done -= __popc(uint32_t(uni(L.sc->relmask)));
+        if (X) done -= __popc(uint32_t(uni(L.sc->relmask)));
         // a batch that ends with header segments: build the tree now (queries read it next)
-        if (s.height == 0 && s.status == MTR_OK && cursor + s.ops_done >= int(dd.op_count)) finish_load(L, s);
-        store_doc(L, P, s, d);
+        if (s.height == 0 && s.status == MTR_OK && cursor + done >= int(dd.op_count)) finish_load(L, s);
+        store_doc(L, P, s, d, done);
     }
 
     // ------------------------------------------------------------ SharedMatrix
@@ -4177,7 +4203,8 @@ struct Eng {
         St s0, s1;
         load_doc(L0, P, s0, d);
         load_doc(L1, P, s1, d1);
-        s1.ops_done = 0;
+        int done = 0;
+        unsigned long long acc_s = 0, acc_l = 0;
         const gptr<const mtr_op> ops = gp(P.ops) + dd.op_begin + cursor;
         for (int k = 0; k < n_ops; k++) {
             if (GN) gen_pair_op(L0, L1, P, s0, s1, dd, cursor + k);
@@ -4192,7 +4219,7 @@ struct Eng {
                 // vector's SnapshotLoader start (below, by MTR_F_COLS)
                 ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k) && apply_op(L1, P, s1, op, dd, false, 0, cursor + k);
             } else if (op.type == MTR_OP_SETCELL) {
-                s0.sum_s += (unsigned long long)(s0.nseg + s1.nseg);  // both vectors are resolved
+                acc_s += (unsigned long long)(s0.nseg + s1.nseg);  // both vectors are resolved
                 View v;
                 v.ref = op.ref_seq;
                 v.client = enc_client(int(int16_t(op.client)));
@@ -4216,22 +4243,27 @@ struct Eng {
                             put_record(L0, s0, cursor + k, rh, ch, MTR_DELTA_CELL);
                     }
                 }
-                if (s0.status != MTR_OK) s0.fail_op = cursor + k;
-                if (s1.status != MTR_OK) s1.fail_op = cursor + k;
+                if (s0.status != MTR_OK) set_fail(L0, cursor + k);
+                if (s1.status != MTR_OK) set_fail(L1, cursor + k);
                 ok = s0.status == MTR_OK && s1.status == MTR_OK;
             } else if (op.flags & MTR_F_COLS) {
+                const int n0 = s1.nseg;
                 ok = apply_op(L1, P, s1, op, dd, false, 0, cursor + k);
+                if (ok && counts_s(op)) acc_s += (unsigned long long)n0;
             } else {
+                const int n0 = s0.nseg;
                 ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k);
+                if (ok && counts_s(op)) acc_s += (unsigned long long)n0;
             }
             if (!ok) break;
-            s0.ops_done = k + 1;
+            done = k + 1;
         }
-        s0.sum_s += s1.sum_s;  // the matrix's counters are kept with its rows document
-        s1.sum_s = 0;
-        store_doc(L0, P, s0, d);
-        s1.ops_done = 0;  // the cols vector's op cursor stays at 0 (it has no op list of its own)
-        store_doc(L1, P, s1, d1);
+        if (lane_id() == 0) {  // the matrix's counters are kept with its rows document
+            L0.sc->sum_s += acc_s;
+            L0.sc->sum_l += acc_l;
+        }
+        store_doc(L0, P, s0, d, done);
+        store_doc(L1, P, s1, d1, 0);  // the cols vector's op cursor stays at 0 (it has no op list of its own)
     }
 };
 
