@@ -22,6 +22,7 @@ OP_ROLLBACK = 18
 OP_REGENERATE = 19
 OP_REF_CREATE = 20
 OP_REF_REMOVE = 21
+OP_LOCAL_SETCELL = 22
 REF_SLIDE = 1
 REF_LOCALVIEW = 2
 # ReferenceType (ops.ts:9-36)

@@ -556,7 +556,13 @@ class MatrixLog(DocLog):
     whose segment specs are ``[length, start]`` (PermutationSegment.fromJSONObject,
     permutationvector.ts:45-48; the remote ``start`` is discarded by ``reset()`` on INSERT); a set-cell
     message becomes one MTR_OP_SETCELL record.  Both vectors share this log's client table (short ids
-    are only compared for equality and mapped back to long ids in summaries)."""
+    are only compared for equality and mapped back to long ids in summaries).
+
+    The client's own edits (a live SharedMatrix, matrix.ts:202-418): row / col inserts and removes are local
+    merge-tree ops on that vector, pending until its own message comes back (an MTR_OP_ACK); a cell write is an
+    MTR_OP_LOCAL_SETCELL record (CellMatrixLog keeps the value and the pending write)."""
+
+    local_seq: int = 0  # the vectors' collabWindow.localSeq, kept equal by submitVectorMessage / nextLocalSeq
 
     def start_collab(self, long_id: str, min_seq: int = 0, current_seq: int = 0) -> None:
         """startOrUpdateCollaboration on both vectors (SharedMatrix.onConnect, matrix.ts:523-532)."""
@@ -567,8 +573,6 @@ class MatrixLog(DocLog):
         cid = "null" if cid is None else str(cid)
         if msg.get("type") != "op":
             return  # SharedMatrix has no MSN handler: only its vectors' own messages move their windows
-        if cid == self.observer_id:
-            raise Unsupported("message authored by the observer (local ack path)")
         short = self.short_id(cid)
         seq = int(msg["sequenceNumber"])
         ref = int(msg["referenceSequenceNumber"])
@@ -577,9 +581,13 @@ class MatrixLog(DocLog):
         if isinstance(contents, str):
             contents = parse(contents)
         target = contents.get("target")
+        own = cid == self.observer_id
         if target is None:  # MatrixOp.set (matrix/src/ops.ts:8-12)
             if contents.get("type") != 2:
                 raise Unsupported("matrix message without a target")
+            if own:  # the ACK of a local write (matrix.ts:652-668): host state only
+                self._own_set_ack()
+                return
             self.ops.append((abi.OP_SETCELL, 0, short, seq, ref, msn, int(contents["row"]), int(contents["col"]), 0, 0))
             return
         if target not in ("rows", "cols"):
@@ -594,6 +602,11 @@ class MatrixLog(DocLog):
             t = op.get("type")
             if "relativePos1" in op or "relativePos2" in op:
                 raise Unsupported("relative positions")
+            if own:  # the vector's applyMsg(msg, local): ackPendingSegment per member (client.ts:866-869)
+                if t not in (0, 1):
+                    raise Unsupported(f"ack of vector op type {t}")
+                self.ops.append((abi.OP_ACK, last, short, seq, ref, msn, 0, 0, 0, t))
+                continue
             if t == 0:
                 seg = op.get("seg")
                 if seg is None:
@@ -668,6 +681,29 @@ class MatrixLog(DocLog):
                     self._perm_seg(spec, abi.OP_INSERT, abi.F_APPEND | tf)
         self.observer_id = long_id
         self.collaborating = True
+
+    def _own_set_ack(self) -> None:
+        """A SharedMatrix observer has no pending cell writes (CellMatrixLog keeps them)."""
+        raise Unsupported("ack of a cell write without the cell store")
+
+    # -- the client's own edits (SharedMatrix.insertRows / removeRows / insertCols / removeCols, matrix.ts:363-418)
+    def local_vector_op(self, target: str, op: dict) -> None:
+        """A local insert ({type 0, pos1, seg: [count, start]}) or remove ({type 1, pos1, pos2}) on the rows or
+        cols PermutationVector (PermutationVector.insert / remove -> Client.insertSegmentLocal / removeRangeLocal,
+        permutationvector.ts:174-195), then submitVectorMessage's localSeq sync (matrix.ts:321-345)."""
+        tf = abi.F_COLS if target == "cols" else 0
+        t = op.get("type")
+        if t == 0:
+            seg = op.get("seg")
+            if not (isinstance(seg, list) and len(seg) == 2):
+                raise Unsupported("PermutationSegment spec")
+            self.ops.append((abi.OP_LOCAL_INSERT, tf, 0, self._local_seq(), 0, 0, int(op["pos1"]), -1, 0, int(seg[0])))
+        elif t == 1:
+            self.ops.append((abi.OP_LOCAL_REMOVE, tf, 0, self._local_seq(), 0, 0, int(op["pos1"]), int(op["pos2"]), 0, 0))
+        else:
+            raise Unsupported(f"local vector op type {t}")
+        if self.collaborating:
+            self.local_seq += 1
 
     def cols_log(self) -> DocLog:
         """The cols vector's engine document: no ops of its own, the same client table."""

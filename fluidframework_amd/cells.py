@@ -129,13 +129,43 @@ class SparseArray2D:
 class CellMatrixLog(MatrixLog):
     """A MatrixLog that also keeps the matrix's cells: every op it packs is flagged MTR_F_DELTA (the
     engine then reports cell writes and handle recycling for this matrix), and ``resolve`` replays
-    the records of the last batch into the cell store."""
+    the records of the last batch into the cell store.
+
+    Local cell writes (SharedMatrix.setCell, matrix.ts:202-310) write the cell at once and, while attached,
+    enter ``pending`` (the SparseArray2D of the latest unacked local write per cell, :97, 308): a remote write
+    to such a cell is skipped (it happened before, :681-690), and the ACK of the local write clears the entry
+    when it is still the latest (isLatestPendingWrite, :652-668, 738-759).  The cells blob holds both tries."""
 
     def __init__(self) -> None:
         super().__init__()
         self.cells = SparseArray2D()
-        self.pending = SparseArray2D()  # pending local writes: always empty for an observer
+        self.pending = SparseArray2D()  # SharedMatrix.pending: localSeq of the latest unacked write per cell
         self.values: dict[int, Any] = {}
+        self.local_sets: dict[int, int] = {}  # record index of a local write -> its localSeq (attached)
+        self.local_meta: list = []            # (row handle, col handle, localSeq) of unacked writes, in order
+        self.events: list = []                # (records before it, event): acks of local writes in this batch
+        self.ops_kind: dict[int, str] = {}    # record index of a local write before attaching (no pending entry)
+
+    def local_set_cell(self, row: int, col: int, value: Any) -> None:
+        """SharedMatrix.setCell(row, col, value) of this client (local positions)."""
+        k = len(self.ops)
+        self.ops.append((abi.OP_LOCAL_SETCELL, abi.F_DELTA, 0, 0, 0, 0, int(row), int(col), 0, 0))
+        self.values[k] = value
+        if self.collaborating:  # sendSetCellOp: localSeq = nextLocalSeq()
+            self.local_seq += 1
+            self.local_sets[k] = self.local_seq
+        else:  # detached: setCellCore writes the cell and sends nothing
+            self.ops_kind[k] = "local"
+
+    def local_vector_op(self, target: str, op: dict) -> None:
+        lo = len(self.ops)
+        super().local_vector_op(target, op)
+        for k in range(lo, len(self.ops)):  # (handle recycling on the vector is reported as records)
+            rec = self.ops[k]
+            self.ops[k] = (rec[0], rec[1] | abi.F_DELTA) + tuple(rec[2:])
+
+    def _own_set_ack(self) -> None:
+        self.events.append((len(self.ops), "ack"))
 
     def message(self, msg: dict, interner: Interner) -> None:
         lo = len(self.ops)
@@ -151,13 +181,30 @@ class CellMatrixLog(MatrixLog):
 
     def resolve(self, rows: np.ndarray, cols: np.ndarray) -> None:
         """Apply the last batch's records (engine.deltas(rows doc), engine.deltas(cols doc)) in op
-        order; within one op the rows records come first (a vector op touches one vector)."""
+        order; within one op the rows records come first (a vector op touches one vector); the acks of local
+        writes in this batch come between the records at their place in the message stream."""
         recs = [(int(r["op"]), 0, i, r) for i, r in enumerate(rows)] + [(int(r["op"]), 1, i, r) for i, r in enumerate(cols)]
+        recs += [(pos - 0.5, 2, i, None) for i, (pos, _) in enumerate(self.events)]
         recs.sort(key=lambda x: (x[0], x[1], x[2]))
         for op, which, _, r in recs:
+            if which == 2:  # isLatestPendingWrite (matrix.ts:738-759) for the oldest unacked local write
+                a, b, lseq = self.local_meta.pop(0)
+                p = self.pending.get_cell(a, b)
+                if p is not None and p < lseq:
+                    raise AssertionError("0x023")
+                if p == lseq:
+                    self.pending.set_cell(a, b, None)
+                continue
             kind, a, b = int(r["kind"]), int(r["pos"]), int(r["len"])
             if kind == DELTA_CELL:
-                self.cells.set_cell(a, b, self.values[op])
+                if op in self.local_sets:  # a local write: the cell now, the pending entry until its ACK
+                    self.cells.set_cell(a, b, self.values[op])
+                    self.pending.set_cell(a, b, self.local_sets[op])
+                    self.local_meta.append((a, b, self.local_sets[op]))
+                elif self.ops_kind.get(op) == "local":
+                    self.cells.set_cell(a, b, self.values[op])
+                elif self.pending.get_cell(a, b) is None:  # no pending local write to the cell (:681-690)
+                    self.cells.set_cell(a, b, self.values[op])
             elif kind == DELTA_RECYCLE:
                 if which == 0:
                     self.cells.clear_rows(a, b)
@@ -168,6 +215,9 @@ class CellMatrixLog(MatrixLog):
             else:
                 raise ValueError(f"unexpected matrix record kind {kind}")
         self.values = {}
+        self.local_sets = {}
+        self.events = []
+        self.ops_kind = {}
 
     def cells_blob(self) -> bytes:
         """The ``cells`` blob of SharedMatrix.summarizeCore (matrix.ts:458-462):

@@ -228,6 +228,9 @@ struct KParams {
 enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBLOCK, P_COMPACT, P_FINDUID,
        P_TEXTGC, P_LOADSTORE, P_TEXTCOPY, P_UPDSEQ, P_NZBLOCK, P_NCOMPACT, P_SCOUR1, P_PACK, P_NLQ, P_PMATCH,
        P_TAPPEND, P_HEAP, P_OVERFLOW, P_NPACK, P_NMERGE, P_NPMATCH, P_NNLQ, P_SPLIT1, P_INS1, P_FETCH, P_X1, P_X2,
+       // two-level view scan (HBM-resident documents): chunk-summary rounds, dirty-chunk full scans, the scan
+       // array of the op's region, summary upkeep; counts: chunks visited, listed chunks, dirty unlisted chunks
+       P_PFSUM, P_PFDIRTY, P_MAT, P_CSUM, P_NCH, P_NLISTED, P_NDIRTY,
        P_COUNT };
 
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
@@ -634,6 +637,7 @@ struct Eng {
     static MTR_DI A<int> cs_pre(const D& L) { return L.E + L.cap; }  // inclusive chunk prefix of a view
     // recompute the summaries of the chunks covering slots [lo, hi)
     static MTR_DI void csum_update(D& L, const St& s, int lo, int hi) {
+        PROF(P_CSUM);
         if constexpr (G) {
             if (!s.chunked) return;
             hi = min(hi, s.nseg);
@@ -702,6 +706,14 @@ struct Eng {
                 listed[h] = dirty[h] && nl[h] <= kChunkList;
                 any = any || listed[h];
             }
+#ifdef MTR_PROF
+            if (lane_id() == 0) {
+                L.sc->prof[P_NCH] += (unsigned long long)min(64 * RR, nch - cb);
+                int nlist = 0;
+                for (int h = 0; h < RR; h++) nlist += __popcll(__ballot(listed[h]));
+                L.sc->prof[P_NLISTED] += (unsigned long long)nlist;
+            }
+#endif
             if (__ballot(any)) {
                 int sl[RR][kChunkList];
 #pragma unroll
@@ -729,6 +741,10 @@ struct Eng {
             for (int h = 0; h < RR; h++) {
                 const int c0 = cb + 64 * h;
                 uint64_t dm = __ballot(dirty[h] && !listed[h]);
+#ifdef MTR_PROF
+                if (lane_id() == 0) L.sc->prof[P_NDIRTY] += (unsigned long long)__popcll(dm);
+                ProfScope _prof_dirty(L.sc, P_PFDIRTY);
+#endif
                 while (dm) {  // more than kChunkList leaves in the window: the chunk's leaves, GK chunks at a time
                     int lq[GK];
                     Hot hq[GK];
@@ -758,6 +774,7 @@ struct Eng {
     }
     // the scan array E of chunks [c0, c1] from the chunk prefix
     static MTR_DI void materialize(D& L, const St& s, const View& v, int newlen, int c0, int c1) {
+        PROF(P_MAT);
         const int S = s.nseg;
         const A<int> cp = cs_pre(L);
         for (int c = c0; c <= c1; c++) {
@@ -4093,6 +4110,26 @@ struct Eng {
     }
 
     // ------------------------------------------------------------ SharedMatrix
+    // one op of vector La (its partner Lo): the merge-tree op; a local row / col op then brings the partner's
+    // localSeq along (submitVectorMessage, matrix.ts:321-345; assert 0x01c: this vector's is never behind)
+    static MTR_DI bool vector_op(D& La, D& Lo, const KParams& P, St& sa, const mtr_op& op, const mtr_doc_desc& dd,
+                                 int gidx, unsigned long long& acc_s) {
+        const int n0 = sa.nseg;
+        bool ok = apply_op(La, P, sa, op, dd, false, 0, gidx);
+        if (ok && counts_s(op)) acc_s += (unsigned long long)n0;
+        if (ok && sa.collab && op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE) {
+            const int la = uni(La.ghdr()->lseq), lo = uni(Lo.ghdr()->lseq);
+            if (la < lo) {
+                sa.status = MTR_ERR_ASSERT | 0x01c;
+                set_fail(La, gidx);
+                ok = false;
+            } else if (lane_id() == 0) {
+                Lo.ghdr()->lseq = la;
+            }
+            wsync();
+        }
+        return ok;
+    }
     // PermutationVector.adjustPosition (permutationvector.ts:232-247): getContainingSegment at the
     // op's (refSeq, clientId) view (mergeTree.ts:795-813), undefined for a removed segment, else
     // its local-view position (getPosition, mergeTree.ts:768-785) plus the offset.  -1 = undefined.
@@ -4246,14 +4283,25 @@ struct Eng {
                 if (s0.status != MTR_OK) set_fail(L0, cursor + k);
                 if (s1.status != MTR_OK) set_fail(L1, cursor + k);
                 ok = s0.status == MTR_OK && s1.status == MTR_OK;
+            } else if (op.type == MTR_OP_LOCAL_SETCELL) {  // setCellCore -> sendSetCellOp (matrix.ts:254-310)
+                acc_s += (unsigned long long)(s0.nseg + s1.nseg);
+                const int rh = allocated_handle(L0, P, s0, op.pos1, false);
+                const int ch = s0.status == MTR_OK ? allocated_handle(L1, P, s1, op.pos2, false) : -1;
+                if (s0.status == MTR_OK && s1.status == MTR_OK) {
+                    if (s0.collab && lane_id() == 0) {  // nextLocalSeq (matrix.ts:484-492): both windows advance
+                        L0.ghdr()->lseq = L0.ghdr()->lseq + 1;
+                        L1.ghdr()->lseq = L1.ghdr()->lseq + 1;
+                    }
+                    wsync();
+                    if (DL && (op.flags & MTR_F_DELTA)) put_record(L0, s0, cursor + k, rh, ch, MTR_DELTA_CELL);
+                }
+                if (s0.status != MTR_OK) set_fail(L0, cursor + k);
+                if (s1.status != MTR_OK) set_fail(L1, cursor + k);
+                ok = s0.status == MTR_OK && s1.status == MTR_OK;
             } else if (op.flags & MTR_F_COLS) {
-                const int n0 = s1.nseg;
-                ok = apply_op(L1, P, s1, op, dd, false, 0, cursor + k);
-                if (ok && counts_s(op)) acc_s += (unsigned long long)n0;
+                ok = vector_op(L1, L0, P, s1, op, dd, cursor + k, acc_s);
             } else {
-                const int n0 = s0.nseg;
-                ok = apply_op(L0, P, s0, op, dd, false, 0, cursor + k);
-                if (ok && counts_s(op)) acc_s += (unsigned long long)n0;
+                ok = vector_op(L0, L1, P, s0, op, dd, cursor + k, acc_s);
             }
             if (!ok) break;
             done = k + 1;

@@ -181,6 +181,7 @@ __global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
         pend = pend || op.type == MTR_OP_ACK || op.type == MTR_OP_ROLLBACK || op.type == MTR_OP_REGENERATE ||
                (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE && op.seq == -1);
         ext = ext || op.type == MTR_OP_RELPOS || op.type == MTR_OP_HANDLES || (op.flags & MTR_F_REL) ||
+              op.type == MTR_OP_LOCAL_SETCELL ||
               (op.type == MTR_OP_ANNOTATE && op.payload2 != 0) ||
               ((op.flags & MTR_F_MARKER) && op.payload2 != 0 &&
                (op.type == MTR_OP_INSERT || op.type == MTR_OP_LOCAL_INSERT || op.type == MTR_OP_LOAD));
@@ -467,7 +468,7 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
                 if (!(op.flags & MTR_F_DELTA)) continue;
                 flagged = true;
                 if (kind == 1) {
-                    if (op.type == MTR_OP_SETCELL) need[d] += 1;
+                    if (op.type == MTR_OP_SETCELL || op.type == MTR_OP_LOCAL_SETCELL) need[d] += 1;
                 } else if (op.type == MTR_OP_INSERT) {
                     need[d] += 1;
                 } else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) {
@@ -601,8 +602,8 @@ static int run_impl(mtr_engine* e, int gen) {
     P.gen = gen;
 #ifdef MTR_PROF
     if (!e->prof.p) {
-        if (e->prof.ensure(32)) return -1;
-        HIPCHK(hipMemset(e->prof.p, 0, 32 * sizeof(unsigned long long)));
+        if (e->prof.ensure(64)) return -1;
+        HIPCHK(hipMemset(e->prof.p, 0, 64 * sizeof(unsigned long long)));
     }
     P.prof = e->prof.p;
 #endif
@@ -1468,18 +1469,18 @@ int mtr_last_timing(mtr_engine* e, double* out, int32_t n) {
 
 int mtr_profile(mtr_engine* e, uint64_t* out, int32_t n, int32_t reset) {
     if (!e || !out) return MTR_ERR_BAD_OP;
-    unsigned long long v[32] = {0};
+    unsigned long long v[64] = {0};
 #ifdef MTR_PROF
     if (hipStreamSynchronize(e->stream) != hipSuccess) return MTR_ERR_ASSERT;
     if (!e->prof.p) {
-        if (e->prof.ensure(32) || hipMemset(e->prof.p, 0, sizeof(v)) != hipSuccess) return MTR_ERR_ASSERT;
+        if (e->prof.ensure(64) || hipMemset(e->prof.p, 0, sizeof(v)) != hipSuccess) return MTR_ERR_ASSERT;
     }
     if (hipMemcpy(v, e->prof.p, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return MTR_ERR_ASSERT;
     if (reset && hipMemset(e->prof.p, 0, sizeof(v)) != hipSuccess) return MTR_ERR_ASSERT;
 #else
     (void)reset;
 #endif
-    for (int i = 0; i < n && i < 32; i++) out[i] = v[i];
+    for (int i = 0; i < n && i < 64; i++) out[i] = v[i];
 #ifdef MTR_PROF
     return MTR_OK;
 #else

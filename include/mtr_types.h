@@ -79,6 +79,14 @@ enum {
                                    document's references are numbered by creation, from 0. */
     MTR_OP_REF_REMOVE = 21,     /* Client.removeLocalReferencePosition (client.ts:394-396 -> mergeTree.ts:2190-2207) of
                                    reference payload */
+    MTR_OP_LOCAL_SETCELL = 22,  /* SharedMatrix.setCell of the local client (matrix.ts:202-310, setCellCore -> sendSetCellOp):
+                                   pos1 = row, pos2 = col at the local view; PermutationVector.getAllocatedHandle on
+                                   the rows vector, then the cols vector (permutationvector.ts:209-230: a split to the
+                                   one position and a new handle when it has none); while collaborating nextLocalSeq
+                                   advances both vectors' localSeq (matrix.ts:484-492).  With MTR_F_DELTA one
+                                   MTR_DELTA_CELL record {op, row handle, col handle}.  A local row / col op (a local
+                                   insert / remove record, MTR_F_COLS for cols) sets the other vector's localSeq to its
+                                   own (submitVectorMessage, matrix.ts:321-345). */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for

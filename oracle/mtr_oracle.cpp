@@ -2067,7 +2067,30 @@ struct oracle_doc {
                 tree.deltas.push_back({tree.curOpIndex, rh, ch, MTR_DELTA_CELL});
             return tree.status != MTR_OK ? tree.status : cols.status;
         }
-        return (op.flags & MTR_F_COLS) ? cols.apply(op, dd) : tree.apply(op, dd);
+        if (op.type == MTR_OP_LOCAL_SETCELL) {  // setCellCore -> sendSetCellOp (matrix.ts:254-310), this client
+            if (!tree.pendingLoad.empty()) tree.reloadFromSegments();
+            if (!cols.pendingLoad.empty()) cols.reloadFromSegments();
+            if (op.pos1 < 0 || op.pos1 >= tree.blockLocalLength(tree.root) || op.pos2 < 0 ||
+                op.pos2 >= cols.blockLocalLength(cols.root))
+                return MTR_ERR_ASSERT | 0x01a;  // "Trying to set out-of-bounds cell!"
+            const int rh = tree.getAllocatedHandle(op.pos1);
+            const int ch = cols.getAllocatedHandle(op.pos2);
+            if (tree.collaborating) {  // nextLocalSeq (matrix.ts:484-492): both windows' localSeq advance
+                cols.localSeqCounter++;
+                tree.localSeqCounter++;
+            }
+            if (op.flags & MTR_F_DELTA) tree.deltas.push_back({tree.curOpIndex, rh, ch, MTR_DELTA_CELL});
+            return tree.status != MTR_OK ? tree.status : cols.status;
+        }
+        Tree& t = (op.flags & MTR_F_COLS) ? cols : tree;
+        const int st = t.apply(op, dd);
+        // submitVectorMessage (matrix.ts:321-345): a local row / col op brings the other vector's localSeq along
+        if (st == MTR_OK && t.collaborating && op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE) {
+            Tree& o = (op.flags & MTR_F_COLS) ? tree : cols;
+            if (t.localSeqCounter < o.localSeqCounter) return MTR_ERR_ASSERT | 0x01c;
+            o.localSeqCounter = t.localSeqCounter;
+        }
+        return st;
     }
 };
 
@@ -2228,6 +2251,15 @@ int32_t oracle_doc_ref_info(oracle_doc* d, uint32_t id, int32_t* out) {
     out[2] = r.refType;
     out[3] = (s && s->localRefs && t.refsHas(s->localRefs, int(id))) ? 1 : 0;
     return out[0];
+}
+
+int32_t oracle_doc_handle_at(oracle_doc* d, int32_t pos) {
+    Tree& t = d->view();
+    if (!t.pendingLoad.empty()) t.reloadFromSegments();
+    int off = 0;
+    Seg* s = t.containingSegment(pos, t.currentSeq, t.localClientId, off);
+    if (!s) return -1;
+    return s->start >= 1 ? s->start + off : MTR_HANDLE_UNALLOCATED;
 }
 
 int32_t oracle_doc_marker_position(oracle_doc* d, uint32_t ordinal, int32_t ref_seq, int32_t client) {

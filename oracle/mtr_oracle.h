@@ -113,6 +113,10 @@ int64_t oracle_doc_ref_positions(oracle_doc* d, int32_t* out, int64_t cap);
  * held by its segment's LocalReferenceCollection] */
 int32_t oracle_doc_ref_info(oracle_doc* d, uint32_t id, int32_t* out);
 
+/* PermutationVector.getMaybeHandle at local position pos of the selected vector (permutationvector.ts:196-207):
+ * the handle, MTR_HANDLE_UNALLOCATED, or -1 when no segment holds pos */
+int32_t oracle_doc_handle_at(oracle_doc* d, int32_t pos);
+
 /* Length of the doc in the (ref_seq, client) view (MergeTree.getLength, mergeTree.ts:757) */
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client);
 /* MergeTree.getPosition (mergeTree.ts:768-785) of the marker mapped to a host marker ordinal, -1 if none */

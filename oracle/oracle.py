@@ -73,6 +73,8 @@ def lib():
         L.oracle_doc_length.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         L.oracle_doc_ref_positions.restype = C.c_int64
         L.oracle_doc_ref_positions.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_doc_handle_at.restype = C.c_int32
+        L.oracle_doc_handle_at.argtypes = [C.c_void_p, C.c_int32]
         L.oracle_doc_ref_info.restype = C.c_int32
         L.oracle_doc_ref_info.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         _LIB = L
@@ -215,6 +217,10 @@ class OracleDoc:
 
     def length(self, ref_seq, client):
         return lib().oracle_doc_length(self.h, ref_seq, client)
+
+    def handle_at(self, pos: int) -> int:
+        """The handle at local position pos of the selected vector (HANDLE_UNALLOCATED, -1 = no segment)."""
+        return lib().oracle_doc_handle_at(self.h, pos)
 
     def ref_positions(self) -> list:
         """localReferencePositionToPosition of every local reference, by id (-1 = detached)."""
