@@ -216,8 +216,8 @@ def test_matrix_local_farm_engine_matches_oracle():
         grids = farm(seed, s)
         assert grids[0] == grids[1] == grids[2], f"seed {seed}"
         assert s.checks > 0
-        s.eng.summarize()
         last = s.flush()
+        s.eng.summarize()
         for m, c in enumerate(s.clients):
             for w in (0, 1):
                 assert s.eng.summary(2 * m + w) == c.doc.select(w).summarize(last, 2 * m), (seed, c.name, w)
