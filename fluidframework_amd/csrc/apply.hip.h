@@ -86,7 +86,16 @@ constexpr uint32_t PEND_KEY = 0x40000000u;
 // event, the length of its leaves whose visibility no view in the collaboration window can change, and
 // the slots of the other leaves (up to kChunkList; more = the chunk is scanned whole)
 constexpr int kChunkList = 8;
-constexpr int kCsumRows = 4 + kChunkList;
+constexpr int kCsumRows = 4 + kChunkList;  // ints per chunk record
+// superchunks (64 chunks) a view scan loads the chunk records of together
+constexpr int kDirtyBatch = 4;
+__host__ __device__ constexpr int sup_rows(int segcap) { return segcap / 4096 + 2; }
+// ints of one document's chunk summaries: the chunk records, then its superchunks' lengths and newest events
+// (a multiple of 4: every document's records stay 16-byte aligned)
+__host__ __device__ constexpr size_t csum_ints(int segcap) {
+    return (size_t(kCsumRows) * size_t(segcap / 64 + 1) + 2 * size_t(sup_rows(segcap)) + 3) & ~size_t(3);
+}
+typedef int v4i __attribute__((ext_vector_type(4), may_alias));
 enum { PK_INSERT = 1, PK_REMOVE = 2, PK_ANNOTATE = 3 };
 // a pending local "rewrite" annotate's cells and ring entry carry PK_REWRITE beside PK_ANNOTATE: while one is
 // pending, remote changes to the segment are blocked (pendingRewriteCount, segmentPropertiesManager.ts:72-80)
@@ -231,6 +240,11 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
        // two-level view scan (HBM-resident documents): chunk-summary rounds, dirty-chunk full scans, the scan
        // array of the op's region, summary upkeep; counts: chunks visited, listed chunks, dirty unlisted chunks
        P_PFSUM, P_PFDIRTY, P_MAT, P_CSUM, P_NCH, P_NLISTED, P_NDIRTY,
+       P_SPREAD, P_CHUNKOF, P_NSPREAD,
+       // snapshot-load records + the tree build, apply_op's prologue (to the dispatch), whole view scans,
+       // the tail (deltas, zamboni, updateSeqNumbers)
+       P_LOAD, P_PRE, P_VIEW, P_POST,
+       P_NSUP, P_NDCH,  // counts: superchunks with events after refSeq, their chunks with such events
        P_COUNT };
 
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
@@ -247,6 +261,7 @@ struct Sc {
     int relmask;  // which of rel[] are pending: bit 0 pos1, bit 1 pos2
     int nrefs, refcap;  // local references of the document (DocHdr.nrefs) and the table's capacity
     int fail_op, max_heap, heap_need;  // DocHdr's, for this launch
+    int sepoch;  // view scans of this launch (HBM-resident documents: Eng::prefix2's fill epochs)
     unsigned long long sum_s, sum_l;   // B_op counters: leaves before each op, inserted units
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];
@@ -282,6 +297,7 @@ struct Doc {
     A<uint32_t> meta, text, props, uid, huid;
     lptr<Sc> sc;
     lptr<mtr_synth_state> gst;
+    lptr<int> sx;  // HBM-resident documents: superchunk rows and the dirty-chunk list (Eng::prefix2)
     int dcap;  // capacity of this document's delta records in this batch
     int cap, lhcap, rtmask;
     // cold pointers (read from LDS at the use site, made wave-uniform)
@@ -377,7 +393,11 @@ constexpr size_t kScBytes = kScOnly + ((sizeof(mtr_synth_state) + 15) & ~size_t(
 __host__ __device__ inline size_t lds_bytes(int cap, int lhcap, bool gen = true) {
     return size_t(cap) * 4 * 8 + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
 }
-__host__ __device__ inline size_t lds_bytes_global_mode() { return kScBytes; }
+// (HBM-resident documents: Sc, the generator state, five superchunk rows, prefix2's dirty-chunk list
+// and a chunk-prefix row per 64 slots)
+__host__ __device__ inline size_t lds_bytes_global_mode(int segcap) {
+    return kScBytes + ((size_t(4) * (5 * sup_rows(segcap) + 4 * 64 * kDirtyBatch + segcap / 64 + 1) + 15) & ~size_t(15));
+}
 
 // Phase timers (builds with -DMTR_PROF only): lane-0 clock cycles per phase, summed over
 // documents into g_prof (mtr_profile()).
@@ -393,11 +413,16 @@ struct ProfScope {
     }
 };
 #define PROF(id) ProfScope _prof_scope(L.sc, id)
+#define PROF_T0(v) const long long v = clock64()
+#define PROF_ADD(id, v) \
+    if (threadIdx.x == 0) L.sc->prof[id] += (unsigned long long)(clock64() - (v))
 #define PROF_COUNT(id) \
     if (threadIdx.x == 0) L.sc->prof[id]++
 #else
 #define PROF(id)
 #define PROF_COUNT(id)
+#define PROF_T0(v)
+#define PROF_ADD(id, v)
 #endif
 
 // G: leaves in HBM (documents larger than LDS); PM: PermutationVector documents (SharedMatrix
@@ -629,21 +654,37 @@ struct Eng {
     // refSeq -- each leaf was inserted by then, and removed by then or not at all -- so its view length
     // is its local length; only the other chunks are scanned leaf by leaf.  This restates what
     // PartialSequenceLengths does per block (partialLengths.ts:698-735) for chunks of the flat leaf order.
-    static MTR_DI gptr<int> cs_len(const D& L) { return L.gcsum(); }
-    static MTR_DI gptr<int> cs_ev(const D& L) { return L.gcsum() + (L.cap / 64 + 1); }
-    static MTR_DI gptr<int> cs_base(const D& L) { return L.gcsum() + 2 * (L.cap / 64 + 1); }
-    static MTR_DI gptr<int> cs_n(const D& L) { return L.gcsum() + 3 * (L.cap / 64 + 1); }
-    static MTR_DI gptr<int> cs_slot(const D& L, int q) { return L.gcsum() + (4 + q) * (L.cap / 64 + 1); }
-    static MTR_DI A<int> cs_pre(const D& L) { return L.E + L.cap; }  // inclusive chunk prefix of a view
-    // recompute the summaries of the chunks covering slots [lo, hi)
+    // 64 chunks form a superchunk with the same two figures (the chunks' sum and max), so a view reads
+    // one pair per 4096 slots plus the chunk records of the superchunks with events after its refSeq.
+    // A chunk's record: kCsumRows ints (16-byte aligned) -- local length, newest event, the length of its
+    // leaves whose visibility no view in the collaboration window can change, the count of the other
+    // leaves, then their slots (up to kChunkList; more = the chunk is scanned whole).
+    static MTR_DI int nsup(const D& L) { return sup_rows(L.cap); }
+    static MTR_DI gptr<int> cs_rec(const D& L, int c) { return L.gcsum() + c * kCsumRows; }
+    static MTR_DI gptr<int> cs_sl(const D& L) { return L.gcsum() + kCsumRows * (L.cap / 64 + 1); }
+    static MTR_DI gptr<int> cs_se(const D& L) { return cs_sl(L) + nsup(L); }
+    // LDS rows (Doc::sx, lds_bytes_global_mode): a view's inclusive superchunk prefix, the view epoch that
+    // filled a superchunk's chunk-prefix row, "superchunk figures stale" marks, the superchunks' local
+    // lengths and newest events (the launch's copy of the HBM rows), prefix2's dirty-chunk list, and a
+    // view's chunk prefix (inclusive within each superchunk).  (Rows a wave writes and reads back stay in
+    // LDS: a global load issued right after this wave's own store to the word can return the old value.)
+    static MTR_DI lptr<int> sup_pre(const D& L) { return L.sx; }
+    static MTR_DI lptr<int> sup_fill(const D& L) { return L.sx + nsup(L); }
+    static MTR_DI lptr<int> sup_mark(const D& L) { return L.sx + 2 * nsup(L); }
+    static MTR_DI lptr<int> sup_len(const D& L) { return L.sx + 3 * nsup(L); }
+    static MTR_DI lptr<int> sup_ev(const D& L) { return L.sx + 4 * nsup(L); }
+    static MTR_DI lptr<int> dlist(const D& L) { return L.sx + 5 * nsup(L); }
+    static MTR_DI lptr<int> cs_pre(const D& L) { return L.sx + 5 * nsup(L) + 4 * 64 * kDirtyBatch; }
+    static MTR_DI v4i ld4(gptr<const int> p) { return *(gptr<const v4i>)p; }
+    // recompute the records of the chunks covering slots [lo, hi); their superchunks go stale
     static MTR_DI void csum_update(D& L, const St& s, int lo, int hi) {
         PROF(P_CSUM);
         if constexpr (G) {
             if (!s.chunked) return;
             hi = min(hi, s.nseg);
             if (lo >= hi) return;
-            const gptr<int> cl = cs_len(L), ce = cs_ev(L), cb = cs_base(L), cn = cs_n(L);
-            for (int c = max(lo, 0) >> 6; c <= (hi - 1) >> 6; c++) {
+            const int c0 = max(lo, 0) >> 6, c1 = (hi - 1) >> 6;
+            for (int c = c0; c <= c1; c++) {
                 const int i = c * 64 + lane_id();
                 const bool in = i < s.nseg;
                 const int ic = min(i, s.nseg - 1);
@@ -662,163 +703,270 @@ struct Eng {
                 fx = rdlane(wave_incl_scan(fx), 63);
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
-                if (win && nw <= kChunkList) cs_slot(L, __popcll(wm & lanes_below()))[c] = i;
-                if (lane_id() == 0) {
-                    cl[c] = x;
-                    ce[c] = ev;
-                    cb[c] = fx;
-                    cn[c] = min(nw, kChunkList + 1);
+                const gptr<int> r = cs_rec(L, c);
+                if (win && nw <= kChunkList) r[4 + __popcll(wm & lanes_below())] = i;
+                if (lane_id() == 0) *(gptr<v4i>)r = v4i{x, ev, fx, min(nw, kChunkList + 1)};
+            }
+            for (int q = (c0 >> 6) + lane_id(); q <= (c1 >> 6); q += 64) sup_mark(L)[q] = 1;
+            wsync();
+        }
+    }
+    // the figures of the superchunks marked stale (before a view reads them, and before the launch ends)
+    static MTR_DI void sup_refresh(D& L, const St& s) {
+        if constexpr (G) {
+            if (!s.chunked || s.nseg <= 0) return;
+            const int nch = (s.nseg + 63) >> 6, ns = (nch + 63) >> 6, ln = lane_id();
+            const lptr<int> mk = sup_mark(L), sl = sup_len(L), se = sup_ev(L);
+            for (int b = 0; b < ns; b += 64) {
+                uint64_t m = __ballot(b + ln < ns && mk[min(b + ln, ns - 1)] != 0);
+                while (m) {  // kDirtyBatch superchunks' chunk records in flight together
+                    int q[kDirtyBatch];
+                    v4i r[kDirtyBatch];
+#pragma unroll
+                    for (int k = 0; k < kDirtyBatch; k++) {
+                        q[k] = m ? b + first_lane(m) : -1;
+                        m &= m - 1;
+                        r[k] = ld4(cs_rec(L, min(max(q[k], 0) * 64 + ln, nch - 1)));
+                    }
+#pragma unroll
+                    for (int k = 0; k < kDirtyBatch; k++) {
+                        if (q[k] < 0) break;
+                        const bool ok = q[k] * 64 + ln < nch;
+                        const int sum = rdlane(wave_incl_scan(ok ? r[k].x : 0), 63);
+                        int ev = ok ? r[k].y : 0;
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
+                        if (ln == 0) {
+                            sl[q[k]] = sum;
+                            se[q[k]] = ev;
+                            mk[q[k]] = 0;
+                        }
+                    }
                 }
             }
             wsync();
         }
     }
-    // the view's chunk lengths, their inclusive prefix in cs_pre; returns the view's total length
+    // the superchunk rows between launches: read at launch start, refreshed and written back at its end
+    static MTR_DI void sup_load(D& L, const St& s) {
+        if constexpr (G) {
+            if (!s.chunked || s.nseg <= 0 || !L.gcsum()) return;  // (query kernels carry no summaries)
+            const int ns = (((s.nseg + 63) >> 6) + 63) >> 6;
+            const gptr<int> gl = cs_sl(L), ge = cs_se(L);
+            for (int q = lane_id(); q < ns; q += 64) {
+                sup_len(L)[q] = gl[q];
+                sup_ev(L)[q] = ge[q];
+            }
+            wsync();
+        }
+    }
+    static MTR_DI void sup_flush(D& L, const St& s) {
+        if constexpr (G) {
+            if (!s.chunked || s.nseg <= 0 || !L.gcsum()) return;
+            sup_refresh(L, s);
+            const int ns = (((s.nseg + 63) >> 6) + 63) >> 6;
+            const gptr<int> gl = cs_sl(L), ge = cs_se(L);
+            for (int q = lane_id(); q < ns; q += 64) {
+                gl[q] = sup_len(L)[q];
+                ge[q] = sup_ev(L)[q];
+            }
+            wsync();
+        }
+    }
+    // the view's superchunk lengths, their inclusive prefix in sup_pre (and the chunk-prefix rows of the
+    // superchunks it scanned chunk by chunk); returns the view's total length
     static MTR_DI int prefix2(D& L, const St& s, const View& v, int newlen) {
         PROF(P_PREFIX);
-        const int S = s.nseg, nch = (S + 63) >> 6;
-        const gptr<int> cl = cs_len(L), ce = cs_ev(L), cbs = cs_base(L), cn = cs_n(L);
-        const A<int> cp = cs_pre(L);
+        sup_refresh(L, s);
+        const int S = s.nseg, nch = (S + 63) >> 6, ns = (nch + 63) >> 6;
         const int ln = lane_id();
+        const int ep = uni(L.sc->sepoch) + 1;
+        if (ln == 0) L.sc->sepoch = ep;
+        const lptr<int> sl = sup_len(L), se = sup_ev(L), cp = cs_pre(L);
+        const lptr<int> spre = sup_pre(L), sfill = sup_fill(L), lst = dlist(L);
         int carry = 0;
-        // RR rounds of 64 chunks per iteration: their summary, list and leaf loads are issued together,
-        // so one wave keeps RR independent chains of loads in flight
-        constexpr int RR = 2;
-        for (int cb = 0; cb < nch; cb += 64 * RR) {
-            int cc[RR], len[RR], ev[RR], nl[RR], fx[RR];
-            bool in[RR], dirty[RR], listed[RR];
-#pragma unroll
-            for (int h = 0; h < RR; h++) {  // unconditional (clamped) loads
-                const int c = cb + 64 * h + ln;
-                in[h] = c < nch;
-                cc[h] = min(c, nch - 1);
-                len[h] = cl[cc[h]];
-                ev[h] = ce[cc[h]];
-                nl[h] = cn[cc[h]];
-                fx[h] = cbs[cc[h]];
-            }
-            bool any = false;
-#pragma unroll
-            for (int h = 0; h < RR; h++) {
-                if (!in[h]) len[h] = 0;
-                dirty[h] = in[h] && !v.local && ev[h] > v.ref;
-                // a chunk with events after refSeq: its fixed length plus its listed in-window leaves'
-                listed[h] = dirty[h] && nl[h] <= kChunkList;
-                any = any || listed[h];
-            }
+        for (int b = 0; b < ns; b += 64) {
+            const int q = b + ln, qc = min(q, ns - 1);
+            const int sl0 = sl[qc], se0 = se[qc];
+            int slen = q < ns ? sl0 : 0;
+            uint64_t dq = __ballot(q < ns && !v.local && se0 > v.ref);
 #ifdef MTR_PROF
-            if (lane_id() == 0) {
-                L.sc->prof[P_NCH] += (unsigned long long)min(64 * RR, nch - cb);
-                int nlist = 0;
-                for (int h = 0; h < RR; h++) nlist += __popcll(__ballot(listed[h]));
-                L.sc->prof[P_NLISTED] += (unsigned long long)nlist;
+            if (ln == 0) {
+                L.sc->prof[P_NCH] += (unsigned long long)min(64, ns - b);
+                L.sc->prof[P_NSUP] += (unsigned long long)__popcll(dq);
             }
 #endif
-            if (__ballot(any)) {
-                int sl[RR][kChunkList];
+            while (dq) {  // superchunks with events after refSeq: kDirtyBatch at a time
+                int sq[kDirtyBatch];
+                v4i r[kDirtyBatch];
 #pragma unroll
-                for (int h = 0; h < RR; h++)
+                for (int k = 0; k < kDirtyBatch; k++) {
+                    sq[k] = dq ? b + first_lane(dq) : -1;
+                    dq &= dq - 1;
+                    r[k] = ld4(cs_rec(L, min(max(sq[k], 0) * 64 + ln, nch - 1)));
+                }
+                // their chunks with events after refSeq go to the LDS list, one entry each
+                int vl[kDirtyBatch], ent[kDirtyBatch];
+                uint64_t dm[kDirtyBatch];
+                int n = 0;
 #pragma unroll
-                    for (int q = 0; q < kChunkList; q++) sl[h][q] = (listed[h] && q < nl[h]) ? cs_slot(L, q)[cc[h]] : 0;
-                Hot hq[RR][kChunkList];
+                for (int k = 0; k < kDirtyBatch; k++) {
+                    const int c = max(sq[k], 0) * 64 + ln;
+                    const bool cin = sq[k] >= 0 && c < nch;
+                    const bool dirty = cin && r[k].y > v.ref;
+                    vl[k] = cin ? r[k].x : 0;
+                    dm[k] = __ballot(dirty);
+                    ent[k] = n + __popcll(dm[k] & lanes_below());
+                    if (dirty) {
+                        lst[4 * ent[k]] = c;
+                        lst[4 * ent[k] + 1] = r[k].z;
+                        lst[4 * ent[k] + 2] = r[k].w;
+                    }
+                    n += __popcll(dm[k]);
+                }
+                wsync();
+#ifdef MTR_PROF
+                if (ln == 0) L.sc->prof[P_NDCH] += (unsigned long long)n;
+#endif
+                for (int e0 = 0; e0 < n; e0 += 64) {  // one lane per listed chunk
+                    const int e = e0 + ln, ec = min(e, n - 1);
+                    const int c = lst[4 * ec], fx = lst[4 * ec + 1], nl = lst[4 * ec + 2];
+                    const bool listed = e < n && nl <= kChunkList;
+                    const v4i s0 = ld4(cs_rec(L, c) + 4), s1 = ld4(cs_rec(L, c) + 8);
+                    const int slt[kChunkList] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                    Hot hq[kChunkList];
 #pragma unroll
-                for (int h = 0; h < RR; h++)
+                    for (int j = 0; j < kChunkList; j++)
+                        hq[j] = ld_hot(L, (listed && j < nl) ? min(max(slt[j], 0), S - 1) : 0);
+                    int sum = fx;
 #pragma unroll
-                    for (int q = 0; q < kChunkList; q++) hq[h][q] = ld_hot(L, min(sl[h][q], S - 1));
-#pragma unroll
-                for (int h = 0; h < RR; h++) {
-                    int sum = fx[h];
-#pragma unroll
-                    for (int q = 0; q < kChunkList; q++) {
-                        const bool on = listed[h] && q < nl[h];
-                        const int x0 = vis_hot(L, hq[h][q], sl[h][q], v, newlen, s.minseq, on);
+                    for (int j = 0; j < kChunkList; j++) {
+                        const bool on = listed && j < nl;
+                        const int x0 = vis_hot(L, hq[j], on ? slt[j] : 0, v, newlen, s.minseq, on);
                         sum += on ? max(x0, 0) : 0;
                     }
-                    if (listed[h]) len[h] = sum;
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < RR; h++) {
-                const int c0 = cb + 64 * h;
-                uint64_t dm = __ballot(dirty[h] && !listed[h]);
+                    if (listed) lst[4 * ec + 3] = sum;
+                    uint64_t um = __ballot(e < n && !listed);
 #ifdef MTR_PROF
-                if (lane_id() == 0) L.sc->prof[P_NDIRTY] += (unsigned long long)__popcll(dm);
-                ProfScope _prof_dirty(L.sc, P_PFDIRTY);
+                    if (ln == 0) L.sc->prof[P_NDIRTY] += (unsigned long long)__popcll(um);
+                    ProfScope _prof_dirty(L.sc, P_PFDIRTY);
 #endif
-                while (dm) {  // more than kChunkList leaves in the window: the chunk's leaves, GK chunks at a time
-                    int lq[GK];
-                    Hot hq[GK];
+                    while (um) {  // more than kChunkList leaves in the window: the chunk's leaves, GK chunks at a time
+                        int lq[GK];
+                        Hot hw[GK];
 #pragma unroll
-                    for (int q = 0; q < GK; q++) {
-                        lq[q] = dm ? first_lane(dm) : -1;
-                        dm &= dm - 1;
-                        const int i = (c0 + max(lq[q], 0)) * 64 + ln;
-                        hq[q] = ld_hot(L, min(i, S - 1));
-                    }
+                        for (int g = 0; g < GK; g++) {
+                            lq[g] = um ? first_lane(um) : -1;
+                            um &= um - 1;
+                            const int i = rdlane(c, max(lq[g], 0)) * 64 + ln;
+                            hw[g] = ld_hot(L, min(i, S - 1));
+                        }
 #pragma unroll
-                    for (int q = 0; q < GK; q++) {
-                        if (lq[q] < 0) break;
-                        const int i = (c0 + lq[q]) * 64 + ln;
-                        const int x0 = vis_hot(L, hq[q], i, v, newlen, s.minseq, i < S);
-                        const int sum = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
-                        if (ln == lq[q]) len[h] = sum;
+                        for (int g = 0; g < GK; g++) {
+                            if (lq[g] < 0) break;
+                            const int i = rdlane(c, lq[g]) * 64 + ln;
+                            const int x0 = vis_hot(L, hw[g], i, v, newlen, s.minseq, i < S);
+                            const int tot = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
+                            if (ln == lq[g]) lst[4 * ec + 3] = tot;
+                        }
                     }
                 }
-                const int inc = wave_incl_scan(len[h]);
-                if (in[h]) cp[c0 + ln] = carry + inc;
-                carry += rdlane(inc, 63);
+                wsync();
+#pragma unroll
+                for (int k = 0; k < kDirtyBatch; k++) {  // chunk prefix rows and the superchunks' view lengths
+                    if (sq[k] < 0) break;
+                    const int c = sq[k] * 64 + ln;
+                    if ((dm[k] >> ln) & 1) vl[k] = lst[4 * ent[k] + 3];
+                    const int inc = wave_incl_scan(vl[k]);
+                    if (c < nch) cp[c] = inc;
+                    const int tot = rdlane(inc, 63);
+                    if (ln == sq[k] - b) slen = tot;
+                    if (ln == 0) sfill[sq[k]] = ep;
+                }
+                wsync();
             }
+            const int inc = wave_incl_scan(slen);
+            if (q < ns) spre[q] = carry + inc;
+            carry += rdlane(inc, 63);
         }
         wsync();
         return carry;
     }
+    // lane l: the inclusive prefix of chunk 64 q + l within superchunk q in the current view (filled now
+    // when prefix2 did not scan it: each of its chunks shows its local length)
+    static MTR_DI int sup_row(D& L, const St& s, int q) {
+        const int nch = (s.nseg + 63) >> 6, c = q * 64 + lane_id(), cc = min(c, nch - 1);
+        const int ep = uni(L.sc->sepoch);
+        if (uni(sup_fill(L)[q]) == ep) return cs_pre(L)[cc];
+        const int x = cs_rec(L, cc)[0];
+        const int inc = wave_incl_scan(c < nch ? x : 0);
+        if (c < nch) cs_pre(L)[c] = inc;
+        if (lane_id() == 0) sup_fill(L)[q] = ep;
+        wsync();
+        return inc;
+    }
     // the scan array E of chunks [c0, c1] from the chunk prefix
     static MTR_DI void materialize(D& L, const St& s, const View& v, int newlen, int c0, int c1) {
         PROF(P_MAT);
-        const int S = s.nseg;
-        const A<int> cp = cs_pre(L);
-        for (int c = c0; c <= c1; c++) {
-            const int i = c * 64 + lane_id();
-            const int base = c > 0 ? uni(cp[c - 1]) : 0;
-            const Hot h = ld_hot(L, min(i, S - 1));
-            const int x0 = vis_hot(L, h, i, v, newlen, s.minseq, i < S);
-            const int x = i < S ? x0 : 0;
-            const int inc = wave_incl_scan(max(x, 0));
-            if (i < S) L.E[i] = (base + inc) | (x < 0 ? int(0x80000000u) : 0);
+        const int S = s.nseg, ln = lane_id();
+        const lptr<int> spre = sup_pre(L);
+        int qcur = -1, rel = 0;
+        for (int cb = c0; cb <= c1; cb += GK) {
+            Hot h[GK];
+#pragma unroll
+            for (int k = 0; k < GK; k++) h[k] = ld_hot(L, min(min(cb + k, c1) * 64 + ln, S - 1));
+#pragma unroll
+            for (int k = 0; k < GK; k++) {
+                const int c = cb + k;
+                if (c > c1) break;
+                const int q = c >> 6;
+                if (q != qcur && (c & 63)) {
+                    rel = sup_row(L, s, q);
+                    qcur = q;
+                }
+                const int base = (q > 0 ? uni(spre[q - 1]) : 0) + ((c & 63) ? rdlane(rel, (c & 63) - 1) : 0);
+                const int i = c * 64 + ln;
+                const int x0 = vis_hot(L, h[k], i, v, newlen, s.minseq, i < S);
+                const int x = i < S ? x0 : 0;
+                const int inc = wave_incl_scan(max(x, 0));
+                if (i < S) L.E[i] = (base + inc) | (x < 0 ? int(0x80000000u) : 0);
+            }
         }
         wsync();
     }
     // first chunk whose inclusive prefix reaches pos (the last chunk if none)
-    static MTR_DI int chunk_of(const D& L, int nch, int pos) {
-        const A<int> cp = cs_pre(L);
-        int lo = 0, hi = nch;
-        const int ln = lane_id();
-        while (hi - lo > 64) {
-            const int stride = (hi - lo + 64) >> 6;
-            const int idx = lo + (ln + 1) * stride - 1;
-            const uint64_t m = __ballot((idx >= hi) | (cp[min(idx, hi - 1)] >= pos));
-            const int k = first_lane(m);
-            const int nlo = lo + k * stride;
-            hi = min(hi, lo + (k + 1) * stride - 1);
-            lo = nlo;
+    static MTR_DI int chunk_of(D& L, const St& s, int nch, int pos) {
+        PROF(P_CHUNKOF);
+        const int ns = (nch + 63) >> 6, ln = lane_id();
+        const lptr<int> spre = sup_pre(L);
+        int q = -1;
+        for (int b = 0; b < ns; b += 64) {
+            const uint64_t m = __ballot(b + ln < ns && spre[min(b + ln, ns - 1)] >= pos);
+            if (m) {
+                q = b + first_lane(m);
+                break;
+            }
         }
-        const int i = lo + ln;
-        const uint64_t m = __ballot((i < hi) & (cp[min(i, max(hi - 1, 0))] >= pos));
-        return min(m ? lo + first_lane(m) : hi, nch - 1);
+        if (q < 0) return nch - 1;
+        const int rel = sup_row(L, s, q);
+        const int base = q > 0 ? uni(spre[q - 1]) : 0;
+        const uint64_t m = __ballot(q * 64 + ln < nch && base + rel >= pos);
+        return m ? q * 64 + first_lane(m) : nch - 1;
     }
     // The op's view scan: flat (prefix) or two-level, with E valid over the chunks around positions
     // [p_lo, p_hi] (one chunk before, two after: the searches' windows and the walk's reach).  Returns
     // the view's total length.
     static MTR_DI int view_scan(D& L, St& s, const View& v, int newlen, int p_lo, int p_hi) {
+        PROF(P_VIEW);
         if constexpr (G) {
             L.rhi = 0;
             if (s.chunked && s.nseg > 0) {
                 const int total = prefix2(L, s, v, newlen);
                 const int nch = (s.nseg + 63) >> 6;
-                const int c0 = max(0, chunk_of(L, nch, p_lo) - 1);
+                const int c0 = max(0, chunk_of(L, s, nch, p_lo) - 1);
                 // (to the chunk of the first leaf past p_hi: chunks with no length in the view -- runs of
                 // holes, leaves removed for it -- may lie between, and breakTie's candidates reach that leaf)
-                const int c1 = min(nch - 1, chunk_of(L, nch, p_hi + 1) + 2);
+                const int c1 = min(nch - 1, chunk_of(L, s, nch, p_hi + 1) + 2);
                 materialize(L, s, v, newlen, c0, c1);
                 L.rlo = c0 * 64;
                 L.rhi = (c1 + 1) * 64;
@@ -1184,6 +1332,8 @@ struct Eng {
     // to slot k + k / (kGapEvery - 1).  Moves run from the top down, so no leaf is overwritten before it
     // is read.  Only between ops (no leaf index is held).
     static MTR_DI void spread(D& L, St& s, int cap) {
+        PROF(P_SPREAD);
+        PROF_COUNT(P_NSPREAD);
         s.chunked = 0;
         if (s.holes) {
             compact(L, s, 0);
@@ -3356,6 +3506,7 @@ struct Eng {
     // MergeTree.reloadFromSegments (mergeTree.ts:678-728): MaxNodesInBlock - 1 = 7 children per block,
     // built bottom-up, so leaf i starts a level-l block iff 7^l divides i; leaf 0 starts every level
     static MTR_DI void finish_load(D& L, St& s) {
+        PROF(P_LOAD);
         const int S = s.nseg;
         int H = 1;
         for (int n = S; n > kMaxNodesInBlock - 1; n = (n + kMaxNodesInBlock - 2) / (kMaxNodesInBlock - 1)) H++;
@@ -3599,6 +3750,7 @@ struct Eng {
         }
         wsync();
         s.htop = s.heapn > 0 ? uni(L.hseq[1]) : 0;
+        sup_load(L, s);
     }
 
     static MTR_DI void store_doc(D& L, const KParams& P, const St& s, uint32_t d, int ops_done) {
@@ -3675,6 +3827,9 @@ struct Eng {
             L.lhcap = P.hcap;
             L.sc = (lptr<Sc>)(smem);
             L.gst = (lptr<mtr_synth_state>)(smem + ((sizeof(Sc) + 15) & ~size_t(15)));
+            L.sx = (lptr<int>)(smem + kScBytes);
+            for (int q = lane_id(); q < 2 * sup_rows(L.cap); q += 64) L.sx[sup_rows(L.cap) + q] = 0;  // fills, marks
+            if (threadIdx.x == 0) L.sc->sepoch = 0;
         } else {
             const int cap = CAP > 0 ? CAP : P.cap, lhcap = P.lhcap;
             char* p = smem;
@@ -3695,6 +3850,7 @@ struct Eng {
             L.huid = (A<uint32_t>)(take(4 * size_t(lhcap)));
             L.sc = (lptr<Sc>)(take(sizeof(Sc)));
             L.gst = (lptr<mtr_synth_state>)(GN ? take(sizeof(mtr_synth_state)) : p);
+            L.sx = (lptr<int>)(p);
             L.cap = cap;
             L.lhcap = lhcap;
         }
@@ -3719,7 +3875,7 @@ struct Eng {
             L.sc->cp[CP_VEQ] = (unsigned long long)P.val_eq;
             L.sc->cp[CP_HDR] = (unsigned long long)(P.hdr + d);
             L.sc->cp[CP_PEND] = (unsigned long long)(P.pend ? P.pend + size_t(d) * kPendRing * 4 : nullptr);
-            L.sc->cp[CP_CSUM] = (unsigned long long)(P.csum ? P.csum + size_t(d) * kCsumRows * (P.segcap / 64 + 1) : nullptr);
+            L.sc->cp[CP_CSUM] = (unsigned long long)(P.csum ? P.csum + size_t(d) * csum_ints(P.segcap) : nullptr);
             L.sc->cp[CP_UMAP] = (unsigned long long)(P.umap ? P.umap + size_t(d) * 2 * P.segcap : nullptr);
             L.sc->cp[CP_REFS] = (unsigned long long)(P.refs ? P.refs + size_t(d) * 3 * size_t(P.refcap) : nullptr);
             L.sc->refcap = P.refs ? P.refcap : 0;
@@ -3805,6 +3961,7 @@ struct Eng {
     // (s.status != MTR_OK; s.fail_op = gidx).
     static MTR_DI bool apply_op(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd, bool pre,
                                 uint32_t pf, int gidx) {
+        PROF_T0(_t_pre);
         if (DL) s.cur_op = gidx;
         // positions resolved by the MTR_OP_RELPOS records ahead of this op (getValidOpRange, client.ts:527-545)
         int pos1 = op.pos1, pos2 = op.pos2;
@@ -3845,6 +4002,7 @@ struct Eng {
             wsync();
         }
         if (op.type == MTR_OP_LOAD) {  // SnapshotLoader.loadHeader segment
+            PROF(P_LOAD);
             load_leaf(L, P, s, op, dd);
             if (s.status != MTR_OK) {
                 set_fail(L, gidx);
@@ -3891,6 +4049,7 @@ struct Eng {
             v.client = client;
             v.local = (!s.collab || uint32_t(s.local) == client) ? 1 : 0;
         }
+        PROF_ADD(P_PRE, _t_pre);
         // (each op type calls the view scan itself: one hoisted call site measured 2.5 % slower at C3)
         if (X && op.type == MTR_OP_RELPOS) view_scan(L, s, v, P.new_length_calc, 0, 0);
         switch (op.type) {
@@ -4009,6 +4168,7 @@ struct Eng {
                 s.status = MTR_ERR_BAD_OP;
                 break;
         }
+        PROF_T0(_t_post);
         // mergeTreeDeltaCallback (mergeTree.ts:1414, 1943, 2028) fires before zamboni
         if (DL && !PM && (op.flags & MTR_F_DELTA) && s.status == MTR_OK &&
             (op.type == MTR_OP_INSERT || op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE))
@@ -4025,6 +4185,7 @@ struct Eng {
             }
             if (zrun) zamboni(L, P, s);
         }
+        PROF_ADD(P_POST, _t_post);
         if (s.status != MTR_OK) {
             set_fail(L, gidx);
             return false;
@@ -4106,6 +4267,7 @@ struct Eng {
         if (X) done -= __popc(uint32_t(uni(L.sc->relmask)));
         // a batch that ends with header segments: build the tree now (queries read it next)
         if (s.height == 0 && s.status == MTR_OK && cursor + done >= int(dd.op_count)) finish_load(L, s);
+        sup_flush(L, s);  // the superchunk figures the launch's ops left stale, back to HBM
         store_doc(L, P, s, d, done);
     }
 
@@ -4320,8 +4482,13 @@ struct Eng {
 #ifndef MTR_WPE
 #define MTR_WPE 5
 #endif
+// (HBM-resident documents are few per CU -- C5 puts about one per SIMD -- so their kernels take the
+// registers of two waves per SIMD instead of spilling)
+#ifndef MTR_WPE_G
+#define MTR_WPE_G 2
+#endif
 template <bool G, int CAP = 0, bool DL = false, bool GN = false>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MTR_WPE))) apply_kernel(KParams P) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G ? MTR_WPE_G : MTR_WPE))) apply_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];

@@ -109,7 +109,7 @@ struct mtr_engine {
                                       // appends and removals in the X kernels only, so every launch is one
     DevBuf<uint32_t> refs;            // [doc][3][ref_slots] local references (allocated on first use)
     DevBuf<int32_t> qbuf;             // query results (reference positions)
-    DevBuf<int32_t> csum;             // [doc][kCsumRows][segcap / 64 + 1] chunk summaries (first HBM-resident launch)
+    DevBuf<int32_t> csum;             // [doc][csum_ints(segcap)] chunk records + superchunk rows (first HBM-resident launch)
     DevBuf<int32_t> umap;             // [doc][2 * segcap] uid -> slot hints (with csum)
     DevBuf<int32_t> red;              // small reduction / query-result buffer
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
@@ -671,7 +671,7 @@ static int run_impl(mtr_engine* e, int gen) {
                 // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
                 if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
                 if (!e->csum.p) {  // for every document the engine may hold: it must never move
-                    const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * kCsumRows * (size_t(P.segcap) / 64 + 1);
+                    const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * csum_ints(int(P.segcap));
                     if (e->csum.ensure(n)) return -1;
                     if (e->umap.ensure(size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * size_t(P.segcap))) return -1;
                     HIPCHK(hipMemsetAsync(e->umap.p, 0xff, e->umap.n * sizeof(int32_t), e->stream));
@@ -682,7 +682,7 @@ static int run_impl(mtr_engine* e, int gen) {
                 P.scratch = e->scratch.p;
                 cap = P.segcap;
                 lhcap = P.hcap;
-                lds = lds_bytes_global_mode();
+                lds = lds_bytes_global_mode(int(P.segcap));
                 if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             }
             const int kk = tight && !P.global_mode ? k : std::max(1, std::min(k, (cap - maxseg - 8) / 2));
@@ -1286,7 +1286,7 @@ int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t
     P.new_length_calc = e->opt.new_length_calc;
     P.n_docs = e->n_docs;
     if (e->red.ensure(16)) return -1;
-    containing_kernel<<<1, NT, lds_bytes_global_mode(), e->stream>>>(P, doc, pos, ref_seq, client, e->red.p);
+    containing_kernel<<<1, NT, lds_bytes_global_mode(int(P.segcap)), e->stream>>>(P, doc, pos, ref_seq, client, e->red.p);
     HIPCHK(hipGetLastError());
     int32_t r[11];
     HIPCHK(hipMemcpyAsync(r, e->red.p, sizeof(r), hipMemcpyDeviceToHost, e->stream));
@@ -1346,7 +1346,7 @@ static int ref_query(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int
     P.refs = e->refs.p;
     P.refcap = int(e->caps.ref_slots);
     if (e->qbuf.ensure(size_t(std::max<int64_t>(words, 4)))) return -1;
-    refs_kernel<<<1, NT, lds_bytes_global_mode(), e->stream>>>(P, doc, e->qbuf.p, info_id);
+    refs_kernel<<<1, NT, lds_bytes_global_mode(int(P.segcap)), e->stream>>>(P, doc, e->qbuf.p, info_id);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(out, e->qbuf.p, size_t(words) * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
