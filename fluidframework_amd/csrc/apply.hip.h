@@ -86,9 +86,10 @@ constexpr uint32_t PEND_KEY = 0x40000000u;
 // event, the length of its leaves whose visibility no view in the collaboration window can change, and
 // the slots of the other leaves (up to kChunkList; more = the chunk is scanned whole)
 constexpr int kChunkList = 8;
-constexpr int kCsumRows = 4 + kChunkList;  // ints per chunk record
-// superchunks (64 chunks) a view scan loads the chunk records of together
+constexpr int kCsumRows = 4 + 5 * kChunkList;  // ints per chunk record (Eng::csum_update)
+// superchunks (64 chunks) whose chunk lengths one round of loads fetches; prefix2's list capacity
 constexpr int kDirtyBatch = 4;
+constexpr int kListCap = 256;
 __host__ __device__ constexpr int sup_rows(int segcap) { return segcap / 4096 + 2; }
 // ints of one document's chunk summaries: the chunk records, then its superchunks' lengths and newest events
 // (a multiple of 4: every document's records stay 16-byte aligned)
@@ -262,6 +263,7 @@ struct Sc {
     int nrefs, refcap;  // local references of the document (DocHdr.nrefs) and the table's capacity
     int fail_op, max_heap, heap_need;  // DocHdr's, for this launch
     int sepoch;  // view scans of this launch (HBM-resident documents: Eng::prefix2's fill epochs)
+    int vref;    // the last two-level view's refSeq (INT32_MAX: a local view)
     unsigned long long sum_s, sum_l;   // B_op counters: leaves before each op, inserted units
 #ifdef MTR_PROF
     unsigned long long prof[P_COUNT];
@@ -393,10 +395,10 @@ constexpr size_t kScBytes = kScOnly + ((sizeof(mtr_synth_state) + 15) & ~size_t(
 __host__ __device__ inline size_t lds_bytes(int cap, int lhcap, bool gen = true) {
     return size_t(cap) * 4 * 8 + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
 }
-// (HBM-resident documents: Sc, the generator state, five superchunk rows, prefix2's dirty-chunk list
-// and a chunk-prefix row per 64 slots)
+// (HBM-resident documents: Sc, the generator state, six superchunk rows, prefix2's chunk list and two
+// words per 64 slots)
 __host__ __device__ inline size_t lds_bytes_global_mode(int segcap) {
-    return kScBytes + ((size_t(4) * (5 * sup_rows(segcap) + 4 * 64 * kDirtyBatch + segcap / 64 + 1) + 15) & ~size_t(15));
+    return kScBytes + ((size_t(4) * (6 * sup_rows(segcap) + kListCap + 2 * (segcap / 64 + 1)) + 15) & ~size_t(15));
 }
 
 // Phase timers (builds with -DMTR_PROF only): lane-0 clock cycles per phase, summed over
@@ -652,29 +654,34 @@ struct Eng {
     // not removed) and its newest event (the largest seq, and removedSeq of a removed leaf, over its
     // leaves).  A chunk whose newest event is <= the view's refSeq looks the same to every client at that
     // refSeq -- each leaf was inserted by then, and removed by then or not at all -- so its view length
-    // is its local length; only the other chunks are scanned leaf by leaf.  This restates what
+    // is its local length; only the other chunks are evaluated leaf by leaf.  This restates what
     // PartialSequenceLengths does per block (partialLengths.ts:698-735) for chunks of the flat leaf order.
-    // 64 chunks form a superchunk with the same two figures (the chunks' sum and max), so a view reads
-    // one pair per 4096 slots plus the chunk records of the superchunks with events after its refSeq.
-    // A chunk's record: kCsumRows ints (16-byte aligned) -- local length, newest event, the length of its
+    // 64 chunks form a superchunk with the same two figures (the chunks' sum and max), so a view reads one
+    // pair per 4096 slots plus the newest events of the chunks of the superchunks with later events.
+    // A chunk's record: kCsumRows ints (16-byte aligned) -- {local length, newest event, the length of its
     // leaves whose visibility no view in the collaboration window can change, the count of the other
-    // leaves, then their slots (up to kChunkList; more = the chunk is scanned whole).
+    // leaves}, then those leaves' visibility fields {len, removedSeq, seq, meta} (up to kChunkList; more =
+    // the chunk is scanned whole) and their slots (for the remover lists of overlapping removes).  A view
+    // evaluates a chunk with later events from its record alone: one round of loads for 64 such chunks.
     static MTR_DI int nsup(const D& L) { return sup_rows(L.cap); }
+    static MTR_DI int nchr(const D& L) { return L.cap / 64 + 1; }
     static MTR_DI gptr<int> cs_rec(const D& L, int c) { return L.gcsum() + c * kCsumRows; }
-    static MTR_DI gptr<int> cs_sl(const D& L) { return L.gcsum() + kCsumRows * (L.cap / 64 + 1); }
+    static MTR_DI gptr<int> cs_sl(const D& L) { return L.gcsum() + kCsumRows * nchr(L); }
     static MTR_DI gptr<int> cs_se(const D& L) { return cs_sl(L) + nsup(L); }
-    // LDS rows (Doc::sx, lds_bytes_global_mode): a view's inclusive superchunk prefix, the view epoch that
-    // filled a superchunk's chunk-prefix row, "superchunk figures stale" marks, the superchunks' local
-    // lengths and newest events (the launch's copy of the HBM rows), prefix2's dirty-chunk list, and a
-    // view's chunk prefix (inclusive within each superchunk).  (Rows a wave writes and reads back stay in
-    // LDS: a global load issued right after this wave's own store to the word can return the old value.)
+    // LDS rows (Doc::sx, lds_bytes_global_mode): per superchunk a view's inclusive prefix, the view epoch
+    // that filled its chunk-prefix row, "figures stale" marks, its local length and newest event (the
+    // launch's copy of the HBM rows), a view's length change from its chunks with later events; prefix2's
+    // list of those chunks; per chunk its newest event (the launch's copy of the records'), and a view's
+    // length of the chunk (a chunk with later events), then its inclusive prefix within its superchunk
     static MTR_DI lptr<int> sup_pre(const D& L) { return L.sx; }
     static MTR_DI lptr<int> sup_fill(const D& L) { return L.sx + nsup(L); }
     static MTR_DI lptr<int> sup_mark(const D& L) { return L.sx + 2 * nsup(L); }
     static MTR_DI lptr<int> sup_len(const D& L) { return L.sx + 3 * nsup(L); }
     static MTR_DI lptr<int> sup_ev(const D& L) { return L.sx + 4 * nsup(L); }
-    static MTR_DI lptr<int> dlist(const D& L) { return L.sx + 5 * nsup(L); }
-    static MTR_DI lptr<int> cs_pre(const D& L) { return L.sx + 5 * nsup(L) + 4 * 64 * kDirtyBatch; }
+    static MTR_DI lptr<int> sup_dlen(const D& L) { return L.sx + 5 * nsup(L); }
+    static MTR_DI lptr<int> dlist(const D& L) { return L.sx + 6 * nsup(L); }
+    static MTR_DI lptr<int> ch_ev(const D& L) { return dlist(L) + kListCap; }
+    static MTR_DI lptr<int> ch_x(const D& L) { return ch_ev(L) + nchr(L); }
     static MTR_DI v4i ld4(gptr<const int> p) { return *(gptr<const v4i>)p; }
     // recompute the records of the chunks covering slots [lo, hi); their superchunks go stale
     static MTR_DI void csum_update(D& L, const St& s, int lo, int hi) {
@@ -704,8 +711,15 @@ struct Eng {
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
                 const gptr<int> r = cs_rec(L, c);
-                if (win && nw <= kChunkList) r[4 + __popcll(wm & lanes_below())] = i;
-                if (lane_id() == 0) *(gptr<v4i>)r = v4i{x, ev, fx, min(nw, kChunkList + 1)};
+                if (win && nw <= kChunkList) {
+                    const int k = __popcll(wm & lanes_below());
+                    *(gptr<v4i>)(r + 4 + 4 * k) = v4i{len, rs, sq, int(m)};  // Hot's field order
+                    r[4 + 4 * kChunkList + k] = i;
+                }
+                if (lane_id() == 0) {
+                    *(gptr<v4i>)r = v4i{x, ev, fx, min(nw, kChunkList + 1)};
+                    ch_ev(L)[c] = ev;
+                }
             }
             for (int q = (c0 >> 6) + lane_id(); q <= (c1 >> 6); q += 64) sup_mark(L)[q] = 1;
             wsync();
@@ -716,24 +730,24 @@ struct Eng {
         if constexpr (G) {
             if (!s.chunked || s.nseg <= 0) return;
             const int nch = (s.nseg + 63) >> 6, ns = (nch + 63) >> 6, ln = lane_id();
-            const lptr<int> mk = sup_mark(L), sl = sup_len(L), se = sup_ev(L);
+            const lptr<int> mk = sup_mark(L), sl = sup_len(L), se = sup_ev(L), ce = ch_ev(L);
             for (int b = 0; b < ns; b += 64) {
                 uint64_t m = __ballot(b + ln < ns && mk[min(b + ln, ns - 1)] != 0);
-                while (m) {  // kDirtyBatch superchunks' chunk records in flight together
-                    int q[kDirtyBatch];
-                    v4i r[kDirtyBatch];
+                while (m) {  // kDirtyBatch superchunks' chunk lengths in flight together
+                    int q[kDirtyBatch], x[kDirtyBatch];
 #pragma unroll
                     for (int k = 0; k < kDirtyBatch; k++) {
                         q[k] = m ? b + first_lane(m) : -1;
                         m &= m - 1;
-                        r[k] = ld4(cs_rec(L, min(max(q[k], 0) * 64 + ln, nch - 1)));
+                        x[k] = cs_rec(L, min(max(q[k], 0) * 64 + ln, nch - 1))[0];
                     }
 #pragma unroll
                     for (int k = 0; k < kDirtyBatch; k++) {
                         if (q[k] < 0) break;
-                        const bool ok = q[k] * 64 + ln < nch;
-                        const int sum = rdlane(wave_incl_scan(ok ? r[k].x : 0), 63);
-                        int ev = ok ? r[k].y : 0;
+                        const int c = q[k] * 64 + ln;
+                        const bool ok = c < nch;
+                        const int sum = rdlane(wave_incl_scan(ok ? x[k] : 0), 63);
+                        int ev = ok ? ce[min(c, nch - 1)] : 0;
 #pragma unroll
                         for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
                         if (ln == 0) {
@@ -747,16 +761,18 @@ struct Eng {
             wsync();
         }
     }
-    // the superchunk rows between launches: read at launch start, refreshed and written back at its end
+    // the superchunk rows and chunk newest events between launches: read at launch start, refreshed and
+    // written back at its end (the records themselves live in HBM)
     static MTR_DI void sup_load(D& L, const St& s) {
         if constexpr (G) {
             if (!s.chunked || s.nseg <= 0 || !L.gcsum()) return;  // (query kernels carry no summaries)
-            const int ns = (((s.nseg + 63) >> 6) + 63) >> 6;
+            const int nch = (s.nseg + 63) >> 6, ns = (nch + 63) >> 6;
             const gptr<int> gl = cs_sl(L), ge = cs_se(L);
             for (int q = lane_id(); q < ns; q += 64) {
                 sup_len(L)[q] = gl[q];
                 sup_ev(L)[q] = ge[q];
             }
+            for (int c = lane_id(); c < nch; c += 64) ch_ev(L)[c] = cs_rec(L, c)[1];
             wsync();
         }
     }
@@ -773,118 +789,105 @@ struct Eng {
             wsync();
         }
     }
-    // the view's superchunk lengths, their inclusive prefix in sup_pre (and the chunk-prefix rows of the
-    // superchunks it scanned chunk by chunk); returns the view's total length
+    // view lengths of the listed chunks (dlist[0, n)) into ch_x, their change from the local lengths into
+    // their superchunks' sup_dlen
+    static MTR_DI void dirty_chunks(D& L, const St& s, const View& v, int newlen, int n) {
+        const int S = s.nseg, ln = lane_id();
+        const lptr<int> lst = dlist(L), cx = ch_x(L), sd = sup_dlen(L);
+        for (int e0 = 0; e0 < n; e0 += 64) {  // one lane per chunk: its whole record in one round of loads
+            const int e = e0 + ln;
+            const int c = lst[min(e, n - 1)];
+            const gptr<int> r = cs_rec(L, c);
+            const v4i h = ld4(r);
+            v4i hv[kChunkList];
+#pragma unroll
+            for (int j = 0; j < kChunkList; j++) hv[j] = ld4(r + 4 + 4 * j);
+            const v4i s0 = ld4(r + 4 + 4 * kChunkList), s1 = ld4(r + 8 + 4 * kChunkList);
+            const int slt[kChunkList] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const bool listed = e < n && h.w <= kChunkList;
+            int sum = h.z;
+#pragma unroll
+            for (int j = 0; j < kChunkList; j++) {
+                const bool on = listed && j < h.w;
+                const Hot hj{hv[j].x, hv[j].y, hv[j].z, uint32_t(hv[j].w)};
+                const int x0 = vis_hot(L, hj, on ? slt[j] : 0, v, newlen, s.minseq, on);
+                sum += on ? max(x0, 0) : 0;
+            }
+            int vl = sum;
+            uint64_t um = __ballot(e < n && !listed);
+#ifdef MTR_PROF
+            if (ln == 0) L.sc->prof[P_NDIRTY] += (unsigned long long)__popcll(um);
+            ProfScope _prof_dirty(L.sc, P_PFDIRTY);
+#endif
+            while (um) {  // more than kChunkList leaves in the window: the chunk's leaves, GK chunks at a time
+                int lq[GK];
+                Hot hw[GK];
+#pragma unroll
+                for (int g = 0; g < GK; g++) {
+                    lq[g] = um ? first_lane(um) : -1;
+                    um &= um - 1;
+                    const int i = rdlane(c, max(lq[g], 0)) * 64 + ln;
+                    hw[g] = ld_hot(L, min(i, S - 1));
+                }
+#pragma unroll
+                for (int g = 0; g < GK; g++) {
+                    if (lq[g] < 0) break;
+                    const int i = rdlane(c, lq[g]) * 64 + ln;
+                    const int x0 = vis_hot(L, hw[g], i, v, newlen, s.minseq, i < S);
+                    const int tot = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
+                    if (ln == lq[g]) vl = tot;
+                }
+            }
+            if (e < n) {
+                cx[c] = vl;
+                __atomic_fetch_add(&sd[c >> 6], vl - h.x, __ATOMIC_RELAXED);
+            }
+        }
+        wsync();
+    }
+    // the view's superchunk lengths and their inclusive prefix in sup_pre; returns the view's total length
     static MTR_DI int prefix2(D& L, const St& s, const View& v, int newlen) {
         PROF(P_PREFIX);
         sup_refresh(L, s);
-        const int S = s.nseg, nch = (S + 63) >> 6, ns = (nch + 63) >> 6;
-        const int ln = lane_id();
+        const int nch = (s.nseg + 63) >> 6, ns = (nch + 63) >> 6, ln = lane_id();
         const int ep = uni(L.sc->sepoch) + 1;
-        if (ln == 0) L.sc->sepoch = ep;
-        const lptr<int> sl = sup_len(L), se = sup_ev(L), cp = cs_pre(L);
-        const lptr<int> spre = sup_pre(L), sfill = sup_fill(L), lst = dlist(L);
+        if (ln == 0) {
+            L.sc->sepoch = ep;
+            L.sc->vref = v.local ? INT32_MAX : v.ref;  // (a local view: every chunk shows its local length)
+        }
+        const lptr<int> sl = sup_len(L), se = sup_ev(L), sd = sup_dlen(L), spre = sup_pre(L), ce = ch_ev(L),
+                        lst = dlist(L);
         int carry = 0;
         for (int b = 0; b < ns; b += 64) {
             const int q = b + ln, qc = min(q, ns - 1);
             const int sl0 = sl[qc], se0 = se[qc];
-            int slen = q < ns ? sl0 : 0;
-            uint64_t dq = __ballot(q < ns && !v.local && se0 > v.ref);
+            const uint64_t dq0 = __ballot(q < ns && !v.local && se0 > v.ref);
+            if ((dq0 >> ln) & 1) sd[q] = 0;
+            wsync();
 #ifdef MTR_PROF
             if (ln == 0) {
                 L.sc->prof[P_NCH] += (unsigned long long)min(64, ns - b);
-                L.sc->prof[P_NSUP] += (unsigned long long)__popcll(dq);
+                L.sc->prof[P_NSUP] += (unsigned long long)__popcll(dq0);
             }
 #endif
-            while (dq) {  // superchunks with events after refSeq: kDirtyBatch at a time
-                int sq[kDirtyBatch];
-                v4i r[kDirtyBatch];
-#pragma unroll
-                for (int k = 0; k < kDirtyBatch; k++) {
-                    sq[k] = dq ? b + first_lane(dq) : -1;
-                    dq &= dq - 1;
-                    r[k] = ld4(cs_rec(L, min(max(sq[k], 0) * 64 + ln, nch - 1)));
-                }
-                // their chunks with events after refSeq go to the LDS list, one entry each
-                int vl[kDirtyBatch], ent[kDirtyBatch];
-                uint64_t dm[kDirtyBatch];
-                int n = 0;
-#pragma unroll
-                for (int k = 0; k < kDirtyBatch; k++) {
-                    const int c = max(sq[k], 0) * 64 + ln;
-                    const bool cin = sq[k] >= 0 && c < nch;
-                    const bool dirty = cin && r[k].y > v.ref;
-                    vl[k] = cin ? r[k].x : 0;
-                    dm[k] = __ballot(dirty);
-                    ent[k] = n + __popcll(dm[k] & lanes_below());
-                    if (dirty) {
-                        lst[4 * ent[k]] = c;
-                        lst[4 * ent[k] + 1] = r[k].z;
-                        lst[4 * ent[k] + 2] = r[k].w;
-                    }
-                    n += __popcll(dm[k]);
-                }
-                wsync();
+            int n = 0;
+            for (uint64_t dq = dq0; dq;) {  // their chunks with later events, listed from the LDS newest events
+                const int c = (b + first_lane(dq)) * 64 + ln;
+                dq &= dq - 1;
+                const bool dirty = c < nch && ce[min(c, nch - 1)] > v.ref;
+                const uint64_t dm = __ballot(dirty);
+                if (dirty) lst[n + __popcll(dm & lanes_below())] = c;
+                n += __popcll(dm);
+                if (n > kListCap - 64 || !dq) {
+                    wsync();
 #ifdef MTR_PROF
-                if (ln == 0) L.sc->prof[P_NDCH] += (unsigned long long)n;
+                    if (ln == 0) L.sc->prof[P_NDCH] += (unsigned long long)n;
 #endif
-                for (int e0 = 0; e0 < n; e0 += 64) {  // one lane per listed chunk
-                    const int e = e0 + ln, ec = min(e, n - 1);
-                    const int c = lst[4 * ec], fx = lst[4 * ec + 1], nl = lst[4 * ec + 2];
-                    const bool listed = e < n && nl <= kChunkList;
-                    const v4i s0 = ld4(cs_rec(L, c) + 4), s1 = ld4(cs_rec(L, c) + 8);
-                    const int slt[kChunkList] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-                    Hot hq[kChunkList];
-#pragma unroll
-                    for (int j = 0; j < kChunkList; j++)
-                        hq[j] = ld_hot(L, (listed && j < nl) ? min(max(slt[j], 0), S - 1) : 0);
-                    int sum = fx;
-#pragma unroll
-                    for (int j = 0; j < kChunkList; j++) {
-                        const bool on = listed && j < nl;
-                        const int x0 = vis_hot(L, hq[j], on ? slt[j] : 0, v, newlen, s.minseq, on);
-                        sum += on ? max(x0, 0) : 0;
-                    }
-                    if (listed) lst[4 * ec + 3] = sum;
-                    uint64_t um = __ballot(e < n && !listed);
-#ifdef MTR_PROF
-                    if (ln == 0) L.sc->prof[P_NDIRTY] += (unsigned long long)__popcll(um);
-                    ProfScope _prof_dirty(L.sc, P_PFDIRTY);
-#endif
-                    while (um) {  // more than kChunkList leaves in the window: the chunk's leaves, GK chunks at a time
-                        int lq[GK];
-                        Hot hw[GK];
-#pragma unroll
-                        for (int g = 0; g < GK; g++) {
-                            lq[g] = um ? first_lane(um) : -1;
-                            um &= um - 1;
-                            const int i = rdlane(c, max(lq[g], 0)) * 64 + ln;
-                            hw[g] = ld_hot(L, min(i, S - 1));
-                        }
-#pragma unroll
-                        for (int g = 0; g < GK; g++) {
-                            if (lq[g] < 0) break;
-                            const int i = rdlane(c, lq[g]) * 64 + ln;
-                            const int x0 = vis_hot(L, hw[g], i, v, newlen, s.minseq, i < S);
-                            const int tot = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
-                            if (ln == lq[g]) lst[4 * ec + 3] = tot;
-                        }
-                    }
+                    dirty_chunks(L, s, v, newlen, n);
+                    n = 0;
                 }
-                wsync();
-#pragma unroll
-                for (int k = 0; k < kDirtyBatch; k++) {  // chunk prefix rows and the superchunks' view lengths
-                    if (sq[k] < 0) break;
-                    const int c = sq[k] * 64 + ln;
-                    if ((dm[k] >> ln) & 1) vl[k] = lst[4 * ent[k] + 3];
-                    const int inc = wave_incl_scan(vl[k]);
-                    if (c < nch) cp[c] = inc;
-                    const int tot = rdlane(inc, 63);
-                    if (ln == sq[k] - b) slen = tot;
-                    if (ln == 0) sfill[sq[k]] = ep;
-                }
-                wsync();
             }
+            const int slen = q < ns ? sl0 + (((dq0 >> ln) & 1) ? sd[q] : 0) : 0;
             const int inc = wave_incl_scan(slen);
             if (q < ns) spre[q] = carry + inc;
             carry += rdlane(inc, 63);
@@ -892,15 +895,17 @@ struct Eng {
         wsync();
         return carry;
     }
-    // lane l: the inclusive prefix of chunk 64 q + l within superchunk q in the current view (filled now
-    // when prefix2 did not scan it: each of its chunks shows its local length)
+    // lane l: the inclusive prefix of chunk 64 q + l within superchunk q in the current view (the row is
+    // filled on first use: chunks with later events from ch_x, the others' local lengths from their records)
     static MTR_DI int sup_row(D& L, const St& s, int q) {
         const int nch = (s.nseg + 63) >> 6, c = q * 64 + lane_id(), cc = min(c, nch - 1);
         const int ep = uni(L.sc->sepoch);
-        if (uni(sup_fill(L)[q]) == ep) return cs_pre(L)[cc];
-        const int x = cs_rec(L, cc)[0];
+        if (uni(sup_fill(L)[q]) == ep) return ch_x(L)[cc];
+        const int vref = uni(L.sc->vref);
+        const int cl = cs_rec(L, cc)[0];
+        const int x = ch_ev(L)[cc] > vref ? ch_x(L)[cc] : cl;
         const int inc = wave_incl_scan(c < nch ? x : 0);
-        if (c < nch) cs_pre(L)[c] = inc;
+        if (c < nch) ch_x(L)[c] = inc;
         if (lane_id() == 0) sup_fill(L)[q] = ep;
         wsync();
         return inc;
@@ -4482,10 +4487,10 @@ struct Eng {
 #ifndef MTR_WPE
 #define MTR_WPE 5
 #endif
-// (HBM-resident documents are few per CU -- C5 puts about one per SIMD -- so their kernels take the
-// registers of two waves per SIMD instead of spilling)
+// (HBM-resident documents are few per CU -- C5 puts about one per SIMD -- so their kernels may take a
+// whole SIMD's registers instead of spilling: a spilling build of the lean one produced wrong views)
 #ifndef MTR_WPE_G
-#define MTR_WPE_G 2
+#define MTR_WPE_G 1
 #endif
 template <bool G, int CAP = 0, bool DL = false, bool GN = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G ? MTR_WPE_G : MTR_WPE))) apply_kernel(KParams P) {
@@ -4508,7 +4513,7 @@ bool launch_fixed_cap_p2(int cap, uint32_t grid, size_t lds, hipStream_t st, con
 // SharedMatrix pairs: one wave applies a matrix's op list to its two PermutationVectors, each with
 // its own LDS region of `pair_region` bytes (HBM-resident arrays in global mode)
 template <bool G, bool DL = false, bool GN = false>
-__global__ void __launch_bounds__(NT) apply_pair_kernel(KParams P, uint32_t pair_region) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, G ? 1 : 8))) apply_pair_kernel(KParams P, uint32_t pair_region) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
