@@ -1407,6 +1407,19 @@ struct Eng {
     // ------------------------------------------------------------ searches (ballots)
     // start of the level-`level` block holding leaf x: last i <= x with i == 0 or bnd >= level
     static MTR_DI int block_start(const D& L, int x, int level) {
+        if constexpr (G) {  // HBM: GK rounds of loads in flight per step
+            for (int base = x;; base -= 64 * GK) {
+                uint32_t mq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) mq[q] = L.meta[max(base - 64 * q - lane_id(), 0)];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = base - 64 * q - lane_id();
+                    const uint64_t m = __ballot((i <= 0) | (bnd_of(mq[q]) >= level));
+                    if (m) return max(0, base - 64 * q - first_lane(m));
+                }
+            }
+        }
         for (int base = x;; base -= 64) {
             const int i = base - lane_id();
             const uint32_t mi = L.meta[max(i, 0)];
@@ -1417,6 +1430,19 @@ struct Eng {
     // end (exclusive) of the level-`level` block holding leaf x
     static MTR_DI int block_end(const D& L, const St& s, int x, int level) {
         const int S = s.nseg;
+        if constexpr (G) {
+            for (int base = x + 1;; base += 64 * GK) {
+                uint32_t mq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) mq[q] = L.meta[max(min(base + 64 * q + lane_id(), S - 1), 0)];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = base + 64 * q + lane_id();
+                    const uint64_t m = __ballot((i >= S) | (bnd_of(mq[q]) >= level));
+                    if (m) return base + 64 * q + first_lane(m);
+                }
+            }
+        }
         for (int base = x + 1;; base += 64) {
             const int i = base + lane_id();
             const uint32_t mi = L.meta[max(min(i, S - 1), 0)];
@@ -1451,6 +1477,17 @@ struct Eng {
     // number of leaves in [bs, be) with bnd >= minb
     static MTR_DI int count_bnd(const D& L, int bs, int be, int minb) {
         int c = 0;
+        if constexpr (G) {
+            for (int base = bs; base < be; base += 64 * GK) {
+                uint32_t mq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) mq[q] = L.meta[min(base + 64 * q + lane_id(), be - 1)];
+#pragma unroll
+                for (int q = 0; q < GK; q++)
+                    c += __popcll(__ballot((base + 64 * q + lane_id() < be) & (bnd_of(mq[q]) >= minb)));
+            }
+            return c;
+        }
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
             const uint32_t mi = L.meta[min(i, be - 1)];
@@ -1475,6 +1512,16 @@ struct Eng {
     // leaves of [bs, be) that are not hole slots; the index of the n-th (0-based) of them
     static MTR_DI int count_live(const D& L, int bs, int be) {
         int c = 0;
+        if constexpr (G) {
+            for (int base = bs; base < be; base += 64 * GK) {
+                uint32_t mq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) mq[q] = L.meta[min(base + 64 * q + lane_id(), be - 1)];
+#pragma unroll
+                for (int q = 0; q < GK; q++) c += __popcll(__ballot((base + 64 * q + lane_id() < be) & !(mq[q] & M_DEL)));
+            }
+            return c;
+        }
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
             c += __popcll(__ballot((i < be) & !(L.meta[min(i, be - 1)] & M_DEL)));
@@ -3090,13 +3137,21 @@ struct Eng {
                     if (pe - ps > 64 || scour_par(L, P, s, ps, pe) < 0) scour_range(L, P, s, ps, pe);
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
+                constexpr int ZK = G ? GK : 1;  // (HBM: GK rounds of loads in flight)
                 int T = 0;
                 uint32_t m1r = M_DEL;  // a one-round range keeps its meta words in registers
-                for (int wb = ps; wb < pe; wb += 64) {
-                    const int i = wb + lane_id();
-                    const uint32_t m = i < pe ? L.meta[i] : M_DEL;
-                    if (wb == ps) m1r = m;
-                    T += __popcll(__ballot(!(m & M_DEL) && (l == 2 || bnd_of(m) >= l - 2)));
+                for (int wb = ps; wb < pe; wb += 64 * ZK) {
+                    uint32_t mq[ZK];
+#pragma unroll
+                    for (int q = 0; q < ZK; q++) {
+                        const int i = wb + 64 * q + lane_id();
+                        mq[q] = L.meta[min(i, pe - 1)];
+                        if (i >= pe) mq[q] = M_DEL;
+                    }
+                    if (wb == ps) m1r = mq[0];
+#pragma unroll
+                    for (int q = 0; q < ZK; q++)
+                        T += __popcll(__ballot(!(mq[q] & M_DEL) && (l == 2 || bnd_of(mq[q]) >= l - 2)));
                 }
                 int c = 0;
                 if (T > 0) {  // rebalance into c blocks: the first `rem` get base+1 items
@@ -3106,20 +3161,30 @@ struct Eng {
                     const int rem = T % c;
                     const int big = rem * (base + 1);
                     int item0 = 0;
-                    for (int wb = ps; wb < pe; wb += 64) {
-                        const int i = wb + lane_id();
-                        uint32_t m = pe - ps <= 64 ? m1r : (i < pe ? L.meta[i] : M_DEL);
-                        const bool it = !(m & M_DEL) && (l == 2 || bnd_of(m) >= l - 2);
-                        const uint64_t mask = __ballot(it);
-                        if (it) {
-                            const int item = item0 + __popcll(mask & lanes_below());
-                            const bool isStart = item < big ? item % (base + 1) == 0 : (item - big) % base == 0;
-                            const int nb = item == 0 ? top : (isStart ? l - 1 : (l == 2 ? 0 : l - 2));
-                            m = set_bnd(m, nb);
-                            if (l == 2 && isStart) m = set_ns(m, NS_UNDEF);
-                            L.meta[i] = m;
+                    for (int wb = ps; wb < pe; wb += 64 * ZK) {
+                        uint32_t mq[ZK];
+#pragma unroll
+                        for (int q = 0; q < ZK; q++) {
+                            const int i = wb + 64 * q + lane_id();
+                            mq[q] = pe - ps <= 64 ? m1r : L.meta[min(i, pe - 1)];
+                            if (i >= pe) mq[q] = M_DEL;
                         }
-                        item0 += __popcll(mask);
+#pragma unroll
+                        for (int q = 0; q < ZK; q++) {
+                            const int i = wb + 64 * q + lane_id();
+                            uint32_t m = mq[q];
+                            const bool it = !(m & M_DEL) && (l == 2 || bnd_of(m) >= l - 2);
+                            const uint64_t mask = __ballot(it);
+                            if (it) {
+                                const int item = item0 + __popcll(mask & lanes_below());
+                                const bool isStart = item < big ? item % (base + 1) == 0 : (item - big) % base == 0;
+                                const int nb = item == 0 ? top : (isStart ? l - 1 : (l == 2 ? 0 : l - 2));
+                                m = set_bnd(m, nb);
+                                if (l == 2 && isStart) m = set_ns(m, NS_UNDEF);
+                                L.meta[i] = m;
+                            }
+                            item0 += __popcll(mask);
+                        }
                     }
                     wsync();
                 }
@@ -3506,6 +3571,46 @@ struct Eng {
         wsync();
         s.nseg = i + 1;
         set_merge_info(L, P, s, i, op, dd);
+    }
+
+    // A run of plain header segments (text, no props, no removers) from the records lanes [t0, tend) of
+    // the loop's 64-record window hold (lane t: the 8 words of record t): one lane per segment, as
+    // load_leaf + set_merge_info would append them one by one.  Returns how many were appended (0: the
+    // record at t0 takes the one-by-one path: a marker, props, removers, or room running short).
+    static MTR_DI int load_run(D& L, const KParams& P, St& s, const uint32_t (&ow)[8], int t0, int tend,
+                               gptr<const uint16_t> btext) {
+        PROF(P_LOAD);
+        const int ln = lane_id();
+        const uint32_t ty = ow[0] & 0xffu, fl = (ow[0] >> 8) & 0xffu;
+        const bool el = ln >= t0 && ln < tend && ty == MTR_OP_LOAD &&
+                        !(fl & (MTR_F_MARKER | MTR_F_PROPS | MTR_F_REL)) && int(ow[3]) <= 0;
+        const uint64_t bad = __ballot(!el) & ~((uint64_t(1) << t0) - 1);
+        const int cnt = (bad ? first_lane(bad) : 64) - t0;
+        if (cnt <= 0) return 0;
+        const bool act = ln >= t0 && ln < t0 + cnt;
+        const int len = act ? int(ow[7]) : 0;
+        const int incl = wave_incl_scan(len);
+        const int tot = rdlane(incl, 63);
+        // (the one-by-one path would neither yield for leaf room nor collect the text arena on the way)
+        if (s.nseg + cnt + 3 > L.cap || s.textused + tot + 4096 > text_end(s, P)) return 0;
+        if (act) {
+            const int i = s.nseg + (ln - t0);
+            const uint32_t t = uint32_t(s.textused + incl - len);
+            const gptr<const uint16_t> src = btext + ow[6];
+            for (int q = 0; q < len; q++) L.gtext()[t + q] = src[q];
+            L.len[i] = len;
+            L.seq[i] = int(ow[1]);
+            L.rseq[i] = int(ow[2]) >= 0 ? int(ow[2]) : RNONE;
+            L.meta[i] = enc_client(int(int16_t(ow[0] >> 16))) | M_NLQ | ((fl & MTR_F_NOREF) ? M_NOREF : 0u);
+            L.text[i] = t;
+            L.props[i] = NONE32;
+            L.uid[i] = uint32_t(s.uidnext + (ln - t0));
+        }
+        wsync();
+        s.nseg += cnt;
+        s.uidnext += cnt;
+        s.textused += tot;
+        return cnt;
     }
 
     // MergeTree.reloadFromSegments (mergeTree.ts:678-728): MaxNodesInBlock - 1 = 7 children per block,
@@ -4202,8 +4307,11 @@ struct Eng {
     static MTR_DI void run(char* smem, const KParams& P, uint32_t d) {
         const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
         const int cursor = uni(gp(P.hdr)[d].op_cursor);
-        const int n_ops = min(int(dd.op_count) - cursor, P.ops_this_launch);
+        int n_ops = min(int(dd.op_count) - cursor, P.ops_this_launch);
         if (n_ops <= 0 || uni(gp(P.hdr)[d].status) != MTR_OK) return;
+        // a document loading header segments (one lane each, load_run) takes 64 launches' worth of records
+        if (!GN && !PM && (uniu(((gptr<const uint32_t>)(gp(P.ops) + dd.op_begin + cursor))[0]) & 0xffu) == MTR_OP_LOAD)
+            n_ops = min(int(dd.op_count) - cursor, 64 * P.ops_this_launch);
         if (P.dkind && uniu(gp(P.dkind)[d]) != 0) {  // a cols vector has no op list of its own
             if (lane_id() == 0) {
                 gp(P.hdr)[d].status = MTR_ERR_BAD_OP;
@@ -4254,6 +4362,17 @@ struct Eng {
                         npre = 1;
                         npf = uint32_t(ln) < len1 ? uint32_t(btext[off1 + ln]) : 0u;
                     }
+                }
+            }
+            if (!GN && !PM && op.type == MTR_OP_LOAD && s.height == 0 && !s.collab && s.status == MTR_OK) {
+                // a run of header segments: one lane each
+                const int w0 = k - (k & 63);
+                const int cnt = load_run(L, P, s, ow, k & 63, min(64, n_ops - w0), btext);
+                if (cnt > 0) {
+                    k += cnt - 1;
+                    done = k + 1;
+                    npre = 0;
+                    continue;
                 }
             }
             const uint32_t nseg0 = uint32_t(s.nseg);
