@@ -43,6 +43,7 @@ if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     out["hbm_write_bytes_per_launch"] = write
     out["hbm_bytes_per_launch"] = 2.0 * fetch + write
     out["note"] = "hbm_bytes = 2*FETCH_SIZE (gfx950 correction) + WRITE_SIZE, KiB->bytes"
+    out["hbm_bytes_per_step"] = out["hbm_bytes_per_launch"] * a.launches  # the averaged launches' total
 if "SQ_LDS_BANK_CONFLICT" in per and "SQ_LDS_IDX_ACTIVE" in per:
     out["lds_bank_conflict_rate"] = per["SQ_LDS_BANK_CONFLICT"] / max(1.0, per["SQ_LDS_IDX_ACTIVE"])
 if "SQ_WAVES" in per and "SQ_INSTS_VALU" in per:
