@@ -298,9 +298,11 @@ def main(argv=None):
     elif grow:
         cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=doc_lo,
                        text_cap=2 * grow + 18 * ops + 16)
-        # (slots: the leaves plus one hole per 16 -- HBM-resident documents keep hole slots)
+        # (slots: the leaves plus one hole per 16 -- HBM-resident documents keep hole slots, DESIGN.md §2;
+        # text: each half of the arena twice the document's text, so its collection runs rarely -- 6 MB per
+        # document, 6 GB for C5's 1,000 of 288 GB)
         eng = Engine(n, device=local, max_segments=grow + grow // 14 + 2 * ops + 128, heap_entries=grow + 2 * ops + 128,
-                     text_units=2 * int(cfg.text_cap) + 16384, prop_words=65536, remover_cells=65536,
+                     text_units=4 * int(cfg.text_cap) + 16384, prop_words=65536, remover_cells=65536,
                      ops_per_launch=a.ops_per_launch)
     else:
         cfg = make_cfg(n, ops, writers=a.writers, max_lag=a.max_lag, doc_base=doc_lo)

@@ -85,7 +85,7 @@ constexpr uint32_t PEND_KEY = 0x40000000u;
 // chunk summaries of HBM-resident documents (Eng::csum_update): per 64-slot chunk its local length, newest
 // event, the length of its leaves whose visibility no view in the collaboration window can change, and
 // the slots of the other leaves (up to kChunkList; more = the chunk is scanned whole)
-constexpr int kChunkList = 8;
+constexpr int kChunkList = 12;  // (a multiple of 4: the record's slot list is read 16 bytes at a time)
 constexpr int kCsumRows = 4 + 5 * kChunkList;  // ints per chunk record (Eng::csum_update)
 // superchunks (64 chunks) whose chunk lengths one round of loads fetches; prefix2's list capacity
 constexpr int kDirtyBatch = 4;
@@ -802,8 +802,15 @@ struct Eng {
             v4i hv[kChunkList];
 #pragma unroll
             for (int j = 0; j < kChunkList; j++) hv[j] = ld4(r + 4 + 4 * j);
-            const v4i s0 = ld4(r + 4 + 4 * kChunkList), s1 = ld4(r + 8 + 4 * kChunkList);
-            const int slt[kChunkList] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            int slt[kChunkList];
+#pragma unroll
+            for (int j = 0; j < kChunkList; j += 4) {
+                const v4i sj = ld4(r + 4 + 4 * kChunkList + j);
+                slt[j] = sj.x;
+                slt[j + 1] = sj.y;
+                slt[j + 2] = sj.z;
+                slt[j + 3] = sj.w;
+            }
             const bool listed = e < n && h.w <= kChunkList;
             int sum = h.z;
 #pragma unroll
