@@ -2953,11 +2953,43 @@ struct Eng {
     // range where a leaf longer than 256 units would link falls back to the serial walk.
     // Returns #kept, or -1 when the caller must run the serial walk (nothing was modified).
     static MTR_DI int scour_par(D& L, const KParams& P, St& s, int cs, int ce) {
+        return scour_lanes(L, P, s, cs, cs + lane_id(), cs + lane_id() < ce, ce - 1);
+    }
+    // HBM-resident documents: a range of more than 64 slots whose leaves (hole slots aside) fit in 64
+    // lanes -- each lane takes one of them in slot order; -1 when more than 64 remain
+    static MTR_DI int scour_gather(D& L, const KParams& P, St& s, int cs, int ce) {
+        if constexpr (G) {
+            const lptr<int> slot = dlist(L);  // (prefix2's chunk list: not in use during zamboni)
+            int n = 0;
+            for (int b = cs; b < ce; b += 64 * GK) {
+                uint32_t mq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) mq[q] = L.meta[min(b + 64 * q + lane_id(), ce - 1)];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = b + 64 * q + lane_id();
+                    // a hole slot (M_DEL, no block start) takes no part in the scour's chains or boundaries
+                    const bool keep = i < ce && !((mq[q] & M_DEL) && bnd_of(mq[q]) == 0);
+                    const uint64_t km = __ballot(keep);
+                    const int at = n + __popcll(km & lanes_below());
+                    if (keep && at < 64) slot[at] = i;
+                    n += __popcll(km);
+                }
+                if (n > 64) return -1;
+            }
+            wsync();
+            const bool in = lane_id() < n;
+            const int mine = in ? slot[lane_id()] : cs;
+            wsync();
+            return scour_lanes(L, P, s, cs, mine, in, ce - 1);
+        }
+        return -1;
+    }
+    // the lane-parallel scour over the leaves lanes hold (slot i, in = the lane holds one), in slot order
+    static MTR_DI int scour_lanes(D& L, const KParams& P, St& s, int cs, int i, bool in, int clamp) {
         const int minseq = s.minseq;
         const int ln = lane_id();
-        const int i = cs + ln;
-        const bool in = i < ce;
-        const int ic = min(i, ce - 1);
+        const int ic = in ? i : min(cs, clamp);
         const uint32_t vm0 = L.meta[ic], vp = L.props[ic], vt = L.text[ic];
         const int vr0 = L.rseq[ic], vs = L.seq[ic], vl0 = L.len[ic];
         const uint32_t vu = X ? L.uid[ic] : 0u;  // (local references follow appends)
@@ -3043,7 +3075,7 @@ struct Eng {
                         }
                 }
                 if (PM) {  // BaseSegment.append: lengths only
-                    if (ln == 0) L.len[cs + h] = total;
+                    if (ln == 0) L.len[rdlane(i, h)] = total;
                     PROF_COUNT(P_NMERGE);
                     wsync();
                     continue;
@@ -3070,9 +3102,10 @@ struct Eng {
                 const uint32_t me = rdlane(vm, e), mh = rdlane(vm, h);
                 const bool nonl = __ballot(mine && !(vm & M_NONL)) == 0 && (mh & M_NONL);
                 if (ln == 0) {
-                    L.len[cs + h] = total;
-                    L.text[cs + h] = base;
-                    L.meta[cs + h] = (mh & ~(M_NL | M_NLQ | M_NONL)) | (me & (M_NL | M_NLQ)) | (nonl ? M_NONL : 0u);
+                    const int hs = rdlane(i, h);
+                    L.len[hs] = total;
+                    L.text[hs] = base;
+                    L.meta[hs] = (mh & ~(M_NL | M_NLQ | M_NONL)) | (me & (M_NL | M_NLQ)) | (nonl ? M_NONL : 0u);
                 }
                 PROF_COUNT(P_NMERGE);
                 wsync();
@@ -3099,7 +3132,7 @@ struct Eng {
         int kept;
         {
             PROF(P_SCOUR1);
-            kept = re1 - rs1 <= 64 ? scour_par(L, P, s, rs1, re1) : -1;
+            kept = re1 - rs1 <= 64 ? scour_par(L, P, s, rs1, re1) : scour_gather(L, P, s, rs1, re1);
             if (kept < 0) kept = scour_range(L, P, s, rs1, re1);
         }
         // block.needsScour = false, kept on the block's first surviving leaf (a block of an HBM-resident
@@ -3141,7 +3174,8 @@ struct Eng {
                     // scoured: scourNode is not idempotent (a dropped tombstone no longer resets
                     // the merge candidate), zamboni.ts:68-73,122-193.
                     PROF(P_SPLIT1);
-                    if (pe - ps > 64 || scour_par(L, P, s, ps, pe) < 0) scour_range(L, P, s, ps, pe);
+                    if ((pe - ps <= 64 ? scour_par(L, P, s, ps, pe) : scour_gather(L, P, s, ps, pe)) < 0)
+                        scour_range(L, P, s, ps, pe);
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
                 constexpr int ZK = G ? GK : 1;  // (HBM: GK rounds of loads in flight)
