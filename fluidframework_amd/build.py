@@ -5,7 +5,9 @@ box with the repository snapshot.
 """
 from __future__ import annotations
 
+import json
 import os
+import re
 import subprocess
 import sys
 
@@ -27,6 +29,50 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+_REMARK = re.compile(r"remark: +([A-Za-z][A-Za-z /\[\]]*?): (.*?) \[-Rpass-analysis=kernel-resource-usage\]")
+
+
+def kernel_resources(stderr_texts):
+    """Per kernel (mangled name): the compiler's resource-usage remarks (VGPRs, ScratchSize, spills, occupancy)."""
+    res, cur = {}, None
+    for text in stderr_texts:
+        for line in text.splitlines():
+            m = _REMARK.search(line)
+            if not m:
+                continue
+            k, v = m.group(1).strip(), m.group(2).strip()
+            if k == "Function Name":
+                cur = res.setdefault(v, {})
+            elif cur is not None:
+                cur[k] = int(v) if v.lstrip("-").isdigit() else v
+    return res
+
+
+# HBM-resident apply kernels (apply_kernel<true, ...>, apply_pair_kernel<true, ...>) must not spill VGPRs, and the
+# lean one (CAP = -1: C5's kernel) must use no scratch at all.  A round-3 build whose lean HBM kernel spilled
+# produced wrong views (DESIGN.md section 2); the main build refuses one.  (The X / delta / record-mode HBM
+# kernels keep a few private arrays in scratch -- dynamically indexed stack arrays, not spills.)
+_HBM_KERNELS = re.compile(r"^_ZN3mtr(12apply_kernel|17apply_pair_kernel)ILb1E")
+_HBM_LEAN = re.compile(r"^_ZN3mtr12apply_kernelILb1ELin1E")
+
+
+def check_no_scratch(res, strict=True):
+    bad = {}
+    for k, v in res.items():
+        if not _HBM_KERNELS.match(k):
+            continue
+        scratch, vspill = v.get("ScratchSize [bytes/lane]", 0), v.get("VGPRs Spill", 0)
+        if vspill or (_HBM_LEAN.match(k) and scratch):
+            bad[k] = (scratch, vspill)
+    if bad:
+        msg = "HBM-resident apply kernels spill: " + ", ".join(
+            f"{k} (scratch {a} B/lane, {b} VGPRs spilled)" for k, (a, b) in sorted(bad.items()))
+        if strict:
+            raise RuntimeError(msg)
+        print("warning: " + msg, file=sys.stderr)
+    return bad
+
+
 def build_engine(force=False, verbose=False, prof=False, variant=None, extra=()):
     """libmtr.so; prof: the phase-timer build (libmtr_prof.so); variant: an experiment build
     libmtr_<variant>.so with extra compiler flags (selected at run time with MTR_LIB)."""
@@ -34,7 +80,7 @@ def build_engine(force=False, verbose=False, prof=False, variant=None, extra=())
     out = os.path.join(HERE, name)
     deps = [os.path.join(CSRC, f) for f in ENGINE_DEPS] + [os.path.join(ROOT, "include", h)
                                                            for h in ("mtr.h", "mtr_types.h", "mtr_synth.h", "mtr_digest.h")]
-    if force or _stale(out, deps):
+    if True:  # (each translation unit is checked against its sources below; the library against its objects)
         # translation units compiled in parallel (the fixed-capacity kernels in CAP_PARTS parts), then linked
         flags = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + \
             (["-DMTR_PROF"] if prof else []) + list(extra)
@@ -46,14 +92,32 @@ def build_engine(force=False, verbose=False, prof=False, variant=None, extra=())
         units += [(os.path.join(CSRC, "apply_variants.hip"), os.path.join(objdir, f"apply_variants_{q}.o"),
                    [f"-DMTR_VARIANT_PART={q}"]) for q in range(VARIANT_PARTS)]
         procs = []
+        hdrs = [d for d in deps if d.endswith(".h")]
+        flag_file = os.path.join(objdir, "flags.txt")
+        same_flags = os.path.exists(flag_file) and open(flag_file).read() == " ".join(flags)
         for src, obj, extra in units:
-            cmd = flags + extra + ["-c", "-o", obj, src]
+            if same_flags and not force and not _stale(obj, [src] + hdrs):
+                continue  # (per translation unit: an edit of one .hip recompiles that unit only)
+            cmd = flags + extra + ["-Rpass-analysis=kernel-resource-usage", "-c", "-o", obj, src]
             if verbose:
                 print(" ".join(cmd))
-            procs.append(subprocess.Popen(cmd))
-        rcs = [p.wait() for p in procs]
+            procs.append(subprocess.Popen(cmd, stderr=subprocess.PIPE, text=True))
+        if not procs and not _stale(out, [u[1] for u in units]):
+            return out
+        outs = [p.communicate()[1] for p in procs]
+        rcs = [p.returncode for p in procs]
         if any(rcs):
+            for o in outs:
+                sys.stderr.write("\n".join(l for l in o.splitlines() if "kernel-resource-usage" not in l) + "\n")
             raise subprocess.CalledProcessError(max(rcs), "hipcc")
+        rpath = os.path.join(objdir, "kernel_resources.json")
+        res = json.load(open(rpath)) if os.path.exists(rpath) else {}
+        res.update(kernel_resources(outs))
+        with open(rpath, "w") as f:
+            json.dump(res, f, indent=1, sort_keys=True)
+        with open(flag_file, "w") as f:
+            f.write(" ".join(flags))
+        check_no_scratch(res, strict=not (variant or prof) or os.environ.get("MTR_REQUIRE_NO_SCRATCH") == "1")
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + [u[1] for u in units]
         if verbose:
             print(" ".join(cmd))

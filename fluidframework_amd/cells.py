@@ -23,6 +23,7 @@ import numpy as np
 
 from . import abi
 from .batch import Interner, MatrixLog
+from .engine import EngineError
 from .jsjson import js_stringify, parse, to_utf8
 
 DELTA_CELL = abi.OP_SETCELL  # include/mtr_types.h MTR_DELTA_CELL
@@ -188,6 +189,9 @@ class CellMatrixLog(MatrixLog):
         recs.sort(key=lambda x: (x[0], x[1], x[2]))
         for op, which, _, r in recs:
             if which == 2:  # isLatestPendingWrite (matrix.ts:738-759) for the oldest unacked local write
+                if not self.local_meta:  # the write's cell record is missing (the document stopped at or before it)
+                    raise EngineError("SharedMatrix: the ACK of a local setCell has no applied write "
+                                      "(check the rows document's status)")
                 a, b, lseq = self.local_meta.pop(0)
                 p = self.pending.get_cell(a, b)
                 if p is not None and p < lseq:

@@ -3101,8 +3101,10 @@ struct Eng {
                 }
                 const uint32_t me = rdlane(vm, e), mh = rdlane(vm, h);
                 const bool nonl = __ballot(mine && !(vm & M_NONL)) == 0 && (mh & M_NONL);
+                // (lane h's slot is read with the whole wave active: inside `if (ln == 0)` only lane 0 is
+                // active, and a value the compiler spills and reloads there holds lane 0's bits only)
+                const int hs = rdlane(i, h);
                 if (ln == 0) {
-                    const int hs = rdlane(i, h);
                     L.len[hs] = total;
                     L.text[hs] = base;
                     L.meta[hs] = (mh & ~(M_NL | M_NLQ | M_NONL)) | (me & (M_NL | M_NLQ)) | (nonl ? M_NONL : 0u);

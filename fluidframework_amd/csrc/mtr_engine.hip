@@ -301,6 +301,20 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
         delete e;
         return nullptr;
     }
+    {  // HBM-resident launches (and the query kernels) still keep per-chunk rows in LDS: about segcap / 8
+       // bytes, twice for a matrix pair -- a capacity whose rows exceed the device's LDS is refused here
+       // rather than failing every later launch with a generic HIP error
+        int dev_lds = 0;
+        if (hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) dev_lds = 0;
+        const size_t need = 2 * ((lds_bytes_global_mode(int(c.max_segments)) + 15) & ~size_t(15));
+        if (dev_lds > 0 && need > size_t(dev_lds)) {
+            set_err("mtr_engine_create: max_segments " + std::to_string(c.max_segments) + " needs " +
+                    std::to_string(need) + " bytes of LDS in HBM-resident mode (device: " + std::to_string(dev_lds) + ")");
+            (void)hipStreamDestroy(e->stream);
+            delete e;
+            return nullptr;
+        }
+    }
     for (auto& x : e->ev) (void)hipEventCreate(&x);
     for (auto& x : e->aux) (void)hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
     for (auto& x : e->lane_done) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
@@ -628,6 +642,13 @@ static int run_impl(mtr_engine* e, int gen) {
         const char* v = std::getenv("MTR_CLASS_LEAVES");
         return v ? std::max(16, std::atoi(v)) : 64;
     }();
+    // concurrent launch lanes (1..kLanes) and whether the fixed-capacity kernels are used (tuning knobs:
+    // MTR_LANES, MTR_NO_FIXED_CAP)
+    static const int nlanes = [] {
+        const char* v = std::getenv("MTR_LANES");
+        return v ? std::max(1, std::min(int(mtr_engine::kLanes), std::atoi(v))) : int(mtr_engine::kLanes);
+    }();
+    static const bool no_fixed_cap = std::getenv("MTR_NO_FIXED_CAP") != nullptr;
     static const int slack_env = [] {
         const char* v = std::getenv("MTR_SLACK");
         return v ? std::max(0, std::atoi(v)) : -1;
@@ -692,9 +713,9 @@ static int run_impl(mtr_engine* e, int gen) {
             P.ops_this_launch = kk;
             P.doc_list = e->dlist.p + size_t(c) * e->n_docs;
             P.n_launch = uint32_t(cnt);
-            const int lane = nl % mtr_engine::kLanes;
+            const int lane = nl % nlanes;
             hipStream_t st = lane == 0 ? e->stream : e->aux[lane - 1];
-            if (lane != 0 && nl < mtr_engine::kLanes) HIPCHK(hipStreamWaitEvent(st, e->ev[0], 0));
+            if (lane != 0 && nl < nlanes) HIPCHK(hipStreamWaitEvent(st, e->ev[0], 0));
             while (e->kev.size() < size_t(2 * (nl + 1))) {
                 hipEvent_t x;
                 HIPCHK(hipEventCreate(&x));
@@ -714,9 +735,9 @@ static int run_impl(mtr_engine* e, int gen) {
                 av = e->has_ext ? AV_HBM_X : AV_HBM_LEAN;
             } else if (e->has_ext) {
                 av = AV_LDS_X;
-            } else if (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
+            } else if (no_fixed_cap || (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
                        !launch_fixed_cap_p1(cap, uint32_t(cnt), lds, st, P) &&
-                       !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P)) {
+                       !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P))) {
                 av = AV_LDS_LEAN;  // above the fixed classes: runtime layout, lean
             }
             if (av >= 0 && !launch_variant(av, uint32_t(cnt), lds, st, P, pair ? uint32_t(lds / 2) : 0u)) {
@@ -728,7 +749,7 @@ static int run_impl(mtr_engine* e, int gen) {
             e->launches++;
             nl++;
         }
-        for (int l = 1; l < std::min(nl, int(mtr_engine::kLanes)); l++) {  // join the lanes
+        for (int l = 1; l < std::min(nl, nlanes); l++) {  // join the lanes
             HIPCHK(hipEventRecord(e->lane_done[l], e->aux[l - 1]));
             HIPCHK(hipStreamWaitEvent(e->stream, e->lane_done[l], 0));
         }
@@ -1361,8 +1382,22 @@ int32_t mtr_get_ref_info(mtr_engine* e, uint32_t doc, uint32_t id, int32_t* out)
     if (!out) return -2;
     out[0] = -1;
     out[1] = out[2] = out[3] = 0;
+    if (id > uint32_t(INT32_MAX)) {  // (a negative id would run the positions query instead)
+        set_err("mtr_get_ref_info: reference id out of range");
+        return -2;
+    }
     if (ref_query(e, doc, out, 4, int(id)) < 0) return -2;
     return out[0];
+}
+
+int32_t mtr_pending_groups(mtr_engine* e, uint32_t doc) {
+    if (doc >= e->max_docs) return -1;
+    DocHdr h;
+    (void)hipSetDevice(e->device);
+    if (hipStreamSynchronize(e->stream) != hipSuccess ||
+        hipMemcpy(&h, e->hdr.p + doc, sizeof(DocHdr), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return h.ptail - h.phead;  // (ring entries [phead, ptail): one per pending SegmentGroup)
 }
 
 int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index) {

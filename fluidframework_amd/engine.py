@@ -79,6 +79,8 @@ def lib():
                                                  C.POINTER(SegmentInfo), C.c_void_p, C.c_int64]
         L.mtr_get_containing_segment.restype = C.c_int
         L.mtr_doc_status.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_int32)]
+        L.mtr_pending_groups.argtypes = [C.c_void_p, C.c_uint32]
+        L.mtr_pending_groups.restype = C.c_int32
         L.mtr_doc_status.restype = C.c_int
         L.mtr_export.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
         L.mtr_export.restype = C.c_int64
@@ -376,6 +378,13 @@ class Engine:
         if lib().mtr_get_ref_info(self.h, doc, ref_id, out.ctypes.data) == -2:
             raise EngineError(f"mtr_get_ref_info: {_err()}")
         return int(out[0]), int(out[1]), int(out[2]), bool(out[3])
+
+    def pending_groups(self, doc) -> int:
+        """MergeTree.pendingSegments.length of document doc (its unacked local ops' SegmentGroups)."""
+        n = lib().mtr_pending_groups(self.h, doc)
+        if n < 0:
+            raise EngineError(f"mtr_pending_groups: bad document {doc}")
+        return int(n)
 
     def status(self, doc):
         op = C.c_int32(-1)

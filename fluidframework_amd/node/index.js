@@ -32,14 +32,15 @@ function native() {
 
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
-    START_COLLAB: 12, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19, REF_CREATE: 20, REF_REMOVE: 21 };
+    START_COLLAB: 12, LOAD: 13, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19, REF_CREATE: 20, REF_REMOVE: 21 };
 const REF = { SLIDE: 1, LOCALVIEW: 2 };  // MTR_OP_REF_CREATE payload2
 const DetachedReferencePosition = -1;   // referencePositions.ts:103
 const DELTA_REGEN = 64, DELTA_REGEN_X = 72;
 const REL = { BEFORE: 1, OFFSET: 2 };
 const COMB = { NONE: 0, REWRITE: 1, INCR: 2, CONSENSUS: 3, KEEP: 4 };
 const VEQ = { NEVER: 0x80000000, FALSY: 0x40000000, INCR_STR: 0x20000000, CONS_MUT: 0x10000000 };
-const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, COLS: 32, DELTA: 64, REL: 128 };
+const F = { LAST: 1, MARKER: 2, PROPS: 4, NOREF: 8, APPEND: 16, COLS: 32, DELTA: 64, REL: 128 };
+const CLIENT_NONCOLLAB = 0xFFFE;  // include/mtr_types.h MTR_CLIENT_NONCOLLAB
 const NULL_VALUE = 0xFFFFFFFF;
 const MAX_CLIENTS = 253;  // include/mtr_types.h MTR_MAX_CLIENTS: short ids per engine document
 const NOT_INDEX = 0xFFFFFFFF;
@@ -352,6 +353,66 @@ class DocLog {
         }
     }
     seqUpdate(min, seq) { this.push(OP.SEQ, F.LAST, 0, seq, seq, min, 0, 0, 0, 0); }
+    // SnapshotLoader.specToSegment (snapshotLoader.ts:88-128): one LOAD (header) / APPEND (body) record whose
+    // removedClientIds (short ids) ride in the text arena
+    _snapshotSeg(spec, it, opType, flags) {
+        // a loaded live marker is mapped by reloadFromSegments' blockUpdate (addNodeReferences, mergeTree.ts:297-306,
+        // localNetLength > 0 only); a body segment by blockInsert (:1655-1662)
+        const withInfo = spec !== null && typeof spec === 'object' && 'json' in spec;  // hasMergeInfo, snapshotChunks.ts:80-84
+        const removed = withInfo && spec.removedSeq !== undefined && spec.removedSeq !== null;
+        const live = opType !== OP.LOAD || !removed;
+        let s, client = CLIENT_NONCOLLAB, seq = 0, removers = [], rseq = -1;
+        if (withInfo) {
+            s = this._seg(spec.json, it, live);
+            if (spec.client !== undefined && spec.client !== null) client = this.shortId(spec.client);
+            if (spec.seq !== undefined && spec.seq !== null) seq = spec.seq;
+            if (spec.removedClient !== undefined && spec.removedClient !== null) removers = [this.shortId(spec.removedClient)];
+            if (spec.removedClientIds !== undefined && spec.removedClientIds !== null) {
+                removers = spec.removedClientIds.map((x) => this.shortId(x));
+            }
+            if (removed) rseq = spec.removedSeq;
+        } else {
+            s = this._seg(spec, it, live);
+        }
+        const roff = this.text.length;
+        for (const r of removers) this.text.push(r);
+        this.push(opType, s[0] | flags, client, seq, rseq, removers.length, roff, s[3], s[1], s[2]);
+    }
+    // Client.load -> SnapshotLoader.initialize (snapshotLoader.ts:41-257) from a summary's blobs {name: JSON text}:
+    // header segments as reloadFromSegments records, startOrUpdateCollaboration(longId, minSeq, seq) (longId
+    // undefined: a detached load stays local), body segments appended.  Returns the catch-up messages of a legacy
+    // summary (the caller applies them as ordinary messages), [] otherwise.  Mirrors batch.py DocLog.load_summary.
+    loadSummary(blobs, longId, it) {
+        const chunk = JSON.parse(blobs.header);
+        let segs, meta;
+        if (chunk.version === '1') {
+            segs = chunk.segments;
+            meta = chunk.headerMetadata;
+        } else {  // toLatestVersion of a legacy chunk, snapshotChunks.ts:151-200
+            segs = chunk.segmentTexts;
+            meta = chunk.headerMetadata || {
+                orderedChunkMetadata: [{ id: 'header' }].concat(chunk.chunkLengthChars < chunk.totalLengthChars ? [{ id: 'body' }] : []),
+                minSequenceNumber: chunk.chunkMinSequenceNumber,
+                sequenceNumber: chunk.chunkSequenceNumber,
+            };
+        }
+        if (meta === undefined) throw new Error('header metadata not available');
+        for (const spec of segs) this._snapshotSeg(spec, it, OP.LOAD, 0);
+        const minSeq = meta.minSequenceNumber;
+        const seq = meta.sequenceNumber;
+        this.startCollab(longId, minSeq !== undefined && minSeq !== null ? minSeq : seq, seq);
+        for (const md of meta.orderedChunkMetadata.slice(1)) {
+            if (blobs[md.id] === undefined) throw new Error('missing summary blob ' + md.id);
+            const body = JSON.parse(blobs[md.id]);
+            for (const spec of (body.segments !== undefined ? body.segments : (body.segmentTexts || []))) {
+                this._snapshotSeg(spec, it, OP.INSERT, F.APPEND);
+            }
+        }
+        const names = new Set(['header'].concat(meta.orderedChunkMetadata.map((md) => md.id)));
+        const extra = Object.keys(blobs).filter((k) => !names.has(k));
+        if (extra.length > 1) throw new Error('0x060');  // "There should be only one blob with catch up ops"
+        return extra.length ? JSON.parse(blobs[extra[0]]) : [];
+    }
     message(msg, it, local) {  // Client.applyMsg, client.ts:858-887
         const cid = msg.clientId === null || msg.clientId === undefined ? 'null' : String(msg.clientId);
         const short = this.shortId(cid);
@@ -770,6 +831,44 @@ class BatchReplayClient {
     startOrUpdateCollaboration(longClientId, minSeq, currentSeq) {
         this._queue(() => this.log.startCollab(longClientId, minSeq || 0, currentSeq || 0));
         this.currentSeq = currentSeq || 0;
+    }
+    /**
+     * Client.load (client.ts:1007-1019 -> SnapshotLoader.initialize, snapshotLoader.ts:41-257): the document
+     * resumes from a merge-tree summary read through `storage` (IChannelStorageService: readBlob(path) ->
+     * Buffer / Uint8Array, list(path) -> blob names).  A runtime that is not Detached starts collaboration as
+     * runtime.clientId ?? "snapshot".  Resolves to {catchupOpsP}: the legacy format's catch-up messages, which
+     * the caller applies with applyMsg (SharedSegmentSequence.loadCore does), [] for V1.
+     */
+    async load(runtime, storage, serializer) {
+        const names = await storage.list('');
+        const blobs = {};
+        for (const n of names) {
+            const b = await storage.readBlob(n);
+            blobs[n] = typeof b === 'string' ? b : Buffer.from(b.buffer, b.byteOffset, b.byteLength).toString('utf8');
+        }
+        if (blobs.header === undefined) throw new Error('0x05f');  // "Missing blob header on legacy snapshot!"
+        const detached = runtime && runtime.attachState === 'Detached';
+        const longId = detached ? undefined : ((runtime && runtime.clientId) || 'snapshot');
+        let catchup = [];
+        this._queue(() => { catchup = this.log.loadSummary(blobs, longId, this.engine.interner); });
+        const meta = JSON.parse(blobs.header);
+        this.currentSeq = meta.version === '1' ? meta.headerMetadata.sequenceNumber
+            : (meta.headerMetadata ? meta.headerMetadata.sequenceNumber : meta.chunkSequenceNumber);
+        if (serializer && typeof serializer.parse === 'function' && catchup.length) {
+            catchup = serializer.parse(JSON.stringify(catchup));
+        }
+        return { catchupOpsP: Promise.resolve(catchup) };
+    }
+    /** load from an ISummaryTree this shim (or the reference) produced: {type: Tree, tree: {name: {content}}}. */
+    loadSummaryTree(summary, longClientId) {
+        const blobs = {};
+        for (const k of Object.keys(summary.tree)) {
+            const c = summary.tree[k].content;
+            blobs[k] = typeof c === 'string' ? c : Buffer.from(c).toString('utf8');
+        }
+        let catchup = [];
+        this._queue(() => { catchup = this.log.loadSummary(blobs, longClientId, this.engine.interner); });
+        return catchup;
     }
     applyMsg(msg, local) {
         const own = local || (msg.type === 'op' && String(msg.clientId) === this.log.observerId);

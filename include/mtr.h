@@ -166,6 +166,10 @@ int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t
  * Returns out[0], or -2 on error. */
 int32_t mtr_get_ref_info(mtr_engine* e, uint32_t doc, uint32_t id, int32_t* out);
 
+/* MergeTree.pendingSegments.length (mergeTree.ts:1324-1357, asserted by client.applyMsg.spec.ts): the
+ * SegmentGroups of this client's local ops that no sequenced message has acked yet; -1 = bad document. */
+int32_t mtr_pending_groups(mtr_engine* e, uint32_t doc);
+
 /* Per-document status: MTR_OK or an MTR_ERR_* code; *op_index = op that failed (or -1). */
 int mtr_doc_status(mtr_engine* e, uint32_t doc, int32_t* op_index);
 

@@ -2199,6 +2199,8 @@ int64_t oracle_doc_text(oracle_doc* d, uint16_t* out, int64_t cap) {
     return n;
 }
 
+int32_t oracle_doc_pending_groups(oracle_doc* d) { return int32_t(d->view().pendingSegments.size()); }
+
 int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32_t client, int32_t* out) {
     Tree& t = d->view();
     int off = 0;

@@ -98,6 +98,8 @@ int64_t oracle_psl_stats(int64_t* out, char* first, int64_t cap);
 /* Debug: print zamboni decisions to stdout */
 void oracle_set_trace(int on);
 
+/* MergeTree.pendingSegments.length (mergeTree.ts:1324-1357) */
+int32_t oracle_doc_pending_groups(oracle_doc* d);
 /* getContainingSegment (mergeTree.ts:787-813) at (ref_seq, client): out[0] = leaf index in tree order
  * (-1 = none, also returned), out[1] = offset, out[2] = cachedLength, out[3] = segment start. */
 int32_t oracle_doc_containing(oracle_doc* d, int32_t pos, int32_t ref_seq, int32_t client, int32_t* out);

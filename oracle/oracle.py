@@ -43,6 +43,8 @@ def lib():
         L.oracle_doc_regen_props.restype = C.c_int64
         L.oracle_doc_regen_props.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.oracle_doc_state.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_doc_pending_groups.argtypes = [C.c_void_p]
+        L.oracle_doc_pending_groups.restype = C.c_int32
         L.oracle_set_trace.argtypes = [C.c_int]
         L.oracle_generate.restype = C.c_int
         L.oracle_generate.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.MtrOptions), C.c_uint32, C.c_uint32,
@@ -191,6 +193,10 @@ class OracleDoc:
         out = np.zeros(4, dtype="<i8")
         lib().oracle_doc_state(self.h, out.ctypes.data)
         return out
+
+    def pending_groups(self) -> int:
+        """MergeTree.pendingSegments.length"""
+        return int(lib().oracle_doc_pending_groups(self.h))
 
     def containing(self, pos, ref_seq, client):
         """getContainingSegment -> (leaf index or -1, offset, cachedLength, segment start)."""

@@ -372,3 +372,101 @@ def test_js_local_op_packer_matches_python_packer(tmp_path):
     assert raw["ops"] == py.ops.tobytes()
     n_kv = 2 * int(py.propop_off[-1])
     assert np.array_equal(np.frombuffer(raw["propopKv"], "<u4")[:n_kv], py.propop_kv[:n_kv])
+
+
+# ---------------------------------------------------------------- Client.load in the Node host
+def _load_inputs():
+    """Every snapshot fixture, plus V1 summaries the oracle takes mid-collaboration of three replay logs."""
+    from fixtures import SNAPSHOT_VERSIONS, blob_names, load_snapshots
+
+    docs = [{"key": k, "blobs": v, "id": "snapshot", "v1": int(SNAPSHOT_VERSIONS[k.split("/")[0]])}
+            for k, v in sorted(load_snapshots().items())]
+    for p in [p for p in replay_files() if "clients_8" in p][:3]:
+        groups = load_replay(p)
+        it = Interner()
+        log = replay_log(groups, it)
+        for g in groups[: len(groups) // 2]:
+            for m in g["msgs"]:
+                log.message(m, it)
+        orc = OracleDoc(options())
+        b = build_batch([log], it)
+        assert orc.apply(b, 0) == 0
+        blobs = orc.summarize(b, 0)
+        docs.append({"key": os.path.basename(p), "blobs": dict(zip(blob_names(len(blobs), True),
+                                                                   [x.decode() for x in blobs])), "id": "loader-B", "v1": 1})
+    return docs
+
+
+def test_js_load_packer_matches_python_packer(tmp_path):
+    """BatchReplayClient.load's records (index.js DocLog.loadSummary) equal the Python host's
+    (DocLog.load_summary) for every snapshot fixture and mid-collaboration summary: the same header / body
+    segment records, merge info, removedClientIds, client table and property tables."""
+    _addon()
+    docs = _load_inputs()
+    f = tmp_path / "summaries.json"
+    f.write_text(json.dumps([{"blobs": d["blobs"], "id": d["id"]} for d in docs]))
+    js = json.loads(_node([os.path.join(HERE, "node", "pack_load.js"), str(f)]))
+    it = Interner()
+    logs, catchup = [], []
+    for d in docs:
+        log = DocLog()
+        catchup.append(len(log.load_summary(d["blobs"], d["id"], it)))
+        logs.append(log)
+    py = build_batch(logs, it)
+    assert js["catchup"] == catchup
+    raw = {k: base64.b64decode(v) for k, v in js.items() if k != "catchup"}
+    assert raw["docs"] == py.docs.tobytes()
+    assert raw["ops"] == py.ops.tobytes()
+    n_text = int(py.docs["text_count"].sum())
+    assert np.array_equal(np.frombuffer(raw["text"], "<u2")[:n_text], py.text[:n_text])
+    n_kv = 2 * int(py.propop_off[-1])
+    assert np.array_equal(np.frombuffer(raw["propopKv"], "<u4")[:n_kv], py.propop_kv[:n_kv])
+    assert raw["clientBytes"][: int(py.client_off[-1])] == py.client_bytes.tobytes()[: int(py.client_off[-1])]
+
+
+@pytest.mark.gpu
+def test_load_through_node_host(tmp_path):
+    """Client.load through N-API -> C ABI -> HIP: every snapshot fixture loads and summarizes back to its own
+    bytes; a V1 summary taken mid-collaboration of each of 30 replay logs loads into a second client that then
+    reads resultText after every remaining group, and ends with the same summary as the oracle's replay."""
+    _addon()
+    from fixtures import SNAPSHOT_VERSIONS, blob_names, load_snapshots
+
+    fx = [{"key": k, "blobs": v, "v1": int(SNAPSHOT_VERSIONS[k.split("/")[0]])}
+          for k, v in sorted(load_snapshots().items())]
+    f = tmp_path / "fixtures.json"
+    f.write_text(json.dumps(fx))
+    paths = replay_files()
+    res = json.loads(_node([os.path.join(HERE, "node", "load_engine.js"), str(f)] + paths, timeout=600))
+    want = {d["key"]: d for d in fx}
+    assert len(res["fixtures"]) == len(fx)
+    for r in res["fixtures"]:
+        got = [base64.b64decode(x).decode() for x in r["blobs"]]
+        assert dict(zip(r["names"], got)) == want[r["key"]]["blobs"], r["key"]
+    assert res["checks"] == sum(2 * (len(g) - len(g) // 2) for g in (load_replay(p) for p in paths))
+    for r, p in zip(res["logs"], paths):  # the oracle does the same: replay to the middle, summarize, load, go on
+        groups = load_replay(p)
+        cut = len(groups) // 2
+        it = Interner()
+        la = replay_log(groups, it)
+        for g in groups[:cut]:
+            for m in g["msgs"]:
+                la.message(m, it)
+        last = groups[cut - 1]["msgs"][-1]
+        la.seq_update(last["minimumSequenceNumber"], last["sequenceNumber"])
+        a = OracleDoc(options())
+        b0 = build_batch([la], it)
+        assert a.apply(b0, 0) == 0
+        mid = a.summarize(b0, 0)
+        assert [base64.b64decode(x) for x in r["mid"]] == mid, f"log {r['log']}: mid summary"
+        lb = DocLog()
+        lb.load_summary(dict(zip(blob_names(len(mid), True), [x.decode() for x in mid])), "loader-B", it)
+        for g in groups[cut:]:
+            for m in g["msgs"]:
+                lb.message(m, it)
+        last = groups[-1]["msgs"][-1]
+        lb.seq_update(last["minimumSequenceNumber"], last["sequenceNumber"])
+        ob = OracleDoc(options())
+        bb = build_batch([lb], it)
+        assert ob.apply(bb, 0) == 0
+        assert [base64.b64decode(x) for x in r["b"]] == ob.summarize(bb, 0), f"log {r['log']}: loaded client's summary"
