@@ -53,21 +53,28 @@ GROW = {"C5": 200_000}
 MATRIX = {"C4"}
 
 
-def host_cores() -> int:
-    """Host cores this process may use: its CPU affinity, capped by the cgroup CPU quota and by
-    OMP_NUM_THREADS when the environment sets it (the GPU box gives one GPU's job a 16-core share of
-    a much larger machine, which os.cpu_count() does not show)."""
+def host_cores_limit() -> tuple[int, str]:
+    """Host cores this process may use and the limit that set it: its CPU affinity, capped by the cgroup
+    CPU quota and by OMP_NUM_THREADS when the environment sets it (the GPU box gives one GPU's job a
+    16-core share of a much larger machine, which os.cpu_count() does not show)."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    why = f"CPU affinity mask ({n} cores)"
     try:
         quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
         if quota != "max":
-            n = min(n, max(1, -(-int(quota) // int(period))))
+            q = max(1, -(-int(quota) // int(period)))
+            if q < n:
+                n, why = q, f"cgroup cpu.max quota {quota}/{period} ({q} cores)"
     except (OSError, ValueError):
         pass
     omp = os.environ.get("OMP_NUM_THREADS", "")
-    if omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(1, n)
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, why = int(omp), f"OMP_NUM_THREADS={omp} (the job's allotment on the GPU box)"
+    return max(1, n), why
+
+
+def host_cores() -> int:
+    return host_cores_limit()[0]
 
 
 def parse(argv=None):
@@ -177,7 +184,9 @@ def cpu_baseline(a, eng, n, ops, grow, matrix, hashes, fixture_batch, messages):
     reproduce the engine's summary digests."""
     from oracle.oracle import psl_answer, replay_batch, replay_matrix_batch
 
-    threads = a.cpu_threads or host_cores()
+    threads, cores_why = host_cores_limit()
+    if a.cpu_threads:
+        threads, cores_why = a.cpu_threads, "--cpu-threads"
     # bounded sample: ~6e7 messages of C2/C3 documents; one pre-grown C5 document per host thread
     k = min(a.cpu_sample_docs or (threads if grow else max(1, 60_000_000 // ops)), n)
     if fixture_batch is not None:
@@ -217,6 +226,7 @@ def cpu_baseline(a, eng, n, ops, grow, matrix, hashes, fixture_batch, messages):
         "value": round(k * per_doc / secs, 1),
         "unit": "ops/s",
         "cores": threads,
+        "cores_limit": cores_why,
         "kind": "port",
         "algorithm": "PartialSequenceLengths",
         "sample": f"first {k} of the {n} {'matrices' if matrix else 'documents'} ({int(k * per_doc)} messages"

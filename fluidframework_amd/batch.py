@@ -407,6 +407,19 @@ class DocLog:
         else:
             raise Unsupported(f"local op type {t}")
 
+    def apply_stashed_op(self, op: dict, interner: Interner):
+        """Client.applyStashedOp (client.ts:830-856): a stashed op of this client (its contents, from a previous
+        session) applied as a local op; a GROUP applies each member.  Returns the local op metadata the reference
+        returns (one token per member op: the pending SegmentGroup it made, which regeneratePendingOp later takes
+        from the head of the pending queue)."""
+        if op.get("type") == 3:
+            return [self.apply_stashed_op(m, interner) for m in op["ops"]]
+        if not self.collaborating:  # peekPendingSegmentGroups() is undefined: "Applying op must generate a pending segment"
+            raise AssertionError("0x2db")
+        self.local_op(op, interner)
+        self.n_stashed = getattr(self, "n_stashed", 0) + 1
+        return {"stashed": self.n_stashed, "type": op.get("type")}
+
     def start_collab(self, long_id: str | None, min_seq: int = 0, current_seq: int = 0) -> None:
         """Client.startOrUpdateCollaboration (client.ts:1133-1155): an undefined id keeps the client
         local (detached container); the first id registers a new short id (addLongClientId, even for

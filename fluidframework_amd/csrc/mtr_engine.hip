@@ -1444,10 +1444,13 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
             }
         }
         int32_t* r = out + 8 * k++;
+        // (pending local values are kept above every sequence number, LOCAL_BASE + localSeq: reported as the
+        // reference holds them, UnassignedSequenceNumber, as the oracle export does)
+        const int32_t sq = int32_t(hd.seg[F_SEQ * sc + i]);
         r[0] = int32_t(hd.seg[F_LEN * sc + i]);
-        r[1] = int32_t(hd.seg[F_SEQ * sc + i]);
+        r[1] = sq >= LOCAL_BASE ? -1 : sq;
         r[2] = dec_client(m & M_CLIENT_MASK);
-        r[3] = rs == RNONE ? INT32_MIN : rs;
+        r[3] = rs == RNONE ? INT32_MIN : (rs >= LOCAL_BASE ? -1 : rs);
         r[4] = nrem;
         r[5] = int32_t((m & M_BND_MASK) >> M_BND_SHIFT);
         // PermutationSegment: its start handle (the oracle export does the same)

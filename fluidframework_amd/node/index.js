@@ -907,6 +907,18 @@ class BatchReplayClient {
     }
     removeRangeLocal(start, end) { this._queue(() => this.log.localRemove(start, end)); }
     /** Client.localTransaction (client.ts:1029-1048): every member op as a local (pending) op. */
+    /**
+     * Client.applyStashedOp(op) (client.ts:830-856): a stashed op of this client applied as a local op (GROUP: each
+     * member); returns the local op metadata (one token per member: its pending SegmentGroup, which
+     * regeneratePendingOp takes from the head of the pending queue).
+     */
+    applyStashedOp(op) {
+        if (op.type === 3) return op.ops.map((o) => this.applyStashedOp(o));
+        if (!this.log.collaborating) throw new Error('0x2db');  // "Applying op must generate a pending segment"
+        this._queue(() => this.log.localOp(op, this.engine.interner));
+        this.nStashed = (this.nStashed || 0) + 1;
+        return { stashed: this.nStashed, type: op.type };
+    }
     localTransaction(groupOp) {
         this._queue(() => { for (const op of groupOp.ops) this.log.localOp(op, this.engine.interner); });
     }

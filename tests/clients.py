@@ -89,6 +89,12 @@ class Clients:
         recs = regen.records(d.deltas())
         return regen.regenerated_op(op, recs, first, lambda r: regen.props_dict(d.regen_props(r), self.it))
 
+    def stash(self, c, op):
+        """Client.applyStashedOp (client.ts:830-856) -> the local op metadata"""
+        meta = self.logs[c].apply_stashed_op(op, self.it)
+        self.flush()
+        return meta
+
     def rollback(self, c, op):
         """Client.rollback (client.ts:421-423) of the newest pending op (its contents)."""
         self.logs[c].rollback(op, self.it)
