@@ -36,6 +36,9 @@ REFTYPE_SLIDE_ON_REMOVE = 0x40
 REFTYPE_STAY_ON_REMOVE = 0x80
 REFTYPE_TRANSIENT = 0x100
 DETACHED_POSITION = -1
+REF_ST_SEGMENT = 1  # mtr_get_ref_states bits (include/mtr.h)
+REF_ST_HELD = 2
+REF_ST_REMOVED = 4
 DELTA_REGEN = 64
 DELTA_REGEN_X = 72
 REL_BEFORE = 1

@@ -191,13 +191,16 @@ def combine_absent(co: dict, seq: int) -> Any:
 
 
 def _local_comb(co: Any) -> int:
-    """A local annotate's combiningOp: none, or "rewrite" (PropertiesManager.pendingRewriteCount,
-    segmentPropertiesManager.ts:72-80, 109-112); its ack / rollback records carry the same code (pos1)."""
+    """A local annotate's combiningOp as its ack / rollback records carry it (pos1): none, "rewrite"
+    (PropertiesManager.pendingRewriteCount, segmentPropertiesManager.ts:72-80, 109-112), or another name (its
+    pending key counts are kept like a plain annotate's, :126-138)."""
     if not js_truthy(co):
         return abi.COMB_NONE
-    if isinstance(co, dict) and co.get("name") == "rewrite":
+    if not isinstance(co, dict):
+        raise Unsupported("combiningOp")
+    if co.get("name") == "rewrite":
         return abi.COMB_REWRITE
-    raise Unsupported("local annotate with a combiningOp other than rewrite")
+    return {"incr": abi.COMB_INCR, "consensus": abi.COMB_CONSENSUS}.get(co.get("name"), abi.COMB_KEEP)
 
 
 @dataclass
@@ -217,6 +220,9 @@ class DocLog:
     marker_dup: set = field(default_factory=set)  # ids mapped to two markers: block-update order decides
     marker_id_annotated: bool = False              # an annotate touched "markerId": remapped by blockUpdate
     n_refs: int = 0                                # local references created (MTR_OP_REF_CREATE ids)
+    # the merge-tree client's currentSeq (collabWindow.currentSeq) as the host sees it: interval ops do not move it
+    current_seq: int = 0
+    intervals: Any = None                          # fluidframework_amd.intervals.IntervalCollections, when used
 
     def short_id(self, long_id: str) -> int:
         """Client.getOrAddShortClientId (client.ts:673-677)."""
@@ -345,7 +351,12 @@ class DocLog:
         if isinstance(props, dict) and "markerId" in props:
             self.marker_id_annotated = True
         comb = _local_comb(combining_op)
-        self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, self._local_seq(), 0, 0, start, end, interner.propop(props), comb))
+        if comb in (abi.COMB_NONE, abi.COMB_REWRITE):
+            pp = interner.propop(props)
+        else:  # combine(op, previousValue, undefined, seq) at UnassignedSequenceNumber (while collaborating) or
+            # UniversalSequenceNumber: the prop-op holds each key's absent-key result (a remote one's encoding)
+            pp, comb = interner.combining(props, combining_op, -1 if self.collaborating else 0)
+        self.ops.append((abi.OP_LOCAL_ANNOTATE, 0, 0, self._local_seq(), 0, 0, start, end, pp, comb))
 
     def rollback(self, op: dict, interner: Interner) -> None:
         """Client.rollback (client.ts:421-423 -> MergeTree.rollback, mergeTree.ts:2049-2159) of the newest
@@ -431,6 +442,7 @@ class DocLog:
             self.observer_id = long_id
             me = self.add_long_id(long_id)
             self.collaborating = True
+            self.current_seq = current_seq
             self.ops.append((abi.OP_START_COLLAB, 0, me, current_seq, 0, min_seq, 0, 0, 0, 0))
         else:
             me = self.client_ix[self.observer_id]
@@ -496,6 +508,7 @@ class DocLog:
 
     def seq_update(self, min_seq: int, seq: int) -> None:
         """Client.updateSeqNumbers(min, seq) outside a message (client.ts:877), e.g. summarize's catch-up."""
+        self.current_seq = seq
         self.ops.append((abi.OP_SEQ, abi.F_LAST, 0, seq, seq, min_seq, 0, 0, 0, 0))
 
     # -- sequenced messages (Client.applyMsg)
@@ -507,11 +520,24 @@ class DocLog:
         ref = int(msg["referenceSequenceNumber"])
         msn = int(msg["minimumSequenceNumber"])
         if msg.get("type") != "op":
+            self.current_seq = seq
             self.ops.append((abi.OP_SEQ, abi.F_LAST, short, seq, ref, msn, 0, 0, 0, 0))
             return
         contents = msg["contents"]
         if isinstance(contents, str):
             contents = parse(contents)
+        if contents.get("type") == "act":  # an interval collection's op (SharedSegmentSequence.processCore,
+            # sequence.ts:620-646: handled by the DefaultMap, never reaches the merge-tree client)
+            from .intervals import IntervalCollections, IntervalUnsupported
+
+            if self.intervals is None:
+                self.intervals = IntervalCollections()
+            try:
+                self.intervals.process(self, contents, msg)
+            except IntervalUnsupported as e:
+                raise Unsupported(str(e)) from e
+            return
+        self.current_seq = seq
         members = contents["ops"] if contents.get("type") == 3 else [contents]
         if not members:
             self.ops.append((abi.OP_SEQ, abi.F_LAST, short, seq, ref, msn, 0, 0, 0, 0))

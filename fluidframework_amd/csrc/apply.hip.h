@@ -318,6 +318,11 @@ struct Doc {
     MTR_DI gptr<uint32_t> gpend() const { return (gptr<uint32_t>)cold(CP_PEND); }  // its pending-group ring
     MTR_DI gptr<int> gcsum() const { return (gptr<int>)cold(CP_CSUM); }          // chunk summaries (len, then ev)
     MTR_DI gptr<int> gumap() const { return (gptr<int>)cold(CP_UMAP); }          // uid -> slot hints
+    // a merge chain's text copy whose load is in flight (Eng::copy_chain): lane l stores unit pc_val at pc_dst when
+    // pc_on; pc_any (uniform) when any lane has one.  The store waits for the next reader of the text arena
+    // (Eng::text_flush), so the load's HBM latency overlaps the work between two zamboni passes.
+    uint32_t pc_dst = 0, pc_val = 0;
+    int pc_on = 0, pc_any = 0;
     int rlo = 0, rhi = 0;  // the op's view-scan region (slots) when the scan was two-level (E valid there)
     int shi = 0;           // end of the slots the last shift_right1 moved (chunk-summary upkeep)
     int wlo = 0, whi = 0;  // slots the last range walk touched
@@ -359,6 +364,29 @@ MTR_DI int wave_incl_scan(int x) {
     x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return x;
 }
+
+// Lane predicates as 0 / -1 words computed on the VALU: a compare into VCC and a select, combined with
+// v_and / v_or.  Written as plain C++ booleans the compiler keeps them as 64-bit lane masks and combines those
+// with s_and_b64 / s_or_b64 on the CU's one scalar unit -- the unit that binds the C3 kernel (SALU ~60 % busy
+// against ~27 % of the VALU issue slots: a wave64 VALU op takes 2 of a SIMD-32's cycles, 4 SIMDs per CU).
+// (asm, so the compiler cannot fold two such selects back into one select of a combined lane mask)
+MTR_DI int vp_lt(int a, int b) {
+    int r;
+    asm("v_cmp_lt_i32_e32 vcc, %1, %2\n\tv_cndmask_b32_e64 %0, 0, -1, vcc" : "=v"(r) : "v"(a), "v"(b) : "vcc");
+    return r;
+}
+MTR_DI int vp_le(int a, int b) {
+    int r;
+    asm("v_cmp_le_i32_e32 vcc, %1, %2\n\tv_cndmask_b32_e64 %0, 0, -1, vcc" : "=v"(r) : "v"(a), "v"(b) : "vcc");
+    return r;
+}
+MTR_DI int vp_eq(uint32_t a, uint32_t b) {
+    int r;
+    asm("v_cmp_eq_u32_e32 vcc, %1, %2\n\tv_cndmask_b32_e64 %0, 0, -1, vcc" : "=v"(r) : "v"(a), "v"(b) : "vcc");
+    return r;
+}
+MTR_DI int vp_bit(uint32_t m, int bit) { return -int((m >> bit) & 1u); }  // -1 when bit `bit` of m is set
+MTR_DI int vp_sel(int mask, int a, int b) { return (a & mask) | (b & ~mask); }  // mask ? a : b (v_bfi_b32)
 
 // matchProperties (properties.ts:71-105) with values compared by equivalence class; a value flagged
 // MTR_VEQ_NEVER (NaN, a consensus {value: undefined, seq}) matches nothing, not even itself, so a set
@@ -532,39 +560,42 @@ struct Eng {
     }
     static MTR_DI int vis_hot(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
         const int r = vis_leaf(L, h, i, v, newlen, minseq, valid);
-        if constexpr (G) return (h.meta & M_DEL) ? -1 : r;  // a hole slot is no leaf (Eng::spread)
+        if constexpr (G) return r | vp_bit(h.meta, 25);  // a hole slot (M_DEL) is no leaf (Eng::spread)
         return r;
     }
     static MTR_DI int vis_leaf(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
+        static_assert(M_DEL == 1u << 25 && M_OVERLAP == 1u << 21, "vis_hot / vis_leaf bit positions");
         const int len = h.len;
         const int rseq = h.rseq;
         const uint32_t m = h.meta;
         const int seq = h.seq;
-        const bool removed = rseq != RNONE;
         if (v.local) {  // localNetLength, mergeTree.ts:613-634 (a uniform branch)
+            const bool removed = rseq != RNONE;
             const int rl = newlen ? 0 : (rseq > minseq ? 0 : -1);
             return removed ? rl : len;
         }
-        // Every lane evaluates the same select chain (bitwise predicates: no divergent branches and
-        // no lane masks carried across them); only lanes whose answer depends on a later remover in
-        // the overlap list walk it, behind one ballot.
-        const bool vis = ((m & M_CLIENT_MASK) == v.client) | (seq <= v.ref);
-        const bool first = removed & (((m >> M_FREM_SHIFT) & 0xffu) == v.client);
+        // Every lane evaluates the same chain of 0 / -1 predicate words (vp_*: VALU only, no lane masks and
+        // no divergent branches); only lanes whose answer depends on a later remover in the overlap list walk
+        // it, behind one ballot.
+        const int rem = ~vp_eq(uint32_t(rseq), uint32_t(RNONE));
+        const int vis = vp_eq(m & M_CLIENT_MASK, v.client) | vp_le(seq, v.ref);
+        const int first = rem & vp_eq((m >> M_FREM_SHIFT) & 0xffu, v.client);
+        const int after = vp_lt(v.ref, rseq);  // removed after the view's refSeq
         // lanes whose result still depends on removedClientIds[1..] (mergeTree.ts:935-1003)
-        const bool walk = valid & removed & !first & ((m & M_OVERLAP) != 0) & (rseq > v.ref) &
-                          (newlen ? rseq > minseq : vis);
-        int inr = first ? 1 : 0;
-        if (__ballot(walk)) inr |= later_remover(L, i, walk, v.client);
+        const int walk = (valid ? -1 : 0) & rem & ~first & vp_bit(m, 21) & after &
+                         (newlen ? vp_lt(minseq, rseq) : vis);
+        int inr = first;
+        if (__ballot(walk != 0)) inr |= -later_remover(L, i, walk != 0, v.client);
         if (newlen) {  // mergeTree.ts:935-965
-            const int live = vis ? len : 0;
-            const int gone = ((rseq <= v.ref) | (inr != 0)) ? 0 : live;
-            return removed ? (rseq <= minseq ? -1 : gone) : live;
+            const int live = vis & len;
+            const int gone = live & ~(~after | inr);
+            return vp_sel(rem, vp_le(rseq, minseq) | gone, live);
         }
         // mergeTree.ts:967-1003
-        const int seen = (removed & (inr != 0)) ? 0 : len;
+        const int seen = len & ~(rem & inr);
         // (a pending local remove is no removal here: removedSeq !== UnassignedSequenceNumber, :993-998)
-        const int r = vis ? seen : ((removed & (!X | (rseq < LOCAL_BASE))) ? -1 : 0);
-        return (removed & (rseq <= v.ref)) ? -1 : r;
+        const int r = vp_sel(vis, seen, rem & (X ? vp_lt(rseq, LOCAL_BASE) : -1));
+        return r | (rem & ~after);
     }
     // 1 when client c is in leaf i's removedClientIds[1..] (the overlap list), for the lanes in `walk`
     static MTR_DI int later_remover(const D& L, int i, bool walk, uint32_t c) {
@@ -623,9 +654,10 @@ struct Eng {
                     if (base + 64 * q >= S) break;
                     const int i = base + 64 * q + ln;
                     const int x0 = vis_hot(L, hk[q], i, v, newlen, s.minseq, i < S);
-                    const int x = i < S ? x0 : 0;
+                    const int in = vp_lt(i, S);
+                    const int x = x0 & in;
                     const int inc = wave_incl_scan(max(x, 0));
-                    if (i < S) L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
+                    L.E[vp_sel(in, i, S)] = (carry + inc) | (x & int(0x80000000u));  // (lanes past the end: slot S)
                     carry += rdlane(inc, 63);
                 }
             }
@@ -641,9 +673,12 @@ struct Eng {
             const Hot cur = h;
             if (base + 64 < S) h = ld_hot(L, i + 64);
             const int x0 = vis_hot(L, cur, i, v, newlen, s.minseq, i < S);
-            const int x = i < S ? x0 : 0;
+            const int in = vp_lt(i, S);
+            const int x = x0 & in;
             const int inc = wave_incl_scan(max(x, 0));
-            if (i < S) L.E[i] = (carry + inc) | (x < 0 ? int(0x80000000u) : 0);
+            // (no exec-mask block around the store: lanes past the last leaf write slot S, which holds no leaf --
+            // an op starts with nseg + 2 < cap)
+            L.E[vp_sel(in, i, S)] = (carry + inc) | (x & int(0x80000000u));
             carry += rdlane(inc, 63);
         }
         wsync();
@@ -1060,6 +1095,9 @@ struct Eng {
     // segment, its segment is gone (unlinked, merged away) or no longer holds it (a Transient one is never held),
     // else its offset (0 on a removed segment) plus the segment's local-view position.  info_id >= 0: out =
     // {leaf ordinal of its segment (-1: none or gone), offset, ReferenceType, held} of that reference instead.
+    // info_id == -2: two words per reference, {that position, state bits}: MTR_REF_ST_SEGMENT (it has a segment),
+    // MTR_REF_ST_HELD (that segment's LocalReferenceCollection holds it), MTR_REF_ST_REMOVED (its leaf, found in the
+    // tree, is removed) -- what an interval collection's compare needs beside the position.
     static MTR_DI void ref_query(char* smem, const KParams& P, uint32_t d, int32_t* out, int info_id) {
         D L;
         carve(L, smem, P, d);
@@ -1087,7 +1125,7 @@ struct Eng {
             const uint32_t u = rf_uid(L)[rc], o = rf_off(L)[rc], t = rf_ty(L)[rc];
             const bool live = (r < n) & (u != NONE32) & ((t & (RF_HELD | RT_TRANSIENT)) != 0);
             int res = MTR_DETACHED_POSITION;
-            bool found = false;
+            bool found = false, onrm = false;
             int carry = 0;
             for (int base = 0; base < S && __ballot(live & !found); base += 64) {
                 const int i = base + lane_id();
@@ -1105,11 +1143,20 @@ struct Eng {
                     const int el = rdlane(excl, l), rl = rdlane(rm, l);
                     const bool hit = live & !found & (ul == u);
                     res = hit ? (rl ? 0 : int(o)) + el : res;
+                    onrm = onrm | (hit & (rl != 0));
                     found = found | hit;
                 }
                 carry += rdlane(inc, 63);
             }
-            if (r < n) out[r] = res;
+            if (info_id == -2) {
+                if (r < n) {
+                    out[2 * r] = res;
+                    out[2 * r + 1] = (u != NONE32 ? MTR_REF_ST_SEGMENT : 0) | ((t & RF_HELD) ? MTR_REF_ST_HELD : 0) |
+                                     (onrm ? MTR_REF_ST_REMOVED : 0);
+                }
+            } else if (r < n) {
+                out[r] = res;
+            }
         }
     }
 
@@ -2703,10 +2750,34 @@ struct Eng {
     // Every lane copies units c0 + lane, c0 + lane + 64, ...: the loads of a batch of 8 rounds
     // are all in flight before its stores (one HBM round trip per 512 units, not per 8 units of
     // one lane's piece).
-    static MTR_DI void copy_chain(const D& L, uint32_t dst, int c0, int total, uint64_t pieces, uint32_t vt,
-                                  int off) {
+    // the deferred store of copy_chain's last short chain: before anything reads the text arena, and at the
+    // end of the launch
+    static MTR_DI void text_flush(D& L) {
+        if (L.pc_any) {
+            if (L.pc_on) L.gtext()[L.pc_dst] = uint16_t(L.pc_val);
+            L.pc_on = 0;
+            L.pc_any = 0;
+            wsync();
+        }
+    }
+    static MTR_DI void copy_chain(D& L, uint32_t dst, int c0, int total, uint64_t pieces, uint32_t vt, int off) {
         const int ln = lane_id();
+        text_flush(L);  // (its sources may be the last chain's destination)
         const gptr<uint16_t> t = L.gtext();
+        if (total - c0 <= 64) {  // the common chain: one round; its load now, its store at the next text_flush
+            const int pos = c0 + ln;
+            uint32_t src = 0;
+            for (uint64_t pm = pieces; pm; pm &= pm - 1) {
+                const int j = first_lane(pm);
+                const int pj = rdlane(off, j);
+                src = vp_sel(vp_le(pj, pos), int(rdlane(vt, j) + uint32_t(pos - pj)), int(src));
+            }
+            L.pc_on = pos < total;
+            L.pc_dst = dst + uint32_t(pos);
+            L.pc_val = t[src];
+            L.pc_any = 1;
+            return;
+        }
         for (int b0 = c0; b0 < total; b0 += 8 * 64) {
             uint16_t u[8];
             uint32_t src[8];
@@ -2735,6 +2806,7 @@ struct Eng {
     // of a; the caller keeps M_NL.
     static MTR_DI void text_append(D& L, const KParams& P, St& s, int a, int b) {
         PROF(P_TAPPEND);
+        text_flush(L);
         PROF_COUNT(P_NMERGE);
         const int tend = text_end(s, P);
         const uint32_t oa = uniu(L.text[a]), ob = uniu(L.text[b]);
@@ -2772,6 +2844,7 @@ struct Eng {
     // leaf order (prefix scan of lengths), then switch halves.
     static MTR_DI void text_gc(D& L, const KParams& P, St& s) {
         PROF(P_TEXTGC);
+        text_flush(L);
         const int S = s.nseg;
         const int half = P.tcap / 2;
         const int dst0 = s.texthalf ? 0 : half;
@@ -2872,6 +2945,7 @@ struct Eng {
                 if (__ballot(q)) {
                     PROF(P_NLQ);
                     PROF_COUNT(P_NNLQ);
+                    text_flush(L);
                     if (q) {
                         const uint16_t u = L.gtext()[L.text[i] + uint32_t(vl) - 1];
                         vm = (vm & ~(M_NLQ | M_NL)) | (u == u'\n' ? M_NL : 0u);
@@ -3004,6 +3078,7 @@ struct Eng {
             if (__ballot(q)) {
                 PROF(P_NLQ);
                 PROF_COUNT(P_NNLQ);
+                text_flush(L);
                 if (q) {
                     const uint16_t u = L.gtext()[vt + uint32_t(vl) - 1];
                     vm = (vm & ~(M_NLQ | M_NL)) | (u == u'\n' ? M_NL : 0u);
@@ -4180,8 +4255,8 @@ struct Eng {
             v.ref = s.curseq;
             v.local = 1;
             if (s.collab) {  // a pending local op (seq = UnassignedSequenceNumber, the local client)
-                if (!X || (op.type == MTR_OP_LOCAL_ANNOTATE && op.payload2 != 0 && op.payload2 != MTR_COMB_REWRITE)) {
-                    s.status = MTR_ERR_UNSUPPORTED;  // (pending combining annotates other than rewrite: not built)
+                if (!X) {  // (the local-op path lives in the X instantiations only)
+                    s.status = MTR_ERR_UNSUPPORTED;
                     set_fail(L, gidx);
                     return false;
                 }
@@ -4434,6 +4509,7 @@ struct Eng {
         if (X) done -= __popc(uint32_t(uni(L.sc->relmask)));
         // a batch that ends with header segments: build the tree now (queries read it next)
         if (s.height == 0 && s.status == MTR_OK && cursor + done >= int(dd.op_count)) finish_load(L, s);
+        text_flush(L);    // the last merge chain's text
         sup_flush(L, s);  // the superchunk figures the launch's ops left stale, back to HBM
         store_doc(L, P, s, d, done);
     }

@@ -1347,8 +1347,8 @@ static int ref_query(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int
     DocHdr h;
     HIPCHK(hipMemcpy(&h, e->hdr.p + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
     const int64_t n = e->refs.p ? h.nrefs : 0;
-    const int64_t words = info_id >= 0 ? 4 : n;
-    if (info_id < 0 && (n > cap || n == 0 || !out)) return int(n);
+    const int64_t words = info_id >= 0 ? 4 : info_id == -2 ? 2 * n : n;
+    if (info_id < 0 && (words > cap || n == 0 || !out)) return int(n);
     KParams P{};
     P.hdr = e->hdr.p;
     P.seg = e->seg.p;
@@ -1376,6 +1376,10 @@ static int ref_query(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int
 
 int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap) {
     return ref_query(e, doc, out, cap, -1);
+}
+
+int64_t mtr_get_ref_states(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap) {
+    return ref_query(e, doc, out, cap, -2);
 }
 
 int32_t mtr_get_ref_info(mtr_engine* e, uint32_t doc, uint32_t id, int32_t* out) {

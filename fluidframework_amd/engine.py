@@ -108,6 +108,8 @@ def lib():
         L.mtr_download_batch.restype = C.c_int
         L.mtr_get_ref_positions.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.mtr_get_ref_positions.restype = C.c_int64
+        L.mtr_get_ref_states.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
+        L.mtr_get_ref_states.restype = C.c_int64
         L.mtr_get_ref_info.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         L.mtr_get_ref_info.restype = C.c_int32
         _LIB = L
@@ -371,6 +373,17 @@ class Engine:
         out = np.zeros(n, dtype="<i4")
         self._check(int(lib().mtr_get_ref_positions(self.h, doc, out.ctypes.data, n) != n), "mtr_get_ref_positions")
         return [int(x) for x in out]
+
+    def ref_states(self, doc) -> list:
+        """[(position, state bits abi.REF_ST_*)] of every local reference of `doc`, by id (mtr_get_ref_states)."""
+        n = lib().mtr_get_ref_states(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"mtr_get_ref_states: {_err()}")
+        if n == 0:
+            return []
+        out = np.zeros(2 * n, dtype="<i4")
+        self._check(int(lib().mtr_get_ref_states(self.h, doc, out.ctypes.data, 2 * n) != n), "mtr_get_ref_states")
+        return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
 
     def ref_info(self, doc, ref_id):
         """(leaf index of the reference's segment or -1, offset, refType, held by the segment's collection)"""

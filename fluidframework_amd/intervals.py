@@ -1,0 +1,364 @@
+"""Interval collections of a SharedString on the replay engine.
+
+The reference keeps each collection (sequence/src/intervalCollection.ts:1428 ``IntervalCollection``, :788
+``LocalIntervalCollection``) as two red-black trees over ``SequenceInterval``s whose endpoints are local
+references (``createSequenceInterval``, :726-767) -- ordered by ``SequenceInterval.compare`` (:505-525:
+start, then end, then the id string; ``compareReferencePositions``, merge-tree/src/referencePositions.ts:113-121)
+-- and summarizes a collection as the in-order walk of the start tree (``LocalIntervalCollection.serialize``,
+:1105-1112).  Here the endpoints are engine references (MTR_OP_REF_CREATE records in the document's batch,
+created at the op's view and slid as ``createPositionReference`` does, :697-724) and the host keeps only the
+intervals and their properties: the order is computed once, when a summary is written, from the
+references' positions (mtr_get_ref_states).
+
+Why the order needs no tree: a tree keeps a collection sorted by the current comparator as long as no two
+intervals change their relative order without one of them being re-inserted.  Between two references that
+order only changes when one of them slides (inserts, splits and zamboni keep it; a removed segment's
+references are moved by ``slideAckedRemovedSegmentReferences``, mergeTree.ts:849-884), and every slide of an
+interval endpoint re-inserts that interval (``addIntervalListeners``, intervalCollection.ts:1114-1159).  So the
+in-order walk is the sort by the comparator at summary time, and at that time an endpoint is either held by a
+live segment -- where the comparator is the position order -- or has no segment at all (position -1, the
+smallest).  Anything else (an endpoint left on a removed segment, one whose segment dropped it, duplicate
+ids, transient intervals, local ops while collaborating) is reported as Unsupported: such a document falls
+back.  The oracle (oracle/intervals.py) restates the trees and the slide listeners themselves; the tests
+compare the two.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any
+
+from . import abi
+from .jsjson import js_key_order, js_number, js_stringify, js_truthy, parse, utf16_less
+
+VALUE_TYPE = "sharedStringIntervalCollection"  # SequenceIntervalCollectionValueType.Name, intervalCollection.ts:1195
+RANGE_LABELS = "referenceRangeLabels"         # reservedRangeLabelsKey
+INTERVAL_ID = "intervalId"                     # reservedIntervalIdKey
+LEGACY_PREFIX = "legacy"                       # LocalIntervalCollection.legacyIdPrefix, :795
+
+# IntervalType (intervalCollection.ts:56-77)
+SIMPLE, NEST, SLIDE_ON_REMOVE, TRANSIENT = 0x0, 0x1, 0x2, 0x4
+
+
+class IntervalUnsupported(Exception):
+    """The document's intervals take a path this host does not restate (the caller falls back)."""
+
+
+def _js_to_string(v: Any) -> str:
+    """`${v}` of a JSON value (SequenceInterval.getIntervalId, :554-560)."""
+    if isinstance(v, str):
+        return v
+    if v is True:
+        return "true"
+    if v is False:
+        return "false"
+    if v is None:
+        return "null"
+    if isinstance(v, (int, float)):
+        return js_number(v)
+    raise IntervalUnsupported("an interval id that is not a string or number")
+
+
+def add_props(props: dict, new: dict) -> None:
+    """PropertiesManager.addProperties without combining ops or pending keys (segmentPropertiesManager.ts:60-157):
+    each key of `new` in JS key order; null deletes, anything else sets (a re-added key goes last, as in JS)."""
+    for k in js_key_order(new.keys()):
+        v = new[k]
+        if v is None:
+            props.pop(k, None)
+        else:
+            props[k] = v
+
+
+def _ref_types(itype: int, from_op_or_snapshot: bool) -> tuple[int, int]:
+    """createSequenceInterval's endpoint ReferenceTypes (:735-756)."""
+    if itype == TRANSIENT:
+        raise IntervalUnsupported("transient interval")
+    if itype == NEST:
+        b, e = abi.REFTYPE_NEST_BEGIN, abi.REFTYPE_NEST_END
+    else:
+        b, e = abi.REFTYPE_RANGE_BEGIN, abi.REFTYPE_RANGE_END
+    f = abi.REFTYPE_SLIDE_ON_REMOVE if from_op_or_snapshot else abi.REFTYPE_STAY_ON_REMOVE
+    return b | f, e | f
+
+
+def _int_pos(v: Any, what: str) -> int:
+    if isinstance(v, bool) or not isinstance(v, (int, float)) or v != int(v):
+        raise IntervalUnsupported(f"interval {what} that is not an integer position")
+    return int(v)
+
+
+@dataclass
+class Interval:
+    """One SequenceInterval: its endpoint references (engine ids), intervalType and property bag."""
+
+    start: int
+    end: int
+    itype: Any
+    props: dict
+    kind: str  # "op" (a sequenced op: a detached endpoint is allowed, :685-694), "snapshot" or "local"
+
+    def id(self) -> str | None:
+        v = self.props.get(INTERVAL_ID)
+        return None if v is None else _js_to_string(v)
+
+
+@dataclass
+class Collection:
+    """IntervalCollection + LocalIntervalCollection of one label: LocalIntervalCollection.intervalIdMap (:791),
+    which holds every interval of the collection (two intervals with one id are not restated)."""
+
+    label: str
+    saved: list | None = None          # savedSerializedIntervals until attachGraph (:1465-1470, 1559-1578)
+    by_id: dict = field(default_factory=dict)
+
+    def _create(self, log, start: int, end: int, itype: Any, view: tuple | None, kind: str) -> Interval:
+        """createSequenceInterval (:726-767) -> the two MTR_OP_REF_CREATE records, start first: an op's at its
+        view, slid (getSlideToSegment); a snapshot's or a local one's at the local view."""
+        if isinstance(itype, bool) or not isinstance(itype, (int, float)) or itype not in (SIMPLE, NEST, SLIDE_ON_REMOVE):
+            raise IntervalUnsupported(f"intervalType {itype!r}")
+        bt, et = _ref_types(int(itype), kind != "local")
+        s = log.create_ref(start, bt, view=view, slide=kind == "op")
+        e = log.create_ref(end, et, view=view, slide=kind == "op")
+        return Interval(s, e, itype, {RANGE_LABELS: [self.label]}, kind)
+
+    def _add(self, iv: Interval) -> None:
+        """LocalIntervalCollection.add (:1078-1082): the index and the id map."""
+        i = iv.id()
+        if i is None:
+            raise AssertionError("0x2c0")  # "ID must be created before adding interval to collection"
+        if i in self.by_id or i == "":
+            raise IntervalUnsupported("two intervals with one id")  # the trees' put keeps the first key
+        self.by_id[i] = iv
+
+    def _remove(self, iv: Interval) -> None:
+        """removeExistingInterval (:1015-1021)."""
+        del self.by_id[iv.id()]
+
+    def attach(self, log) -> None:
+        """attachGraph (:1531-1579): the saved intervals, created from the snapshot (local view,
+        SlideOnRemove endpoints), in order."""
+        saved, self.saved = self.saved or [], None
+        for si in saved:
+            props = ensure_serialized_id(si)
+            iv = self._create(log, _int_pos(si.get("start"), "start"), _int_pos(si.get("end"), "end"),
+                              si.get("intervalType"), None, "snapshot")
+            add_props(iv.props, props)
+            self._add(iv)
+
+    def local_add(self, log, start: int, end: int, itype: int, props: dict | None) -> Interval:
+        """IntervalCollection.add (:1635-1672) on a client that is not collaborating (a detached SharedString,
+        generateSharedStrings.ts:42-52): StayOnRemove endpoints at the local view; the id must be given
+        (otherwise addInterval draws a uuid, :1048)."""
+        if log.collaborating:
+            raise IntervalUnsupported("local interval ops while collaborating")
+        if isinstance(itype, int) and itype & TRANSIENT:
+            raise ValueError("Can not add transient intervals")
+        if not props or props.get(INTERVAL_ID) is None:
+            raise IntervalUnsupported("a local interval without an id (a random uuid)")
+        iv = self._create(log, int(start), int(end), itype, None, "local")
+        add_props(iv.props, props)
+        self._add(iv)
+        return iv
+
+    def ack_add(self, log, si: dict, msg: dict) -> None:
+        """ackAdd of a remote op (:2141-2184): ensureSerializedId, addInterval(start, end, type, props, op)."""
+        ensure_serialized_id(si)
+        view = (int(msg["referenceSequenceNumber"]), _client(msg))
+        iv = self._create(log, _int_pos(si.get("start"), "start"), _int_pos(si.get("end"), "end"),
+                          si.get("intervalType"), view, "op")
+        props = si.get("properties")
+        if isinstance(props, dict):
+            add_props(iv.props, props)
+        if INTERVAL_ID not in iv.props:  # properties[reservedIntervalIdKey] ??= uuid()
+            raise IntervalUnsupported("an interval without an id (a random uuid)")
+        self._add(iv)
+
+    def ack_delete(self, si: dict) -> None:
+        """ackDelete of a remote op (:2187-2208)."""
+        i = ensure_serialized_id(si).get(INTERVAL_ID)
+        iv = self.by_id.get(i) if isinstance(i, str) else None  # Map.get with the raw id
+        if iv is not None:
+            self._remove(iv)
+
+    def ack_change(self, log, si: dict, msg: dict) -> None:
+        """ackChange of a remote op (:1859-1932): changeInterval (modify, :600-656: a new reference for each
+        given endpoint, the others shared) when start or end is given, then addProperties(newProps, true, seq)."""
+        props = si.get("properties")
+        props = props if isinstance(props, dict) else {}
+        if INTERVAL_ID not in props:
+            raise AssertionError("0x3fe")  # id must exist on the interval
+        i = props[INTERVAL_ID]
+        new_props = {k: v for k, v in props.items() if k != INTERVAL_ID}
+        iv = self.by_id.get(i) if isinstance(i, str) else None
+        if iv is None:
+            return
+        start, end = si.get("start"), si.get("end")
+        if ("start" in si and start is None) or ("end" in si and end is None):
+            raise IntervalUnsupported("a change op with a null endpoint")
+        if start is not None or end is not None:
+            if iv.kind == "local":  # createPositionReference asserts an op's references SlideOnRemove (0x2f5)
+                raise IntervalUnsupported("a remote change of a local (StayOnRemove) interval")
+            view = (int(msg["referenceSequenceNumber"]), _client(msg))
+            s, e = iv.start, iv.end
+            # modify keeps each endpoint's ReferenceType (getRefType with an op)
+            st, et = _ref_types(int(iv.itype), True)
+            if start is not None:
+                s = log.create_ref(_int_pos(start, "start"), st, view=view, slide=True)
+            if end is not None:
+                e = log.create_ref(_int_pos(end, "end"), et, view=view, slide=True)
+            nv = Interval(s, e, iv.itype, dict(iv.props), "op")  # propertyManager.copyTo
+            self._remove(iv)
+            self._add(nv)
+            iv = nv
+        add_props(iv.props, new_props)
+
+    def serialize(self, states: list, current_seq: int) -> dict:
+        """LocalIntervalCollection.serialize (:1105-1112): the intervals in compare order, each
+        compressInterval(interval.serialize()) (:139-151, 472-487)."""
+        keyed = []
+        for iv in self.by_id.values():
+            a, b = _endpoint(states, iv.start, iv.kind == "op"), _endpoint(states, iv.end, iv.kind == "op")
+            keyed.append((a, b, iv))
+        keyed = _sorted(keyed)
+        out = []
+        for a, b, iv in keyed:
+            props = {k: v for k, v in iv.props.items() if k != RANGE_LABELS}
+            out.append([a, b, current_seq, iv.itype, props])
+        return {"label": self.label, "intervals": out, "version": 2}
+
+
+def _endpoint(states: list, ref: int, from_op: bool) -> int:
+    """An endpoint's position, where the position order is compareReferencePositions' order."""
+    pos, st = states[ref]
+    seg, held, removed = st & abi.REF_ST_SEGMENT, st & abi.REF_ST_HELD, st & abi.REF_ST_REMOVED
+    if seg and held and not removed and pos >= 0:
+        return pos
+    if not seg and from_op:
+        return abi.DETACHED_POSITION  # no segment: smaller than any (referencePositions.ts:119)
+    if not seg:
+        raise IntervalUnsupported("an endpoint created without an op has no segment (the reference throws)")
+    raise IntervalUnsupported("an interval endpoint on a removed segment, or dropped by its segment")
+
+
+def _sorted(keyed: list) -> list:
+    """Sort by (start, end, id) with SequenceInterval.compare's id rule (JS string order)."""
+    import functools
+
+    def cmp(x, y):
+        if x[0] != y[0]:
+            return -1 if x[0] < y[0] else 1
+        if x[1] != y[1]:
+            return -1 if x[1] < y[1] else 1
+        a, b = x[2].id(), y[2].id()
+        if a and b:
+            return 1 if utf16_less(b, a) else -1 if utf16_less(a, b) else 0
+        return 0
+
+    return sorted(keyed, key=functools.cmp_to_key(cmp))
+
+
+def _client(msg: dict) -> str:
+    c = msg.get("clientId")
+    return "null" if c is None else str(c)
+
+
+def ensure_serialized_id(si: dict) -> dict:
+    """LocalIntervalCollection.ensureSerializedId (:838-858): a legacy id `legacy{start}-{end}` when the
+    serialized interval has none.  Returns its (possibly new) property bag."""
+    props = si.get("properties")
+    if not isinstance(props, dict) or props.get(INTERVAL_ID) is None:
+        lid = f"{LEGACY_PREFIX}{_js_to_string(si.get('start'))}-{_js_to_string(si.get('end'))}"
+        props = dict(props) if isinstance(props, dict) else {}
+        props[INTERVAL_ID] = lid
+        si["properties"] = props
+    return props
+
+
+def decompress(ci: list, label: str) -> dict:
+    """decompressInterval (:122-133)."""
+    props = dict(ci[4]) if len(ci) > 4 and isinstance(ci[4], dict) else {}
+    props[RANGE_LABELS] = [label]
+    return {"start": ci[0], "end": ci[1], "sequenceNumber": ci[2], "intervalType": ci[3], "properties": props}
+
+
+class IntervalCollections:
+    """SharedSegmentSequence.intervalCollections (sequence/src/sequence.ts:186, a DefaultMap of
+    IntervalCollection, defaultMap.ts): populate from the summary's `header` blob, attach after the merge-tree
+    load, remote "act" ops, local adds before collaboration, and the `header` blob of a summary."""
+
+    def __init__(self):
+        self.data: dict[str, Collection] = {}  # DefaultMap.data (a Map: insertion order)
+        self.attached = False
+
+    def populate(self, header: str | dict) -> None:
+        """DefaultMap.populate (defaultMap.ts:254-282): Object.entries of the parsed blob (JS key order)."""
+        j = parse(header) if isinstance(header, str) else header
+        for key in js_key_order(j.keys()):
+            ser = j[key]
+            if ser.get("type") in ("Plain", "Shared"):
+                continue
+            if ser.get("type") != VALUE_TYPE:
+                raise IntervalUnsupported(f"value type {ser.get('type')!r}")
+            label = key[len("intervalCollections/"):] if key.startswith("intervalCollections/") else key
+            v = ser.get("value")
+            if isinstance(v, list):
+                saved = [dict(x) for x in v]
+            else:
+                saved = [decompress(ci, v["label"]) for ci in v["intervals"]]
+            c = Collection(label, saved=saved)
+            # IntervalCollection.attachGraph(client, key) uses the DefaultMap key (sequence.ts:797-800)
+            self.data[label] = c
+
+    def attach(self, log) -> None:
+        """SharedSegmentSequence.loadFinished -> initializeIntervalCollections (sequence.ts:750-801)."""
+        for c in self.data.values():
+            c.attach(log)
+        self.attached = True
+
+    def get(self, label: str) -> Collection:
+        """DefaultMap.get -> createCore (defaultMap.ts:210-213, 339-349): a new, attached, empty collection."""
+        c = self.data.get(label)
+        if c is None:
+            c = self.data[label] = Collection(label)
+        return c
+
+    def local_add(self, log, label: str, start: int, end: int, itype: int, props: dict | None) -> Interval:
+        return self.get(label).local_add(log, start, end, itype, props)
+
+    def process(self, log, contents: dict, msg: dict) -> None:
+        """DefaultMap's "act" handler (defaultMap.ts:386-395) and the ops map (intervalCollection.ts:1266-1326)
+        for a sequenced message of another client."""
+        if _client(msg) == log.observer_id:
+            raise IntervalUnsupported("acks of local interval ops")
+        key = contents.get("key")
+        if not isinstance(key, str):
+            raise IntervalUnsupported("an interval op without a string key")
+        value = contents.get("value") or {}
+        name = value.get("opName")
+        params = value.get("value")
+        c = self.get(key)
+        if name not in ("add", "delete", "change"):
+            raise IntervalUnsupported(f"interval op {name!r}")  # getOpHandler throws
+        if name != "delete" and not js_truthy(params):
+            return  # "if params is undefined, the interval was deleted during rebasing"
+        if not isinstance(params, dict):
+            raise IntervalUnsupported("interval op parameters")
+        params = dict(params)
+        if name == "add":
+            c.ack_add(log, params, msg)
+        elif name == "delete":
+            c.ack_delete(params)
+        else:
+            c.ack_change(log, params, msg)
+
+    def serialize(self, states: list, current_seq: int) -> str | None:
+        """summarizeCore's `header` blob (sequence.ts:467-480): JSON.stringify of {key: {type, value}} over the
+        collections (DefaultMap.serialize, defaultMap.ts:231-248); None when there are none."""
+        if not self.data:
+            return None
+        out = {}
+        for key, c in self.data.items():
+            if c.saved is not None:
+                raise IntervalUnsupported("a collection that was never attached")
+            out[key] = {"type": VALUE_TYPE, "value": c.serialize(states, current_seq)}
+        return js_stringify(out)

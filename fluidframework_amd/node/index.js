@@ -309,7 +309,15 @@ class DocLog {
     removeRef(id) { this.push(OP.REF_REMOVE, 0, 0, 0, 0, 0, 0, 0, id, 0); }
     localAnnotate(start, end, props, it, combiningOp) {
         if (props && typeof props === 'object' && 'markerId' in props) this.markerIdAnnotated = true;
-        this.push(OP.LOCAL_ANNOTATE, 0, 0, this.localSeq(), 0, 0, start, end, it.propop(props), localComb(combiningOp));
+        let comb = localComb(combiningOp), pp;
+        if (comb === COMB.NONE || comb === COMB.REWRITE) {
+            pp = it.propop(props);
+        } else {  // combine(op, previousValue, undefined, seq): each key's absent-key result, as for a remote one
+            const c = it.combining(props, combiningOp, this.collaborating ? -1 : 0);
+            pp = c[0];
+            comb = c[1];
+        }
+        this.push(OP.LOCAL_ANNOTATE, 0, 0, this.localSeq(), 0, 0, start, end, pp, comb);
     }
     rollback(op, it) {  // Client.rollback (client.ts:421-423 -> MergeTree.rollback, mergeTree.ts:2049-2159)
         let pp = 0, comb = 0;
@@ -725,10 +733,11 @@ function regeneratedOp(resetOp, recs, first, propsOf) {
 
 // a local annotate's combiningOp: none or "rewrite" (pendingRewriteCount, segmentPropertiesManager.ts:72-80); its
 // ack and rollback records carry the same code (pos1)
-function localComb(co) {
+function localComb(co) {  // a local annotate's combiningOp as its ack / rollback records carry it (batch.py _local_comb)
     if (!co) return COMB.NONE;
-    if (typeof co === 'object' && co.name === 'rewrite') return COMB.REWRITE;
-    throw new UnsupportedError('local annotate with a combiningOp other than rewrite');
+    if (typeof co !== 'object') throw new UnsupportedError('combiningOp');
+    if (co.name === 'rewrite') return COMB.REWRITE;
+    return co.name === 'incr' ? COMB.INCR : co.name === 'consensus' ? COMB.CONSENSUS : COMB.KEEP;
 }
 
 class BatchReplayEngine {

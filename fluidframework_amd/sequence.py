@@ -174,6 +174,13 @@ def ops_from_deltas(members: list[dict], ranges: np.ndarray, op_index: list[int]
     return ops
 
 
+def _is_interval_op(msg: dict) -> bool:
+    c = msg.get("contents")
+    if isinstance(c, str):
+        c = parse(c)
+    return isinstance(c, dict) and c.get("type") == "act"
+
+
 class SequenceLog(DocLog):
     """A DocLog that also keeps SharedSegmentSequence's ``messagesSinceMSNChange``.
 
@@ -189,6 +196,10 @@ class SequenceLog(DocLog):
         self.msn = 0
 
     def message(self, msg: dict, interner: Interner) -> None:
+        if msg.get("type") == "op" and _is_interval_op(msg):
+            # handled by the interval collections (sequence.ts:636-645): not a merge-tree message, not kept
+            super().message(msg, interner)
+            return
         self.msn = max(self.msn, int(msg["minimumSequenceNumber"]))
         if msg.get("type") != "op" or not self.legacy:
             super().message(msg, interner)
@@ -268,9 +279,45 @@ class SequenceLog(DocLog):
             return None
         return to_utf8(js_stringify(self.stash))
 
-    def load(self, blobs: dict, long_id: str, interner: Interner) -> None:
-        """Client.load of a summary plus the catch-up messages, each checked against the collab
-        window and applied as an ordinary message (sequence.ts:557-604)."""
+    def load(self, blobs: dict, long_id: str, interner: Interner, header: str | None = None) -> None:
+        """SharedSegmentSequence.loadCore (sequence.ts:557-611): the interval collections' `header` blob (if
+        any) populated first, Client.load of the merge-tree summary `blobs` plus the catch-up messages, each
+        checked against the collab window and applied as an ordinary message, then loadFinished attaches the
+        collections (their intervals' references are created after the catch-up ops, sequence.ts:750-801)."""
+        if header is not None:
+            from .intervals import IntervalCollections
+
+            self.intervals = IntervalCollections()
+            self._intervals_call(self.intervals.populate, header)
+        self._load_merge_tree(blobs, long_id, interner)
+        if self.intervals is not None:
+            self._intervals_call(self.intervals.attach, self)
+
+    def _intervals_call(self, fn, *args):
+        from .intervals import IntervalUnsupported
+
+        try:
+            return fn(*args)
+        except IntervalUnsupported as e:
+            raise Unsupported(str(e)) from e
+
+    def interval_collection(self, label: str):
+        """SharedSegmentSequence.getIntervalCollection (sequence.ts:445-447): created when absent."""
+        from .intervals import IntervalCollections
+
+        if self.intervals is None:
+            self.intervals = IntervalCollections()
+        return self.intervals.get(label)
+
+    def interval_header(self, states: list) -> bytes | None:
+        """The summary's `header` blob (summarizeCore, sequence.ts:467-480): the interval collections, ordered
+        from the references' states at summary time (Engine.ref_states(doc)); None when there are none."""
+        if self.intervals is None:
+            return None
+        h = self._intervals_call(self.intervals.serialize, states, self.current_seq)
+        return None if h is None else to_utf8(h)
+
+    def _load_merge_tree(self, blobs: dict, long_id: str, interner: Interner) -> None:
         msgs = self.load_summary(blobs, long_id, interner)
         # the loaded window: minSeq / currentSeq from the header (legacy: both the summary's minSeq)
         header = blobs["header"]

@@ -160,6 +160,13 @@ int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t
  * MTR_DETACHED_POSITION (-1) when it has no position.  Returns the document's reference count (out written
  * only when it fits in cap), -1 on error. */
 int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap);
+/* Every local reference of document doc as out[2r] = its position (as mtr_get_ref_positions) and out[2r+1] = state
+ * bits: MTR_REF_ST_SEGMENT (LocalReference.getSegment() is defined, localReference.ts:106), MTR_REF_ST_HELD (that
+ * segment's LocalReferenceCollection holds it, :357-384), MTR_REF_ST_REMOVED (that segment is in the tree and
+ * removed).  An interval collection's compare (compareReferencePositions, referencePositions.ts:113-121) agrees
+ * with the position order exactly when every endpoint is held by a live segment or has no segment at all
+ * (DESIGN.md section 9).  Returns the reference count (out written only when 2*count fits in cap), -1 on error. */
+int64_t mtr_get_ref_states(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap);
 /* Reference `id` of document doc: out[0] = index (tree order) of the leaf of its segment (LocalReference.
  * getSegment, localReference.ts:106; -1 = none, or the segment is no longer in the tree), out[1] = getOffset,
  * out[2] = refType, out[3] = 1 when the segment's LocalReferenceCollection holds it (has(), :357-384).

@@ -116,6 +116,10 @@ enum {
 };
 /* localReferencePositionToPosition of a reference with no position (referencePositions.ts:103) */
 #define MTR_DETACHED_POSITION (-1)
+/* mtr_get_ref_states bits (include/mtr.h) */
+#define MTR_REF_ST_SEGMENT 1
+#define MTR_REF_ST_HELD 2
+#define MTR_REF_ST_REMOVED 4
 
 /*
  * Marker ordinals (MergeTree.idToSegment, mergeTree.ts:549,668): an insert / load record of a Marker whose

@@ -251,6 +251,13 @@ class Tree {
 
     mtr_options opt;
     Block* root;
+    // LocalReferencePosition.callbacks (localReference.ts:43-46): the interval collection's beforeSlide /
+    // afterSlide listeners (sequence/src/intervalCollection.ts:1114-1159), one hook for every reference
+    oracle_slide_hook slideHook = nullptr;
+    void* slideCtx = nullptr;
+    void slideEvent(int id, int phase) {
+        if (slideHook) slideHook(slideCtx, id, phase);
+    }
     // CollaborationWindow (mergeTreeNodes.ts:656)
     int localClientId = kLocalClientId;
     bool collaborating = false;
@@ -810,7 +817,11 @@ class Tree {
         const std::vector<int> ids = refsOf(s->localRefs);
         if (!ns) {
             for (int id : ids)
-                if (!(refs[size_t(id)].refType & kStay)) refsRemove(s->localRefs, id);
+                if (!(refs[size_t(id)].refType & kStay)) {
+                    slideEvent(id, 0);  // ref.callbacks?.beforeSlide (mergeTree.ts:866-871)
+                    refsRemove(s->localRefs, id);
+                    slideEvent(id, 1);
+                }
             return;
         }
         if (!ns->localRefs) ns->localRefs = newLocalRefs(ns, size_t(ns->len));
@@ -825,6 +836,7 @@ class Tree {
         for (int id : ids) {
             LRef& r = refs[size_t(id)];
             if (r.refType & kStay) continue;
+            if (r.refType & kSlide) slideEvent(id, 0);  // lref.callbacks?.beforeSlide (localReference.ts:441,477)
             refsRemove(r.segment->localRefs, id);  // link() with a new list node leaves the old collection
             if (r.refType & kSlide) {
                 if (after) dst.push_back(id);
@@ -833,6 +845,7 @@ class Tree {
                 r.offset = off;
                 r.list = k;
                 c->refCount++;
+                slideEvent(id, 1);  // afterSlide (:451,484)
             } else {
                 r.segment = nullptr;  // lref.link(undefined, 0, undefined)
                 r.offset = 0;
@@ -1724,8 +1737,8 @@ class Tree {
                                  collaborating ? kUnassignedSeq : kUniversalSeq);
                 return status;
             case MTR_OP_LOCAL_ANNOTATE:
-                // (pending combining ops other than rewrite: not built)
-                if (op.payload2 != MTR_COMB_NONE && !(op.payload2 == MTR_COMB_REWRITE)) return MTR_ERR_UNSUPPORTED;
+                // (a combining annotate: payload2 = MTR_COMB_* | NaN value id << 3, its prop-op the host's combine of
+                // each key's default as for a remote one -- combine(op, undefined, undefined, UnassignedSequenceNumber))
                 annotateRange(op.pos1, op.pos2, op.payload, currentSeq, localClientId,
                               collaborating ? kUnassignedSeq : kUniversalSeq, op.payload2);
                 return status;
@@ -2253,6 +2266,38 @@ int32_t oracle_doc_ref_info(oracle_doc* d, uint32_t id, int32_t* out) {
     out[2] = r.refType;
     out[3] = (s && s->localRefs && t.refsHas(s->localRefs, int(id))) ? 1 : 0;
     return out[0];
+}
+
+int64_t oracle_doc_ref_states(oracle_doc* d, int32_t* out, int64_t cap) {
+    Tree& t = d->view();
+    if (!t.pendingLoad.empty()) t.reloadFromSegments();
+    const int64_t n = int64_t(t.refs.size());
+    if (2 * n > cap) return -n;
+    for (int64_t i = 0; i < n; i++) {
+        const LRef& r = t.refs[size_t(i)];
+        Seg* s = r.segment;
+        const bool held = s && s->localRefs && t.refsHas(s->localRefs, int(i));
+        const bool live = held || (r.refType & MTR_REFTYPE_TRANSIENT);
+        out[2 * i] = t.refPosition(int(i));
+        out[2 * i + 1] = (s ? MTR_REF_ST_SEGMENT : 0) | (held ? MTR_REF_ST_HELD : 0) |
+                         (live && s && s->parent && s->removed ? MTR_REF_ST_REMOVED : 0);
+    }
+    return n;
+}
+
+int32_t oracle_doc_ref_key(oracle_doc* d, uint32_t id, int32_t* out) {
+    Tree& t = d->view();
+    if (id >= t.refs.size()) return -3;
+    const LRef& r = t.refs[id];
+    Seg* s = r.segment;
+    out[0] = !s ? -1 : s->parent ? t.leafIndex(s) : -2;
+    out[1] = r.offset;
+    return out[0];
+}
+
+void oracle_doc_set_slide_hook(oracle_doc* d, oracle_slide_hook hook, void* ctx) {
+    d->tree.slideHook = d->cols.slideHook = hook;
+    d->tree.slideCtx = d->cols.slideCtx = ctx;
 }
 
 int32_t oracle_doc_handle_at(oracle_doc* d, int32_t pos) {

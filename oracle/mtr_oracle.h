@@ -115,6 +115,18 @@ int64_t oracle_doc_ref_positions(oracle_doc* d, int32_t* out, int64_t cap);
  * held by its segment's LocalReferenceCollection] */
 int32_t oracle_doc_ref_info(oracle_doc* d, uint32_t id, int32_t* out);
 
+/* mtr_get_ref_states (include/mtr.h) restated: out[2i] = position, out[2i+1] = MTR_REF_ST_* bits.  Returns the
+ * count, -count when 2*count exceeds cap. */
+int64_t oracle_doc_ref_states(oracle_doc* d, int32_t* out, int64_t cap);
+/* compareReferencePositions' view of reference id (referencePositions.ts:113-121): out[0] = index in tree order of
+ * its segment (its ordinal's rank), -1 = no segment (detached), -2 = a segment no longer in the tree; out[1] =
+ * getOffset().  Returns out[0], -3 for a bad id. */
+int32_t oracle_doc_ref_key(oracle_doc* d, uint32_t id, int32_t* out);
+/* The references' beforeSlide (phase 0) / afterSlide (phase 1) callbacks (localReference.ts:441-451,477-484,
+ * mergeTree.ts:866-871), called while a batch applies; NULL clears. */
+typedef void (*oracle_slide_hook)(void* ctx, int32_t ref_id, int32_t phase);
+void oracle_doc_set_slide_hook(oracle_doc* d, oracle_slide_hook hook, void* ctx);
+
 /* PermutationVector.getMaybeHandle at local position pos of the selected vector (permutationvector.ts:196-207):
  * the handle, MTR_HANDLE_UNALLOCATED, or -1 when no segment holds pos */
 int32_t oracle_doc_handle_at(oracle_doc* d, int32_t pos);

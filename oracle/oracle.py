@@ -77,6 +77,12 @@ def lib():
         L.oracle_doc_ref_positions.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.oracle_doc_handle_at.restype = C.c_int32
         L.oracle_doc_handle_at.argtypes = [C.c_void_p, C.c_int32]
+        L.oracle_doc_ref_states.restype = C.c_int64
+        L.oracle_doc_ref_states.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_doc_ref_key.restype = C.c_int32
+        L.oracle_doc_ref_key.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        L.oracle_doc_set_slide_hook.restype = None
+        L.oracle_doc_set_slide_hook.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_doc_ref_info.restype = C.c_int32
         L.oracle_doc_ref_info.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         _LIB = L
@@ -235,6 +241,28 @@ class OracleDoc:
         out = np.zeros(max(n, 1), dtype="<i4")
         lib().oracle_doc_ref_positions(self.h, out.ctypes.data, n)
         return [int(x) for x in out[:n]]
+
+    def ref_states(self) -> list:
+        """[(position, abi.REF_ST_* bits)] of every local reference, by id (as Engine.ref_states)."""
+        n = lib().oracle_doc_ref_states(self.h, None, 0)
+        n = -n if n < 0 else n
+        out = np.zeros(max(2 * n, 1), dtype="<i4")
+        lib().oracle_doc_ref_states(self.h, out.ctypes.data, 2 * n)
+        return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+    def ref_key(self, ref_id: int):
+        """(tree-order index of the reference's segment: -1 none, -2 no longer in the tree; getOffset())"""
+        out = np.zeros(2, dtype="<i4")
+        if lib().oracle_doc_ref_key(self.h, ref_id, out.ctypes.data) == -3:
+            raise ValueError(f"no local reference {ref_id}")
+        return int(out[0]), int(out[1])
+
+    SLIDE_HOOK = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32)
+
+    def set_slide_hook(self, fn) -> None:
+        """fn(ref_id, phase) -- phase 0 = beforeSlide, 1 = afterSlide -- during apply(); None clears."""
+        self._hook = None if fn is None else self.SLIDE_HOOK(lambda ctx, r, ph: fn(r, ph))
+        lib().oracle_doc_set_slide_hook(self.h, C.cast(self._hook, C.c_void_p) if self._hook else None, None)
 
     def ref_info(self, ref_id: int):
         """(leaf index of the reference's segment or -1, offset, refType, held by the segment's collection)"""

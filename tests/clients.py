@@ -141,6 +141,14 @@ class Clients:
         reference's PartialSequenceLengths answer is compared with the leaf sum)"""
         return self._record(c, "length", (ref, client), int(self.docs[c].length(ref, client)))
 
+    def props(self, c, pos, ref=None, client=None):
+        """the properties of getContainingSegment(pos)'s segment as (key, value) pairs in JS key order (None: undefined)"""
+        ref = self.cur[c] if ref is None else ref
+        client = self.logs[c].short_id(c) if client is None else client
+        r = self.docs[c].containing_props(pos, ref, client)
+        p = None if r is None or r[1] is None else list(regen.props_dict(r[1], self.it).items())
+        return self._record(c, "props", (pos, ref, client), p)
+
     def ref_positions(self, c):
         """localReferencePositionToPosition of every reference, by id"""
         return self._record(c, "refpos", (), self.docs[c].ref_positions())
@@ -178,6 +186,9 @@ class Clients:
                 elif kind == "leaf":
                     r = eng.export(d)[0][args[0]]
                     got = (int(r[0]), int(r[1]), int(r[2]), int(r[3]))
+                elif kind == "props":
+                    r = eng.containing_segment(d, *args)
+                    got = None if r is None or r["props"] < 0 else list(regen.props_dict(eng.props(d, r["props"]), self.it).items())
                 elif kind == "refpos":
                     got = eng.ref_positions(d)
                 elif kind == "refinfo":

@@ -10,7 +10,8 @@ Sources (data files only; no reference source text is copied):
     referenceSequenceNumber, minimumSequenceNumber, type, contents.
   * packages/dds/sequence/src/test/snapshots/*/*.json -- ITree summaries compared by
     snapshotVersion.spec.ts:137-160.  Kept: the `content` subtree's blob contents (the merge-tree
-    summary); the top-level interval `header` blob is out of scope.
+    summary) -> snapshots.json.gz, and the top-level `header` blob (the interval collections, present in
+    the four withIntervals / withV1Intervals files) -> interval_headers.json.
 """
 import glob
 import gzip
@@ -65,6 +66,18 @@ def snapshots():
         json.dump(res, fh, separators=(",", ":"))
 
 
+def interval_headers():
+    res = {}
+    for f in sorted(glob.glob(f"{REF}/sequence/src/test/snapshots/*/*.json")):
+        tree = json.load(open(f))
+        h = [e for e in tree["entries"] if e["path"] == "header"]
+        if h:
+            res[f"{os.path.basename(os.path.dirname(f))}/{os.path.basename(f)[:-5]}"] = h[0]["value"]["contents"]
+    with open(os.path.join(HERE, "interval_headers.json"), "w", encoding="utf-8") as fh:
+        json.dump(res, fh, indent=1)
+
+
 if __name__ == "__main__":
     replay()
     snapshots()
+    interval_headers()
