@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mtr.h"
@@ -83,6 +84,7 @@ struct mtr_engine {
     static constexpr int kLanes = 4;
     hipStream_t aux[kLanes - 1] = {};
     hipEvent_t lane_done[kLanes] = {};
+    hipEvent_t grp_fork[kLanes] = {}, grp_cls[kLanes] = {};  // per document group: round start, class counts read
     std::vector<hipEvent_t> kev;  // per-launch start/stop events (kernel durations)
     // persistent document state
     DevBuf<DocHdr> hdr;
@@ -209,9 +211,9 @@ __global__ void scan_state_kernel(const DocHdr* h, const mtr_doc_desc* docs, uin
 // of the two vectors; they launch apply_pair_kernel with two LDS regions.
 constexpr int kClasses = 64;
 constexpr int kAllClasses = 2 * kClasses;
-__global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t n,
-                                                      const uint32_t* dkind, const uint32_t* dpart, int32_t* cls,
-                                                      uint32_t* list, int class_leaves) {
+__global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t lo,
+                                                      uint32_t hi, const uint32_t* dkind, const uint32_t* dpart,
+                                                      int32_t* cls, uint32_t* list, int class_leaves) {
     // block-local histogram in LDS, then one global atomic per (block, class): the per-document
     // atomics on a handful of addresses would serialise at the memory side
     __shared__ int lcnt[kAllClasses], lmax[kAllClasses], lheap[kAllClasses], lbase[kAllClasses];
@@ -220,9 +222,11 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
     if (t < kAllClasses) lcnt[t] = lmax[t] = lheap[t] = 0;
     if (t == 0) lrem = 0;
     __syncthreads();
-    const uint32_t d = blockIdx.x * blockDim.x + t;
+    // (documents [lo, hi): one group of the round loop; its class lists are [class][hi - lo])
+    const uint32_t n = hi - lo;
+    const uint32_t d = lo + blockIdx.x * blockDim.x + t;
     int c = -1, rank = 0;
-    if (d < n) {
+    if (d < hi) {
         const DocHdr x = h[d];
         const int rem = x.status == MTR_OK ? int(docs[d].op_count) - x.op_cursor : 0;
         if (rem > 0) {
@@ -318,6 +322,8 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
     for (auto& x : e->ev) (void)hipEventCreate(&x);
     for (auto& x : e->aux) (void)hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
     for (auto& x : e->lane_done) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
+    for (auto& x : e->grp_fork) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
+    for (auto& x : e->grp_cls) (void)hipEventCreateWithFlags(&x, hipEventDisableTiming);
     const size_t D = std::max<uint32_t>(max_docs, 1);
     e->h_kind.assign(D, 0);
     e->h_part.assign(D, 0);
@@ -384,6 +390,10 @@ int mtr_engine_destroy(mtr_engine* e) {
     for (auto& x : e->kev)
         if (x) (void)hipEventDestroy(x);
     for (auto& x : e->lane_done)
+        if (x) (void)hipEventDestroy(x);
+    for (auto& x : e->grp_fork)
+        if (x) (void)hipEventDestroy(x);
+    for (auto& x : e->grp_cls)
         if (x) (void)hipEventDestroy(x);
     for (auto& x : e->aux)
         if (x) {
@@ -653,22 +663,74 @@ static int run_impl(mtr_engine* e, int gen) {
         const char* v = std::getenv("MTR_SLACK");
         return v ? std::max(0, std::atoi(v)) : -1;
     }();
+    // Independent document groups (tuning knob MTR_GROUPS, 1..kLanes): each group runs its own round loop
+    // (classify -> one launch per size class -> classify ...) on its own streams, so one group's launches fill
+    // the device while another's last documents of a round finish (a round is quantised by how many of its
+    // documents the device holds at once).  SharedMatrix pairs keep one group.
+    static const int groups_env = [] {
+        const char* v = std::getenv("MTR_GROUPS");
+        return v ? std::max(1, std::min(int(mtr_engine::kLanes), std::atoi(v))) : 1;
+    }();
+    bool any_pair = false;
+    for (uint32_t d = 0; d < e->n_docs && d < e->h_kind.size(); d++) any_pair = any_pair || e->h_kind[d] != 0;
+    const int G = any_pair ? 1 : std::max(1, std::min<int>(groups_env, int(e->n_docs)));
+    const int L = std::max(1, nlanes / G);  // lanes (streams) per group
     const size_t ncls = 1 + 3 * kAllClasses;
-    if (e->cls.ensure(ncls) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
-    if (!e->h_cls) HIPCHK(hipHostMalloc((void**)&e->h_cls, ncls * sizeof(int32_t), hipHostMallocDefault));
-    int32_t* cls = e->h_cls;
-    for (;;) {
-        HIPCHK(hipMemsetAsync(e->cls.p, 0, ncls * sizeof(int32_t), e->stream));
-        classify_kernel<<<(e->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, e->n_docs, e->dkind.p,
-                                                                           e->dpart.p, e->cls.p, e->dlist.p, class_leaves);
+    if (e->cls.ensure(ncls * mtr_engine::kLanes) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
+    if (!e->h_cls)
+        HIPCHK(hipHostMalloc((void**)&e->h_cls, ncls * mtr_engine::kLanes * sizeof(int32_t), hipHostMallocDefault));
+    auto lane_stream = [&](int g, int l) -> hipStream_t {
+        const int si = g * L + l;
+        return si == 0 ? e->stream : e->aux[si - 1];
+    };
+    struct Grp {
+        uint32_t lo = 0, hi = 0;
+        bool done = false;
+    };
+    std::vector<Grp> grp(static_cast<size_t>(G));
+    for (int g = 0; g < G; g++) {
+        grp[size_t(g)].lo = uint32_t(uint64_t(e->n_docs) * uint64_t(g) / uint64_t(G));
+        grp[size_t(g)].hi = uint32_t(uint64_t(e->n_docs) * uint64_t(g + 1) / uint64_t(G));
+    }
+    // the groups' lanes start after everything queued on the engine stream (the batch upload)
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    for (int g = 0; g < G; g++)
+        for (int l = 0; l < L; l++)
+            if (g * L + l > 0) HIPCHK(hipStreamWaitEvent(lane_stream(g, l), e->ev[0], 0));
+    // classify group g (on its first lane) and read its class counts back
+    auto classify = [&](int g) -> int {
+        Grp& gr = grp[size_t(g)];
+        hipStream_t st = lane_stream(g, 0);
+        int32_t* dcls = e->cls.p + size_t(g) * ncls;
+        HIPCHK(hipMemsetAsync(dcls, 0, ncls * sizeof(int32_t), st));
+        const uint32_t n = gr.hi - gr.lo;
+        classify_kernel<<<(n + 255) / 256, 256, 0, st>>>(e->hdr.p, e->docs.p, gr.lo, gr.hi, e->dkind.p, e->dpart.p,
+                                                         dcls, e->dlist.p + size_t(kAllClasses) * gr.lo, class_leaves);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(cls, e->cls.p, ncls * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        const int rem = cls[0];
-        if (rem <= 0) break;
-        const int k = std::min(K, rem);
-        bool stuck = false;
-        HIPCHK(hipEventRecord(e->ev[0], e->stream));
+        HIPCHK(hipMemcpyAsync(e->h_cls + size_t(g) * ncls, dcls, ncls * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(e->grp_cls[g], st));
+        return 0;
+    };
+    // HBM-resident launches need the scratch / chunk-record buffers: allocated by the first such launch
+    auto ensure_global = [&]() -> int {
+        if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
+        if (!e->csum.p) {  // for every document the engine may hold: it must never move
+            const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * csum_ints(int(P.segcap));
+            if (e->csum.ensure(n)) return -1;
+            if (e->umap.ensure(size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * size_t(P.segcap))) return -1;
+            HIPCHK(hipMemsetAsync(e->umap.p, 0xff, e->umap.n * sizeof(int32_t), e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+        }
+        return 0;
+    };
+    // one round of group g: a launch per size class, spread over the group's lanes, joined on its first lane
+    auto issue_round = [&](int g, bool& stuck) -> int {
+        Grp& gr = grp[size_t(g)];
+        const int32_t* cls = e->h_cls + size_t(g) * ncls;
+        const uint32_t n = gr.hi - gr.lo;
+        const int k = std::min(K, cls[0]);
+        hipStream_t st0 = lane_stream(g, 0);
+        HIPCHK(hipEventRecord(e->grp_fork[g], st0));
         int nl = 0;  // launches of this round
         for (int c = kAllClasses - 1; c >= 0; c--) {  // one launch per size class: matrix pairs, then the
             const bool pair = c >= kClasses;              // SharedString classes, largest documents first
@@ -687,86 +749,117 @@ static int run_impl(mtr_engine* e, int gen) {
                                                                        : round64(maxheap + 2 * k + 8)));
             size_t lds = lds_bytes(cap, lhcap, P.gen != 0);
             if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
-            P.global_mode = 0;
+            KParams Q = P;
+            Q.global_mode = 0;
             if (lds > lds_limit) {
                 // documents larger than LDS: leaves, heap and scan arrays stay in the HBM slab
-                if (e->scratch.ensure(size_t(e->n_docs) * 2 * P.segcap)) return -1;
-                if (!e->csum.p) {  // for every document the engine may hold: it must never move
-                    const size_t n = size_t(std::max<uint32_t>(e->max_docs, 1)) * csum_ints(int(P.segcap));
-                    if (e->csum.ensure(n)) return -1;
-                    if (e->umap.ensure(size_t(std::max<uint32_t>(e->max_docs, 1)) * 2 * size_t(P.segcap))) return -1;
-                    HIPCHK(hipMemsetAsync(e->umap.p, 0xff, e->umap.n * sizeof(int32_t), e->stream));
-                }
-                P.csum = e->csum.p;
-                P.umap = e->umap.p;
-                P.global_mode = 1;
-                P.scratch = e->scratch.p;
-                cap = P.segcap;
-                lhcap = P.hcap;
-                lds = lds_bytes_global_mode(int(P.segcap));
+                if (ensure_global()) return -1;
+                Q.csum = e->csum.p;
+                Q.umap = e->umap.p;
+                Q.global_mode = 1;
+                Q.scratch = e->scratch.p;
+                cap = Q.segcap;
+                lhcap = Q.hcap;
+                lds = lds_bytes_global_mode(int(Q.segcap));
                 if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             }
-            const int kk = tight && !P.global_mode ? k : std::max(1, std::min(k, (cap - maxseg - 8) / 2));
-            if (cap - maxseg - 8 < 2 && cap >= P.segcap) stuck = true;  // no room and no larger LDS class
-            P.cap = cap;
-            P.lhcap = lhcap;
-            P.ops_this_launch = kk;
-            P.doc_list = e->dlist.p + size_t(c) * e->n_docs;
-            P.n_launch = uint32_t(cnt);
-            const int lane = nl % nlanes;
-            hipStream_t st = lane == 0 ? e->stream : e->aux[lane - 1];
-            if (lane != 0 && nl < nlanes) HIPCHK(hipStreamWaitEvent(st, e->ev[0], 0));
-            while (e->kev.size() < size_t(2 * (nl + 1))) {
+            const int kk = tight && !Q.global_mode ? k : std::max(1, std::min(k, (cap - maxseg - 8) / 2));
+            if (cap - maxseg - 8 < 2 && cap >= Q.segcap) stuck = true;  // no room and no larger LDS class
+            Q.cap = cap;
+            Q.lhcap = lhcap;
+            Q.ops_this_launch = kk;
+            Q.doc_list = e->dlist.p + size_t(kAllClasses) * gr.lo + size_t(c) * n;
+            Q.n_launch = uint32_t(cnt);
+            const int lane = nl % L;
+            hipStream_t st = lane_stream(g, lane);
+            if (lane != 0 && nl < L) HIPCHK(hipStreamWaitEvent(st, e->grp_fork[g], 0));
+            const size_t q = size_t(e->launches);
+            while (e->kev.size() < 2 * (q + 1)) {
                 hipEvent_t x;
                 HIPCHK(hipEventCreate(&x));
                 e->kev.push_back(x);
             }
-            HIPCHK(hipEventRecord(e->kev[2 * nl], st));
+            HIPCHK(hipEventRecord(e->kev[2 * q], st));
             int av = -1;
             if (pair) {
-                av = P.gen ? (P.global_mode ? AV_PAIR_HBM_GN : AV_PAIR_LDS_GN)  // record mode (mtr_generate_matrix)
-                     : P.doff ? (P.global_mode ? AV_PAIR_HBM_DL : AV_PAIR_LDS_DL)  // a matrix tracked for its cells
-                     : (P.global_mode ? AV_PAIR_HBM : AV_PAIR_LDS);
-            } else if (P.gen) {  // record mode: the generating instantiation
-                av = P.global_mode ? AV_HBM_GN : AV_LDS_GN;
-            } else if (P.doff) {  // a batch with MTR_F_DELTA ops: the delta-reporting instantiation
-                av = P.global_mode ? AV_HBM_DL : AV_LDS_DL;
-            } else if (P.global_mode) {  // HBM-resident: the lean instantiation unless the batch has rare records
+                av = Q.gen ? (Q.global_mode ? AV_PAIR_HBM_GN : AV_PAIR_LDS_GN)  // record mode (mtr_generate_matrix)
+                     : Q.doff ? (Q.global_mode ? AV_PAIR_HBM_DL : AV_PAIR_LDS_DL)  // a matrix tracked for its cells
+                     : (Q.global_mode ? AV_PAIR_HBM : AV_PAIR_LDS);
+            } else if (Q.gen) {  // record mode: the generating instantiation
+                av = Q.global_mode ? AV_HBM_GN : AV_LDS_GN;
+            } else if (Q.doff) {  // a batch with MTR_F_DELTA ops: the delta-reporting instantiation
+                av = Q.global_mode ? AV_HBM_DL : AV_LDS_DL;
+            } else if (Q.global_mode) {  // HBM-resident: the lean instantiation unless the batch has rare records
                 av = e->has_ext ? AV_HBM_X : AV_HBM_LEAN;
             } else if (e->has_ext) {
                 av = AV_LDS_X;
-            } else if (no_fixed_cap || (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, P) &&
-                       !launch_fixed_cap_p1(cap, uint32_t(cnt), lds, st, P) &&
-                       !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, P))) {
+            } else if (no_fixed_cap || (!launch_fixed_cap_p0(cap, uint32_t(cnt), lds, st, Q) &&
+                       !launch_fixed_cap_p1(cap, uint32_t(cnt), lds, st, Q) &&
+                       !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, Q))) {
                 av = AV_LDS_LEAN;  // above the fixed classes: runtime layout, lean
             }
-            if (av >= 0 && !launch_variant(av, uint32_t(cnt), lds, st, P, pair ? uint32_t(lds / 2) : 0u)) {
+            if (av >= 0 && !launch_variant(av, uint32_t(cnt), lds, st, Q, pair ? uint32_t(lds / 2) : 0u)) {
                 set_err("no apply kernel variant " + std::to_string(av));
                 return -1;
             }
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(e->kev[2 * nl + 1], st));
+            HIPCHK(hipEventRecord(e->kev[2 * q + 1], st));
             e->launches++;
             nl++;
         }
-        for (int l = 1; l < std::min(nl, nlanes); l++) {  // join the lanes
-            HIPCHK(hipEventRecord(e->lane_done[l], e->aux[l - 1]));
-            HIPCHK(hipStreamWaitEvent(e->stream, e->lane_done[l], 0));
+        for (int l = 1; l < std::min(nl, L); l++) {  // join the lanes
+            const int si = g * L + l;
+            HIPCHK(hipEventRecord(e->lane_done[si], lane_stream(g, l)));
+            HIPCHK(hipStreamWaitEvent(st0, e->lane_done[si], 0));
         }
-        HIPCHK(hipEventRecord(e->ev[1], e->stream));
-        HIPCHK(hipEventSynchronize(e->ev[1]));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
-        e->t_apply += ms;
-        for (int q = 0; q < nl; q++) {
-            float kms = 0;
-            HIPCHK(hipEventElapsedTime(&kms, e->kev[2 * q], e->kev[2 * q + 1]));
-            e->t_kernels += kms;
+        return 0;
+    };
+    const size_t launches0 = size_t(e->launches);
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));  // (timing start: after the forks above)
+    for (int g = 0; g < G; g++)
+        if (classify(g)) return -1;
+    int left = G;
+    bool stuck = false;
+    while (left > 0) {
+        bool progressed = false;
+        for (int g = 0; g < G; g++) {
+            Grp& gr = grp[size_t(g)];
+            if (gr.done) continue;
+            const hipError_t q = hipEventQuery(e->grp_cls[g]);
+            if (q == hipErrorNotReady) continue;
+            HIPCHK(q);
+            progressed = true;
+            const int32_t* cls = e->h_cls + size_t(g) * ncls;
+            if (cls[0] <= 0) {
+                gr.done = true;
+                left--;
+                continue;
+            }
+            if (issue_round(g, stuck)) return -1;
+            if (stuck) break;
+            if (classify(g)) return -1;  // queued behind the round's launches
         }
-        if (stuck) {
-            set_err("document exceeds the leaf capacity");
-            return MTR_ERR_CAPACITY;
+        if (stuck) break;
+        if (!progressed) std::this_thread::yield();
+    }
+    for (int g = 0; g < G; g++)
+        if (g > 0) {  // join every group into the engine stream
+            HIPCHK(hipEventRecord(e->lane_done[g * L], lane_stream(g, 0)));
+            HIPCHK(hipStreamWaitEvent(e->stream, e->lane_done[g * L], 0));
         }
+    HIPCHK(hipEventRecord(e->ev[2], e->stream));
+    HIPCHK(hipEventSynchronize(e->ev[2]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev[1], e->ev[2]));
+    e->t_apply += ms;
+    for (size_t q = launches0; q < size_t(e->launches); q++) {
+        float kms = 0;
+        HIPCHK(hipEventElapsedTime(&kms, e->kev[2 * q], e->kev[2 * q + 1]));
+        e->t_kernels += kms;
+    }
+    if (stuck) {
+        set_err("document exceeds the leaf capacity");
+        return MTR_ERR_CAPACITY;
     }
     e->summarized = false;
     return MTR_OK;

@@ -73,6 +73,14 @@ export class BatchReplayClient {
 	getText(): string; // MergeTreeTextHelper.getText, MergeTreeTextHelper.ts:20
 	getLength(): number;
 	getCurrentSeq(): number;
+	/** interval collections (sequence/src/intervalCollection.ts): the summary's `header` blob before load ... */
+	loadIntervals(header: string): void;
+	/** ... and loadFinished (sequence.ts:750-801) after load and its catch-up messages */
+	loadFinished(): void;
+	/** a detached string's collection: add(start, end, intervalType, props with an intervalId) */
+	getIntervalCollection(label: string): { add(start: number, end: number, intervalType: number, props: object): void };
+	/** the summary's `header` blob (sequence.ts:467-480); undefined when there are no collections */
+	summarizeIntervals(): string | undefined;
 	summarize(
 		runtime: { deltaManager: { minimumSequenceNumber: number; lastSequenceNumber: number } },
 		handle: unknown,

@@ -23,6 +23,7 @@
  * Written for Node >= 12 (no optional chaining).
  */
 const path = require('path');
+const { IntervalCollections, IntervalUnsupported } = require('./intervals.js');
 
 let addon = null;
 function native() {
@@ -204,6 +205,16 @@ class DocLog {
         // MergeTree.idToSegment (mergeTree.ts:549,668) as the host sees it: id key -> marker ordinal
         this.nMarkers = 0; this.markerIds = new Map(); this.markerDup = new Set(); this.markerIdAnnotated = false;
         this.nRefs = 0;  // local references created (MTR_OP_REF_CREATE ids)
+        this.currentSeq = 0;  // collabWindow.currentSeq as the host sees it (interval ops do not move it)
+        this.intervals = undefined;  // ./intervals.js IntervalCollections, when used
+    }
+    _intervals(fn) {  // an interval path this host does not restate is an UnsupportedError (the document falls back)
+        try {
+            return fn();
+        } catch (e) {
+            if (e instanceof IntervalUnsupported) throw new UnsupportedError(e.message);
+            throw e;
+        }
     }
     static _idKey(v) {  // SameValueZero keys; objects only match themselves (never from JSON)
         if (typeof v === 'boolean') return 'b' + v;
@@ -352,6 +363,7 @@ class DocLog {
             this.observerId = longId;
             const me = this.addLongId(longId);
             this.collaborating = true;
+            this.currentSeq = currentSeq;
             this.push(OP.START_COLLAB, 0, me, currentSeq, 0, minSeq, 0, 0, 0, 0);
         } else {  // reconnect under a new id: the observer's short id is renamed
             const me = this.clientIx.get(this.observerId);
@@ -360,7 +372,7 @@ class DocLog {
             this.clients[me] = longId;
         }
     }
-    seqUpdate(min, seq) { this.push(OP.SEQ, F.LAST, 0, seq, seq, min, 0, 0, 0, 0); }
+    seqUpdate(min, seq) { this.currentSeq = seq; this.push(OP.SEQ, F.LAST, 0, seq, seq, min, 0, 0, 0, 0); }
     // SnapshotLoader.specToSegment (snapshotLoader.ts:88-128): one LOAD (header) / APPEND (body) record whose
     // removedClientIds (short ids) ride in the text arena
     _snapshotSeg(spec, it, opType, flags) {
@@ -425,9 +437,15 @@ class DocLog {
         const cid = msg.clientId === null || msg.clientId === undefined ? 'null' : String(msg.clientId);
         const short = this.shortId(cid);
         const seq = msg.sequenceNumber, ref = msg.referenceSequenceNumber, msn = msg.minimumSequenceNumber;
-        if (msg.type !== 'op') { this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
+        if (msg.type !== 'op') { this.currentSeq = seq; this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
         let contents = msg.contents;
         if (typeof contents === 'string') contents = JSON.parse(contents);
+        if (contents && contents.type === 'act') {  // an interval collection's op (sequence.ts:620-646): not a merge-tree op
+            if (this.intervals === undefined) this.intervals = new IntervalCollections();
+            this._intervals(() => this.intervals.process(this, contents, msg));
+            return;
+        }
+        this.currentSeq = seq;
         const members = contents.type === 3 ? contents.ops : [contents];  // MergeTreeDeltaType.GROUP
         if (members.length === 0) { this.push(OP.SEQ, F.LAST, short, seq, ref, msn, 0, 0, 0, 0); return; }
         if (cid === this.observerId || local) {  // ackPendingSegment per member (client.ts:641-663, 866-869)
@@ -899,9 +917,12 @@ class BatchReplayClient {
             }
             const lo = this.log.ops.length;
             this.log.message(msg, this.engine.interner, local);
-            if (!this.engine.options.snapshotV1 && msg.type === 'op') this.engine.catchUps[this.doc].add(msg, this.log, lo);
+            // (an interval op is handled by the collections and kept by no catch-up list, sequence.ts:636-645)
+            if (!this.engine.options.snapshotV1 && msg.type === 'op' && this.log.currentSeq === msg.sequenceNumber) {
+                this.engine.catchUps[this.doc].add(msg, this.log, lo);
+            }
         });
-        this.currentSeq = msg.sequenceNumber;
+        this.currentSeq = this.log.currentSeq;
     }
     updateSeqNumbers(min, seq) {
         this._queue(() => this.log.seqUpdate(min, seq));
@@ -994,6 +1015,35 @@ class BatchReplayClient {
         return { leafIndex: r[0], offset: r[1], held: r[3] === 1 };
     }
     getCurrentSeq() { return this.currentSeq; }
+    // ---- interval collections (sequence/src/intervalCollection.ts; SharedSegmentSequence, sequence.ts:445-801)
+    /** DefaultMap.populate of the SharedString summary's `header` blob, before load(). */
+    loadIntervals(header) {
+        this._queue(() => {
+            this.log.intervals = new IntervalCollections();
+            this.log._intervals(() => this.log.intervals.populate(header));
+        });
+    }
+    /** loadFinished (sequence.ts:750-801): after load() and its catch-up messages, the collections attach. */
+    loadFinished() {
+        if (this.log.intervals !== undefined) this._queue(() => this.log._intervals(() => this.log.intervals.attach(this.log)));
+    }
+    /** getIntervalCollection(label) (sequence.ts:445-447): add(start, end, intervalType, props) on a string
+     * that is not collaborating yet (a detached SharedString); remote ops arrive through applyMsg. */
+    getIntervalCollection(label) {
+        if (this.log.intervals === undefined) this.log.intervals = new IntervalCollections();
+        const c = this.log.intervals.get(label);
+        return { add: (start, end, intervalType, props) => {
+            this._queue(() => this.log._intervals(() => c.add(this.log, start, end, intervalType, props)));
+        } };
+    }
+    /** The summary's `header` blob (summarizeCore, sequence.ts:467-480), undefined when there are no collections. */
+    summarizeIntervals() {
+        if (this.log.intervals === undefined) return undefined;
+        this.engine.flush();
+        this._check();
+        const st = native().getRefStates(this.engine.h, this.doc);
+        return this.log._intervals(() => this.log.intervals.serialize(st, this.log.currentSeq));
+    }
     getText() {
         this.engine.flush();
         this._check();

@@ -107,7 +107,7 @@ void finalize_engine(napi_env, void* data, void*) {
 }
 
 // createEngine(maxDocs, {device, newLengthCalc, snapshotV1, chunkSize, maxSegments, heapEntries,
-//                        textUnits, propWords, removerCells, opsPerLaunch})     client.ts:107
+//                        textUnits, propWords, removerCells, opsPerLaunch, refSlots})     client.ts:107
 napi_value CreateEngine(napi_env env, napi_callback_info info) {
     napi_value argv[2];
     if (!get_args(env, info, 2, argv)) return nullptr;
@@ -124,6 +124,7 @@ napi_value CreateEngine(napi_env env, napi_callback_info info) {
     c.prop_words = uint32_t(num_prop(env, argv[1], "propWords", 0));
     c.remover_cells = uint32_t(num_prop(env, argv[1], "removerCells", 0));
     c.ops_per_launch = uint32_t(num_prop(env, argv[1], "opsPerLaunch", 0));
+    c.ref_slots = uint32_t(num_prop(env, argv[1], "refSlots", 0));
     const int device = int(num_prop(env, argv[1], "device", 0));
     mtr_engine* e = mtr_engine_create(&o, device, max_docs, &c);
     if (!e) return throw_engine(env, "mtr_engine_create");
@@ -347,6 +348,26 @@ napi_value GetRefPositions(napi_env env, napi_callback_info info) {
     return r;
 }
 
+// getRefStates(h, doc) -> Int32Array [position, MTR_REF_ST_* bits] per local reference (mtr_get_ref_states): what an
+// interval collection's summary order needs (sequence/src/intervalCollection.ts:1105-1112)
+napi_value GetRefStates(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    const int64_t n = mtr_get_ref_states(e, doc, nullptr, 0);
+    if (n < 0) return throw_engine(env, "mtr_get_ref_states");
+    void* data = nullptr;
+    napi_value ab, r;
+    NAPI_CALL(env, napi_create_arraybuffer(env, size_t(n) * 8, &data, &ab));
+    if (n > 0 && mtr_get_ref_states(e, doc, static_cast<int32_t*>(data), 2 * n) != n)
+        return throw_engine(env, "mtr_get_ref_states");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, size_t(2 * n), ab, 0, &r));
+    return r;
+}
+
 // getRefInfo(h, doc, id) -> [leaf, offset, refType, held] (LocalReference.getSegment/getOffset, localReference.ts:106-112)
 napi_value GetRefInfo(napi_env env, napi_callback_info info) {
     napi_value argv[3];
@@ -539,7 +560,8 @@ napi_value Init(napi_env env, napi_value exports) {
                {"stats", Stats},               {"reset", Reset},         {"setMatrix", SetMatrix},
                {"getDeltas", GetDeltas},       {"submitRunAsync", SubmitRunAsync},
                {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment},
-               {"getProps", GetProps}, {"getRefPositions", GetRefPositions}, {"getRefInfo", GetRefInfo}};
+               {"getProps", GetProps}, {"getRefPositions", GetRefPositions}, {"getRefInfo", GetRefInfo},
+               {"getRefStates", GetRefStates}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||

@@ -49,7 +49,7 @@ def test_addon_loads_and_fails_loudly_without_a_gpu():
     assert json.loads(lines[0]) == sorted(["createEngine", "submitRun", "summarize", "getSummary", "getText",
                                            "docStatus", "stats", "reset", "setMatrix", "getDeltas",
                                            "submitRunAsync", "summarizeAsync", "getContainingSegment", "getProps",
-                                           "getRefPositions", "getRefInfo"])
+                                           "getRefPositions", "getRefInfo", "getRefStates"])
     if lines[1] != "ENGINE":  # no HIP device here: construction must throw, never fall back
         assert lines[1].startswith("ERR mtr_engine_create")
 
@@ -470,3 +470,71 @@ def test_load_through_node_host(tmp_path):
         bb = build_batch([lb], it)
         assert ob.apply(bb, 0) == 0
         assert [base64.b64decode(x) for x in r["b"]] == ob.summarize(bb, 0), f"log {r['log']}: loaded client's summary"
+
+
+def _interval_sessions():
+    """Interval sessions for the Node host: the four fixture loads, the detached recipe, and two farms."""
+    import interval_farm as F
+    from fixtures import load_snapshots, snapshot_recipe
+
+    snaps = load_snapshots()
+    out = []
+    for name in F.FIXTURES:
+        out.append({"header": F.HEADERS[name], "blobs": snaps[name], "want": F.V2_HEADER})
+    out.append({"local": [[o[1], o[2]] for o in snapshot_recipe("withIntervals")],
+                "adds": [list(x) for x in F.fixture_ids()], "want": F.V2_HEADER})
+    for seed in (1, 2):
+        init, msgs, obs = F.farm(seed)
+        out.append({"initial": init, "msgs": msgs, "want": obs.summarize_header(), "text": obs.text()})
+    return out
+
+
+def test_js_interval_host_matches_python_host(tmp_path):
+    """The Node host's interval collections (intervals.js) pack the same records as the Python host
+    (fluidframework_amd/intervals.py) for the fixture loads, the detached recipe and two farms, and -- given the
+    CPU oracle's reference states for those records -- write the oracle's `header` blob."""
+    _addon()
+    import interval_farm as F
+
+    sessions = _interval_sessions()
+    py = []
+    for s in sessions:
+        h = F.HostString("oracle")
+        if "header" in s:
+            h.log.load(s["blobs"], "loader", h.it, header=s["header"])
+        for pos, text in s.get("local", []):
+            h.log.local_insert(pos, text, h.it)
+        for label, a, b, t, i in s.get("adds", []):
+            h.log.interval_collection(label).local_add(h.log, a, b, t, {"intervalId": i})
+        if "initial" in s:
+            h.log.local_insert(0, s["initial"], h.it)
+            h.log.start_collab("observer")
+        for m in s.get("msgs", []):
+            h.log.message(dict(m), h.it)
+        b = build_batch([h.log], h.it)
+        doc = OracleDoc(options())
+        assert doc.apply(b, 0) == 0
+        s["states"] = [x for st in doc.ref_states() for x in st]
+        py.append((b, h.log.interval_header(doc.ref_states()).decode()))
+    f = tmp_path / "sessions.json"
+    f.write_text(json.dumps(sessions))
+    js = json.loads(_node([os.path.join(HERE, "node", "intervals_pack.js"), str(f)]))
+    for s, (b, header), j in zip(sessions, py, js):
+        assert base64.b64decode(j["ops"]) == b.ops.tobytes()
+        assert base64.b64decode(j["docs"]) == b.docs.tobytes()
+        assert j["header"] == header == s["want"]
+
+
+@pytest.mark.gpu
+def test_intervals_through_node_host(tmp_path):
+    """Interval collections through N-API -> C ABI -> HIP: the fixtures load and summarize back to their V2 header,
+    the detached recipe writes it, and two farms' observers write the oracle's header and text."""
+    _addon()
+    sessions = _interval_sessions()
+    f = tmp_path / "sessions.json"
+    f.write_text(json.dumps(sessions))
+    res = json.loads(_node([os.path.join(HERE, "node", "intervals_engine.js"), str(f)], timeout=600))
+    for s, r in zip(sessions, res):
+        assert r["header"] == s["want"]
+        if "text" in s:
+            assert r["text"] == s["text"]
