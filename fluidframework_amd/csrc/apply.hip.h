@@ -334,7 +334,9 @@ MTR_DI uint32_t ns_of(uint32_t m) { return (m & M_NS_MASK) >> M_NS_SHIFT; }
 MTR_DI uint32_t set_ns(uint32_t m, uint32_t ns) { return (m & ~M_NS_MASK) | (ns << M_NS_SHIFT); }
 
 // ------------------------------------------------------------------ wave primitives
-MTR_DI int lane_id() { return int(threadIdx.x); }  // blockDim.x == 64
+// (a wave's own lane: apply_pair2_kernel runs two waves per workgroup; with 64-thread launch bounds the mask
+// folds away)
+MTR_DI int lane_id() { return int(threadIdx.x & 63u); }
 constexpr uint64_t LO32 = 0x00000000ffffffffull, HI32 = 0xffffffff00000000ull;  // lanes 0-31, 32-63
 MTR_DI uint64_t lanes_below() { return (uint64_t(1) << lane_id()) - 1; }
 MTR_DI int first_lane(uint64_t m) { return __ffsll((long long)m) - 1; }
@@ -439,15 +441,15 @@ struct ProfScope {
     __device__ ProfScope(lptr<Sc> s, int i) : sc(s), id(i), t(clock64()) {}
     __device__ ~ProfScope() {
         const long long d = clock64() - t;
-        if (threadIdx.x == 0) sc->prof[id] += (unsigned long long)d;
+        if (lane_id() == 0) sc->prof[id] += (unsigned long long)d;
     }
 };
 #define PROF(id) ProfScope _prof_scope(L.sc, id)
 #define PROF_T0(v) const long long v = clock64()
 #define PROF_ADD(id, v) \
-    if (threadIdx.x == 0) L.sc->prof[id] += (unsigned long long)(clock64() - (v))
+    if (lane_id() == 0) L.sc->prof[id] += (unsigned long long)(clock64() - (v))
 #define PROF_COUNT(id) \
-    if (threadIdx.x == 0) L.sc->prof[id]++
+    if (lane_id() == 0) L.sc->prof[id]++
 #else
 #define PROF(id)
 #define PROF_COUNT(id)
@@ -880,10 +882,18 @@ struct Eng {
                     if (ln == lq[g]) vl = tot;
                 }
             }
-            if (e < n) {
-                cx[c] = vl;
-                __atomic_fetch_add(&sd[c >> 6], vl - h.x, __ATOMIC_RELAXED);
-            }
+            if (e < n) cx[c] = vl;
+            // each superchunk's change: the listed chunks come superchunk by superchunk, so lanes of one
+            // superchunk are contiguous -- a segmented sum (one scan, one shuffle) and one plain add by the
+            // segment's last lane, instead of 64 same-address LDS atomics that serialize
+            const int key = e < n ? (c >> 6) : -1;
+            const int dv = e < n ? vl - h.x : 0;
+            const int inc = wave_incl_scan(dv);
+            const int kprev = __shfl(key, max(ln - 1, 0)), knext = __shfl(key, min(ln + 1, 63));
+            const uint64_t starts = __ballot(ln == 0 || key != kprev);
+            const int first = last_lane(starts & ((uint64_t(2) << ln) - 1));
+            const int base = __shfl(inc, first) - __shfl(dv, first);
+            if (e < n && (ln == 63 || knext != key)) sd[key] += inc - base;
         }
         wsync();
     }
@@ -3150,7 +3160,8 @@ struct Eng {
                         }
                 }
                 if (PM) {  // BaseSegment.append: lengths only
-                    if (ln == 0) L.len[rdlane(i, h)] = total;
+                    const int hs = rdlane(i, h);  // (read with the whole wave active, as below)
+                    if (ln == 0) L.len[hs] = total;
                     PROF_COUNT(P_NMERGE);
                     wsync();
                     continue;
@@ -3892,7 +3903,7 @@ struct Eng {
         const gptr<mtr_op> rec = gp(P.gen_ops) + dd.op_begin + idx;
         if (idx < P.gen_grow) return;  // a pre-grown snapshot segment, written by synth_grow_kernel
         if (idx == P.gen_grow) {
-            if (threadIdx.x == 0) {
+            if (lane_id() == 0) {
                 mtr_op z{};
                 z.type = MTR_OP_START_COLLAB;
                 st_struct(rec, z);
@@ -3900,7 +3911,7 @@ struct Eng {
             wsync();
             return;
         }
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             mtr_op op;
             mtr_synth_state st = ld_struct<mtr_synth_state>(L.gst);
             mtr_synth_begin(&P.gen_cfg, &st, idx - P.gen_grow, &op);
@@ -3915,7 +3926,7 @@ struct Eng {
         v.client = enc_client(uni(L.sc->gen_client));
         v.local = 0;
         const int len = view_scan(L, s, v, P.new_length_calc, 0, 0);
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             mtr_op op = ld_struct<mtr_op>(rec);
             mtr_synth_state st = ld_struct<mtr_synth_state>(L.gst);
             mtr_synth_finish(&P.gen_cfg, &st, len, &op, P.gen_text + dd.text_base);
@@ -3940,10 +3951,10 @@ struct Eng {
             s.chunked = G ? h.chunked : 0;
         }
         if (PM && s.textused == 0) {  // new HandleTable: handles = [1] (handletable.ts:24)
-            if (threadIdx.x == 0) handles(L)[0] = 1;
+            if (lane_id() == 0) handles(L)[0] = 1;
             s.textused = 1;
         }
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             L.sc->relmask = 0;
             L.sc->nrefs = gp((const DocHdr*)P.hdr)[d].nrefs;
             L.sc->fail_op = gp((const DocHdr*)P.hdr)[d].fail_op;
@@ -3960,7 +3971,7 @@ struct Eng {
             const int S = s.nseg;
             const int cs = P.segcap;
             const gptr<const uint32_t> g = gp((const uint32_t*)P.seg) + size_t(d) * NF * cs;
-            for (int i = threadIdx.x; i < S; i += 64) {
+            for (int i = lane_id(); i < S; i += 64) {
                 L.len[i] = int(g[F_LEN * cs + i]);
                 L.seq[i] = int(g[F_SEQ * cs + i]);
                 L.rseq[i] = int(g[F_RSEQ * cs + i]);
@@ -3971,7 +3982,7 @@ struct Eng {
             }
             const int hn = s.heapn;
             const gptr<const uint32_t> gh = gp((const uint32_t*)P.heap) + size_t(d) * 2 * P.hcap;
-            for (int i = threadIdx.x; i <= hn; i += 64) {
+            for (int i = lane_id(); i <= hn; i += 64) {
                 L.hseq[i] = int(gh[i]);
                 L.huid[i] = gh[P.hcap + i];
             }
@@ -3987,7 +3998,7 @@ struct Eng {
             const int S = s.nseg;
             const int cs = P.segcap;
             const gptr<uint32_t> g = gp(P.seg) + size_t(d) * NF * cs;
-            for (int i = threadIdx.x; i < S; i += 64) {
+            for (int i = lane_id(); i < S; i += 64) {
                 g[F_LEN * cs + i] = uint32_t(L.len[i]);
                 g[F_SEQ * cs + i] = uint32_t(L.seq[i]);
                 g[F_RSEQ * cs + i] = uint32_t(L.rseq[i]);
@@ -3998,12 +4009,12 @@ struct Eng {
             }
             const int hn = s.heapn;
             const gptr<uint32_t> gh = gp(P.heap) + size_t(d) * 2 * P.hcap;
-            for (int i = threadIdx.x; i <= hn; i += 64) {
+            for (int i = lane_id(); i <= hn; i += 64) {
                 gh[i] = uint32_t(L.hseq[i]);
                 gh[P.hcap + i] = L.huid[i];
             }
         }
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             const gptr<DocHdr> hp = gp(P.hdr) + d;
             DocHdr h = ld_struct<DocHdr>(hp);
             h.nseg = s.nseg; h.height = s.height; h.minseq = s.minseq; h.curseq = s.curseq;
@@ -4057,7 +4068,7 @@ struct Eng {
             L.gst = (lptr<mtr_synth_state>)(smem + ((sizeof(Sc) + 15) & ~size_t(15)));
             L.sx = (lptr<int>)(smem + kScBytes);
             for (int q = lane_id(); q < 2 * sup_rows(L.cap); q += 64) L.sx[sup_rows(L.cap) + q] = 0;  // fills, marks
-            if (threadIdx.x == 0) L.sc->sepoch = 0;
+            if (lane_id() == 0) L.sc->sepoch = 0;
         } else {
             const int cap = CAP > 0 ? CAP : P.cap, lhcap = P.lhcap;
             char* p = smem;
@@ -4090,7 +4101,7 @@ struct Eng {
             delta = (unsigned long long)(P.delta + o * 4);
             L.dcap = int(gp(P.doff)[d + 1] - o);
         }
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             const unsigned long long rm = (unsigned long long)(P.rm + size_t(d) * (size_t(P.rcap) + 2 * size_t(P.rtab)));
             L.sc->cp[CP_TEXT] = (unsigned long long)(P.text + size_t(d) * P.tcap);
             L.sc->cp[CP_PROP] = (unsigned long long)(P.prop + size_t(d) * P.pcap);
@@ -4595,7 +4606,7 @@ struct Eng {
     static MTR_DI void gen_pair_op(D& L0, D& L1, const KParams& P, St& s0, St& s1, const mtr_doc_desc& dd, int idx) {
         const gptr<mtr_op> rec = gp(P.gen_ops) + dd.op_begin + idx;
         if (idx == 0) {
-            if (threadIdx.x == 0) {
+            if (lane_id() == 0) {
                 mtr_op z{};
                 z.type = MTR_OP_START_COLLAB;
                 st_struct(rec, z);
@@ -4603,7 +4614,7 @@ struct Eng {
             wsync();
             return;
         }
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             mtr_op op;
             mtr_synth_state st = ld_struct<mtr_synth_state>(L0.gst);
             mtr_synth_begin(&P.gen_cfg, &st, idx, &op);
@@ -4621,7 +4632,7 @@ struct Eng {
         const int lr = s0.nseg > 0 ? (uni(L0.E[s0.nseg - 1]) & EMASK) : 0;
         prefix(L1, s1, v, P.new_length_calc);
         const int lc = s1.nseg > 0 ? (uni(L1.E[s1.nseg - 1]) & EMASK) : 0;
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             mtr_op op = ld_struct<mtr_op>(rec);
             mtr_synth_state st = ld_struct<mtr_synth_state>(L0.gst);
             mtr_synth_matrix_finish(&P.gen_cfg, &st, lr, lc, &op);
@@ -4718,6 +4729,75 @@ struct Eng {
         store_doc(L0, P, s0, d, done);
         store_doc(L1, P, s1, d1, 0);  // the cols vector's op cursor stays at 0 (it has no op list of its own)
     }
+
+    // A matrix pair on two waves (apply_pair2_kernel): wave w owns vector w (0 = rows, 1 = cols), each in its own
+    // LDS region, and both walk the pair's op list.  The two PermutationVectors share nothing but that list: a
+    // setCell resolves the row on wave 0 and the col on wave 1 at the same time (the single-wave kernel's find2,
+    // split across waves), and each allocates its own handle once both positions are defined (matrix.ts:669-689);
+    // a row / col op runs on its own vector's wave.  The waves meet at a workgroup barrier after every op (and
+    // between a setCell's resolution and its allocations), exchanging `defined` / `ok` words in LDS, so both stop
+    // at the same op.  Replay only: local ops (partner localSeq), delta records and record mode keep run_pair.
+    static MTR_DI void run_pair2(char* smem, size_t region, const KParams& P, uint32_t d) {
+        const int w = int(threadIdx.x >> 6);  // this wave's vector
+        const uint32_t d1 = uniu(gp(P.dpart)[d]);
+        const uint32_t dw = w ? d1 : d;
+        const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
+        const int cursor = uni(gp(P.hdr)[d].op_cursor);
+        const int n_ops = min(int(dd.op_count) - cursor, P.ops_this_launch);
+        // (both waves read the same words: they take the same branch)
+        if (n_ops <= 0 || uni(gp(P.hdr)[d].status) != MTR_OK || uni(gp(P.hdr)[d1].status) != MTR_OK) return;
+        // the exchange words sit behind the two regions: [0..1] defined, [2..5] ok (by op parity), [6..7] counters
+        const lptr<int> xch = (lptr<int>)(smem + 2 * region);
+        D L;
+        carve(L, smem + (w ? region : 0), P, dw);
+        St s;
+        load_doc(L, P, s, dw);
+        int done = 0;
+        unsigned long long acc_s = 0;
+        const gptr<const mtr_op> ops = gp(P.ops) + dd.op_begin + cursor;
+        for (int k = 0; k < n_ops; k++) {
+            const mtr_op op = uni_struct(ld_struct<mtr_op>(ops + k));
+            bool ok = true;
+            if (op.type == MTR_OP_START_COLLAB && !(op.flags & MTR_F_APPEND)) {  // both vectors (matrix.ts:514-532)
+                ok = apply_op(L, P, s, op, dd, false, 0, cursor + k);
+            } else if (op.type == MTR_OP_SETCELL) {
+                acc_s += (unsigned long long)s.nseg;  // (each wave counts its own vector's leaves)
+                View v;
+                v.ref = op.ref_seq;
+                v.client = enc_client(int(int16_t(op.client)));
+                v.local = (!s.collab || uint32_t(s.local) == v.client) ? 1 : 0;
+                const int pos = w ? op.pos2 : op.pos1;
+                int f, b, off = 0;
+                find1(L, s, v, pos, f, b, P.new_length_calc);
+                const int idx = adjust_position(L, s, pos, f, b, off);
+                if (lane_id() == 0) xch[w] = idx >= 0 ? 1 : 0;
+                __syncthreads();
+                const bool both = xch[0] != 0 && xch[1] != 0;  // (the row undefined: the col is not allocated)
+                if (both) (void)handle_at(L, P, s, idx, off);
+                if (s.status != MTR_OK) set_fail(L, cursor + k);
+                ok = s.status == MTR_OK;
+            } else if (((op.flags & MTR_F_COLS) != 0) == (w == 1)) {
+                const int n0 = s.nseg;
+                ok = apply_op(L, P, s, op, dd, false, 0, cursor + k);
+                if (ok && counts_s(op)) acc_s += (unsigned long long)n0;
+            }
+            // (the ok words alternate by op parity: a wave writes op k + 1's word while the other may still be
+            // reading op k's, never op k - 1's -- it passed this barrier of op k only after reading that)
+            const int q = 2 + 2 * (k & 1);
+            if (lane_id() == 0) xch[q + w] = ok ? 1 : 0;
+            __syncthreads();
+            if (xch[q] == 0 || xch[q + 1] == 0) break;
+            done = k + 1;
+        }
+        if (w == 1 && lane_id() == 0) {
+            xch[6] = int(acc_s & 0xffffffffull);
+            xch[7] = int(acc_s >> 32);
+        }
+        __syncthreads();
+        if (w == 0 && lane_id() == 0)  // the matrix's counters are kept with its rows document
+            L.sc->sum_s += acc_s + (unsigned long long)uint32_t(xch[6]) + ((unsigned long long)uint32_t(xch[7]) << 32);
+        store_doc(L, P, s, dw, w ? 0 : done);
+    }
 };
 
 // GN: record mode (synthetic workloads, untimed) as its own instantiation, so the replay kernels
@@ -4758,12 +4838,23 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, G ? 
     Eng<G, true, 0, DL, GN>::run_pair(smem, pair_region, P, d);
 }
 
+// SharedMatrix pairs on two waves (run_pair2): a 128-thread workgroup, one wave per vector
+template <bool G>
+__global__ void __launch_bounds__(2 * NT) __attribute__((amdgpu_waves_per_eu(1, G ? 1 : 8))) apply_pair2_kernel(KParams P, uint32_t pair_region) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (blockIdx.x >= P.n_launch) return;
+    const uint32_t d = P.doc_list[blockIdx.x];
+    Eng<G, true, 0, false, false>::run_pair2(smem, pair_region, P, d);
+}
+constexpr size_t kPair2Xch = 64;  // bytes behind the two regions: run_pair2's exchange words
+
 // the runtime-layout instantiations, launched by name from mtr_engine.hip and compiled in kVariantParts
 // translation units (apply_variants.hip): X = the rare records compiled in, LEAN = without them, DL = delta
 // reporting, GN = record mode; PAIR = SharedMatrix pairs
 enum ApplyVariant {
     AV_LDS_X = 0, AV_HBM_X, AV_LDS_LEAN, AV_HBM_LEAN, AV_LDS_DL, AV_HBM_DL, AV_LDS_GN, AV_HBM_GN,
-    AV_PAIR_LDS, AV_PAIR_HBM, AV_PAIR_LDS_DL, AV_PAIR_HBM_DL, AV_PAIR_LDS_GN, AV_PAIR_HBM_GN, AV_COUNT
+    AV_PAIR_LDS, AV_PAIR_HBM, AV_PAIR_LDS_DL, AV_PAIR_HBM_DL, AV_PAIR_LDS_GN, AV_PAIR_HBM_GN, AV_PAIR2_LDS,
+    AV_PAIR2_HBM, AV_COUNT
 };
 constexpr int kVariantParts = 5;
 bool launch_variant_p0(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);

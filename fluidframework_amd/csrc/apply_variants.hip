@@ -25,6 +25,14 @@ static void go(void (*k)(Args...), bool& attr, uint32_t grid, size_t lds, hipStr
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, st, args...);
 }
+template <class... Args>
+static void go2(void (*k)(Args...), bool& attr, uint32_t grid, size_t lds, hipStream_t st, Args... args) {
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(2 * NT), lds, st, args...);  // two waves per workgroup
+}
 
 // one variant, instantiated only in the part that owns it (V % kVariantParts)
 template <int V>
@@ -46,6 +54,8 @@ static bool try_variant(int v, uint32_t grid, size_t lds, hipStream_t st, const 
         if constexpr (V == AV_PAIR_HBM_DL) go(apply_pair_kernel<true, true>, attr, grid, lds, st, P, region);
         if constexpr (V == AV_PAIR_LDS_GN) go(apply_pair_kernel<false, false, true>, attr, grid, lds, st, P, region);
         if constexpr (V == AV_PAIR_HBM_GN) go(apply_pair_kernel<true, false, true>, attr, grid, lds, st, P, region);
+        if constexpr (V == AV_PAIR2_LDS) go2(apply_pair2_kernel<false>, attr, grid, lds, st, P, region);
+        if constexpr (V == AV_PAIR2_HBM) go2(apply_pair2_kernel<true>, attr, grid, lds, st, P, region);
         return true;
     }
     return false;

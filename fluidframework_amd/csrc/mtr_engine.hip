@@ -659,6 +659,8 @@ static int run_impl(mtr_engine* e, int gen) {
         return v ? std::max(1, std::min(int(mtr_engine::kLanes), std::atoi(v))) : int(mtr_engine::kLanes);
     }();
     static const bool no_fixed_cap = std::getenv("MTR_NO_FIXED_CAP") != nullptr;
+    // matrix pairs on one wave even when two could run them (tuning knob MTR_PAIR1)
+    static const bool pair1 = std::getenv("MTR_PAIR1") != nullptr;
     static const int slack_env = [] {
         const char* v = std::getenv("MTR_SLACK");
         return v ? std::max(0, std::atoi(v)) : -1;
@@ -675,6 +677,9 @@ static int run_impl(mtr_engine* e, int gen) {
     for (uint32_t d = 0; d < e->n_docs && d < e->h_kind.size(); d++) any_pair = any_pair || e->h_kind[d] != 0;
     const int G = any_pair ? 1 : std::max(1, std::min<int>(groups_env, int(e->n_docs)));
     const int L = std::max(1, nlanes / G);  // lanes (streams) per group
+    int n_cu = 0;
+    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
+    const bool few_docs = e->n_docs <= uint32_t(std::max(n_cu, 1));
     const size_t ncls = 1 + 3 * kAllClasses;
     if (e->cls.ensure(ncls * mtr_engine::kLanes) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
     if (!e->h_cls)
@@ -740,7 +745,9 @@ static int run_impl(mtr_engine* e, int gen) {
             // overflow the launch's LDS, so they get `slack` leaves of room; matrix pairs (setCell
             // splits) and record mode (ops drawn once) keep room for every op of the launch
             const bool tight = !pair && !P.gen;
-            const int slack = slack_env >= 0 ? slack_env : 8;
+            // (a batch of fewer documents than CUs has LDS to spare: room for the whole launch, so a document
+            // does not yield and wait for a round of its own)
+            const int slack = slack_env >= 0 ? slack_env : (few_docs ? k + 8 : 8);
             int cap = tight ? round32(maxseg + slack + 8) : round64(maxseg + 2 * k + 8);
             if (cap > P.segcap) cap = P.segcap;
             // LRU heap: what the class holds now plus room for this launch's pushes; a document that
@@ -785,6 +792,12 @@ static int run_impl(mtr_engine* e, int gen) {
                 av = Q.gen ? (Q.global_mode ? AV_PAIR_HBM_GN : AV_PAIR_LDS_GN)  // record mode (mtr_generate_matrix)
                      : Q.doff ? (Q.global_mode ? AV_PAIR_HBM_DL : AV_PAIR_LDS_DL)  // a matrix tracked for its cells
                      : (Q.global_mode ? AV_PAIR_HBM : AV_PAIR_LDS);
+                // replaying remote messages only: a wave per vector (run_pair2), if its exchange words fit
+                if (!Q.gen && !Q.doff && !e->has_ext && !e->pend_seen && !pair1 &&
+                    lds + kPair2Xch <= size_t(std::max(dev_lds, 0))) {
+                    av = Q.global_mode ? AV_PAIR2_HBM : AV_PAIR2_LDS;
+                    lds += kPair2Xch;
+                }
             } else if (Q.gen) {  // record mode: the generating instantiation
                 av = Q.global_mode ? AV_HBM_GN : AV_LDS_GN;
             } else if (Q.doff) {  // a batch with MTR_F_DELTA ops: the delta-reporting instantiation
@@ -798,7 +811,8 @@ static int run_impl(mtr_engine* e, int gen) {
                        !launch_fixed_cap_p2(cap, uint32_t(cnt), lds, st, Q))) {
                 av = AV_LDS_LEAN;  // above the fixed classes: runtime layout, lean
             }
-            if (av >= 0 && !launch_variant(av, uint32_t(cnt), lds, st, Q, pair ? uint32_t(lds / 2) : 0u)) {
+            const uint32_t region = !pair ? 0u : uint32_t((av == AV_PAIR2_LDS || av == AV_PAIR2_HBM ? lds - kPair2Xch : lds) / 2);
+            if (av >= 0 && !launch_variant(av, uint32_t(cnt), lds, st, Q, region)) {
                 set_err("no apply kernel variant " + std::to_string(av));
                 return -1;
             }

@@ -323,13 +323,15 @@ class Engine:
 
     def props(self, doc, ref) -> list:
         """The properties an MTR_DELTA_REGEN_X record references (mtr_get_props): [(key id, value id)]."""
-        n = lib().mtr_get_props(self.h, doc, ref, None, 0)
+        # (a first buffer of 17 words: an empty set's single word fits, so -1 can only mean an error)
+        out = np.zeros(17, dtype="<u4")
+        n = lib().mtr_get_props(self.h, doc, ref, out.ctypes.data, len(out))
         if n == -1:
             raise EngineError(_err())
-        n = -n if n < 0 else n
-        out = np.zeros(max(n, 1), dtype="<u4")
-        if lib().mtr_get_props(self.h, doc, ref, out.ctypes.data, n) != n:
-            raise EngineError(f"mtr_get_props failed: {_err()}")
+        if n < 0:
+            out = np.zeros(-n, dtype="<u4")
+            if lib().mtr_get_props(self.h, doc, ref, out.ctypes.data, len(out)) != len(out):
+                raise EngineError(f"mtr_get_props failed: {_err()}")
         return [(int(out[1 + 2 * k]), int(out[2 + 2 * k])) for k in range(int(out[0]))]
 
     def deltas(self, doc) -> np.ndarray:

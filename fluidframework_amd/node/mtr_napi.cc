@@ -527,7 +527,8 @@ napi_value GetProps(napi_env env, napi_callback_info info) {
     uint32_t doc = 0, ref = 0;
     NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
     NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &ref));
-    int64_t n = mtr_get_props(e, doc, ref, nullptr, 0);
+    uint32_t one = 0;  // (cap 1: an empty set's single word fits, so -1 is always an error)
+    int64_t n = mtr_get_props(e, doc, ref, &one, 1);
     if (n == -1) return throw_engine(env, "mtr_get_props");
     n = n < 0 ? -n : n;
     void* data = nullptr;

@@ -78,7 +78,8 @@ int64_t mtr_get_deltas(mtr_engine* e, uint32_t doc, mtr_delta* out, int64_t cap)
 /* The properties an MTR_DELTA_REGEN_X record references (its len field): [n, key id, value id, ...] in JS
  * own-key order, the ids of the batch tables' keys and values -- the segment's `properties` that
  * createInsertSegmentOp serializes (client.ts:763-768 -> TextSegment / Marker.toJSONObject).  Returns the
- * word count 2n + 1, -(that) when cap is too small, -1 on a bad reference.  Replaces reading
+ * word count 2n + 1, -(that) when cap is too small, -1 on a bad reference (pass cap >= 1: an empty set's one
+ * word then always fits, so -1 is never a size).  Replaces reading
  * segment.properties in resetPendingDeltaToOps (client.ts:708-800). */
 int64_t mtr_get_props(mtr_engine* e, uint32_t doc, uint32_t ref, uint32_t* out, int64_t cap);
 
