@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "sequenced ops applied/sec (whole node) over 100k docs, bit-exact summaries"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: chip-level parameters)
+SALU_PEAK = 256 * 2.4e9  # scalar instructions per second: one SALU per CU per cycle at the 2.4 GHz peak clock
 
 
 # BASELINE.json configs: documents per GPU, messages per document, writers, max lag
@@ -430,8 +431,16 @@ def main(argv=None):
             "counter_hbm_gbs": round(traffic * launches_per_step / apply_s / 1e9, 1) if traffic and apply_s > 0
             else None,
         }
+        # the issue roofline of the scalar unit (one per CU, one SALU instruction per cycle: 256 CUs x 2.4 GHz),
+        # which binds the replay kernels (MI355X_MICROARCH.md; SQ counters of the same build in `source`)
+        salu = ipo.get("salu", 0.0)
+        if salu > 0:
+            per_gpu = value / max(1, world)  # (the counters are one GPU's)
+            issue["salu_roofline"] = {"achieved": round(salu * per_gpu / 1e9, 1), "peak": SALU_PEAK / 1e9,
+                                      "unit": "G SALU instr/s per GPU", "frac": round(salu * per_gpu / SALU_PEAK, 4)}
     roofline = {
-        "bound": "hbm",  # (the contract's vocabulary: the path's roofline is HBM; no MFMA)
+        "bound": "hbm",  # (the contract's vocabulary: the path's roofline is HBM; no MFMA -- what binds is in
+        # `binding` and issue.salu_roofline)
         "binding": "instruction issue" if not grow else "per-wave latency",
         "limiter": "per-wave issue latency: one wave per document applies its ops in order (a chain of "
                    "dependent LDS round trips, ballots and scalar control per op); waves per SIMD are "

@@ -728,34 +728,48 @@ struct Eng {
             hi = min(hi, s.nseg);
             if (lo >= hi) return;
             const int c0 = max(lo, 0) >> 6, c1 = (hi - 1) >> 6;
-            for (int c = c0; c <= c1; c++) {
-                const int i = c * 64 + lane_id();
-                const bool in = i < s.nseg;
-                const int ic = min(i, s.nseg - 1);
-                const uint32_t m = L.meta[ic];
-                const int len = L.len[ic], sq = L.seq[ic], rs = L.rseq[ic];
-                const bool live = in && !(m & M_DEL);
-                const bool rem = rs != RNONE;
-                // in the window: an event after minSeq (a pending local one included), so views differ on it
-                const bool win = live && (sq > s.minseq || (rem && rs > s.minseq));
-                const uint64_t wm = __ballot(win);
-                const int nw = __popcll(wm);
-                int x = (live && !rem) ? len : 0;
-                int fx = (live && !rem && !win) ? len : 0;  // removed at or before minSeq: in no view
-                int ev = live ? max(sq, rem ? rs : 0) : 0;
-                x = rdlane(wave_incl_scan(x), 63);
-                fx = rdlane(wave_incl_scan(fx), 63);
+            for (int cb = c0; cb <= c1; cb += GK) {  // GK chunks' leaf fields in flight per step
+                uint32_t mq[GK];
+                int lq[GK], sqq[GK], rq[GK];
 #pragma unroll
-                for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
-                const gptr<int> r = cs_rec(L, c);
-                if (win && nw <= kChunkList) {
-                    const int k = __popcll(wm & lanes_below());
-                    *(gptr<v4i>)(r + 4 + 4 * k) = v4i{len, rs, sq, int(m)};  // Hot's field order
-                    r[4 + 4 * kChunkList + k] = i;
+                for (int g = 0; g < GK; g++) {
+                    const int ic = min((cb + g) * 64 + lane_id(), s.nseg - 1);
+                    mq[g] = L.meta[ic];
+                    lq[g] = L.len[ic];
+                    sqq[g] = L.seq[ic];
+                    rq[g] = L.rseq[ic];
                 }
-                if (lane_id() == 0) {
-                    *(gptr<v4i>)r = v4i{x, ev, fx, min(nw, kChunkList + 1)};
-                    ch_ev(L)[c] = ev;
+#pragma unroll
+                for (int g = 0; g < GK; g++) {
+                    const int c = cb + g;
+                    if (c > c1) break;
+                    const int i = c * 64 + lane_id();
+                    const bool in = i < s.nseg;
+                    const uint32_t m = mq[g];
+                    const int len = lq[g], sq = sqq[g], rs = rq[g];
+                    const bool live = in && !(m & M_DEL);
+                    const bool rem = rs != RNONE;
+                    // in the window: an event after minSeq (a pending local one included), so views differ on it
+                    const bool win = live && (sq > s.minseq || (rem && rs > s.minseq));
+                    const uint64_t wm = __ballot(win);
+                    const int nw = __popcll(wm);
+                    int x = (live && !rem) ? len : 0;
+                    int fx = (live && !rem && !win) ? len : 0;  // removed at or before minSeq: in no view
+                    int ev = live ? max(sq, rem ? rs : 0) : 0;
+                    x = rdlane(wave_incl_scan(x), 63);
+                    fx = rdlane(wave_incl_scan(fx), 63);
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) ev = max(ev, __shfl_xor(ev, o));
+                    const gptr<int> r = cs_rec(L, c);
+                    if (win && nw <= kChunkList) {
+                        const int k = __popcll(wm & lanes_below());
+                        *(gptr<v4i>)(r + 4 + 4 * k) = v4i{len, rs, sq, int(m)};  // Hot's field order
+                        r[4 + 4 * kChunkList + k] = i;
+                    }
+                    if (lane_id() == 0) {
+                        *(gptr<v4i>)r = v4i{x, ev, fx, min(nw, kChunkList + 1)};
+                        ch_ev(L)[c] = ev;
+                    }
                 }
             }
             for (int q = (c0 >> 6) + lane_id(); q <= (c1 >> 6); q += 64) sup_mark(L)[q] = 1;
@@ -897,8 +911,12 @@ struct Eng {
         }
         wsync();
     }
-    // the view's superchunk lengths and their inclusive prefix in sup_pre; returns the view's total length
-    static MTR_DI int prefix2(D& L, const St& s, const View& v, int newlen) {
+    // the view's superchunk lengths and their inclusive prefix in sup_pre; returns the view's total length.
+    // need < INT32_MAX: the caller reads the view only up to position need - 1 (its searches stop at the first
+    // superchunk whose prefix reaches need, and its windows reach at most one superchunk further), so the scan
+    // stops once the superchunk after the one reaching need is complete -- the dirty chunks of later
+    // superchunks are not evaluated, sup_pre is valid up to there and the returned length is partial.
+    static MTR_DI int prefix2(D& L, const St& s, const View& v, int newlen, int need = INT32_MAX) {
         PROF(P_PREFIX);
         sup_refresh(L, s);
         const int nch = (s.nseg + 63) >> 6, ns = (nch + 63) >> 6, ln = lane_id();
@@ -930,19 +948,36 @@ struct Eng {
                 const uint64_t dm = __ballot(dirty);
                 if (dirty) lst[n + __popcll(dm & lanes_below())] = c;
                 n += __popcll(dm);
-                if (n > kListCap - 64 || !dq) {
+                // (a bounded scan evaluates the list every 128+ entries, so it can stop within a few superchunks
+                // of need)
+                if (n > kListCap - 64 || !dq || (need != INT32_MAX && n >= 128)) {
                     wsync();
 #ifdef MTR_PROF
                     if (ln == 0) L.sc->prof[P_NDCH] += (unsigned long long)n;
 #endif
                     dirty_chunks(L, s, v, newlen, n);
                     n = 0;
+                    if (need != INT32_MAX && dq) {
+                        // superchunks [b, b + lim) are complete (the next dirty one not listed yet): stop when one
+                        // of them starts at or after need -- the one before it reached need
+                        const int lim = first_lane(dq);
+                        const bool in = q < ns && ln < lim;
+                        const int slen = in ? sl0 + (((dq0 >> ln) & 1) ? sd[q] : 0) : 0;
+                        const int inc = wave_incl_scan(slen);
+                        if (__ballot(in && carry + inc - slen >= need)) {
+                            if (in) spre[q] = carry + inc;
+                            wsync();
+                            return carry + rdlane(inc, 63);
+                        }
+                    }
                 }
             }
             const int slen = q < ns ? sl0 + (((dq0 >> ln) & 1) ? sd[q] : 0) : 0;
             const int inc = wave_incl_scan(slen);
             if (q < ns) spre[q] = carry + inc;
+            const bool reached = __ballot(q < ns && carry + inc - slen >= need) != 0;
             carry += rdlane(inc, 63);
+            if (reached) break;  // (the whole batch is complete)
         }
         wsync();
         return carry;
@@ -1013,12 +1048,13 @@ struct Eng {
     // The op's view scan: flat (prefix) or two-level, with E valid over the chunks around positions
     // [p_lo, p_hi] (one chunk before, two after: the searches' windows and the walk's reach).  Returns
     // the view's total length.
-    static MTR_DI int view_scan(D& L, St& s, const View& v, int newlen, int p_lo, int p_hi) {
+    static MTR_DI int view_scan(D& L, St& s, const View& v, int newlen, int p_lo, int p_hi, bool bounded = false) {
         PROF(P_VIEW);
         if constexpr (G) {
             L.rhi = 0;
             if (s.chunked && s.nseg > 0) {
-                const int total = prefix2(L, s, v, newlen);
+                // (a bounded scan only when the caller reads no total: the region's searches stop at need)
+                const int total = prefix2(L, s, v, newlen, bounded ? p_hi + 1 : INT32_MAX);
                 const int nch = (s.nseg + 63) >> 6;
                 const int c0 = max(0, chunk_of(L, s, nch, p_lo) - 1);
                 // (to the chunk of the first leaf past p_hi: chunks with no length in the view -- runs of
@@ -1240,16 +1276,25 @@ struct Eng {
         bool grew = true;
         if constexpr (G) {  // GK rounds per group: every load of the group before its stores (a round's
                             // stores land above every slot the group's lower rounds read)
-            if (s.holes > 0) {  // the first hole at or after `at`, within a bounded window
+            if (s.holes > 0) {  // the first hole at or after `at`, within a bounded window (GK rounds of loads
+                                // in flight per step)
                 const int lim = min(S, at + kHoleWindow);
-                for (int base = at; base < lim; base += 64) {
-                    const int i = base + lane_id();
-                    const uint64_t hm = __ballot(i < lim && (L.meta[min(i, S - 1)] & M_DEL));
-                    if (hm) {
-                        S = base + first_lane(hm);  // move [at, hole) up into the hole
-                        grew = false;
-                        s.holes--;
-                        break;
+                bool found = false;
+                for (int base = at; base < lim && !found; base += 64 * GK) {
+                    uint32_t mq[GK];
+#pragma unroll
+                    for (int q = 0; q < GK; q++) mq[q] = L.meta[min(base + 64 * q + lane_id(), S - 1)];
+#pragma unroll
+                    for (int q = 0; q < GK; q++) {
+                        const int i = base + 64 * q + lane_id();
+                        const uint64_t hm = __ballot(i < lim && (mq[q] & M_DEL));
+                        if (hm) {
+                            S = base + 64 * q + first_lane(hm);  // move [at, hole) up into the hole
+                            grew = false;
+                            s.holes--;
+                            found = true;
+                            break;
+                        }
                     }
                 }
             }
@@ -1538,6 +1583,59 @@ struct Eng {
         const uint64_t m = __ballot((i < hi) & ((ei & EMASK) >= pos));
         return m ? lo + first_lane(m) : hi;
     }
+    // The level-`level` block around slot x (the start of a level-(level - 1) block) and its child count (slots
+    // with bnd >= level - 1): block_start + block_end + count_bnd in one pass that walks both ways at once --
+    // GK rounds of loads in flight per direction -- instead of three passes one after the other (HBM-resident
+    // documents, whose upper blocks can span thousands of slots).  The block's end is the first bnd >= level
+    // after x: none lies between its start and x.
+    static MTR_DI void parent_block(const D& L, const St& s, int x, int level, int& ps, int& pe, int& cnt) {
+        const int S = s.nseg, ln = lane_id();
+        int c = 0;
+        bool bdone = false, fdone = false;
+        ps = 0;
+        pe = S;
+        for (int bb = x, fb = x + 1; !bdone || !fdone; bb -= 64 * GK, fb += 64 * GK) {
+            uint32_t mb[GK], mf[GK];
+#pragma unroll
+            for (int q = 0; q < GK; q++) {
+                mb[q] = L.meta[max(bb - 64 * q - ln, 0)];
+                mf[q] = L.meta[max(min(fb + 64 * q + ln, S - 1), 0)];
+            }
+            if (!bdone) {
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = bb - 64 * q - ln;
+                    const bool child = bnd_of(mb[q]) >= level - 1;
+                    const uint64_t stop = __ballot((i <= 0) | (bnd_of(mb[q]) >= level));
+                    if (stop) {  // slots bb - 64 q down to the block's start (lanes 0 .. k)
+                        const int k = first_lane(stop);
+                        ps = max(0, bb - 64 * q - k);
+                        c += __popcll(__ballot(child) & ((uint64_t(2) << k) - 1));
+                        bdone = true;
+                        break;
+                    }
+                    c += __popcll(__ballot(child));
+                }
+            }
+            if (!fdone) {
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = fb + 64 * q + ln;
+                    const uint64_t stop = __ballot((i >= S) | (bnd_of(mf[q]) >= level));
+                    const uint64_t ch = __ballot((i < S) & (bnd_of(mf[q]) >= level - 1));
+                    if (stop) {  // slots fb + 64 q up to the block's end (lanes below k)
+                        const int k = first_lane(stop);
+                        pe = fb + 64 * q + k;
+                        c += __popcll(ch & ((uint64_t(1) << k) - 1));
+                        fdone = true;
+                        break;
+                    }
+                    c += __popcll(ch);
+                }
+            }
+        }
+        cnt = c;
+    }
     // number of leaves in [bs, be) with bnd >= minb
     static MTR_DI int count_bnd(const D& L, int bs, int be, int minb) {
         int c = 0;
@@ -1606,7 +1704,12 @@ struct Eng {
 
     // [bs, be) = the leaf block holding leaf x, from one ballot over leaves x-31 .. x+32 (leaf
     // blocks hold at most 7 leaves); the loops above take over only if a bound lies outside
+    // (live: the block's slots that are not holes, when both bounds came from this one ballot; else -1)
     static MTR_DI void block_bounds1(const D& L, const St& s, int x, int& bs, int& be) {
+        int live;
+        block_bounds1_live(L, s, x, bs, be, live);
+    }
+    static MTR_DI void block_bounds1_live(const D& L, const St& s, int x, int& bs, int& be, int& live) {
         const int S = s.nseg;
         const int ln = lane_id();
         const int i = x - 31 + ln;
@@ -1617,6 +1720,7 @@ struct Eng {
         const uint64_t em = __ballot((i >= S) | b) & HI32;
         bs = sm ? max(0, x - 31 + last_lane(sm)) : block_start(L, x - 32, 1);
         be = em ? x - 31 + first_lane(em) : block_end(L, s, x + 32, 1);
+        live = (sm && em) ? __popcll(__ballot(in & (i >= bs) & (i < be) & !(mi & M_DEL))) : -1;
     }
 
     // Block overflow after a leaf was added next to x (insertingWalk split + updateRoot,
@@ -1625,9 +1729,10 @@ struct Eng {
     static MTR_DI int overflow_fix(D& L, St& s, int x, int hbs = -1, int hbe = -1) {
         PROF(P_OVERFLOW);
         int level = 1;
-        int bs = hbs, be = hbe;
-        if (bs < 0) block_bounds1(L, s, x, bs, be);
-        int cnt = G && s.holes ? count_live(L, bs, be) : be - bs;  // (holes are no children)
+        int bs = hbs, be = hbe, cnt = -1;
+        if (bs < 0) block_bounds1_live(L, s, x, bs, be, cnt);
+        if (!(G && s.holes)) cnt = be - bs;
+        else if (cnt < 0) cnt = count_live(L, bs, be);  // (holes are no children)
         int xbs = bs;
         while (cnt >= kMaxNodesInBlock) {
             int c5 = bs + kMaxNodesInBlock / 2;
@@ -1645,9 +1750,16 @@ struct Eng {
                 break;
             }
             level++;
-            bs = block_start(L, bs, level);
-            be = block_end(L, s, bs, level);
-            cnt = count_bnd(L, bs, be, level - 1);
+            if constexpr (G) {
+                int nbs, nbe;
+                parent_block(L, s, bs, level, nbs, nbe, cnt);
+                bs = nbs;
+                be = nbe;
+            } else {
+                bs = block_start(L, bs, level);
+                be = block_end(L, s, bs, level);
+                cnt = count_bnd(L, bs, be, level - 1);
+            }
         }
         return xbs;
     }
@@ -3579,6 +3691,12 @@ struct Eng {
             om_known = false;
             wbs = wbe = -1;
         }
+#ifdef MTR_DEBUG_INSERT  // (spill experiment: the insert placement of HBM-resident documents, lane 0)
+        if (G && lane_id() == 0 && S > 0)
+            printf("ins op_begin %llu pos %d slot %d inherit %d nocand %d wbs %d wbe %d E[slot-1] %d E[slot] %d rlo %d rhi %d\n",
+                   (unsigned long long)dd.op_begin, pos, slot, inherit, int(nocand), wbs, wbe, slot > 0 ? int(L.E[slot - 1]) : -9,
+                   slot < S ? int(L.E[slot]) : -9, int(L.rlo), int(L.rhi));
+#endif
         if (slot < 0) return -1;
         const bool grew = shift_right1(L, s, slot);
         if (G && !grew) wbs = wbe = -1;  // a hole was taken: overflow_fix finds the block itself
@@ -4296,7 +4414,7 @@ struct Eng {
             case MTR_OP_LOCAL_INSERT: {
                 int pos = pos1;
                 if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
-                view_scan(L, s, v, P.new_length_calc, pos, pos);
+                view_scan(L, s, v, P.new_length_calc, pos, pos, true);
                 split_at(L, P, s, pos);
                 insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf, lseq ? sseq : seq, lseq);
                 zop = s.collab && !local_op;
@@ -4307,7 +4425,7 @@ struct Eng {
             case MTR_OP_ANNOTATE:
             case MTR_OP_LOCAL_ANNOTATE: {
                 const int is_remove = op.type == MTR_OP_REMOVE || op.type == MTR_OP_LOCAL_REMOVE;
-                view_scan(L, s, v, P.new_length_calc, min(pos1, pos2), max(pos1, pos2));
+                view_scan(L, s, v, P.new_length_calc, min(pos1, pos2), max(pos1, pos2), true);
                 split_at(L, P, s, pos1);
                 split_at(L, P, s, pos2);
                 if (X && lseq) {  // pending: removedSeq = LOCAL_BASE + localSeq; the touched leaves join a group

@@ -669,17 +669,21 @@ static int run_impl(mtr_engine* e, int gen) {
     // (classify -> one launch per size class -> classify ...) on its own streams, so one group's launches fill
     // the device while another's last documents of a round finish (a round is quantised by how many of its
     // documents the device holds at once).  SharedMatrix pairs keep one group.
+    // Default: two groups for batches of 4,096 to 60,000 documents -- the 2- to 8-GPU shares of
+    // C3 gain 5-10 % (profiles/r04_groups.json); above that one group (a round already fills the device), and
+    // more than two leave each group too few lanes.
     static const int groups_env = [] {
         const char* v = std::getenv("MTR_GROUPS");
-        return v ? std::max(1, std::min(int(mtr_engine::kLanes), std::atoi(v))) : 1;
+        return v ? std::max(1, std::min(int(mtr_engine::kLanes), std::atoi(v))) : 0;
     }();
-    bool any_pair = false;
-    for (uint32_t d = 0; d < e->n_docs && d < e->h_kind.size(); d++) any_pair = any_pair || e->h_kind[d] != 0;
-    const int G = any_pair ? 1 : std::max(1, std::min<int>(groups_env, int(e->n_docs)));
-    const int L = std::max(1, nlanes / G);  // lanes (streams) per group
     int n_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->device));
     const bool few_docs = e->n_docs <= uint32_t(std::max(n_cu, 1));
+    bool any_pair = false;
+    for (uint32_t d = 0; d < e->n_docs && d < e->h_kind.size(); d++) any_pair = any_pair || e->h_kind[d] != 0;
+    const int g_want = groups_env > 0 ? groups_env : (e->n_docs >= 4096u && e->n_docs <= 60000u ? 2 : 1);
+    const int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
+    const int L = std::max(1, nlanes / G);  // lanes (streams) per group
     const size_t ncls = 1 + 3 * kAllClasses;
     if (e->cls.ensure(ncls * mtr_engine::kLanes) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
     if (!e->h_cls)
