@@ -23,6 +23,7 @@ OP_REGENERATE = 19
 OP_REF_CREATE = 20
 OP_REF_REMOVE = 21
 OP_LOCAL_SETCELL = 22
+OP_TRACK = 23
 REF_SLIDE = 1
 REF_LOCALVIEW = 2
 # ReferenceType (ops.ts:9-36)
@@ -40,6 +41,10 @@ REF_ST_SEGMENT = 1  # mtr_get_ref_states bits (include/mtr.h)
 REF_ST_HELD = 2
 REF_ST_REMOVED = 4
 DELTA_REGEN = 64
+DELTA_TLINK = 96  # tracking groups (include/mtr_types.h)
+DELTA_TSPLIT = 97
+DELTA_TMERGE = 98
+TRACK_GROUPS = 32
 DELTA_REGEN_X = 72
 REL_BEFORE = 1
 REL_OFFSET = 2

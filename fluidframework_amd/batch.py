@@ -726,23 +726,34 @@ class MatrixLog(DocLog):
         raise Unsupported("ack of a cell write without the cell store")
 
     # -- the client's own edits (SharedMatrix.insertRows / removeRows / insertCols / removeCols, matrix.ts:363-418)
-    def local_vector_op(self, target: str, op: dict) -> None:
+    def local_vector_op(self, target: str, op: dict, track: int = 0, ref_tid: int = -1) -> None:
         """A local insert ({type 0, pos1, seg: [count, start]}) or remove ({type 1, pos1, pos2}) on the rows or
         cols PermutationVector (PermutationVector.insert / remove -> Client.insertSegmentLocal / removeRangeLocal,
-        permutationvector.ts:174-195), then submitVectorMessage's localSeq sync (matrix.ts:321-345)."""
+        permutationvector.ts:174-195), then submitVectorMessage's localSeq sync (matrix.ts:321-345).
+        Undo (fluidframework_amd/undo.py): `track` = the tracking-group bits the op's delta segments join;
+        `ref_tid` >= 0 makes an insert PermutationVector.insertRelative in front of that tracked segment, taking
+        its handles and groups (include/mtr_types.h "Tracking groups")."""
         tf = abi.F_COLS if target == "cols" else 0
         t = op.get("type")
         if t == 0:
             seg = op.get("seg")
             if not (isinstance(seg, list) and len(seg) == 2):
                 raise Unsupported("PermutationSegment spec")
-            self.ops.append((abi.OP_LOCAL_INSERT, tf, 0, self._local_seq(), 0, 0, int(op["pos1"]), -1, 0, int(seg[0])))
-        elif t == 1:
-            self.ops.append((abi.OP_LOCAL_REMOVE, tf, 0, self._local_seq(), 0, 0, int(op["pos1"]), int(op["pos2"]), 0, 0))
+            self.ops.append((abi.OP_LOCAL_INSERT, tf, 0, self._local_seq(), 0, 0, int(op["pos1"]), int(ref_tid),
+                             int(track), int(seg[0])))
+        elif t == 1 and ref_tid < 0:
+            self.ops.append((abi.OP_LOCAL_REMOVE, tf, 0, self._local_seq(), 0, 0, int(op["pos1"]), int(op["pos2"]),
+                             int(track), 0))
         else:
             raise Unsupported(f"local vector op type {t}")
         if self.collaborating:
             self.local_seq += 1
+
+    def track_unlink(self, target: str, tid: int, bits: int) -> None:
+        """TrackingGroup.unlink of the groups `bits` from tracked segment `tid` (-1: from all of them) on the rows or
+        cols vector (MTR_OP_TRACK)."""
+        tf = abi.F_COLS if target == "cols" else 0
+        self.ops.append((abi.OP_TRACK, tf, 0, 0, 0, 0, int(tid), 0, int(bits), 0))
 
     def cols_log(self) -> DocLog:
         """The cols vector's engine document: no ops of its own, the same client table."""

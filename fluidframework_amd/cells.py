@@ -146,6 +146,8 @@ class CellMatrixLog(MatrixLog):
         self.local_meta: list = []            # (row handle, col handle, localSeq) of unacked writes, in order
         self.events: list = []                # (records before it, event): acks of local writes in this batch
         self.ops_kind: dict[int, str] = {}    # record index of a local write before attaching (no pending entry)
+        self.cell_undo: dict = {}             # record index of an undoable local write -> callback(rh, ch, old value)
+        self.tracker = None                   # the undo provider's tracking groups (fluidframework_amd/undo.py)
 
     def local_set_cell(self, row: int, col: int, value: Any) -> None:
         """SharedMatrix.setCell(row, col, value) of this client (local positions)."""
@@ -158,12 +160,17 @@ class CellMatrixLog(MatrixLog):
         else:  # detached: setCellCore writes the cell and sends nothing
             self.ops_kind[k] = "local"
 
-    def local_vector_op(self, target: str, op: dict) -> None:
+    def local_vector_op(self, target: str, op: dict, track: int = 0, ref_tid: int = -1) -> None:
         lo = len(self.ops)
-        super().local_vector_op(target, op)
+        super().local_vector_op(target, op, track, ref_tid)
         for k in range(lo, len(self.ops)):  # (handle recycling on the vector is reported as records)
             rec = self.ops[k]
             self.ops[k] = (rec[0], rec[1] | abi.F_DELTA) + tuple(rec[2:])
+
+    def track_unlink(self, target: str, tid: int, bits: int) -> None:
+        super().track_unlink(target, tid, bits)
+        rec = self.ops[-1]
+        self.ops[-1] = (rec[0], rec[1] | abi.F_DELTA) + tuple(rec[2:])
 
     def _own_set_ack(self) -> None:
         self.events.append((len(self.ops), "ack"))
@@ -200,7 +207,15 @@ class CellMatrixLog(MatrixLog):
                     self.pending.set_cell(a, b, None)
                 continue
             kind, a, b = int(r["kind"]), int(r["pos"]), int(r["len"])
+            if kind in (abi.DELTA_TLINK, abi.DELTA_TSPLIT, abi.DELTA_TMERGE):  # tracking groups (undo.py)
+                if self.tracker is None:
+                    raise ValueError("tracking records without an undo provider")
+                self.tracker.report("cols" if which else "rows", op, kind, a, b)
+                continue
             if kind == DELTA_CELL:
+                if op in self.cell_undo:  # MatrixUndoProvider.cellSet: the handles and the value it replaces
+                    v = self.cells.get_cell(a, b)
+                    self.cell_undo.pop(op)(a, b, v)
                 if op in self.local_sets:  # a local write: the cell now, the pending entry until its ACK
                     self.cells.set_cell(a, b, self.values[op])
                     self.pending.set_cell(a, b, self.local_sets[op])
@@ -222,6 +237,9 @@ class CellMatrixLog(MatrixLog):
         self.local_sets = {}
         self.events = []
         self.ops_kind = {}
+        self.cell_undo = {}
+        if self.tracker is not None:
+            self.tracker.batch_done()
 
     def cells_blob(self) -> bytes:
         """The ``cells`` blob of SharedMatrix.summarizeCore (matrix.ts:458-462):

@@ -3046,6 +3046,115 @@ struct Eng {
                                                       : t == pt + uint32_t(pl);
     }
 
+    // ---- tracking groups of PermutationVector segments (SharedMatrix undo, include/mtr_types.h "Tracking
+    // groups"): a vector's leaves keep their tracking id in the props field (NONE32: never tracked; a permutation
+    // segment has no properties) and the document's property arena holds the group bits per id (propused = ids)
+    static MTR_DI uint32_t tbits(const D& L, uint32_t tid) { return tid == NONE32 ? 0u : uniu(L.gprop()[tid]); }
+    // a fresh id holding `bits` (wave-uniform; NONE32 when the arena is full: s.status)
+    static MTR_DI uint32_t tid_new(const D& L, const KParams& P, St& s, uint32_t bits) {
+        if (uint32_t(s.propused) >= uint32_t(P.pcap)) {
+            s.status = MTR_ERR_CAPACITY;
+            return NONE32;
+        }
+        const uint32_t t = uint32_t(s.propused++);
+        if (lane_id() == 0) L.gprop()[t] = bits;
+        wsync();
+        return t;
+    }
+    // TrackingGroup.link (mergeTreeTracking.ts:41-46) of leaf i into the groups `bits`, reported in link order
+    static MTR_DI void track_link(D& L, const KParams& P, St& s, int i, uint32_t bits) {
+        uint32_t t = uniu(L.props[i]);
+        if (t == NONE32) {
+            t = tid_new(L, P, s, bits);
+            if (t == NONE32) return;
+            if (lane_id() == 0) L.props[i] = t;
+        } else if (lane_id() == 0) {
+            L.gprop()[t] = L.gprop()[t] | bits;
+        }
+        wsync();
+        if (DL && L.dcap > 0) put_record(L, s, s.cur_op, int(t), uni(L.len[i]), MTR_DELTA_TLINK);
+    }
+    // the delta segments of a local remove (range_walk marked them M_TOUCH), in leaf order; `clear`: drop the
+    // marks (a pending remove leaves them to pend_touched)
+    static MTR_DI void track_touched(D& L, const KParams& P, St& s, uint32_t bits, bool clear) {
+        for (int base = 0; base < s.nseg && s.status == MTR_OK; base += 64) {
+            const int i = base + lane_id();
+            const uint32_t m = L.meta[min(i, s.nseg - 1)];
+            const bool t = i < s.nseg && (m & M_TOUCH);
+            uint64_t tm = __ballot(t);
+            if (t && clear) L.meta[i] = m & ~M_TOUCH;
+            wsync();
+            for (; tm && s.status == MTR_OK; tm &= tm - 1) track_link(L, P, s, base + first_lane(tm), bits);
+        }
+    }
+    // BaseSegment.splitAt's trackingCollection.copyTo (mergeTreeNodes.ts:500): the right half of a split of a
+    // tracked leaf (id t) joins its groups under an id of its own; an untracked half keeps none
+    static MTR_DI uint32_t track_split(D& L, const KParams& P, St& s, uint32_t t) {
+        const uint32_t b = tbits(L, t);
+        if (!b) return NONE32;
+        const uint32_t r = tid_new(L, P, s, b);
+        if (r != NONE32 && DL && L.dcap > 0) put_record(L, s, s.cur_op, int(t), int(r), MTR_DELTA_TSPLIT);
+        return r;
+    }
+    // PermutationSegment.transferToReplacement (permutationvector.ts:80-102) from the leaf with id `src` to the
+    // new leaf dst (already linked, so it has an id): the handles and the groups move, the source keeps neither
+    static MTR_DI void track_transfer(D& L, const KParams& P, St& s, int dst, uint32_t src) {
+        int at = -1;
+        for (int base = 0; base < s.nseg && at < 0; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, s.nseg - 1);
+            const uint64_t hit = __ballot(i < s.nseg && !(L.meta[ic] & M_DEL) && L.props[ic] == src);
+            if (hit) at = base + first_lane(hit);
+        }
+        const uint32_t dt = uniu(L.props[dst]);
+        if (at < 0 || at == dst || dt == NONE32) {
+            s.status = MTR_ERR_BAD_OP;
+            return;
+        }
+        if (lane_id() == 0) {
+            L.text[dst] = L.text[at];
+            L.text[at] = uint32_t(MTR_HANDLE_UNALLOCATED);
+            L.gprop()[dt] = L.gprop()[dt] | L.gprop()[src];
+            L.gprop()[src] = 0u;
+        }
+        wsync();
+    }
+    // MergeTree.insertAtReferencePosition (mergeTree.ts:1429-1530) at offset 0 of the leaf with id t: the slot in
+    // front of the run of zero-length leaves that ends at it (backwardExcursion with breakTie against
+    // UnassignedSequenceNumber, which every leaf loses; leaves zamboni may drop -- undefined length -- are skipped
+    // over), -1 when no leaf has the id
+    static MTR_DI int track_ref_slot(const D& L, const KParams& P, const St& s, uint32_t t) {
+        int at = -1;
+        for (int base = 0; base < s.nseg && at < 0; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, s.nseg - 1);
+            const uint64_t hit = __ballot(i < s.nseg && !(L.meta[ic] & M_DEL) && L.props[ic] == t);
+            if (hit) at = base + first_lane(hit);
+        }
+        if (at < 0) return -1;
+        int start = at;
+        for (int j = at - 1; j >= 0; j--) {
+            if (uniu(L.meta[j]) & M_DEL) continue;  // (a hole slot)
+            const int rs = uni(L.rseq[j]);
+            if (rs == RNONE) break;  // a segment the local view shows: positive length
+            if (P.new_length_calc || rs >= LOCAL_BASE || rs > s.minseq) start = j;  // length 0, not undefined
+        }
+        return start;
+    }
+    // MTR_OP_TRACK: TrackingGroup.unlink of the groups `bits` from the leaf with id t (NONE32: from every leaf)
+    static MTR_DI void track_clear(D& L, St& s, uint32_t t, uint32_t bits) {
+        if (t != NONE32) {
+            if (t >= uint32_t(s.propused)) {
+                s.status = MTR_ERR_BAD_OP;
+                return;
+            }
+            if (lane_id() == 0) L.gprop()[t] = L.gprop()[t] & ~bits;
+        } else {
+            for (int q = lane_id(); q < s.propused; q += 64) L.gprop()[q] = L.gprop()[q] & ~bits;
+        }
+        wsync();
+    }
+
     // ------------------------------------------------------------ zamboni
     // scourNode (zamboni.ts:122-193) over the child blocks in [cs, ce): a new child block starts at
     // every leaf with bnd >= 1.  Marks M_DEL; returns #kept (used for a single block).  The leaves
@@ -3089,7 +3198,7 @@ struct Eng {
                 }
                 const int rs = rdlane(vr, t);
                 if (rs != RNONE) {
-                    if (rs > minseq) {
+                    if (rs > minseq || (PM && tbits(L, rdlane(vp, t)))) {  // (a tracked segment is held, zamboni.ts:132)
                         kept++;
                     } else {
                         L.meta[k] = m | M_DEL;  // UNLINK
@@ -3103,10 +3212,14 @@ struct Eng {
                     const uint32_t pk = rdlane(vp, t);
                     const uint32_t tk = rdlane(vt, t);
                     const bool ca = PM ? perm_contig(ptext, plen, tk) : can_append(pmeta, plen, m, lk);
-                    if (prev >= 0 && lk > 0 && ca && props_match_w(L, P, pprops, pk)) {
+                    // (a matrix vector: the same tracking groups, trackingCollection.matches, zamboni.ts:156)
+                    if (prev >= 0 && lk > 0 && ca &&
+                        (PM ? tbits(L, pprops) == tbits(L, pk) : props_match_w(L, P, pprops, pk))) {
                         if constexpr (X && !PM) {  // BaseSegment.append (mergeTreeNodes.ts:527-530)
                             if (nrefs(L)) ref_append(L, uniu(L.uid[k]), uniu(L.uid[prev]), plen);
                         }
+                        if (PM && DL && L.dcap > 0 && tbits(L, pk))  // the appended segment leaves its groups
+                            put_record(L, s, s.cur_op, int(pk), int(pprops), MTR_DELTA_TMERGE);
                         if (PM) {
                             L.len[prev] = plen + lk;
                             wsync();
@@ -3230,13 +3343,21 @@ struct Eng {
         } else {
             link = link & !((vm | pm) & M_MARKER) & !(pm & M_NL);
         }
-        if (__ballot(link & (vp != pp))) {
-            PROF(P_X1);
-            if (link & (vp != pp)) link = props_match(L.gprop(), L.tab(CP_VEQ), pp, vp);
+        // a matrix vector's props field is a tracking id: its group bits (0: none) -- trackingCollection.matches
+        // (zamboni.ts:156) for a merge; a tracked removed segment is held (zamboni.ts:132)
+        uint32_t vb = 0;
+        if (PM && __ballot(in & (vp != NONE32))) vb = (in & (vp != NONE32)) ? L.gprop()[vp] : 0u;
+        if (PM) {
+            link = link & (uint32_t(__shfl(int(vb), ps)) == vb);
+        } else {
+            if (__ballot(link & (vp != pp))) {
+                PROF(P_X1);
+                if (link & (vp != pp)) link = props_match(L.gprop(), L.tab(CP_VEQ), pp, vp);
+            }
+            link = link & !((vp == pp) & pset_never(vp));  // a shared set holding a never-equal value
+            if (__ballot(link & (vl > kGranularity))) return -1;
         }
-        link = link & !((vp == pp) & pset_never(vp));  // a shared set holding a never-equal value
-        if (!PM && __ballot(link & (vl > kGranularity))) return -1;
-        const bool unlink = !pre & removed & !held & (vr <= minseq);
+        const bool unlink = !pre & removed & !held & (vr <= minseq) & (vb == 0u);
         const uint64_t lm = __ballot(link);
         if (unlink | link) L.meta[i] = vm | M_DEL;
         if (PM) {  // UNLINK frees the segment's handles, in leaf order
@@ -3273,6 +3394,9 @@ struct Eng {
                 }
                 if (PM) {  // BaseSegment.append: lengths only
                     const int hs = rdlane(i, h);  // (read with the whole wave active, as below)
+                    if (DL && L.dcap > 0 && rdlane(vb, h))  // the appended segments leave their groups
+                        for (uint64_t mm = mem; mm; mm &= mm - 1)
+                            put_record(L, s, s.cur_op, int(rdlane(vp, first_lane(mm))), int(rdlane(vp, h)), MTR_DELTA_TMERGE);
                     if (ln == 0) L.len[hs] = total;
                     PROF_COUNT(P_NMERGE);
                     wsync();
@@ -3520,7 +3644,8 @@ struct Eng {
                 const uint32_t t0 = rdlane(tj, jl);
                 L.text[r] = t0 == uint32_t(MTR_HANDLE_UNALLOCATED) ? t0 : t0 + uint32_t(off);
             }
-            L.props[r] = rdlane(pj, jl);
+            // (a matrix vector's props field is a tracking id: a tracked leaf's right half gets one of its own)
+            L.props[r] = (PM && rdlane(pj, jl) != NONE32) ? track_split(L, P, s, rdlane(pj, jl)) : rdlane(pj, jl);
             const uint32_t ur = uint32_t(s.uidnext++);
             L.uid[r] = ur;
             if (G && s.chunked && lane_id() == 0) hint(L, ur, r);
@@ -3551,7 +3676,8 @@ struct Eng {
     // seq: breakTie's newSeq; sseq: the seq the new leaf keeps (LOCAL_BASE + localSeq for a pending local
     // insert, which passes lseq > 0 and joins a new SegmentGroup)
     static MTR_DI int insert_at(D& L, const KParams& P, St& s, const View& v, const mtr_op& op, int pos, int seq,
-                                uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf, int sseq, int lseq) {
+                                uint32_t client, const mtr_doc_desc& dd, bool pre, uint32_t pf, int sseq, int lseq,
+                                int force = -1) {
         PROF(P_INSERT);
         const bool marker = (op.flags & MTR_F_MARKER) != 0;
         const int len = marker ? 1 : int(op.payload2);
@@ -3596,7 +3722,10 @@ struct Eng {
         uint32_t om = 0;  // meta of the leaf that starts the block when the new leaf takes its place
         bool om_known = false;
         int wbs = -1, wbe = -1;  // the leaf block around the slot, when the window saw both ends
-        {
+        if (force >= 0) {  // insertAtReferencePosition: in front of leaf `force`, in its leaf block
+            slot = force;
+            inherit = slot == block_start(L, slot, 1) ? 1 : 0;
+        } else {
             PROF(P_INS1);
             if (S == 0) {
                 if (pos == 0) slot = 0;
@@ -4415,8 +4544,24 @@ struct Eng {
                 int pos = pos1;
                 if (op.flags & MTR_F_APPEND) pos = local_length(L, s);
                 view_scan(L, s, v, P.new_length_calc, pos, pos, true);
-                split_at(L, P, s, pos);
-                insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf, lseq ? sseq : seq, lseq);
+                int force = -1;  // PermutationVector.insertRelative (SharedMatrix undo): in front of tracked leaf pos2
+                if (PM && local_op && op.pos2 >= 0) {
+                    force = track_ref_slot(L, P, s, uint32_t(op.pos2));
+                    if (force < 0) {
+                        s.status = MTR_ERR_BAD_OP;
+                        break;
+                    }
+                } else {
+                    split_at(L, P, s, pos);
+                }
+                const int at = insert_at(L, P, s, v, op, pos, seq, client, dd, pre, pf, lseq ? sseq : seq, lseq, force);
+                if (PM && local_op && at >= 0 && s.status == MTR_OK) {  // tracking groups (SharedMatrix undo)
+                    if (op.payload) track_link(L, P, s, at, op.payload);      // VectorUndoProvider.record
+                    if (op.pos2 >= 0 && s.status == MTR_OK) {                 // insertRelative's replacement
+                        if (!op.payload) s.status = MTR_ERR_BAD_OP;
+                        else track_transfer(L, P, s, at, uint32_t(op.pos2));
+                    }
+                }
                 zop = s.collab && !local_op;
                 break;
             }
@@ -4428,14 +4573,18 @@ struct Eng {
                 view_scan(L, s, v, P.new_length_calc, min(pos1, pos2), max(pos1, pos2), true);
                 split_at(L, P, s, pos1);
                 split_at(L, P, s, pos2);
+                // a matrix vector's local remove with tracking bits: its delta segments join those groups
+                const bool track = PM && op.type == MTR_OP_LOCAL_REMOVE && op.payload != 0;
                 if (X && lseq) {  // pending: removedSeq = LOCAL_BASE + localSeq; the touched leaves join a group
                     range_walk(L, P, s, v, pos1, pos2, sseq, client, is_remove, op.payload, is_remove ? 0u : op.payload2,
                                is_remove != 0, true, lseq);
+                    if (track && s.status == MTR_OK) track_touched(L, P, s, op.payload, false);
                     if (s.status == MTR_OK && is_remove) pend_touched(L, P, s, PK_REMOVE, 0u, lseq);
                 } else {
                     range_walk(L, P, s, v, pos1, pos2, seq, client, is_remove, op.payload,
                                (op.type == MTR_OP_ANNOTATE || (X && op.type == MTR_OP_LOCAL_ANNOTATE)) ? op.payload2 : 0u,
-                               DL && !PM && (op.flags & MTR_F_DELTA) != 0);
+                               (DL && !PM && (op.flags & MTR_F_DELTA) != 0) || track);
+                    if (track && s.status == MTR_OK) track_touched(L, P, s, op.payload, true);
                 }
                 if (X && is_remove && !lseq && s.status == MTR_OK && nrefs(L)) ref_slide_walk(L, s, seq);
                 if (G && is_remove) csum_update(L, s, L.wlo, L.whi);
@@ -4504,6 +4653,10 @@ struct Eng {
                 }
                 break;
             }
+            case MTR_OP_TRACK:  // TrackingGroup.unlink (SharedMatrix undo; include/mtr_types.h "Tracking groups")
+                if (!X || !PM) s.status = MTR_ERR_BAD_OP;
+                else track_clear(L, s, op.pos1 < 0 ? NONE32 : uint32_t(op.pos1), op.payload);
+                break;
             case MTR_OP_REF_CREATE:  // a local reference
                 if (!X || PM) s.status = MTR_ERR_BAD_OP;
                 else ref_create(L, P, s, op);
@@ -4780,6 +4933,7 @@ struct Eng {
         for (int k = 0; k < n_ops; k++) {
             if (GN) gen_pair_op(L0, L1, P, s0, s1, dd, cursor + k);
             const mtr_op op = uni_struct(ld_struct<mtr_op>(ops + k));
+            if (DL) s0.cur_op = s1.cur_op = cursor + k;  // (set-cell records split outside apply_op: their reports)
 #ifdef MTR_PROF  // P_X1 = setCell messages, P_X2 = row/col splices
             ProfScope _prof_op(L0.sc, P_OP);
             ProfScope _prof_kind(L0.sc, op.type == MTR_OP_SETCELL ? P_X1 : P_X2);

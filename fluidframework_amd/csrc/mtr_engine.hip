@@ -503,7 +503,9 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
                 }
             }
             if (kind == 1 && flagged) {
-                const uint64_t recycle = uint64_t(e->caps.max_segments) + 2 * uint64_t(dd.op_count);
+                // (+ undo tracking reports: a link per delta segment of a local vector op, a split-off half per
+                // split, a merge per appended segment)
+                const uint64_t recycle = 3 * uint64_t(e->caps.max_segments) + 6 * uint64_t(dd.op_count);
                 need[d] += recycle;
                 const uint32_t d1 = e->h_part[d];
                 if (d1 < b->n_docs) need[d1] += recycle;
@@ -1550,7 +1552,7 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
         }
         uint32_t h = 0;
         const uint32_t pr = hd.seg[F_PROPS * sc + i] & ~MTR_PROPS_NEVER;  // (index flag)
-        if (hd.seg[F_PROPS * sc + i] != NONE32) {
+        if (hd.seg[F_PROPS * sc + i] != NONE32 && !e->h_kind[doc]) {  // (a matrix vector's: a tracking id)
             h = 2166136261u ^ 1u;
             for (uint32_t q = 0; q < hd.prop[pr]; q++) {  // same hash as the oracle export
                 const uint32_t v = hd.prop[pr + 2 + 2 * q];
@@ -1571,6 +1573,30 @@ int64_t mtr_export(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int32
         // PermutationSegment: its start handle (the oracle export does the same)
         r[6] = e->h_kind[doc] ? int32_t(hd.seg[F_TEXT * sc + i]) : ((m & M_MARKER) ? 1 : 0);
         r[7] = int32_t(h);
+    }
+    return k;
+}
+
+int64_t mtr_get_leaves(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap) {
+    HostDoc hd;
+    if (doc >= e->max_docs || !e->h_kind[doc]) {
+        set_err("mtr_get_leaves: not a matrix vector document");
+        return -1;
+    }
+    if (fetch_doc(e, doc, hd)) return -1;
+    const size_t sc = e->caps.max_segments;
+    if (!out || hd.h.nseg - hd.h.holes > cap) return hd.h.nseg - hd.h.holes;  // (a size query)
+    int k = 0;
+    for (int i = 0; i < hd.h.nseg; i++) {
+        const uint32_t m = hd.seg[F_META * sc + i];
+        if (hd.h.holes && (m & M_DEL)) continue;
+        const uint32_t t = hd.seg[F_PROPS * sc + i];
+        int32_t* r = out + 5 * k++;
+        r[0] = int32_t(hd.seg[F_LEN * sc + i]);
+        r[1] = int32_t(hd.seg[F_RSEQ * sc + i]) != RNONE ? 1 : 0;
+        r[2] = int32_t(hd.seg[F_TEXT * sc + i]);
+        r[3] = t == NONE32 ? -1 : int32_t(t);
+        r[4] = t == NONE32 || t >= hd.prop.size() ? 0 : int32_t(hd.prop[t]);
     }
     return k;
 }

@@ -555,7 +555,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
             rs = int(D.rseq[i]);
             sq = int(D.seq[i]);
             m = D.meta[i];
-            pr = D.props[i];
+            pr = D.perm ? NONE32 : D.props[i];  // (a permutation segment's props field is its tracking id)
             tx = D.text[i];
         }
         const int kd = in ? leaf_kind(D, v1, len, rs, m, sq) : 0;

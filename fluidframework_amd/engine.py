@@ -110,6 +110,8 @@ def lib():
         L.mtr_get_ref_positions.restype = C.c_int64
         L.mtr_get_ref_states.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.mtr_get_ref_states.restype = C.c_int64
+        L.mtr_get_leaves.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
+        L.mtr_get_leaves.restype = C.c_int64
         L.mtr_get_ref_info.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         L.mtr_get_ref_info.restype = C.c_int32
         _LIB = L
@@ -386,6 +388,16 @@ class Engine:
         out = np.zeros(2 * n, dtype="<i4")
         self._check(int(lib().mtr_get_ref_states(self.h, doc, out.ctypes.data, 2 * n) != n), "mtr_get_ref_states")
         return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+    def leaves(self, doc) -> np.ndarray:
+        """A matrix vector's segments in tree order, [n, 5] int32: cachedLength, removed, start handle, tracking id
+        (-1: none), tracking-group bits (mtr_get_leaves)."""
+        n = lib().mtr_get_leaves(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"mtr_get_leaves: {_err()}")
+        out = np.zeros(5 * max(n, 1), dtype="<i4")
+        self._check(int(lib().mtr_get_leaves(self.h, doc, out.ctypes.data, n) != n), "mtr_get_leaves")
+        return out[:5 * n].reshape(n, 5)
 
     def ref_info(self, doc, ref_id):
         """(leaf index of the reference's segment or -1, offset, refType, held by the segment's collection)"""

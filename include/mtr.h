@@ -168,6 +168,13 @@ int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t
  * with the position order exactly when every endpoint is held by a live segment or has no segment at all
  * (DESIGN.md section 9).  Returns the reference count (out written only when 2*count fits in cap), -1 on error. */
 int64_t mtr_get_ref_states(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap);
+/* The segments of a SharedMatrix vector document in tree order (walkAllSegments, mergeTreeNodeWalk.ts:170), five
+ * int32 each: cachedLength, 1 when removed (the local view does not show it, localNetLength, mergeTree.ts:613-634),
+ * PermutationSegment.start (permutationvector.ts:53-72; MTR_HANDLE_UNALLOCATED), tracking id (-1: none) and its
+ * group bits (include/mtr_types.h "Tracking groups").  The SharedMatrix undo host reads getPosition,
+ * handleToPosition and the column handles from it (undoprovider.ts:138-170, matrix.ts:371-430).  Returns the
+ * segment count (out written only when it fits in cap segments), -1 on error. */
+int64_t mtr_get_leaves(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap);
 /* Reference `id` of document doc: out[0] = index (tree order) of the leaf of its segment (LocalReference.
  * getSegment, localReference.ts:106; -1 = none, or the segment is no longer in the tree), out[1] = getOffset,
  * out[2] = refType, out[3] = 1 when the segment's LocalReferenceCollection holds it (has(), :357-384).

@@ -87,6 +87,10 @@ enum {
                                    MTR_DELTA_CELL record {op, row handle, col handle}.  A local row / col op (a local
                                    insert / remove record, MTR_F_COLS for cols) sets the other vector's localSeq to its
                                    own (submitVectorMessage, matrix.ts:321-345). */
+    MTR_OP_TRACK = 23,          /* SharedMatrix undo (matrix/src/undoprovider.ts): TrackingGroup.unlink
+                                   (mergeTreeTracking.ts:47-53) on a PermutationVector (MTR_F_COLS: cols) -- clear the
+                                   tracking-group bits `payload` of tracked segment pos1 (-1: of every segment).
+                                   See "Tracking groups" below. */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for
@@ -184,6 +188,30 @@ enum {
  * has no props -- mtr_get_props; -1 = properties undefined). */
 #define MTR_DELTA_REGEN 64
 #define MTR_DELTA_REGEN_X 72
+
+/* Tracking groups (SharedMatrix undo: VectorUndoProvider, matrix/src/undoprovider.ts:17-127, on the merge-tree's
+ * TrackingGroup, mergeTreeTracking.ts).  A PermutationVector segment a group tracks carries a tracking id (tid,
+ * numbered per vector from 0 as segments become tracked, each split-off half of a tracked segment a new one) and
+ * the bit set of the groups that hold it (up to 32 groups live per vector; the host maps groups to bits).  A
+ * segment with a non-empty set is never unlinked by zamboni and merges only with a segment of the same set
+ * (zamboni.ts:132, 156).  Records:
+ *  - MTR_OP_LOCAL_INSERT / MTR_OP_LOCAL_REMOVE of a matrix vector with payload != 0: the op's delta segments (the
+ *    inserted segment; the segments this remove removed first) join the groups of bits `payload`
+ *    (VectorUndoProvider.record -> TrackingGroup.link, undoprovider.ts:30-85);
+ *  - MTR_OP_LOCAL_INSERT of a matrix vector with pos2 >= 0: PermutationVector.insertRelative +
+ *    PermutationSegment.transferToReplacement (permutationvector.ts:80-102, 184-194; matrix.ts:371-380): the new
+ *    segment (at pos1, the host's getPosition of segment pos2 -- insertAtReferencePosition lands there,
+ *    mergeTree.ts:1429-1530) takes segment pos2's handles and groups; payload must be != 0;
+ *  - MTR_OP_TRACK: TrackingGroup.unlink, above.
+ * With MTR_F_DELTA the vector's document reports, in op order: {op, tid, cachedLength, MTR_DELTA_TLINK} per
+ * segment an op linked (link order), {op, tid, tid of the split-off half, MTR_DELTA_TSPLIT} when a tracked
+ * segment splits (BaseSegment.splitAt -> TrackingGroupCollection.copyTo, mergeTreeNodes.ts:500), and {op, tid
+ * of the appended segment, tid of the one it joined, MTR_DELTA_TMERGE} when zamboni appends one tracked segment
+ * to another (zamboni.ts:158-172). */
+#define MTR_DELTA_TLINK 96
+#define MTR_DELTA_TSPLIT 97
+#define MTR_DELTA_TMERGE 98
+#define MTR_TRACK_GROUPS 32
 
 typedef struct mtr_delta {
     uint32_t op;

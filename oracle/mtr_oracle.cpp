@@ -102,6 +102,16 @@ struct Seg : Node {
     int localSeq = -1;
     int localRemovedSeq = -1;
     struct LocalRefs* localRefs = nullptr;  // BaseSegment.localRefs (mergeTreeNodes.ts:380)
+    // BaseSegment.trackingCollection (mergeTreeNodes.ts:373; mergeTreeTracking.ts:62-112): the TrackingGroups
+    // holding the segment, and the id the engine's records and reports name it by (-1: never tracked)
+    std::vector<struct TGroup*> tgroups;
+    int tid = -1;
+};
+
+// TrackingGroup (mergeTreeTracking.ts:12-60): its segments in link order (split-off halves appended); one per
+// group bit of a vector (the host maps the SharedMatrix undo provider's groups to bits)
+struct TGroup {
+    std::vector<Seg*> segs;
 };
 
 // LocalReferenceCollection (localReference.ts:142-571): per offset of its segment the before / at / after
@@ -272,6 +282,9 @@ class Tree {
     int localSeqCounter = 0;
     std::deque<SegGroup*> pendingSegments;
     std::deque<SegGroup> groupPool;
+    // tracking groups (SharedMatrix undo: matrix/src/undoprovider.ts) by bit, and the next tracking id
+    TGroup tgroup[MTR_TRACK_GROUPS];
+    int ntid = 0;
 
     Block* makeBlock() {
         blockPool.emplace_back();
@@ -463,6 +476,11 @@ class Tree {
         r->localSeq = s->localSeq;  // mergeTreeNodes.ts:495-497
         r->localRemovedSeq = s->localRemovedSeq;
         if (s->localRefs) refsSplit(s->localRefs, pos, r);  // mergeTreeNodes.ts:501-503
+        if (!s->tgroups.empty()) {  // trackingCollection.copyTo (mergeTreeNodes.ts:500; mergeTreeTracking.ts:86-92)
+            r->tid = ntid++;
+            for (TGroup* g : s->tgroups) tlink(g, r);
+            if (recycleLog) deltas.push_back({curOpIndex, s->tid, r->tid, MTR_DELTA_TSPLIT});
+        }
         for (SegGroup* g : s->groups) {  // segmentGroups.copyTo -> enqueueOnCopy (segmentGroupCollection.ts:47-62)
             if (g->hasPrevious)  // previousProps of the source segment, duplicated for the copy
                 for (size_t k = 0; k < g->segments.size(); k++)
@@ -474,6 +492,100 @@ class Tree {
             g->segments.push_back(r);
         }
         return r;
+    }
+
+    // ------------------------------------------------------------ tracking groups (mergeTreeTracking.ts)
+    static void tlink(TGroup* g, Seg* s) {  // TrackingGroup.link (:41-46): once per segment
+        if (std::find(g->segs.begin(), g->segs.end(), s) != g->segs.end()) return;
+        g->segs.push_back(s);
+        s->tgroups.push_back(g);
+    }
+    static void tunlink(TGroup* g, Seg* s) {  // TrackingGroup.unlink (:47-53)
+        auto it = std::find(g->segs.begin(), g->segs.end(), s);
+        if (it == g->segs.end()) return;
+        g->segs.erase(it);
+        s->tgroups.erase(std::find(s->tgroups.begin(), s->tgroups.end(), g));
+    }
+    // TrackingGroupCollection.matches (:98-110): the same groups
+    static bool sameGroups(const Seg* a, const Seg* b) {
+        if (a->tgroups.size() != b->tgroups.size()) return false;
+        for (TGroup* g : a->tgroups)
+            if (std::find(b->tgroups.begin(), b->tgroups.end(), g) == b->tgroups.end()) return false;
+        return true;
+    }
+    uint32_t tbits(const Seg* s) const {
+        uint32_t b = 0;
+        for (TGroup* g : s->tgroups) b |= 1u << int(g - tgroup);
+        return b;
+    }
+    // VectorUndoProvider.record (undoprovider.ts:30-85): an op's delta segment joins the groups of `bits`
+    void trackLink(Seg* s, uint32_t bits) {
+        if (s->tid < 0) s->tid = ntid++;
+        for (int b = 0; b < MTR_TRACK_GROUPS; b++)
+            if (bits >> b & 1u) tlink(&tgroup[b], s);
+        if (recycleLog) deltas.push_back({curOpIndex, s->tid, s->len, MTR_DELTA_TLINK});
+    }
+    Seg* findTid(int t) {
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        for (Seg* x : lv)
+            if (x->tid == t) return x;
+        return nullptr;
+    }
+    // MergeTree.insertChildNode (mergeTree.ts:1582-1592)
+    static void insertChildNode(Block* b, Node* child, int idx) {
+        for (int i = b->childCount; i > idx; i--) {
+            b->children[i] = b->children[i - 1];
+            b->children[i]->index = i;
+        }
+        b->childCount++;
+        assignChild(b, child, idx);
+    }
+    // MergeTree.insertAtReferencePosition (mergeTree.ts:1429-1538) at offset 0 of `ref`, for a local segment:
+    // in front of the run of zero-length segments that ends at ref (breakTie against UnassignedSequenceNumber,
+    // segments zamboni may drop skipped), then rebalanceTree
+    void insertAtReferencePosition(Seg* ref, Seg* seg) {
+        if (seg->len == 0) return;
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        int k = int(std::find(lv.begin(), lv.end(), ref) - lv.begin());
+        Seg* start = ref;
+        for (int j = k - 1; j >= 0; j--) {  // backwardExcursion (:1491-1508)
+            const int bl = nodeLength(lv[size_t(j)], currentSeq, localClientId);
+            if (bl == kUndef) continue;
+            if (bl == 0) {
+                if (breakTie(0, lv[size_t(j)], kUnassignedSeq)) start = lv[size_t(j)];
+                continue;
+            }
+            break;
+        }
+        if (collaborating) {
+            seg->localSeq = ++localSeqCounter;
+            seg->seq = kUnassignedSeq;
+        } else {
+            seg->seq = kUniversalSeq;
+        }
+        seg->clientId = localClientId;
+        insertChildNode(start->parent, seg, start->index);
+        for (Block* block = seg->parent; block; block = block->parent) {  // rebalanceTree (:1445-1475)
+            if (block->childCount >= kMaxNodesInBlock) {
+                Block* sn = split(block);
+                if (block == root) updateRoot(sn);
+                else insertChildNode(block->parent, sn, block->index + 1);
+            } else {
+                blockUpdateLength(block, kUnassignedSeq, localClientId);
+            }
+        }
+        recordDeltas({seg}, MTR_OP_INSERT);  // mergeTreeDeltaCallback (:1530-1533)
+        if (collaborating) addToPendingList(seg, nullptr, seg->localSeq);  // (:1535-1537)
+    }
+    // PermutationSegment.transferToReplacement (permutationvector.ts:80-102)
+    static void transferToReplacement(Seg* from, Seg* to) {
+        const std::vector<TGroup*> gs = from->tgroups;
+        for (TGroup* g : gs) tlink(g, to);
+        for (TGroup* g : gs) tunlink(g, from);
+        to->start = from->start;
+        from->start = MTR_HANDLE_UNALLOCATED;
     }
 
     // addToPendingList, mergeTree.ts:1324-1357 (previousProps are kept only for rollback: not modelled)
@@ -1259,7 +1371,7 @@ class Tree {
                     hold.push_back(s);
                     prev = nullptr;
                 } else if (s->removed) {
-                    if (s->removedSeq > minSeq) {
+                    if (s->removedSeq > minSeq || !s->tgroups.empty()) {  // (tracked: held, zamboni.ts:132)
                         hold.push_back(s);
                     } else {
                         // UNLINK; a PermutationVector frees the segment's handles in order
@@ -1275,8 +1387,14 @@ class Tree {
                 } else {
                     if (s->seq <= minSeq) {
                         int ln = localNetLength(s);
-                        bool ok = prev && canAppend(prev, s) && matchProperties(prev, s, tabs.b) && (ln > 0);
+                        bool ok = prev && canAppend(prev, s) && matchProperties(prev, s, tabs.b) &&
+                                  sameGroups(prev, s) && (ln > 0);
                         if (ok) {
+                            if (!s->tgroups.empty()) {  // it leaves its tracking groups (zamboni.ts:171-173)
+                                if (recycleLog) deltas.push_back({curOpIndex, s->tid, prev->tid, MTR_DELTA_TMERGE});
+                                const std::vector<TGroup*> gs = s->tgroups;
+                                for (TGroup* g : gs) tunlink(g, s);
+                            }
                             refsAppend(prev, s);    // BaseSegment.append, mergeTreeNodes.ts:527-530 (before lengths)
                             prev->text += s->text;  // TextSegment.append textSegment.ts:99-103 (BaseSegment.append for perm)
                             prev->len += s->len;
@@ -1513,6 +1631,8 @@ class Tree {
     // SequenceDeltaEvent ranges of MTR_F_DELTA ops (sequenceDeltaEvent.ts: position = getPosition
     // at the local view when the delta callback fires, before zamboni; tree order)
     bool deltaOn = false;
+    bool trackCollect = false;
+    std::vector<Seg*> trackFresh;
     bool recycleLog = false;  // a matrix vector tracked for its cells (MTR_DELTA_RECYCLE records)
     uint32_t curOpIndex = 0;
     std::vector<mtr_delta> deltas;
@@ -1589,6 +1709,7 @@ class Tree {
         // already removed locally, so no event: their sliding references slide now (mergeTree.ts:2023-2025)
         for (Seg* s : localOverlapWithRefs) slideAckedRemovedSegmentReferences(s);
         recordDeltas(fresh, MTR_OP_REMOVE);  // mergeTree.ts:2026-2031
+        if (trackCollect) trackFresh = fresh;  // (the delta segments VectorUndoProvider.record links)
         // newly removed by someone else (or before collaboration): slide after the event (mergeTree.ts:2032-2040)
         if (!collaborating || clientId != localClientId)
             for (Seg* s : fresh) slideAckedRemovedSegmentReferences(s);
@@ -1729,13 +1850,44 @@ class Tree {
             // (a pending op until its ack), UniversalSequenceNumber before
             case MTR_OP_LOCAL_INSERT: {
                 Seg* s = segmentFromSpec(op, dd);
+                if (permMode && op.pos2 >= 0) {  // SharedMatrix._undoRemoveRows / _undoRemoveCols (matrix.ts:371-430)
+                    Seg* ref = findTid(op.pos2);
+                    // insertRelative's op position: referencePositionToLocalPosition (client.ts:252-270)
+                    if (!ref || !op.payload || localPosition(ref) != op.pos1) return MTR_ERR_BAD_OP;
+                    insertAtReferencePosition(ref, s);
+                    trackLink(s, op.payload);
+                    transferToReplacement(ref, s);
+                    return status;
+                }
                 insertSegments(op.pos1, s, currentSeq, localClientId, collaborating ? kUnassignedSeq : kUniversalSeq);
+                if (permMode && op.payload && s->parent && status == MTR_OK) trackLink(s, op.payload);
                 return status;
             }
-            case MTR_OP_LOCAL_REMOVE:
+            case MTR_OP_LOCAL_REMOVE: {
+                std::vector<Seg*>* fresh = permMode && op.payload ? &trackFresh : nullptr;
+                trackFresh.clear();
+                trackCollect = fresh != nullptr;
                 markRangeRemoved(op.pos1, op.pos2, currentSeq, localClientId,
                                  collaborating ? kUnassignedSeq : kUniversalSeq);
+                trackCollect = false;
+                if (fresh && status == MTR_OK)
+                    for (Seg* x : trackFresh) trackLink(x, op.payload);
                 return status;
+            }
+            case MTR_OP_TRACK: {  // TrackingGroup.unlink (the undo provider's revert / discard)
+                if (!permMode) return MTR_ERR_BAD_OP;
+                Seg* one = op.pos1 >= 0 ? findTid(op.pos1) : nullptr;
+                for (int b = 0; b < MTR_TRACK_GROUPS; b++) {
+                    if (!(op.payload >> b & 1u)) continue;
+                    TGroup* g = &tgroup[b];
+                    if (op.pos1 < 0) {
+                        while (!g->segs.empty()) tunlink(g, g->segs.front());
+                    } else if (one) {
+                        tunlink(g, one);
+                    }
+                }
+                return status;
+            }
             case MTR_OP_LOCAL_ANNOTATE:
                 // (a combining annotate: payload2 = MTR_COMB_* | NaN value id << 3, its prop-op the host's combine of
                 // each key's default as for a remote one -- combine(op, undefined, undefined, UnassignedSequenceNumber))
@@ -2307,6 +2459,35 @@ int32_t oracle_doc_handle_at(oracle_doc* d, int32_t pos) {
     Seg* s = t.containingSegment(pos, t.currentSeq, t.localClientId, off);
     if (!s) return -1;
     return s->start >= 1 ? s->start + off : MTR_HANDLE_UNALLOCATED;
+}
+
+// the selected vector's segments in tree order, five int32 each, as mtr_get_leaves (include/mtr.h)
+int64_t oracle_doc_leaves(oracle_doc* d, int32_t* out, int64_t cap) {
+    Tree& t = d->view();
+    if (!t.pendingLoad.empty()) t.reloadFromSegments();
+    std::vector<Seg*> lv;
+    t.leaves(t.root, lv);
+    if (int64_t(lv.size()) > cap) return -int64_t(lv.size());
+    for (size_t i = 0; i < lv.size(); i++) {
+        const Seg* x = lv[i];
+        int32_t* r = out + 5 * i;
+        r[0] = x->len;
+        r[1] = x->removed ? 1 : 0;
+        r[2] = x->start;
+        r[3] = x->tid;
+        r[4] = int32_t(t.tbits(x));
+    }
+    return int64_t(lv.size());
+}
+
+// the tracking ids of group `bit`'s segments in the TrackingGroup's order (test check of the host's lists)
+int64_t oracle_doc_track_group(oracle_doc* d, int32_t bit, int32_t* out, int64_t cap) {
+    Tree& t = d->view();
+    if (bit < 0 || bit >= MTR_TRACK_GROUPS) return -1;
+    const std::vector<Seg*>& g = t.tgroup[bit].segs;
+    if (int64_t(g.size()) > cap) return -int64_t(g.size());
+    for (size_t i = 0; i < g.size(); i++) out[i] = g[i]->tid;
+    return int64_t(g.size());
 }
 
 int32_t oracle_doc_marker_position(oracle_doc* d, uint32_t ordinal, int32_t ref_seq, int32_t client) {

@@ -130,6 +130,8 @@ void oracle_doc_set_slide_hook(oracle_doc* d, oracle_slide_hook hook, void* ctx)
 /* PermutationVector.getMaybeHandle at local position pos of the selected vector (permutationvector.ts:196-207):
  * the handle, MTR_HANDLE_UNALLOCATED, or -1 when no segment holds pos */
 int32_t oracle_doc_handle_at(oracle_doc* d, int32_t pos);
+int64_t oracle_doc_leaves(oracle_doc* d, int32_t* out, int64_t cap);
+int64_t oracle_doc_track_group(oracle_doc* d, int32_t bit, int32_t* out, int64_t cap);
 
 /* Length of the doc in the (ref_seq, client) view (MergeTree.getLength, mergeTree.ts:757) */
 int64_t oracle_doc_length(oracle_doc* d, int32_t ref_seq, int32_t client);

@@ -77,6 +77,10 @@ def lib():
         L.oracle_doc_ref_positions.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.oracle_doc_handle_at.restype = C.c_int32
         L.oracle_doc_handle_at.argtypes = [C.c_void_p, C.c_int32]
+        L.oracle_doc_leaves.restype = C.c_int64
+        L.oracle_doc_leaves.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_doc_track_group.restype = C.c_int64
+        L.oracle_doc_track_group.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64]
         L.oracle_doc_ref_states.restype = C.c_int64
         L.oracle_doc_ref_states.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.oracle_doc_ref_key.restype = C.c_int32
@@ -233,6 +237,22 @@ class OracleDoc:
     def handle_at(self, pos: int) -> int:
         """The handle at local position pos of the selected vector (HANDLE_UNALLOCATED, -1 = no segment)."""
         return lib().oracle_doc_handle_at(self.h, pos)
+
+    def leaves(self) -> np.ndarray:
+        """The selected vector's segments, [n, 5] int32 as Engine.leaves (mtr_get_leaves)."""
+        n = lib().oracle_doc_leaves(self.h, None, 0)
+        n = -n if n < 0 else n
+        out = np.zeros(5 * max(n, 1), dtype="<i4")
+        lib().oracle_doc_leaves(self.h, out.ctypes.data, n)
+        return out[:5 * n].reshape(n, 5)
+
+    def track_group(self, bit: int) -> list:
+        """Tracking ids of the selected vector's tracking group `bit`, in the TrackingGroup's order."""
+        n = lib().oracle_doc_track_group(self.h, bit, None, 0)
+        n = -n if n < 0 else n
+        out = np.zeros(max(n, 1), dtype="<i4")
+        lib().oracle_doc_track_group(self.h, bit, out.ctypes.data, n)
+        return [int(x) for x in out[:n]]
 
     def ref_positions(self) -> list:
         """localReferencePositionToPosition of every local reference, by id (-1 = detached)."""
