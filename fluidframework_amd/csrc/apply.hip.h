@@ -843,6 +843,7 @@ struct Eng {
     // view lengths of the listed chunks (dlist[0, n)) into ch_x, their change from the local lengths into
     // their superchunks' sup_dlen
     static MTR_DI void dirty_chunks(D& L, const St& s, const View& v, int newlen, int n) {
+        PROF(P_PFSUM);  // (the listed chunks' evaluation; P_PFDIRTY: the unlisted ones inside it)
         const int S = s.nseg, ln = lane_id();
         const lptr<int> lst = dlist(L), cx = ch_x(L), sd = sup_dlen(L);
         for (int e0 = 0; e0 < n; e0 += 64) {  // one lane per chunk: its whole record in one round of loads

@@ -650,9 +650,9 @@ static int run_impl(mtr_engine* e, int gen) {
     // Size classes of `class_leaves` leaves (SharedString classes: LDS sized to the class's largest
     // document plus `slack` leaves; a document that runs out of room yields before the op and is
     // classed again next round).  Tuning knobs: MTR_CLASS_LEAVES, MTR_SLACK.
-    static const int class_leaves = [] {
+    static const int class_env = [] {
         const char* v = std::getenv("MTR_CLASS_LEAVES");
-        return v ? std::max(16, std::atoi(v)) : 64;
+        return v ? std::max(16, std::atoi(v)) : 0;
     }();
     // concurrent launch lanes (1..kLanes) and whether the fixed-capacity kernels are used (tuning knobs:
     // MTR_LANES, MTR_NO_FIXED_CAP)
@@ -684,6 +684,11 @@ static int run_impl(mtr_engine* e, int gen) {
     bool any_pair = false;
     for (uint32_t d = 0; d < e->n_docs && d < e->h_kind.size(); d++) any_pair = any_pair || e->h_kind[d] != 0;
     const int g_want = groups_env > 0 ? groups_env : (e->n_docs >= 4096u && e->n_docs <= 60000u ? 2 : 1);
+    // Default class width: 128 leaves for the batches that run two groups (4,096 to 60,000 documents) -- half the
+    // launches per round of 64-leaf classes, which at those sizes cost more than the wider classes' LDS spread
+    // (profiles/r04_class_sweep.json: 12,500 documents 379.0 M vs 341.4 M ops/s, 25,000 395.5 M vs 385.0 M);
+    // 64 above (100,000: 407.7 M vs 400.5 M) and below
+    const int class_leaves = class_env > 0 ? class_env : (e->n_docs >= 4096u && e->n_docs <= 60000u ? 128 : 64);
     const int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
     const int L = std::max(1, nlanes / G);  // lanes (streams) per group
     const size_t ncls = 1 + 3 * kAllClasses;

@@ -1,11 +1,13 @@
 #!/bin/bash
-# One-GPU prediction of the driver's 8-GPU strong-scaling curve: C3's 100,000 documents split over
-# N = 1, 2, 4, 8 ranks leave 100k / N documents per GPU; each is run here on one MI355X.
-# usage: bash scripts/strong_predict.sh <tag>
+# The strong-scaling prediction of C3 on one GPU: 100,000 / N documents per GPU for N = 1, 2, 4, 8 (default
+# policies), and C2 with the default and 64-leaf classes.  usage: bash scripts/strong_predict.sh <tag>
 set -e
-TAG=${1:-r03}
-OUT=gpurun_out/strong_$TAG
+OUT=gpurun_out/strong_${1:-r04}
 mkdir -p $OUT
-for n in 100000 50000 25000 12500; do
-  timeout -k 10 300 python3 -u bench.py --docs $n --steps 3 --warmup 1 --e2e-steps 0 --no-cpu-baseline > $OUT/c3_$n.json 2> $OUT/c3_$n.err
+B="--steps 3 --warmup 1 --e2e-steps 0 --no-cpu-baseline"
+for d in 100000 50000 25000 12500; do
+  timeout -k 10 200 python3 -u bench.py $B --docs $d > $OUT/d$d.json 2> $OUT/d$d.err
 done
+timeout -k 10 300 python3 -u bench.py --config C2 --steps 2 --warmup 1 --e2e-steps 0 --no-cpu-baseline > $OUT/c2.json 2> $OUT/c2.err
+MTR_CLASS_LEAVES=64 timeout -k 10 300 python3 -u bench.py --config C2 --steps 2 --warmup 1 --e2e-steps 0 --no-cpu-baseline > $OUT/c2_cl64.json 2> $OUT/c2_cl64.err
+echo done > $OUT/done
