@@ -687,8 +687,10 @@ static int run_impl(mtr_engine* e, int gen) {
     // Default class width: 128 leaves for the batches that run two groups (4,096 to 60,000 documents) -- half the
     // launches per round of 64-leaf classes, which at those sizes cost more than the wider classes' LDS spread
     // (profiles/r04_class_sweep.json: 12,500 documents 379.0 M vs 341.4 M ops/s, 25,000 395.5 M vs 385.0 M);
-    // 64 above (100,000: 407.7 M vs 400.5 M) and below
-    const int class_leaves = class_env > 0 ? class_env : (e->n_docs >= 4096u && e->n_docs <= 60000u ? 128 : 64);
+    // 64 above (100,000: 407.7 M vs 400.5 M) and below; 128 for matrix pairs too (C4: 46.7 M vs 38.9 M ops/s,
+    // profiles/r04_sched_sweep.json)
+    const int class_leaves = class_env > 0 ? class_env
+                                           : (any_pair || (e->n_docs >= 4096u && e->n_docs <= 60000u) ? 128 : 64);
     const int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
     const int L = std::max(1, nlanes / G);  // lanes (streams) per group
     const size_t ncls = 1 + 3 * kAllClasses;
