@@ -368,6 +368,25 @@ napi_value GetRefStates(napi_env env, napi_callback_info info) {
     return r;
 }
 
+// getLeaves(h, doc) -> Int32Array of 5 ints per segment of a SharedMatrix vector (mtr_get_leaves): cachedLength,
+// removed, start handle, tracking id, tracking-group bits -- what the undo provider reads (undoprovider.ts:138-170)
+napi_value GetLeaves(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    const int64_t n = mtr_get_leaves(e, doc, nullptr, 0);
+    if (n < 0) return throw_engine(env, "mtr_get_leaves");
+    void* data = nullptr;
+    napi_value ab, r;
+    NAPI_CALL(env, napi_create_arraybuffer(env, size_t(n) * 20, &data, &ab));
+    if (n > 0 && mtr_get_leaves(e, doc, static_cast<int32_t*>(data), n) != n) return throw_engine(env, "mtr_get_leaves");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, size_t(5 * n), ab, 0, &r));
+    return r;
+}
+
 // getRefInfo(h, doc, id) -> [leaf, offset, refType, held] (LocalReference.getSegment/getOffset, localReference.ts:106-112)
 napi_value GetRefInfo(napi_env env, napi_callback_info info) {
     napi_value argv[3];
@@ -562,7 +581,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"getDeltas", GetDeltas},       {"submitRunAsync", SubmitRunAsync},
                {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment},
                {"getProps", GetProps}, {"getRefPositions", GetRefPositions}, {"getRefInfo", GetRefInfo},
-               {"getRefStates", GetRefStates}};
+               {"getRefStates", GetRefStates}, {"getLeaves", GetLeaves}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||
