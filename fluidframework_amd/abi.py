@@ -24,8 +24,12 @@ OP_REF_CREATE = 20
 OP_REF_REMOVE = 21
 OP_LOCAL_SETCELL = 22
 OP_TRACK = 23
+OP_REF_ACK = 24  # an interval collection's own ops (include/mtr_types.h)
+OP_REBASE_POS = 25
+OP_LSEQ = 26
 REF_SLIDE = 1
 REF_LOCALVIEW = 2
+REF_LSEQ = 4
 # ReferenceType (ops.ts:9-36)
 REFTYPE_SIMPLE = 0x0
 REFTYPE_TILE = 0x1
@@ -46,6 +50,7 @@ DELTA_TSPLIT = 97
 DELTA_TMERGE = 98
 TRACK_GROUPS = 32
 DELTA_REGEN_X = 72
+DELTA_REBASE = 80
 REL_BEFORE = 1
 REL_OFFSET = 2
 COMB_NONE, COMB_REWRITE, COMB_INCR, COMB_CONSENSUS, COMB_KEEP = 0, 1, 2, 3, 4

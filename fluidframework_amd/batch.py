@@ -400,6 +400,31 @@ class DocLog:
         self.n_refs += 1
         return self.n_refs - 1
 
+    def create_ref_at(self, pos: int, ref_type: int, ref_seq: int, local_seq: int) -> int:
+        """createPositionReference with a localSeq (sequence/src/intervalCollection.ts:697-724, a rebase's
+        changeInterval): getContainingSegment(pos, undefined, localSeq) -- this client's view at (ref_seq =
+        currentSeq, localSeq) -- then createLocalReferencePosition; no segment = a detached reference."""
+        self.ops.append((abi.OP_REF_CREATE, 0, 0, 0, int(ref_seq), int(local_seq), int(pos), 0, int(ref_type),
+                         abi.REF_LSEQ))
+        self.n_refs += 1
+        return self.n_refs - 1
+
+    def ack_ref(self, ref_id: int) -> None:
+        """IntervalCollection.ackInterval for one endpoint reference (MTR_OP_REF_ACK, include/mtr_types.h)."""
+        if not 0 <= ref_id < self.n_refs:
+            raise ValueError(f"no local reference {ref_id}")
+        self.ops.append((abi.OP_REF_ACK, 0, 0, 0, 0, 0, 0, 0, int(ref_id), 0))
+
+    def rebase_position(self, pos: int, seq_from: int, local_seq: int) -> int:
+        """IntervalCollection.rebasePositionWithSegmentSlide(pos, seqNumberFrom, localSeq) (MTR_OP_REBASE_POS);
+        returns the record's index in this batch (its MTR_DELTA_REBASE result carries it)."""
+        self.ops.append((abi.OP_REBASE_POS, abi.F_DELTA, 0, 0, int(seq_from), int(local_seq), int(pos), 0, 0, 0))
+        return len(self.ops) - 1
+
+    def bump_local_seq(self) -> None:
+        """IntervalCollection.getNextLocalSeq: ++collabWindow.localSeq (MTR_OP_LSEQ)."""
+        self.ops.append((abi.OP_LSEQ, 0, 0, 0, 0, 0, 0, 0, 0, 0))
+
     def remove_ref(self, ref_id: int) -> None:
         """Client.removeLocalReferencePosition (client.ts:394-396)."""
         if not 0 <= ref_id < self.n_refs:

@@ -1116,6 +1116,7 @@ struct Eng {
         if (lane_id() == 0) {
             if (i >= s.nseg || pos < 0) {
                 out[0] = -1;
+                out[9] = before;  // (no segment: the view's whole length when pos is past it)
             } else {
                 const uint32_t m = L.meta[i];
                 out[0] = li;
@@ -1171,10 +1172,12 @@ struct Eng {
             const int rc = min(r, n - 1);
             const uint32_t u = rf_uid(L)[rc], o = rf_off(L)[rc], t = rf_ty(L)[rc];
             const bool live = (r < n) & (u != NONE32) & ((t & (RF_HELD | RT_TRANSIENT)) != 0);
-            int res = MTR_DETACHED_POSITION;
+            // (info_id -3: every reference that names a segment is looked for: its leaf is the compare key)
+            const bool want = info_id == -3 ? (r < n) & (u != NONE32) : live;
+            int res = MTR_DETACHED_POSITION, key = -1;
             bool found = false, onrm = false;
             int carry = 0;
-            for (int base = 0; base < S && __ballot(live & !found); base += 64) {
+            for (int base = 0; base < S && __ballot(want & !found); base += 64) {
                 const int i = base + lane_id();
                 const int ic = min(i, S - 1);
                 const uint32_t m = L.meta[ic];
@@ -1188,14 +1191,23 @@ struct Eng {
                 for (int l = 0; l < 64; l++) {  // every reference lane looks for its leaf in this round
                     const uint32_t ul = rdlane(ui, l);
                     const int el = rdlane(excl, l), rl = rdlane(rm, l);
-                    const bool hit = live & !found & (ul == u);
-                    res = hit ? (rl ? 0 : int(o)) + el : res;
-                    onrm = onrm | (hit & (rl != 0));
+                    const bool hit = want & !found & (ul == u);
+                    res = (hit & live) ? (rl ? 0 : int(o)) + el : res;
+                    key = hit ? base + l : key;
+                    onrm = onrm | (hit & live & (rl != 0));
                     found = found | hit;
                 }
                 carry += rdlane(inc, 63);
             }
-            if (info_id == -2) {
+            if (info_id == -3) {
+                if (r < n) {
+                    out[4 * r] = res;
+                    out[4 * r + 1] = (u != NONE32 ? MTR_REF_ST_SEGMENT : 0) | ((t & RF_HELD) ? MTR_REF_ST_HELD : 0) |
+                                     (onrm ? MTR_REF_ST_REMOVED : 0);
+                    out[4 * r + 2] = u == NONE32 ? -1 : (found ? key : -2);
+                    out[4 * r + 3] = int(o);
+                }
+            } else if (info_id == -2) {
                 if (r < n) {
                     out[2 * r] = res;
                     out[2 * r + 1] = (u != NONE32 ? MTR_REF_ST_SEGMENT : 0) | ((t & RF_HELD) ? MTR_REF_ST_HELD : 0) |
@@ -2148,7 +2160,8 @@ struct Eng {
             v.local = (!s.collab || uint32_t(s.local) == v.client) ? 1 : 0;
         }
         int i = 0, before = 0;
-        find1(L, s, v, op.pos1, i, before, P.new_length_calc);
+        if (op.payload2 & MTR_REF_LSEQ) find1_at(L, s, op.ref_seq, op.min_seq, op.pos1, i, before);
+        else find1(L, s, v, op.pos1, i, before, P.new_length_calc);
         int off = op.pos1 - before;
         if (i >= s.nseg || op.pos1 < 0) i = -1;
         if (i >= 0 && (op.payload2 & MTR_REF_SLIDE) && removed_acked(uni(L.rseq[i]))) {
@@ -2199,6 +2212,122 @@ struct Eng {
             for (uint64_t m = __ballot((i < L.whi) & (L.rseq[ic] == seq)); m; m &= m - 1)
                 ref_slide(L, s, base + first_lane(m));
         }
+    }
+
+    // ---- an interval collection's own ops (sequence/src/intervalCollection.ts)
+    // localRemovedSeq of a leaf whose pending local remove a remote remove overtook (removedSeq is the remote one's):
+    // the localSeq of its pending-remove membership cell; -1 = none (per lane, rare)
+    static MTR_DI int pend_lrs(const D& L, uint32_t u) {
+        const gptr<uint32_t> ring = L.gpend();
+        if (!ring) return -1;
+        for (uint32_t c = pd_get(L, u); c != 0xffffffu;) {
+            const uint32_t w0 = L.grm()[c], w1 = L.grm()[c + 1];
+            const uint32_t sl = w1 >> 16;
+            if (((w0 >> 24) & PK_KIND) == PK_REMOVE && sl != ZOMBIE_SLOT) return int(ring[4 * sl]);
+            c = w0 & 0xffffffu;
+        }
+        return -1;
+    }
+    // localNetLength(segment, refSeq, localSeq) (mergeTree.ts:636-662): this client's view at localSeq lseq -- an
+    // acked leaf shows when seq <= ref and it is not removed-and-acked by ref; a pending local insert (seq =
+    // LOCAL_BASE + localSeq) when its localSeq <= lseq; either hides once removed by a local op whose localSeq <= lseq
+    static MTR_DI int lnl_at(const D& L, uint32_t m, int sq, int rs, int ln, uint32_t u, int ref, int lseq) {
+        if (m & M_DEL) return 0;  // a hole slot
+        int lrs = -1;
+        if (rs != RNONE && rs >= LOCAL_BASE) lrs = rs - LOCAL_BASE;
+        else if (rs != RNONE && (m & M_PEND)) lrs = pend_lrs(L, u);
+        bool zero = sq < LOCAL_BASE ? (sq > ref || (rs != RNONE && rs < LOCAL_BASE && rs <= ref)) : sq - LOCAL_BASE > lseq;
+        zero = zero || (lrs >= 0 && lrs <= lseq);
+        return zero ? 0 : ln;
+    }
+    // getContainingSegment(pos, {ref, this client}, lseq) (mergeTree.ts:795-813 with nodeMap's localSeq lengths): the
+    // first leaf whose inclusive prefix exceeds pos (S if none) and the view length before it
+    static MTR_DI void find1_at(const D& L, const St& s, int ref, int lseq, int pos, int& i_out, int& before) {
+        const int S = s.nseg;
+        int c = 0;
+        i_out = S;
+        before = 0;
+        for (int base = 0; base < S; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, S - 1);
+            const int x = i < S ? lnl_at(L, L.meta[ic], L.seq[ic], L.rseq[ic], L.len[ic], L.uid[ic], ref, lseq) : 0;
+            const int inc = wave_incl_scan(x);
+            const uint64_t mm = __ballot((i < S) & (c + inc > pos));
+            if (mm) {
+                const int l = first_lane(mm);
+                i_out = base + l;
+                before = c + rdlane(inc - x, l);
+                return;
+            }
+            c += rdlane(inc, 63);
+        }
+        before = c;
+    }
+    // getPosition(leaf t, ref, this client, lseq) (mergeTree.ts:768-785): findReconnectionPosition (client.ts:699-706)
+    static MTR_DI int pos_at(const D& L, const St& s, int t, int ref, int lseq) {
+        int c = 0;
+        for (int base = 0; base < t; base += 64) {
+            const int i = base + lane_id();
+            const int ic = min(i, s.nseg - 1);
+            const int x = i < t ? lnl_at(L, L.meta[ic], L.seq[ic], L.rseq[ic], L.len[ic], L.uid[ic], ref, lseq) : 0;
+            c += rdlane(wave_incl_scan(x), 63);
+        }
+        return c;
+    }
+    // IntervalCollection.ackInterval (intervalCollection.ts:2054-2138) for one endpoint: a reference its segment
+    // holds is re-created at getSlideToSegment's segment and offset when that differs (none: a detached reference,
+    // createPositionReferenceFromSegoff with an op); its ReferenceType becomes SlideOnRemove (setSlideOnRemove)
+    static MTR_DI void ref_ack(D& L, St& s, uint32_t r) {
+        if (!rf_uid(L) || int(r) >= nrefs(L)) {
+            s.status = MTR_ERR_BAD_OP;
+            return;
+        }
+        const uint32_t u = uniu(rf_uid(L)[r]), t = uniu(rf_ty(L)[r]);
+        uint32_t nu = u, no = uniu(rf_off(L)[r]), nt = (t & ~RT_STAY) | RT_SLIDE;
+        if (u != NONE32 && (t & RF_HELD)) {
+            const int x = find_uid(L, s, u);
+            // (a segment zamboni unlinked: the excursions from it find nothing)
+            const int tg = x < 0 ? -1 : (removed_acked(uni(L.rseq[x])) ? slide_target(L, s, x) : x);
+            if (tg < 0) {
+                nu = NONE32;
+                no = 0;
+                nt &= ~RF_HELD;
+            } else if (tg != x) {
+                nu = uniu(L.uid[tg]);
+                no = tg < x ? uint32_t(uni(L.len[tg]) - 1) : 0u;
+            }
+        }
+        if (lane_id() == 0) {
+            rf_uid(L)[r] = nu;
+            rf_off(L)[r] = no;
+            rf_ty(L)[r] = nt;
+        }
+        wsync();
+    }
+    // IntervalCollection.rebasePositionWithSegmentSlide (intervalCollection.ts:1472-1505): the position an endpoint
+    // created at op.pos1 in the view (op.ref_seq, this client, localSeq op.min_seq) has after a reconnect
+    static MTR_DI void rebase_pos(D& L, St& s, const mtr_op& op, int gidx) {
+        int i = 0, before = 0;
+        find1_at(L, s, op.ref_seq, op.min_seq, op.pos1, i, before);
+        if (op.pos1 < 0 || i >= s.nseg) {
+            s.status = MTR_ERR_ASSERT | 0x54e;  // "No segment found"
+            return;
+        }
+        const int off = op.pos1 - before;
+        int t = i, toff = off;
+        if (removed_acked(uni(L.rseq[i]))) {  // getSlideToSegment (client.ts:1085-1099)
+            t = slide_target(L, s, i);
+            toff = (t >= 0 && t < i) ? uni(L.len[t]) - 1 : 0;
+        }
+        int res = MTR_DETACHED_POSITION;
+        if (t >= 0) {
+            if (off < 0 || off >= uni(L.len[i])) {
+                s.status = MTR_ERR_ASSERT | 0x54f;  // "Invalid offset"
+                return;
+            }
+            res = pos_at(L, s, t, s.curseq, op.min_seq) + toff;
+        }
+        if constexpr (DL) put_record(L, s, gidx, res, 0, MTR_DELTA_REBASE);
     }
 
     // MergeTree.ackPendingSegment (mergeTree.ts:1283-1322) with BaseSegment.ack (mergeTreeNodes.ts:439-479)
@@ -4665,6 +4794,23 @@ struct Eng {
             case MTR_OP_REF_REMOVE:
                 if (!X || PM) s.status = MTR_ERR_BAD_OP;
                 else ref_remove(L, s, op.payload);
+                break;
+            case MTR_OP_REF_ACK:  // IntervalCollection.ackInterval of one endpoint
+                if (!X || PM) s.status = MTR_ERR_BAD_OP;
+                else ref_ack(L, s, op.payload);
+                break;
+            case MTR_OP_REBASE_POS:  // IntervalCollection.rebasePositionWithSegmentSlide
+                if (!X || !DL || PM || !s.collab) s.status = MTR_ERR_BAD_OP;
+                else rebase_pos(L, s, op, gidx);
+                break;
+            case MTR_OP_LSEQ:  // IntervalCollection.getNextLocalSeq: ++collabWindow.localSeq
+                if (!X || PM) {
+                    s.status = MTR_ERR_BAD_OP;
+                } else {
+                    const int ls = uni(L.ghdr()->lseq);
+                    if (lane_id() == 0) L.ghdr()->lseq = ls + 1;
+                    wsync();
+                }
                 break;
             case MTR_OP_START_COLLAB:
                 if (!s.collab) {

@@ -168,7 +168,7 @@ __global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_
     }
 }
 
-// bit 3: local-reference records (MTR_OP_REF_*)
+// bit 3: local-reference records (MTR_OP_REF_*, and an interval collection's MTR_OP_REBASE_POS / MTR_OP_LSEQ)
 // bit 0: an op flagged MTR_F_DELTA (the host sizes delta buffers only then); bit 1: a rare record the
 // fixed-capacity kernels do not carry (Eng::X: relative positions, handle-table loads, combining
 // annotates, marker ordinals); bit 2: the local-op path (MTR_OP_ACK, or a local op recorded while
@@ -179,7 +179,8 @@ __global__ void op_scan_kernel(const mtr_op* ops, uint64_t n, int32_t* out) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         const mtr_op op = ops[i];
         any = any || (op.flags & MTR_F_DELTA) != 0;
-        refs = refs || op.type == MTR_OP_REF_CREATE || op.type == MTR_OP_REF_REMOVE;
+        refs = refs || op.type == MTR_OP_REF_CREATE || op.type == MTR_OP_REF_REMOVE || op.type == MTR_OP_REF_ACK ||
+               op.type == MTR_OP_REBASE_POS || op.type == MTR_OP_LSEQ;
         pend = pend || op.type == MTR_OP_ACK || op.type == MTR_OP_ROLLBACK || op.type == MTR_OP_REGENERATE ||
                (op.type >= MTR_OP_LOCAL_INSERT && op.type <= MTR_OP_LOCAL_ANNOTATE && op.seq == -1);
         ext = ext || op.type == MTR_OP_RELPOS || op.type == MTR_OP_HANDLES || (op.flags & MTR_F_REL) ||
@@ -500,6 +501,8 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
                                                           int64_t(e->caps.max_segments)));
                 } else if (op.type == MTR_OP_REGENERATE) {  // two records per member of the group
                     need[d] += 2 * uint64_t(e->caps.max_segments);
+                } else if (op.type == MTR_OP_REBASE_POS) {
+                    need[d] += 1;
                 }
             }
             if (kind == 1 && flagged) {
@@ -1434,7 +1437,10 @@ int mtr_get_containing_segment(mtr_engine* e, uint32_t doc, int32_t pos, int32_t
     HIPCHK(hipStreamSynchronize(e->stream));
     std::memset(info, 0, sizeof(*info));
     info->leaf = r[0];
-    if (r[0] < 0) return MTR_OK;
+    if (r[0] < 0) {
+        info->start = pos >= 0 ? r[9] : 0;  // the view's length (getLength at that view) when pos is past its end
+        return MTR_OK;
+    }
     info->offset = r[1];
     info->length = r[2];
     // pending local values are kept above every sequence number (LOCAL_BASE + localSeq, apply.hip.h):
@@ -1467,7 +1473,7 @@ static int ref_query(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap, int
     DocHdr h;
     HIPCHK(hipMemcpy(&h, e->hdr.p + doc, sizeof(DocHdr), hipMemcpyDeviceToHost));
     const int64_t n = e->refs.p ? h.nrefs : 0;
-    const int64_t words = info_id >= 0 ? 4 : info_id == -2 ? 2 * n : n;
+    const int64_t words = info_id >= 0 ? 4 : info_id == -3 ? 4 * n : info_id == -2 ? 2 * n : n;
     if (info_id < 0 && (words > cap || n == 0 || !out)) return int(n);
     KParams P{};
     P.hdr = e->hdr.p;
@@ -1500,6 +1506,10 @@ int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t
 
 int64_t mtr_get_ref_states(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap) {
     return ref_query(e, doc, out, cap, -2);
+}
+
+int64_t mtr_get_ref_keys(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap) {
+    return ref_query(e, doc, out, cap, -3);
 }
 
 int32_t mtr_get_ref_info(mtr_engine* e, uint32_t doc, uint32_t id, int32_t* out) {

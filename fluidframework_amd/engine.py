@@ -110,6 +110,8 @@ def lib():
         L.mtr_get_ref_positions.restype = C.c_int64
         L.mtr_get_ref_states.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.mtr_get_ref_states.restype = C.c_int64
+        L.mtr_get_ref_keys.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
+        L.mtr_get_ref_keys.restype = C.c_int64
         L.mtr_get_leaves.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64]
         L.mtr_get_leaves.restype = C.c_int64
         L.mtr_get_ref_info.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
@@ -366,6 +368,14 @@ class Engine:
         r["text"] = None if info.marker else text[:info.length].tobytes().decode("utf-16-le", "surrogatepass")
         return r
 
+    def view_length(self, doc, ref_seq, client) -> int:
+        """nodeLength(root) at the (ref_seq, client) view (mtr_get_containing_segment past the end); this client's own
+        short id at its currentSeq is SharedString.getLength."""
+        info = SegmentInfo()
+        self._check(lib().mtr_get_containing_segment(self.h, doc, 0x7fffffff, ref_seq, client, C.byref(info), None, 0),
+                    "mtr_get_containing_segment")
+        return int(info.start)
+
     def ref_positions(self, doc) -> list:
         """Client.localReferencePositionToPosition of every local reference of `doc`, by id
         (abi.DETACHED_POSITION = -1 when it has none)."""
@@ -388,6 +398,18 @@ class Engine:
         out = np.zeros(2 * n, dtype="<i4")
         self._check(int(lib().mtr_get_ref_states(self.h, doc, out.ctypes.data, 2 * n) != n), "mtr_get_ref_states")
         return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+    def ref_keys(self, doc) -> list:
+        """[(position, state bits, compare key, offset)] of every local reference of `doc`, by id (mtr_get_ref_keys:
+        the key increases in tree order; -1 = no segment, -2 = a segment no longer in the tree)."""
+        n = lib().mtr_get_ref_keys(self.h, doc, None, 0)
+        if n < 0:
+            raise EngineError(f"mtr_get_ref_keys: {_err()}")
+        if n == 0:
+            return []
+        out = np.zeros(4 * n, dtype="<i4")
+        self._check(int(lib().mtr_get_ref_keys(self.h, doc, out.ctypes.data, 4 * n) != n), "mtr_get_ref_keys")
+        return [tuple(int(x) for x in out[4 * i:4 * i + 4]) for i in range(n)]
 
     def leaves(self, doc) -> np.ndarray:
         """A matrix vector's segments in tree order, [n, 5] int32: cachedLength, removed, start handle, tracking id

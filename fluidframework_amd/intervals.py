@@ -87,15 +87,70 @@ def _int_pos(v: Any, what: str) -> int:
     return int(v)
 
 
+UNASSIGNED_SEQ = -1   # UnassignedSequenceNumber (merge-tree/src/constants.ts)
+UNIVERSAL_SEQ = 0     # UniversalSequenceNumber
+_UNDEF = object()     # a JS `undefined` field (dropped by JSON.stringify)
+
+
+class PropertiesManager:
+    """merge-tree's PropertiesManager (segmentPropertiesManager.ts:24-170) as an interval's property bag uses it
+    (SequenceInterval.addProperties, intervalCollection.ts:577-585): no combining ops, so no rewrite counts.  A local
+    change (seq = UnassignedSequenceNumber while collaborating) counts its keys as pending; a sequenced change from
+    another client leaves a pending key alone (shouldModifyKey); the ack of the local change decrements."""
+
+    def __init__(self):
+        self.pending: dict[str, int] | None = None  # pendingKeyUpdateCount
+
+    def ack(self, props: dict) -> None:
+        """ackPendingProperties -> decrementPendingCounts (:33-58)."""
+        for k in js_key_order(props.keys()):
+            if self.pending is not None and k in self.pending:
+                if self.pending[k] <= 0:
+                    raise AssertionError("0x05c")  # "Trying to update more annotate props than do exist!"
+                self.pending[k] -= 1
+                if self.pending[k] == 0:
+                    del self.pending[k]
+
+    def add(self, old: dict, new: dict, seq: int | None = None, collaborating: bool = False) -> dict:
+        """addProperties (:60-157) without a combining op: each key of `new` in JS key order; null deletes.
+        Returns the deltas (previous values, null when absent)."""
+        if self.pending is None:
+            self.pending = {}
+        deltas = {}
+        for k in js_key_order(new.keys()):
+            if collaborating:
+                if seq == UNASSIGNED_SEQ:
+                    self.pending[k] = self.pending.get(k, 0) + 1
+                elif not (seq == UNIVERSAL_SEQ or k not in self.pending):  # shouldModifyKey
+                    continue
+            deltas[k] = old.get(k)
+            v = new[k]
+            if v is None:
+                old.pop(k, None)
+            else:
+                old[k] = v
+        return deltas
+
+    def copy_to(self, old: dict, new: dict, mgr: "PropertiesManager") -> None:
+        """copyTo (:159-180): the properties and the pending counts."""
+        for k in js_key_order(old.keys()):
+            new[k] = old[k]
+        mgr.pending = dict(self.pending or {})
+
+
 @dataclass
 class Interval:
-    """One SequenceInterval: its endpoint references (engine ids), intervalType and property bag."""
+    """One SequenceInterval: its endpoint references (engine ids) and their ReferenceTypes, the intervalType and
+    the property bag with its PropertiesManager."""
 
     start: int
     end: int
     itype: Any
     props: dict
     kind: str  # "op" (a sequenced op: a detached endpoint is allowed, :685-694), "snapshot" or "local"
+    stype: int = 0  # the endpoints' ReferenceTypes as the engine holds them (ackInterval reads StayOnRemove)
+    etype: int = 0
+    pm: PropertiesManager = field(default_factory=PropertiesManager)
 
     def id(self) -> str | None:
         v = self.props.get(INTERVAL_ID)
@@ -119,7 +174,7 @@ class Collection:
         bt, et = _ref_types(int(itype), kind != "local")
         s = log.create_ref(start, bt, view=view, slide=kind == "op")
         e = log.create_ref(end, et, view=view, slide=kind == "op")
-        return Interval(s, e, itype, {RANGE_LABELS: [self.label]}, kind)
+        return Interval(s, e, itype, {RANGE_LABELS: [self.label]}, kind, bt, et)
 
     def _add(self, iv: Interval) -> None:
         """LocalIntervalCollection.add (:1078-1082): the index and the id map."""
@@ -212,6 +267,288 @@ class Collection:
             iv = nv
         add_props(iv.props, new_props)
 
+    # ---------------------------------------------------------------- a collaborating client's own ops
+    # (IntervalCollection.add / change / changeProperties / removeIntervalById, :1635-1793, their acks :1859-2208 and
+    # rebaseLocalInterval :1963-2029).  `live` is the client (fluidframework_amd.live.SharedStringClient): its log, the
+    # executor's answers (sync, local length, reference keys, rebase results) and the op submission.
+    def _pending_changes(self, end: bool) -> dict:
+        name = "pending_end" if end else "pending_start"
+        if not hasattr(self, name):
+            setattr(self, name, {})
+        return getattr(self, name)
+
+    def _lseq_map(self, rebased: bool = False) -> dict:
+        """localSeqToSerializedInterval / localSeqToRebasedInterval (:1435-1442)."""
+        name = "lseq_rebased" if rebased else "lseq_serialized"
+        if not hasattr(self, name):
+            setattr(self, name, {})
+        return getattr(self, name)
+
+    def has_pending_change(self, iid: str, end: bool) -> bool:
+        return bool(self._pending_changes(end).get(iid))
+
+    def _add_pending_change(self, iid: str, ser: dict) -> None:
+        """addPendingChange (:1795-1815)."""
+        if _field(ser, "start") is not _UNDEF:
+            self._pending_changes(False).setdefault(iid, []).append(ser)
+        if _field(ser, "end") is not _UNDEF:
+            self._pending_changes(True).setdefault(iid, []).append(ser)
+
+    def _remove_pending_change(self, ser: dict) -> None:
+        """removePendingChange (:1817-1846)."""
+        props = ser.get("properties") or {}
+        iid = props.get(INTERVAL_ID)
+        for end, key in ((False, "start"), (True, "end")):
+            if _field(ser, key) is _UNDEF:
+                continue
+            pm = self._pending_changes(end)
+            entries = pm.get(iid)
+            if entries:
+                pc = entries.pop(0)
+                if not entries:
+                    del pm[iid]
+                if _field(pc, "start") != _field(ser, "start") or _field(pc, "end") != _field(ser, "end"):
+                    raise AssertionError("Mismatch in pending changes")
+
+    def _check_position(self, live, pos: Any) -> None:
+        """createPositionReference without an op or a localSeq (:697-724): getContainingSegment at the local view must
+        find a segment -- 0 <= pos < the local length (nodeMap, mergeTree.ts:2526-2570) -- or createPositionReference
+        FromSegoff throws (:690-692)."""
+        if isinstance(pos, bool) or not isinstance(pos, int):
+            raise IntervalUnsupported("a local interval endpoint that is not an integer position")
+        if not 0 <= pos < live.length():
+            raise UsageError("Non-transient references need segment")
+
+    def live_add(self, live, start: int, end: int, itype: int, props: dict | None) -> Interval:
+        """IntervalCollection.add (:1635-1672) while collaborating: LocalIntervalCollection.addInterval (:1032-1052)
+        with StayOnRemove endpoints at the local view, then the "add" op with a new localSeq."""
+        if self.saved is not None:
+            raise UsageError("attach must be called prior to adding intervals")
+        if isinstance(itype, int) and itype & TRANSIENT:
+            raise UsageError("Can not add transient intervals")
+        self._check_position(live, start)
+        self._check_position(live, end)
+        iv = self._create(live.log, int(start), int(end), itype, None, "local")
+        if props:
+            iv.pm.add(iv.props, props)
+        if iv.props.get(INTERVAL_ID) is None:  # properties[reservedIntervalIdKey] ??= uuid()
+            import uuid
+
+            iv.props[INTERVAL_ID] = str(uuid.uuid4())
+        self._add(iv)
+        ser = {"end": end, "intervalType": itype, "properties": iv.props, "sequenceNumber": live.current_seq,
+               "start": start}
+        lseq = live.next_local_seq()
+        self._lseq_map()[lseq] = ser
+        live.submit({"key": self.label, "type": "act", "value": {"opName": "add", "value": ser}}, {"localSeq": lseq})
+        return iv
+
+    def live_remove(self, live, iid: str) -> Interval | None:
+        """removeIntervalById (:1706-1715) -> deleteExistingInterval(local) (:1674-1699): the "delete" op carries
+        interval.serialize() (positions from localReferencePositionToPosition, :472-487)."""
+        iv = self.by_id.get(iid) if isinstance(iid, str) else None
+        if iv is None:
+            return None
+        keys = live.ref_keys()
+        self._remove(iv)
+        ser = {"end": keys[iv.end][0], "intervalType": iv.itype, "sequenceNumber": live.current_seq,
+               "start": keys[iv.start][0], "properties": iv.props}
+        lseq = live.next_local_seq()
+        live.submit({"key": self.label, "type": "act", "value": {"opName": "delete", "value": ser}}, {"localSeq": lseq})
+        return iv
+
+    def live_change_properties(self, live, iid: Any, props: dict) -> None:
+        """changeProperties (:1723-1752): pending keys, a "change" op with only the properties (and the id)."""
+        if not isinstance(iid, str):
+            raise UsageError("Change API requires an ID that is a string")
+        if not props:
+            raise UsageError("changeProperties should be called with a property set")
+        iv = self.by_id.get(iid)
+        if iv is None:
+            return
+        iv.pm.add(iv.props, props, UNASSIGNED_SEQ, True)
+        props[INTERVAL_ID] = iv.id()  # (the caller's object: the op's properties)
+        ser = {"intervalType": iv.itype, "sequenceNumber": live.current_seq, "properties": props}
+        lseq = live.next_local_seq()
+        self._lseq_map()[lseq] = ser
+        live.submit({"key": self.label, "type": "act", "value": {"opName": "change", "value": ser}}, {"localSeq": lseq})
+
+    def _change_interval(self, live, iv: Interval, start: Any, end: Any, view: tuple | None = None,
+                         local_seq: int | None = None) -> Interval:
+        """LocalIntervalCollection.changeInterval (:1088-1103) -> SequenceInterval.modify (:600-656): a new reference
+        for each given endpoint (with an op: at its view, slid, the old ReferenceType; without: StayOnRemove at the
+        local view, or at the localSeq view of a rebase), the others shared, the properties and pending counts
+        copied."""
+        def new_ref(pos, old_type):
+            if view is not None:
+                if not old_type & SLIDE_ON_REMOVE_REF:
+                    raise AssertionError("0x2f5")  # "op create references must be SlideOnRemove"
+                return live.log.create_ref(_int_pos(pos, "endpoint"), old_type, view=view, slide=True), old_type
+            t = (old_type & ~SLIDE_ON_REMOVE_REF) | STAY_ON_REMOVE_REF
+            if local_seq is not None:
+                return live.log.create_ref_at(_int_pos(pos, "endpoint"), t, live.current_seq, local_seq), t
+            return live.log.create_ref(_int_pos(pos, "endpoint"), t), t
+
+        s, st, e, et = iv.start, iv.stype, iv.end, iv.etype
+        if start is not _UNDEF and start is not None:
+            s, st = new_ref(start, iv.stype)
+        if end is not _UNDEF and end is not None:
+            e, et = new_ref(end, iv.etype)
+        nv = Interval(s, e, iv.itype, {}, "op" if view is not None else iv.kind, st, et)
+        iv.pm.copy_to(iv.props, nv.props, nv.pm)
+        self._remove(iv)
+        self._add(nv)
+        return nv
+
+    def live_change(self, live, iid: Any, start: Any = _UNDEF, end: Any = _UNDEF) -> Interval | None:
+        """IntervalCollection.change (:1761-1793)."""
+        if not isinstance(iid, str):
+            raise UsageError("Change API requires an ID that is a string")
+        iv = self.by_id.get(iid)
+        if iv is None:
+            return None
+        for v in (start, end):
+            if v is not _UNDEF and v is not None:
+                self._check_position(live, v)
+        nv = self._change_interval(live, iv, start, end)
+        # interval.serialize() with start / end / properties replaced (key order end, intervalType, sequenceNumber,
+        # start, properties; an undefined endpoint is no JSON field)
+        ser = {} if end is _UNDEF else {"end": end}
+        ser.update({"intervalType": iv.itype, "sequenceNumber": live.current_seq})
+        if start is not _UNDEF:
+            ser["start"] = start
+        ser["properties"] = {INTERVAL_ID: iv.id()}
+        lseq = live.next_local_seq()
+        self._lseq_map()[lseq] = ser
+        live.submit({"key": self.label, "type": "act", "value": {"opName": "change", "value": ser}}, {"localSeq": lseq})
+        self._add_pending_change(iid, ser)
+        return nv
+
+    def ack_interval(self, live, iv: Interval) -> None:
+        """ackInterval (:2054-2138): each StayOnRemove-era endpoint without a pending change is slid as
+        getSlideToSegment says (a new reference at the slide-to segment) and becomes SlideOnRemove -- one
+        MTR_OP_REF_ACK record each."""
+        if not (iv.stype & STAY_ON_REMOVE_REF) and not (iv.etype & STAY_ON_REMOVE_REF):
+            return
+        iid = iv.props.get(INTERVAL_ID)
+        if not self.has_pending_change(iid, False):
+            live.log.ack_ref(iv.start)
+            iv.stype = (iv.stype & ~STAY_ON_REMOVE_REF) | SLIDE_ON_REMOVE_REF
+        if not self.has_pending_change(iid, True):
+            live.log.ack_ref(iv.end)
+            iv.etype = (iv.etype & ~STAY_ON_REMOVE_REF) | SLIDE_ON_REMOVE_REF
+
+    def live_process(self, live, name: str, params: Any, msg: dict, local: bool, meta: dict | None) -> None:
+        """The ops map's process handlers (:1281-1325) with ackAdd / ackDelete / ackChange (:1859-1932, 2141-2208)."""
+        if name != "delete" and not js_truthy(params):
+            return  # "if params is undefined, the interval was deleted during rebasing"
+        if not isinstance(params, dict):
+            raise IntervalUnsupported("interval op parameters")
+        si = dict(params)
+        if name == "add":
+            if not local:
+                return self.ack_add(live.log, si, msg)
+            self._lseq_map().pop(meta["localSeq"], None)
+            iv = self.by_id.get((si.get("properties") or {}).get(INTERVAL_ID))
+            if iv is not None:
+                self.ack_interval(live, iv)
+            return
+        if name == "delete":
+            if not local:
+                self.ack_delete(si)
+            return
+        # change
+        if local:
+            self._lseq_map().pop(meta["localSeq"], None)
+            self._remove_pending_change(si)
+        props = si.get("properties")
+        props = props if isinstance(props, dict) else {}
+        if INTERVAL_ID not in props:
+            raise AssertionError("0x3fe")  # id must exist on the interval
+        iid = props[INTERVAL_ID]
+        new_props = {k: v for k, v in props.items() if k != INTERVAL_ID}
+        iv = self.by_id.get(iid) if isinstance(iid, str) else None
+        if iv is None:
+            return  # the interval has been removed locally; no-op
+        if local:
+            iv.pm.ack(props)
+            self.ack_interval(live, iv)
+            return
+        start = _field(si, "start") if not self.has_pending_change(iid, False) else _UNDEF
+        end = _field(si, "end") if not self.has_pending_change(iid, True) else _UNDEF
+        if start is None or end is None:
+            raise IntervalUnsupported("a change op with a null endpoint")
+        if start is not _UNDEF or end is not _UNDEF:
+            view = (int(msg["referenceSequenceNumber"]), _client(msg))
+            iv = self._change_interval(live, iv, start, end, view=view)
+        iv.pm.add(iv.props, new_props, int(msg["sequenceNumber"]), True)
+
+    # ---- reconnect
+    def rebase_positions(self, live, lseqs: list) -> dict:
+        """computeRebasedPositions (:1507-1528) of the pending ops `lseqs`: rebasePositionWithSegmentSlide of each
+        given endpoint (one MTR_OP_REBASE_POS record each, answered after one sync)."""
+        recs = []
+        for lseq in lseqs:
+            original = self._lseq_map().get(lseq)
+            if original is None:
+                raise AssertionError("0x551")  # "Failed to store pending serialized interval info for this localSeq."
+            for key in ("start", "end"):
+                v = _field(original, key)
+                if v is not _UNDEF:
+                    recs.append((lseq, key, live.log.rebase_position(_int_pos(v, key), int(original["sequenceNumber"]),
+                                                                     lseq)))
+        res = live.rebase_results() if recs else {}
+        out: dict = {}
+        for lseq in lseqs:
+            r = dict(self._lseq_map()[lseq])
+            out[lseq] = r
+        for lseq, key, rec in recs:
+            out[lseq][key] = res[rec]
+        return out
+
+    def on_normalize(self, live) -> None:
+        """The client's "normalize" listener (attachGraph, :1542-1551)."""
+        keys = list(self._lseq_map().keys())
+        if keys:
+            self._lseq_map(True).update(self.rebase_positions(live, keys))
+
+    def rebase_local(self, live, name: str, ser: dict, lseq: int) -> dict | None:
+        """rebaseLocalInterval (:1963-2029) -> the resubmitted op's value; None = the op is a no-op."""
+        if name == "delete":
+            return ser  # deletion is by id: no rebasing
+        rb = self._lseq_map(True).get(lseq)
+        if rb is None:
+            rb = self.rebase_positions(live, [lseq])[lseq]
+        props = ser.get("properties")
+        iid = props.get(INTERVAL_ID) if isinstance(props, dict) else None
+        local = self.by_id.get(iid) if isinstance(iid, str) else None
+        rebased = {}
+        for key in ("start", "end"):
+            v = _field(rb, key)
+            if v is not _UNDEF:
+                rebased[key] = v
+        rebased.update({"intervalType": ser.get("intervalType"), "sequenceNumber": live.current_seq,
+                        "properties": props})
+        if name == "change" and (self.has_pending_change(iid, False) or self.has_pending_change(iid, True)):
+            self._remove_pending_change(ser)
+            self._add_pending_change(iid, rebased)
+        if _field(rebased, "start") == abi.DETACHED_POSITION or _field(rebased, "end") == abi.DETACHED_POSITION:
+            if local is not None:
+                self._remove(local)
+            return None
+        if local is not None:
+            self._change_interval(live, local, _field(rebased, "start"), _field(rebased, "end"), local_seq=lseq)
+        return rebased
+
+    # ---- queries (the trees' in-order walks and searches, intervalCollection.ts:864-992)
+    def ordered(self, keys: list) -> list:
+        """The intervals in SequenceInterval.compare order (:505-539; compareReferencePositions,
+        referencePositions.ts:113-121): the start tree's in-order walk."""
+        import functools
+
+        ivs = list(self.by_id.values())
+        return sorted(ivs, key=functools.cmp_to_key(lambda a, b: _iv_cmp(keys, a, b)))
+
     def serialize(self, states: list, current_seq: int) -> dict:
         """LocalIntervalCollection.serialize (:1105-1112): the intervals in compare order, each
         compressInterval(interval.serialize()) (:139-151, 472-487)."""
@@ -225,6 +562,41 @@ class Collection:
             props = {k: v for k, v in iv.props.items() if k != RANGE_LABELS}
             out.append([a, b, current_seq, iv.itype, props])
         return {"label": self.label, "intervals": out, "version": 2}
+
+
+def _field(d: dict, key: str) -> Any:
+    """d[key], _UNDEF when the key is absent (a JS undefined field)."""
+    return d[key] if key in d else _UNDEF
+
+
+class UsageError(Exception):
+    """The reference's UsageError / LoggingError for a bad API call (nothing changes)."""
+
+
+SLIDE_ON_REMOVE_REF = abi.REFTYPE_SLIDE_ON_REMOVE
+STAY_ON_REMOVE_REF = abi.REFTYPE_STAY_ON_REMOVE
+
+
+def _ref_key(keys: list, ref: int) -> tuple:
+    """compareReferencePositions' key of a reference from Engine.ref_keys: no segment sorts first (and equal to any
+    other segment-less reference); else (segment order, offset)."""
+    _, _, k, off = keys[ref]
+    if k == -1:
+        return (0, 0, 0)
+    if k < 0:
+        raise IntervalUnsupported("an interval endpoint on a segment zamboni took out of the tree")
+    return (1, k, off)
+
+
+def _iv_cmp(keys: list, a: Interval, b: Interval) -> int:
+    """SequenceInterval.compare (:505-525)."""
+    for x, y in ((_ref_key(keys, a.start), _ref_key(keys, b.start)), (_ref_key(keys, a.end), _ref_key(keys, b.end))):
+        if x != y:
+            return -1 if x < y else 1
+    ia, ib = a.id(), b.id()
+    if ia and ib:
+        return 1 if utf16_less(ib, ia) else -1 if utf16_less(ia, ib) else 0
+    return 0
 
 
 def _endpoint(states: list, ref: int, from_op: bool) -> int:

@@ -135,7 +135,9 @@ int64_t mtr_get_texts(mtr_engine* e, uint32_t lo, uint32_t hi, uint16_t* out, in
  * mergeTree.ts:787-813): the segment holding position pos in the (ref_seq, client) view, found on the
  * device (one wave scans the document's visibility in that view).  client: a short id, -1
  * (LocalClientId) or -2 (NonCollabClient).  text (cap units, may be NULL) receives a text segment's
- * units.  Returns MTR_OK with info->leaf = -1 when no segment covers pos. */
+ * units.  Returns MTR_OK with info->leaf = -1 when no segment covers pos; then info->start is the view's length
+ * (nodeLength(root) at that view: pos = INT32_MAX is a getLength query, SharedString.getLength for this client's own
+ * view). */
 typedef struct mtr_segment_info {
     int32_t leaf;        /* index of the leaf in tree order, -1 = none */
     int32_t offset;      /* pos - the segment's start in the view (getContainingSegment's offset) */
@@ -168,6 +170,13 @@ int64_t mtr_get_ref_positions(mtr_engine* e, uint32_t doc, int32_t* out, int64_t
  * with the position order exactly when every endpoint is held by a live segment or has no segment at all
  * (DESIGN.md section 9).  Returns the reference count (out written only when 2*count fits in cap), -1 on error. */
 int64_t mtr_get_ref_states(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap);
+/* Every local reference of document doc as four int32: its position and state bits (as mtr_get_ref_states), then
+ * compareReferencePositions' key (referencePositions.ts:113-121): a leaf key increasing in tree order (the segment's
+ * ordinal order; -1 = no segment, -2 = a segment zamboni took out of the tree, whose ordinal the engine no longer
+ * knows) and LocalReference.getOffset (localReference.ts:110).  A live interval collection orders its intervals by it
+ * (SequenceInterval.compare, sequence/src/intervalCollection.ts:505-539), including endpoints left on removed
+ * segments.  Returns the reference count (out written only when 4*count fits in cap), -1 on error. */
+int64_t mtr_get_ref_keys(mtr_engine* e, uint32_t doc, int32_t* out, int64_t cap);
 /* The segments of a SharedMatrix vector document in tree order (walkAllSegments, mergeTreeNodeWalk.ts:170), five
  * int32 each: cachedLength, 1 when removed (the local view does not show it, localNetLength, mergeTree.ts:613-634),
  * PermutationSegment.start (permutationvector.ts:53-72; MTR_HANDLE_UNALLOCATED), tracking id (-1: none) and its

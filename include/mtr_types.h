@@ -91,6 +91,21 @@ enum {
                                    (mergeTreeTracking.ts:47-53) on a PermutationVector (MTR_F_COLS: cols) -- clear the
                                    tracking-group bits `payload` of tracked segment pos1 (-1: of every segment).
                                    See "Tracking groups" below. */
+    /* An interval collection's own ops while collaborating (sequence/src/intervalCollection.ts): */
+    MTR_OP_REF_ACK = 24,        /* IntervalCollection.ackInterval (:2054-2138) for endpoint reference `payload` (the
+                                   host sends it only for an endpoint with no pending change): when the reference's
+                                   segment holds it, getSlideToSegment (:2031-2045 -> client.ts:1085-1099) and, if that
+                                   moves it, the reference is re-created there (createPositionReferenceFromSegoff with
+                                   the op: no segment = a detached reference); either way its ReferenceType becomes
+                                   SlideOnRemove (setSlideOnRemove, :2047-2052) */
+    MTR_OP_REBASE_POS = 25,     /* IntervalCollection.rebasePositionWithSegmentSlide (:1472-1505) for a reconnect:
+                                   getContainingSegment(pos1) at (ref_seq = the op's sequenceNumber, this client,
+                                   localSeq = min_seq), getSlideToSegment, then findReconnectionPosition(segment,
+                                   localSeq) + offset (client.ts:699-706), or DetachedReferencePosition; asserts 0x54e /
+                                   0x54f.  Flag it MTR_F_DELTA: the result is one mtr_delta {op, position, 0,
+                                   MTR_DELTA_REBASE} */
+    MTR_OP_LSEQ = 26,           /* IntervalCollection.getNextLocalSeq (:1584-1590): ++collabWindow.localSeq -- an
+                                   interval op takes a localSeq the merge-tree's later local ops count past */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
                                    MergeTree.posFromRelativePos, mergeTree.ts:1371-1395), resolved at that op's
                                    (ref_seq, client) before the op runs: pos1 = marker ordinal (see below) or -1 for
@@ -105,8 +120,11 @@ enum {
 /* MTR_OP_RELPOS payload2 */
 enum { MTR_REL_BEFORE = 1, MTR_REL_OFFSET = 2 };
 
-/* MTR_OP_REF_CREATE payload2, and the ReferenceType bits (ops.ts:9-36) its payload carries */
-enum { MTR_REF_SLIDE = 1, MTR_REF_LOCALVIEW = 2 };
+/* MTR_OP_REF_CREATE payload2, and the ReferenceType bits (ops.ts:9-36) its payload carries.  MTR_REF_LSEQ: the
+ * local client's view at (ref_seq, localSeq = min_seq) -- getContainingSegment(pos, undefined, localSeq), whose
+ * lengths are localNetLength(segment, refSeq, localSeq), mergeTree.ts:636-662 (IntervalCollection.rebaseLocalInterval's
+ * changeInterval, intervalCollection.ts:2019-2025 -> createPositionReference with a localSeq, :697-724) */
+enum { MTR_REF_SLIDE = 1, MTR_REF_LOCALVIEW = 2, MTR_REF_LSEQ = 4 };
 enum {
     MTR_REFTYPE_SIMPLE = 0x0,
     MTR_REFTYPE_TILE = 0x1,
@@ -188,6 +206,8 @@ enum {
  * has no props -- mtr_get_props; -1 = properties undefined). */
 #define MTR_DELTA_REGEN 64
 #define MTR_DELTA_REGEN_X 72
+/* MTR_OP_REBASE_POS result: pos = the rebased position (MTR_DETACHED_POSITION when the segment slid off) */
+#define MTR_DELTA_REBASE 80
 
 /* Tracking groups (SharedMatrix undo: VectorUndoProvider, matrix/src/undoprovider.ts:17-127, on the merge-tree's
  * TrackingGroup, mergeTreeTracking.ts).  A PermutationVector segment a group tracks carries a tracking id (tid,

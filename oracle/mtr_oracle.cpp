@@ -1909,7 +1909,9 @@ class Tree {
             case MTR_OP_REF_CREATE: {  // createPositionReference, sequence/src/intervalCollection.ts:697-724
                 const bool lv = (op.payload2 & MTR_REF_LOCALVIEW) != 0;
                 int off = 0;
-                Seg* s = containingSegment(op.pos1, lv ? currentSeq : op.ref_seq, lv ? localClientId : int(op.client), off);
+                Seg* s = (op.payload2 & MTR_REF_LSEQ)
+                             ? containingSegmentAt(op.pos1, op.ref_seq, op.min_seq, off)
+                             : containingSegment(op.pos1, lv ? currentSeq : op.ref_seq, lv ? localClientId : int(op.client), off);
                 if (s && (op.payload2 & MTR_REF_SLIDE)) {  // Client.getSlideToSegment, client.ts:1085-1099
                     Seg* t = getSlideToSegment(s);
                     if (t != s) {
@@ -1925,6 +1927,62 @@ class Tree {
                 if (s) refsRemove(s->localRefs, int(op.payload));
                 return status;
             }
+            case MTR_OP_REF_ACK: {  // IntervalCollection.ackInterval (intervalCollection.ts:2054-2138), one endpoint
+                if (op.payload >= refs.size()) return MTR_ERR_BAD_OP;
+                const int id = int(op.payload);
+                const int nt = (refs[size_t(id)].refType & ~kStay) | kSlide;  // setSlideOnRemove (:2047-2052)
+                Seg* s = refs[size_t(id)].segment;
+                if (s && s->localRefs && refsHas(s->localRefs, id)) {  // getSlideToSegment(lref) (:2031-2045)
+                    Seg* t = getSlideToSegment(s);
+                    if (t != s) {  // createPositionReferenceFromSegoff(newStart, refType, op) (:2101-2117)
+                        const int off = (t && leafIndex(t) < leafIndex(s)) ? t->len - 1 : 0;
+                        refsRemove(s->localRefs, id);  // removeLocalReferencePosition(oldInterval.start)
+                        LRef& r = refs[size_t(id)];
+                        r.segment = nullptr;
+                        r.offset = 0;
+                        r.list = -1;
+                        if (t) {
+                            if (!t->localRefs) t->localRefs = newLocalRefs(t, size_t(t->len));
+                            r.segment = t;
+                            r.offset = off;
+                            RefsAtOffset& slot = refSlot(t->localRefs, off);
+                            slot.has[1] = true;
+                            slot.lst[1].push_back(id);
+                            r.list = 1;
+                            t->localRefs->refCount++;
+                        }
+                    }
+                }
+                refs[size_t(id)].refType = nt;
+                return status;
+            }
+            case MTR_OP_REBASE_POS: {  // IntervalCollection.rebasePositionWithSegmentSlide (intervalCollection.ts:1472-1505)
+                if (!collaborating) return MTR_ERR_BAD_OP;
+                int off = 0;
+                Seg* s = containingSegmentAt(op.pos1, op.ref_seq, op.min_seq, off);
+                if (!s) return status = MTR_ERR_ASSERT | 0x54e;  // "No segment found"
+                Seg* t = getSlideToSegment(s);
+                int toff = off;
+                if (t != s) toff = (t && leafIndex(t) < leafIndex(s)) ? t->len - 1 : 0;
+                int res = MTR_DETACHED_POSITION;
+                if (t) {
+                    if (off < 0 || off >= s->len) return status = MTR_ERR_ASSERT | 0x54f;  // "Invalid offset"
+                    // findReconnectionPosition(segment, localSeq), client.ts:699-706
+                    std::vector<Seg*> lv;
+                    leaves(root, lv);
+                    int before = 0;
+                    for (Seg* x : lv) {
+                        if (x == t) break;
+                        before += localNetLengthAt(x, currentSeq, op.min_seq);
+                    }
+                    res = before + toff;
+                }
+                deltas.push_back({curOpIndex, res, 0, MTR_DELTA_REBASE});
+                return status;
+            }
+            case MTR_OP_LSEQ:  // IntervalCollection.getNextLocalSeq (intervalCollection.ts:1584-1590)
+                ++localSeqCounter;
+                return status;
             case MTR_OP_START_COLLAB:  // startOrUpdateCollaboration -> startCollaboration, client.ts:1133, mergeTree.ts:731
                 if (collaborating) return MTR_OK;
                 localClientId = opClient(op);
@@ -1981,6 +2039,25 @@ class Tree {
             offset = pos - before;
         }
         return found;
+    }
+    // getContainingSegment(pos, {refSeq, this client}, localSeq) (mergeTree.ts:795-813): nodeMap over
+    // localNetLength(segment, refSeq, localSeq) (mergeTree.ts:636-662; a block's local partial length is the sum of
+    // its leaves')
+    Seg* containingSegmentAt(int pos, int refSeq, int lseq, int& offset) {
+        std::vector<Seg*> lv;
+        leaves(root, lv);
+        int p = 0;
+        offset = 0;
+        for (Seg* x : lv) {
+            const int l = localNetLengthAt(x, refSeq, lseq);
+            if (l <= 0) continue;
+            if (pos < p + l) {
+                offset = pos - p;
+                return x;
+            }
+            p += l;
+        }
+        return nullptr;
     }
     // MergeTree.idToSegment (mergeTree.ts:549,668) by host marker ordinal; never unmapped
     std::unordered_map<uint32_t, Seg*> idToSegment;
@@ -2433,6 +2510,25 @@ int64_t oracle_doc_ref_states(oracle_doc* d, int32_t* out, int64_t cap) {
         out[2 * i] = t.refPosition(int(i));
         out[2 * i + 1] = (s ? MTR_REF_ST_SEGMENT : 0) | (held ? MTR_REF_ST_HELD : 0) |
                          (live && s && s->parent && s->removed ? MTR_REF_ST_REMOVED : 0);
+    }
+    return n;
+}
+
+// every reference as {position, state, compare key (leaf index; -1 no segment, -2 unlinked), offset}: mtr_get_ref_keys
+int64_t oracle_doc_ref_keys(oracle_doc* d, int32_t* out, int64_t cap) {
+    Tree& t = d->view();
+    if (!t.pendingLoad.empty()) t.reloadFromSegments();
+    const int64_t n = int64_t(t.refs.size());
+    if (4 * n > cap) return -n;
+    std::vector<int32_t> st(size_t(2 * n));
+    oracle_doc_ref_states(d, st.data(), 2 * n);
+    for (int64_t i = 0; i < n; i++) {
+        const LRef& r = t.refs[size_t(i)];
+        Seg* s = r.segment;
+        out[4 * i] = st[size_t(2 * i)];
+        out[4 * i + 1] = st[size_t(2 * i + 1)];
+        out[4 * i + 2] = !s ? -1 : s->parent ? t.leafIndex(s) : -2;
+        out[4 * i + 3] = r.offset;
     }
     return n;
 }

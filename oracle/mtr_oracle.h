@@ -118,6 +118,8 @@ int32_t oracle_doc_ref_info(oracle_doc* d, uint32_t id, int32_t* out);
 /* mtr_get_ref_states (include/mtr.h) restated: out[2i] = position, out[2i+1] = MTR_REF_ST_* bits.  Returns the
  * count, -count when 2*count exceeds cap. */
 int64_t oracle_doc_ref_states(oracle_doc* d, int32_t* out, int64_t cap);
+/* every reference as four int32: position, state bits, compare key (leaf index; -1 no segment, -2 unlinked), offset */
+int64_t oracle_doc_ref_keys(oracle_doc* d, int32_t* out, int64_t cap);
 /* compareReferencePositions' view of reference id (referencePositions.ts:113-121): out[0] = index in tree order of
  * its segment (its ordinal's rank), -1 = no segment (detached), -2 = a segment no longer in the tree; out[1] =
  * getOffset().  Returns out[0], -3 for a bad id. */

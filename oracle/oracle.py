@@ -83,6 +83,8 @@ def lib():
         L.oracle_doc_track_group.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64]
         L.oracle_doc_ref_states.restype = C.c_int64
         L.oracle_doc_ref_states.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.oracle_doc_ref_keys.restype = C.c_int64
+        L.oracle_doc_ref_keys.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.oracle_doc_ref_key.restype = C.c_int32
         L.oracle_doc_ref_key.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         L.oracle_doc_set_slide_hook.restype = None
@@ -269,6 +271,15 @@ class OracleDoc:
         out = np.zeros(max(2 * n, 1), dtype="<i4")
         lib().oracle_doc_ref_states(self.h, out.ctypes.data, 2 * n)
         return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+    def ref_keys(self) -> list:
+        """[(position, state bits, compare key, offset)] of every local reference, by id (as Engine.ref_keys; the key
+        is the segment's leaf index)."""
+        n = lib().oracle_doc_ref_keys(self.h, None, 0)
+        n = -n if n < 0 else n
+        out = np.zeros(max(4 * n, 1), dtype="<i4")
+        lib().oracle_doc_ref_keys(self.h, out.ctypes.data, 4 * n)
+        return [tuple(int(x) for x in out[4 * i:4 * i + 4]) for i in range(n)]
 
     def ref_key(self, ref_id: int):
         """(tree-order index of the reference's segment: -1 none, -2 no longer in the tree; getOffset())"""
