@@ -549,6 +549,15 @@ class Collection:
         ivs = list(self.by_id.values())
         return sorted(ivs, key=functools.cmp_to_key(lambda a, b: _iv_cmp(keys, a, b)))
 
+    def serialize_live(self, keys: list, current_seq: int) -> dict:
+        """LocalIntervalCollection.serialize (:1105-1112) of a live client: the compare order from the references'
+        keys (endpoints on removed segments included), each endpoint at localReferencePositionToPosition."""
+        out = []
+        for iv in self.ordered(keys):
+            props = {k: v for k, v in iv.props.items() if k != RANGE_LABELS}
+            out.append([keys[iv.start][0], keys[iv.end][0], current_seq, iv.itype, props])
+        return {"label": self.label, "intervals": out, "version": 2}
+
     def serialize(self, states: list, current_seq: int) -> dict:
         """LocalIntervalCollection.serialize (:1105-1112): the intervals in compare order, each
         compressInterval(interval.serialize()) (:139-151, 472-487)."""
@@ -723,14 +732,16 @@ class IntervalCollections:
         else:
             c.ack_change(log, params, msg)
 
-    def serialize(self, states: list, current_seq: int) -> str | None:
+    def serialize(self, states: list, current_seq: int, live: bool = False) -> str | None:
         """summarizeCore's `header` blob (sequence.ts:467-480): JSON.stringify of {key: {type, value}} over the
-        collections (DefaultMap.serialize, defaultMap.ts:231-248); None when there are none."""
+        collections (DefaultMap.serialize, defaultMap.ts:231-248); None when there are none.  live: `states` are a
+        live client's reference keys (Engine.ref_keys)."""
         if not self.data:
             return None
         out = {}
         for key, c in self.data.items():
             if c.saved is not None:
                 raise IntervalUnsupported("a collection that was never attached")
-            out[key] = {"type": VALUE_TYPE, "value": c.serialize(states, current_seq)}
+            v = c.serialize_live(states, current_seq) if live else c.serialize(states, current_seq)
+            out[key] = {"type": VALUE_TYPE, "value": v}
         return js_stringify(out)

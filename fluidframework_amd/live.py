@@ -52,6 +52,10 @@ class EngineExecutor:
     def props(self, d: int, ref: int) -> list:
         return self.eng.props(d, ref)
 
+    def summary(self, batch, d: int) -> list[bytes]:
+        self.eng.summarize()
+        return self.eng.summary(d)
+
 
 class LiveSession:
     """Clients of one document family on one executor: `sync()` applies every client's queued records."""
@@ -75,6 +79,12 @@ class LiveSession:
         for c in self.clients:
             if b.docs[c.doc]["op_count"]:
                 self.deltas[c.doc] = self.ex.deltas(c.doc)
+
+
+    def summary(self, doc: int) -> list[bytes]:
+        """Client.summarize's blobs of engine document `doc` (header, body_0, ...: SnapshotV1)."""
+        self.sync()
+        return self.ex.summary(build_batch([c.log for c in self.clients], self.it), doc)
 
 
 class SharedStringClient:
@@ -178,6 +188,13 @@ class SharedStringClient:
         if f is None:
             f = self.facades[label] = LiveIntervalCollection(self, label)
         return f
+
+    def interval_header(self) -> bytes | None:
+        """The summary's `header` blob (summarizeCore, sequence.ts:467-480) of this live client."""
+        from .jsjson import to_utf8
+
+        h = self.log.intervals.serialize(self.ref_keys(), self.current_seq, live=True)
+        return None if h is None else to_utf8(h)
 
     def local_reference_position(self, ref: int) -> int:
         return self.ref_keys()[ref][0]

@@ -23,7 +23,7 @@
  * Written for Node >= 12 (no optional chaining).
  */
 const path = require('path');
-const { IntervalCollections, IntervalUnsupported } = require('./intervals.js');
+const { IntervalCollections, IntervalUnsupported, refKey, cmpKey } = require('./intervals.js');
 
 let addon = null;
 function native() {
@@ -33,8 +33,10 @@ function native() {
 
 // include/mtr_types.h
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
-    START_COLLAB: 12, LOAD: 13, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19, REF_CREATE: 20, REF_REMOVE: 21 };
-const REF = { SLIDE: 1, LOCALVIEW: 2 };  // MTR_OP_REF_CREATE payload2
+    START_COLLAB: 12, LOAD: 13, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19, REF_CREATE: 20, REF_REMOVE: 21,
+    REF_ACK: 24, REBASE_POS: 25, LSEQ: 26 };
+const REF = { SLIDE: 1, LOCALVIEW: 2, LSEQ: 4 };  // MTR_OP_REF_CREATE payload2
+const DELTA_REBASE = 80;
 const DetachedReferencePosition = -1;   // referencePositions.ts:103
 const DELTA_REGEN = 64, DELTA_REGEN_X = 72;
 const REL = { BEFORE: 1, OFFSET: 2 };
@@ -318,6 +320,19 @@ class DocLog {
         return this.nRefs++;
     }
     removeRef(id) { this.push(OP.REF_REMOVE, 0, 0, 0, 0, 0, 0, 0, id, 0); }
+    // createPositionReference with a localSeq (a rebase's changeInterval): getContainingSegment(pos, undefined,
+    // localSeq) -- this client's view at (refSeq, localSeq) -- then createLocalReferencePosition
+    createRefAt(pos, refType, refSeq, localSeq) {
+        this.push(OP.REF_CREATE, 0, 0, 0, refSeq, localSeq, pos, 0, refType, REF.LSEQ);
+        return this.nRefs++;
+    }
+    ackRef(id) { this.push(OP.REF_ACK, 0, 0, 0, 0, 0, 0, 0, id, 0); }  // IntervalCollection.ackInterval, one endpoint
+    // rebasePositionWithSegmentSlide(pos, seqNumberFrom, localSeq): returns the record index its result names
+    rebasePosition(pos, seqFrom, localSeq) {
+        this.push(OP.REBASE_POS, F.DELTA, 0, 0, seqFrom, localSeq, pos, 0, 0, 0);
+        return this.ops.length - 1;
+    }
+    bumpLocalSeq() { this.push(OP.LSEQ, 0, 0, 0, 0, 0, 0, 0, 0, 0); }  // IntervalCollection.getNextLocalSeq
     localAnnotate(start, end, props, it, combiningOp) {
         if (props && typeof props === 'object' && 'markerId' in props) this.markerIdAnnotated = true;
         let comb = localComb(combiningOp), pp;
@@ -843,6 +858,9 @@ class BatchReplayClient {
     constructor(engine, doc) {
         this.engine = engine; this.doc = doc; this.log = engine.logs[doc];
         this.currentSeq = 0;
+        this.localSeq = 0;          // collabWindow.localSeq as this host counts it (interval ops too)
+        this.lastNormalization = 0; // Client.lastNormalizationRefSeq (client.ts:910)
+        this.emitters = new Map();  // label -> the collection's op emitter (IValueOpEmitter)
     }
     _queue(fn) { this.engine._assertIdle(); fn(); this.engine.dirty = true; }
     _check() {
@@ -897,10 +915,18 @@ class BatchReplayClient {
         this._queue(() => { catchup = this.log.loadSummary(blobs, longClientId, this.engine.interner); });
         return catchup;
     }
-    applyMsg(msg, local) {
+    applyMsg(msg, local, localOpMetadata) {
         const own = local || (msg.type === 'op' && String(msg.clientId) === this.log.observerId);
         if (own && !this.engine.options.snapshotV1) {
             throw new UnsupportedError("this client's own message in the legacy catch-up format");
+        }
+        if (msg.type === 'op' && this.log.collaborating && this.log.intervals !== undefined) {
+            const c = typeof msg.contents === 'string' ? JSON.parse(msg.contents) : msg.contents;
+            if (c && c.type === 'act' && (own || this.log.intervals.live)) {  // a live client's interval op
+                this.processIntervalOp(msg, !!own, localOpMetadata);
+                this.currentSeq = this.log.currentSeq;
+                return;
+            }
         }
         this._queue(() => {
             if (!this.engine.options.snapshotV1 && msg.type === 'op' &&
@@ -929,13 +955,16 @@ class BatchReplayClient {
         this.currentSeq = seq;
     }
     insertTextLocal(pos, text, props) {
-        this._queue(() => this.log.localInsert(pos, props ? { text, props } : text, this.engine.interner));
+        this._queue(() => { this.log.localInsert(pos, props ? { text, props } : text, this.engine.interner); this._countLocal(); });
     }
     insertMarkerLocal(pos, refType, props) {
-        this._queue(() => this.log.localInsert(pos, props ? { marker: { refType }, props } : { marker: { refType } },
-            this.engine.interner));
+        this._queue(() => {
+            this.log.localInsert(pos, props ? { marker: { refType }, props } : { marker: { refType } }, this.engine.interner);
+            this._countLocal();
+        });
     }
-    removeRangeLocal(start, end) { this._queue(() => this.log.localRemove(start, end)); }
+    removeRangeLocal(start, end) { this._queue(() => { this.log.localRemove(start, end); this._countLocal(); }); }
+    _countLocal() { if (this.log.collaborating) this.localSeq++; }  // a pending local op takes a localSeq
     /** Client.localTransaction (client.ts:1029-1048): every member op as a local (pending) op. */
     /**
      * Client.applyStashedOp(op) (client.ts:830-856): a stashed op of this client applied as a local op (GROUP: each
@@ -945,15 +974,15 @@ class BatchReplayClient {
     applyStashedOp(op) {
         if (op.type === 3) return op.ops.map((o) => this.applyStashedOp(o));
         if (!this.log.collaborating) throw new Error('0x2db');  // "Applying op must generate a pending segment"
-        this._queue(() => this.log.localOp(op, this.engine.interner));
+        this._queue(() => { this.log.localOp(op, this.engine.interner); this._countLocal(); });
         this.nStashed = (this.nStashed || 0) + 1;
         return { stashed: this.nStashed, type: op.type };
     }
     localTransaction(groupOp) {
-        this._queue(() => { for (const op of groupOp.ops) this.log.localOp(op, this.engine.interner); });
+        this._queue(() => { for (const op of groupOp.ops) { this.log.localOp(op, this.engine.interner); this._countLocal(); } });
     }
     annotateRangeLocal(start, end, props, combiningOp) {  // client.ts:245-260
-        this._queue(() => this.log.localAnnotate(start, end, props, this.engine.interner, combiningOp));
+        this._queue(() => { this.log.localAnnotate(start, end, props, this.engine.interner, combiningOp); this._countLocal(); });
     }
     /** Client.rollback(op, localOpMetadata) (client.ts:421-423) of the newest pending local op `op`. */
     rollback(op) { this._queue(() => this.log.rollback(op, this.engine.interner)); }
@@ -962,6 +991,11 @@ class BatchReplayClient {
      * (`resetOp`, the op that was submitted): flushes the engine and returns the op to resubmit.
      */
     regeneratePendingOp(resetOp) {
+        if (this.log.intervals !== undefined && this.log.currentSeq !== this.lastNormalization) {
+            // client.ts:921-926: the "normalize" event (the interval collections rebase their pending ops) comes first
+            for (const c of this.log.intervals.data.values()) this.log._intervals(() => c.onNormalize(this));
+        }
+        this.lastNormalization = this.log.currentSeq;
         let first = 0;
         this._queue(() => { first = this.log.regenerate(resetOp); });
         this.engine.flush();
@@ -1029,12 +1063,44 @@ class BatchReplayClient {
     }
     /** getIntervalCollection(label) (sequence.ts:445-447): add(start, end, intervalType, props) on a string
      * that is not collaborating yet (a detached SharedString); remote ops arrive through applyMsg. */
-    getIntervalCollection(label) {
+    getIntervalCollection(label, emitter) {
         if (this.log.intervals === undefined) this.log.intervals = new IntervalCollections();
         const c = this.log.intervals.get(label);
-        return { add: (start, end, intervalType, props) => {
-            this._queue(() => this.log._intervals(() => c.add(this.log, start, end, intervalType, props)));
-        } };
+        if (!this.log.collaborating) {
+            return { add: (start, end, intervalType, props) => {
+                this._queue(() => this.log._intervals(() => c.add(this.log, start, end, intervalType, props)));
+            } };
+        }
+        // a collaborating client: IntervalCollection's API (intervalCollection.ts:1620-2338); emitter(opName, value,
+        // localOpMetadata) receives each op to submit
+        if (emitter) this.emitters.set(label, emitter);
+        this.log.intervals.live = true;
+        const run = (fn) => { const r = this.log._intervals(fn); this.engine.dirty = true; return r; };
+        const self = this;
+        const transient = (start, end) => {
+            const ts = self.log.createRef(start, 0x100, undefined, false), te = self.log.createRef(end, 0x100, undefined, false);
+            self.engine.dirty = true;
+            return [ts, te];
+        };
+        return {
+            add: (start, end, intervalType, props) => run(() => c.liveAdd(self, start, end, intervalType, props)),
+            change: (id, start, end) => run(() => c.liveChange(self, id, start, end)),
+            changeProperties: (id, props) => run(() => c.liveChangeProperties(self, id, props)),
+            removeIntervalById: (id) => run(() => c.liveRemove(self, id)),
+            getIntervalById: (id) => c.byId.get(id),
+            /** [start, end] positions (localReferencePositionToPosition of the endpoints) */
+            positions(iv, keys) { const k = keys || self.refKeys(); return [k[4 * iv.start], k[4 * iv.end]]; },
+            [Symbol.iterator]() { return self.log._intervals(() => c.ordered(self.refKeys()))[Symbol.iterator](); },
+            findOverlappingIntervals(start, end) {  // :950-964 (SequenceInterval.overlaps in tree order)
+                if (end < start || c.byId.size === 0) return [];
+                const [ts, te] = transient(start, end);
+                const keys = self.refKeys();
+                return self.log._intervals(() => {
+                    const ks = refKey(keys, ts), ke = refKey(keys, te);
+                    return c.ordered(keys).filter((iv) => cmpKey(refKey(keys, iv.start), ke) <= 0 && cmpKey(refKey(keys, iv.end), ks) >= 0);
+                });
+            },
+        };
     }
     /** The summary's `header` blob (summarizeCore, sequence.ts:467-480), undefined when there are no collections. */
     summarizeIntervals() {
@@ -1049,7 +1115,51 @@ class BatchReplayClient {
         this._check();
         return native().getText(this.engine.h, this.doc);
     }
-    getLength() { return this.getText().length; }
+    /** getLength: the local view's length (root.cachedLength; a marker counts 1). */
+    getLength() {
+        this.engine.flush();
+        this._check();
+        const me = this.log.collaborating ? this.log.clientIx.get(this.log.observerId) : -1;
+        return native().getViewLength(this.engine.h, this.doc, this.log.currentSeq, me);
+    }
+    // ---- a live client's interval collections (what IntervalCollection needs from its Client and emitter)
+    refKeys() { this.engine.flush(); this._check(); return native().getRefKeys(this.engine.h, this.doc); }
+    rebaseResults() {  // {record index -> position} of the MTR_OP_REBASE_POS records just queued
+        this.engine.flush();
+        this._check();
+        const d = native().getDeltas(this.engine.h, this.doc);
+        const out = new Map();
+        for (let i = 0; i < d.length; i += 4) if (d[i + 3] === DELTA_REBASE) out.set(d[i], d[i + 1]);
+        return out;
+    }
+    nextLocalSeq() {  // IntervalCollection.getNextLocalSeq (intervalCollection.ts:1584-1590)
+        this._queue(() => this.log.bumpLocalSeq());
+        return ++this.localSeq;
+    }
+    emit(label, opName, value, localOpMetadata) {  // the collection's IValueOpEmitter: an "act" op to submit
+        const em = this.emitters.get(label);
+        if (em) em(opName, value, localOpMetadata);
+    }
+    /**
+     * SharedSegmentSequence.processCore's interval branch (sequence.ts:636-645) for a live client: `local` with the
+     * op's localOpMetadata for this client's own ops (their acks).
+     */
+    processIntervalOp(msg, local, localOpMetadata) {
+        let contents = msg.contents;
+        if (typeof contents === 'string') contents = JSON.parse(contents);
+        if (this.log.intervals === undefined) this.log.intervals = new IntervalCollections();
+        this.engine._assertIdle();
+        this.log._intervals(() => this.log.intervals.liveProcess(this, contents, msg, local, localOpMetadata));
+        this.engine.dirty = true;
+    }
+    /** DefaultMap's resubmit of an interval op (rebaseLocalInterval, intervalCollection.ts:1270-1279) -> the op to send. */
+    rebaseIntervalOp(contents, localOpMetadata) {
+        const c = this.log.intervals.get(contents.key);
+        const v = contents.value;
+        const rebased = this.log._intervals(() => c.rebaseLocal(this, v.opName, v.value, localOpMetadata.localSeq));
+        this.engine.dirty = true;
+        return Object.assign({}, contents, { value: { opName: v.opName, value: rebased } });
+    }
     /**
      * Client.getContainingSegment(pos, sequenceArgs) (client.ts:1065-1078): the segment holding pos in
      * the view of sequenceArgs = {referenceSequenceNumber, clientId} (default: this client's current

@@ -60,14 +60,76 @@ function decompress(ci, label) {  // decompressInterval (:122-133)
         properties: Object.assign({}, ci[4], { [RANGE_LABELS]: [label] }) };
 }
 
+const UnassignedSequenceNumber = -1, UniversalSequenceNumber = 0;  // merge-tree/src/constants.ts
+
+class UsageError extends Error {  // the reference's UsageError / LoggingError for a bad API call (nothing changes)
+    constructor(msg) { super(msg); this.name = 'UsageError'; }
+}
+
+/** PropertiesManager (segmentPropertiesManager.ts:24-170) as an interval's property bag uses it: no combining ops. */
+class PropertiesManager {
+    constructor() { this.pending = undefined; }  // pendingKeyUpdateCount
+    ack(props) {  // ackPendingProperties -> decrementPendingCounts (:33-58)
+        for (const k of Object.keys(props)) {
+            if (this.pending !== undefined && this.pending[k] !== undefined) {
+                if (!(this.pending[k] > 0)) throw new Error('0x05c');
+                this.pending[k]--;
+                if (this.pending[k] === 0) delete this.pending[k];
+            }
+        }
+    }
+    add(old, newProps, seq, collaborating) {  // addProperties (:60-157) without a combining op
+        if (this.pending === undefined) this.pending = Object.create(null);
+        const deltas = {};
+        for (const k of Object.keys(newProps)) {
+            if (collaborating) {
+                if (seq === UnassignedSequenceNumber) {
+                    this.pending[k] = (this.pending[k] || 0) + 1;
+                } else if (!(seq === UniversalSequenceNumber || this.pending[k] === undefined)) {
+                    continue;  // shouldModifyKey
+                }
+            }
+            deltas[k] = old[k] === undefined ? null : old[k];
+            if (newProps[k] === null) delete old[k];
+            else old[k] = newProps[k];
+        }
+        return deltas;
+    }
+    copyTo(old, newProps, mgr) {  // copyTo (:159-180)
+        for (const k of Object.keys(old)) newProps[k] = old[k];
+        mgr.pending = Object.assign(Object.create(null), this.pending || {});
+    }
+}
+
 class Interval {
-    constructor(start, end, itype, props, kind) {
+    constructor(start, end, itype, props, kind, stype, etype) {
         this.start = start; this.end = end; this.itype = itype; this.props = props; this.kind = kind;
+        this.stype = stype || 0; this.etype = etype || 0;  // the endpoints' ReferenceTypes as the engine holds them
+        this.pm = new PropertiesManager();
     }
     id() {  // getIntervalId (:554-560)
         const v = this.props[INTERVAL_ID];
         return v === undefined || v === null ? undefined : `${v}`;
     }
+}
+
+// compareReferencePositions' key of a reference (referencePositions.ts:113-121) from getRefKeys: no segment sorts
+// first (equal to any other segment-less reference), else (segment order, offset)
+function refKey(keys, ref) {
+    const k = keys[4 * ref + 2];
+    if (k === -1) return [0, 0, 0];
+    if (k < 0) throw new IntervalUnsupported('an interval endpoint on a segment zamboni took out of the tree');
+    return [1, k, keys[4 * ref + 3]];
+}
+function cmpKey(a, b) {
+    for (let i = 0; i < 3; i++) if (a[i] !== b[i]) return a[i] < b[i] ? -1 : 1;
+    return 0;
+}
+function ivCmp(keys, a, b) {  // SequenceInterval.compare (:505-525)
+    const c = cmpKey(refKey(keys, a.start), refKey(keys, b.start)) || cmpKey(refKey(keys, a.end), refKey(keys, b.end));
+    if (c) return c;
+    const ia = a.id(), ib = b.id();
+    return ia && ib ? (ia > ib ? 1 : ia < ib ? -1 : 0) : 0;
 }
 
 class Collection {
@@ -79,7 +141,7 @@ class Collection {
         const [bt, et] = refTypes(itype, kind !== 'local');
         const s = log.createRef(start, bt, view, kind === 'op');
         const e = log.createRef(end, et, view, kind === 'op');
-        return new Interval(s, e, itype, { [RANGE_LABELS]: [this.label] }, kind);
+        return new Interval(s, e, itype, { [RANGE_LABELS]: [this.label] }, kind, bt, et);
     }
     _add(iv) {
         const i = iv.id();
@@ -143,6 +205,192 @@ class Collection {
         }
         addProps(iv.props, newProps);
     }
+    // ---- a collaborating client's own ops (IntervalCollection.add / change / changeProperties / removeIntervalById,
+    // :1635-1793, their acks :1859-2208, rebaseLocalInterval :1963-2029); `live` is the BatchReplayClient (its log,
+    // the engine's answers and the collection's op emitter).  Mirrors fluidframework_amd/intervals.py.
+    _pc(end) { const n = end ? 'pendingEnd' : 'pendingStart'; if (!this[n]) this[n] = new Map(); return this[n]; }
+    _lseqMap(rebased) { const n = rebased ? 'lseqRebased' : 'lseqSerialized'; if (!this[n]) this[n] = new Map(); return this[n]; }
+    hasPendingChange(id, end) { const e = this._pc(end).get(id); return !!(e && e.length); }
+    _addPendingChange(id, ser) {  // addPendingChange (:1795-1815)
+        if (ser.start !== undefined) { if (!this._pc(false).has(id)) this._pc(false).set(id, []); this._pc(false).get(id).push(ser); }
+        if (ser.end !== undefined) { if (!this._pc(true).has(id)) this._pc(true).set(id, []); this._pc(true).get(id).push(ser); }
+    }
+    _removePendingChange(ser) {  // removePendingChange (:1817-1846)
+        const id = ser.properties ? ser.properties[INTERVAL_ID] : undefined;
+        for (const [end, key] of [[false, 'start'], [true, 'end']]) {
+            if (ser[key] === undefined) continue;
+            const entries = this._pc(end).get(id);
+            if (entries) {
+                const pc = entries.shift();
+                if (entries.length === 0) this._pc(end).delete(id);
+                if (!pc || pc.start !== ser.start || pc.end !== ser.end) throw new Error('Mismatch in pending changes');
+            }
+        }
+    }
+    _checkPosition(live, pos) {  // createPositionReference without an op: a segment must hold pos (:690-692)
+        if (typeof pos !== 'number' || !Number.isInteger(pos)) throw new IntervalUnsupported('a local interval endpoint that is not an integer position');
+        if (!(pos >= 0 && pos < live.getLength())) throw new UsageError('Non-transient references need segment');
+    }
+    liveAdd(live, start, end, itype, props) {  // IntervalCollection.add (:1635-1672)
+        if (this.saved !== undefined) throw new UsageError('attach must be called prior to adding intervals');
+        if (itype & IntervalType.Transient) throw new UsageError('Can not add transient intervals');
+        this._checkPosition(live, start);
+        this._checkPosition(live, end);
+        const iv = this._create(live.log, start, end, itype, undefined, 'local');
+        if (props) iv.pm.add(iv.props, props);
+        if (iv.props[INTERVAL_ID] === undefined || iv.props[INTERVAL_ID] === null) {
+            iv.props[INTERVAL_ID] = require('crypto').randomBytes(16).toString('hex');  // (the reference draws a uuid)
+        }
+        this._add(iv);
+        const ser = { end, intervalType: itype, properties: iv.props, sequenceNumber: live.currentSeq, start };
+        const localSeq = live.nextLocalSeq();
+        this._lseqMap(false).set(localSeq, ser);
+        live.emit(this.label, 'add', ser, { localSeq });
+        return iv;
+    }
+    liveRemove(live, id) {  // removeIntervalById (:1706-1715) -> deleteExistingInterval(local) (:1674-1699)
+        const iv = typeof id === 'string' ? this.byId.get(id) : undefined;
+        if (iv === undefined) return undefined;
+        const keys = live.refKeys();
+        this._remove(iv);
+        const ser = { end: keys[4 * iv.end], intervalType: iv.itype, sequenceNumber: live.currentSeq,
+            start: keys[4 * iv.start], properties: iv.props };
+        live.emit(this.label, 'delete', ser, { localSeq: live.nextLocalSeq() });
+        return iv;
+    }
+    liveChangeProperties(live, id, props) {  // changeProperties (:1723-1752)
+        if (typeof id !== 'string') throw new UsageError('Change API requires an ID that is a string');
+        if (!props) throw new UsageError('changeProperties should be called with a property set');
+        const iv = this.byId.get(id);
+        if (iv === undefined) return;
+        iv.pm.add(iv.props, props, UnassignedSequenceNumber, true);
+        props[INTERVAL_ID] = iv.id();
+        const ser = { intervalType: iv.itype, sequenceNumber: live.currentSeq, properties: props };
+        const localSeq = live.nextLocalSeq();
+        this._lseqMap(false).set(localSeq, ser);
+        live.emit(this.label, 'change', ser, { localSeq });
+    }
+    // LocalIntervalCollection.changeInterval (:1088-1103) -> SequenceInterval.modify (:600-656)
+    _changeInterval(live, iv, start, end, view, localSeq) {
+        const newRef = (pos, oldType) => {
+            if (view !== undefined) {
+                if (!(oldType & REFTYPE.SLIDE_ON_REMOVE)) throw new Error('0x2f5');
+                return [live.log.createRef(intPos(pos, 'endpoint'), oldType, view, true), oldType];
+            }
+            const t = (oldType & ~REFTYPE.SLIDE_ON_REMOVE) | REFTYPE.STAY_ON_REMOVE;
+            if (localSeq !== undefined) return [live.log.createRefAt(intPos(pos, 'endpoint'), t, live.currentSeq, localSeq), t];
+            return [live.log.createRef(intPos(pos, 'endpoint'), t, undefined, false), t];
+        };
+        let [s, st, e, et] = [iv.start, iv.stype, iv.end, iv.etype];
+        if (start !== undefined && start !== null) [s, st] = newRef(start, iv.stype);
+        if (end !== undefined && end !== null) [e, et] = newRef(end, iv.etype);
+        const nv = new Interval(s, e, iv.itype, {}, view !== undefined ? 'op' : iv.kind, st, et);
+        iv.pm.copyTo(iv.props, nv.props, nv.pm);
+        this._remove(iv);
+        this._add(nv);
+        return nv;
+    }
+    liveChange(live, id, start, end) {  // IntervalCollection.change (:1761-1793)
+        if (typeof id !== 'string') throw new UsageError('Change API requires an ID that is a string');
+        const iv = this.byId.get(id);
+        if (iv === undefined) return undefined;
+        for (const v of [start, end]) if (v !== undefined && v !== null) this._checkPosition(live, v);
+        const nv = this._changeInterval(live, iv, start, end);
+        const ser = { end, intervalType: iv.itype, sequenceNumber: live.currentSeq, start, properties: { [INTERVAL_ID]: iv.id() } };
+        const localSeq = live.nextLocalSeq();
+        this._lseqMap(false).set(localSeq, ser);
+        live.emit(this.label, 'change', ser, { localSeq });
+        this._addPendingChange(id, ser);
+        return nv;
+    }
+    ackInterval(live, iv) {  // ackInterval (:2054-2138): one MTR_OP_REF_ACK per endpoint without a pending change
+        if (!(iv.stype & REFTYPE.STAY_ON_REMOVE) && !(iv.etype & REFTYPE.STAY_ON_REMOVE)) return;
+        const id = iv.props[INTERVAL_ID];
+        if (!this.hasPendingChange(id, false)) {
+            live.log.ackRef(iv.start);
+            iv.stype = (iv.stype & ~REFTYPE.STAY_ON_REMOVE) | REFTYPE.SLIDE_ON_REMOVE;
+        }
+        if (!this.hasPendingChange(id, true)) {
+            live.log.ackRef(iv.end);
+            iv.etype = (iv.etype & ~REFTYPE.STAY_ON_REMOVE) | REFTYPE.SLIDE_ON_REMOVE;
+        }
+    }
+    liveProcess(live, name, params, msg, local, meta) {  // the ops map (:1281-1325), ackAdd/ackDelete/ackChange
+        if (name !== 'delete' && !params) return;
+        if (!params || typeof params !== 'object') throw new IntervalUnsupported('interval op parameters');
+        const si = Object.assign({}, params);
+        if (name === 'add') {
+            if (!local) return this.ackAdd(live.log, si, msg);
+            this._lseqMap(false).delete(meta.localSeq);
+            const iv = this.byId.get((si.properties || {})[INTERVAL_ID]);
+            if (iv !== undefined) this.ackInterval(live, iv);
+            return undefined;
+        }
+        if (name === 'delete') { if (!local) this.ackDelete(si); return undefined; }
+        if (local) {
+            this._lseqMap(false).delete(meta.localSeq);
+            this._removePendingChange(si);
+        }
+        const props = si.properties && typeof si.properties === 'object' ? si.properties : {};
+        if (!(INTERVAL_ID in props)) throw new Error('0x3fe');
+        const { [INTERVAL_ID]: id, ...newProps } = props;
+        let iv = typeof id === 'string' ? this.byId.get(id) : undefined;
+        if (iv === undefined) return undefined;
+        if (local) { iv.pm.ack(props); this.ackInterval(live, iv); return undefined; }
+        const start = this.hasPendingChange(id, false) ? undefined : si.start;
+        const end = this.hasPendingChange(id, true) ? undefined : si.end;
+        if (start === null || end === null) throw new IntervalUnsupported('a change op with a null endpoint');
+        if (start !== undefined || end !== undefined) {
+            const view = { referenceSequenceNumber: msg.referenceSequenceNumber, clientId: msg.clientId };
+            iv = this._changeInterval(live, iv, start, end, view);
+        }
+        iv.pm.add(iv.props, newProps, msg.sequenceNumber, true);
+        return undefined;
+    }
+    rebasePositions(live, lseqs) {  // computeRebasedPositions (:1507-1528): one MTR_OP_REBASE_POS per endpoint
+        const recs = [];
+        for (const lseq of lseqs) {
+            const original = this._lseqMap(false).get(lseq);
+            if (original === undefined) throw new Error('0x551');
+            for (const key of ['start', 'end']) {
+                if (original[key] !== undefined) {
+                    recs.push([lseq, key, live.log.rebasePosition(intPos(original[key], key), original.sequenceNumber, lseq)]);
+                }
+            }
+        }
+        const res = recs.length ? live.rebaseResults() : new Map();
+        const out = new Map();
+        for (const lseq of lseqs) out.set(lseq, Object.assign({}, this._lseqMap(false).get(lseq)));
+        for (const [lseq, key, rec] of recs) out.get(lseq)[key] = res.get(rec);
+        return out;
+    }
+    onNormalize(live) {  // the client's "normalize" listener (attachGraph, :1542-1551)
+        const keys = Array.from(this._lseqMap(false).keys());
+        if (keys.length) for (const [k, v] of this.rebasePositions(live, keys)) this._lseqMap(true).set(k, v);
+    }
+    rebaseLocal(live, name, ser, localSeq) {  // rebaseLocalInterval (:1963-2029); undefined = the op is a no-op
+        if (name === 'delete') return ser;
+        let rb = this._lseqMap(true).get(localSeq);
+        if (rb === undefined) rb = this.rebasePositions(live, [localSeq]).get(localSeq);
+        const props = ser.properties;
+        const id = props ? props[INTERVAL_ID] : undefined;
+        const local = typeof id === 'string' ? this.byId.get(id) : undefined;
+        const rebased = { start: rb.start, end: rb.end, intervalType: ser.intervalType, sequenceNumber: live.currentSeq,
+            properties: props };
+        if (name === 'change' && (this.hasPendingChange(id, false) || this.hasPendingChange(id, true))) {
+            this._removePendingChange(ser);
+            this._addPendingChange(id, rebased);
+        }
+        if (rebased.start === -1 || rebased.end === -1) {
+            if (local !== undefined) this._remove(local);
+            return undefined;
+        }
+        if (local !== undefined) this._changeInterval(live, local, rebased.start, rebased.end, undefined, localSeq);
+        return rebased;
+    }
+    ordered(keys) {  // the start tree's in-order walk: SequenceInterval.compare order
+        return Array.from(this.byId.values()).sort((a, b) => ivCmp(keys, a, b));
+    }
     serialize(states, currentSeq) {  // LocalIntervalCollection.serialize (:1105-1112) + compressInterval (:139-151)
         const pos = (ref, fromOp) => {
             const p = states[2 * ref], st = states[2 * ref + 1];
@@ -184,6 +432,13 @@ class IntervalCollections {
         if (c === undefined) { c = new Collection(label, undefined); this.data.set(label, c); }
         return c;
     }
+    liveProcess(live, contents, msg, local, meta) {  // a live client's "act" handler: its own acks too
+        if (typeof contents.key !== 'string') throw new IntervalUnsupported('an interval op without a string key');
+        const value = contents.value || {};
+        const name = value.opName;
+        if (name !== 'add' && name !== 'delete' && name !== 'change') throw new IntervalUnsupported('interval op ' + name);
+        this.get(contents.key).liveProcess(live, name, value.value, msg, local, meta);
+    }
     process(log, contents, msg) {  // DefaultMap's "act" handler (defaultMap.ts:386-395), the ops map (:1266-1326)
         const cid = msg.clientId === null || msg.clientId === undefined ? 'null' : String(msg.clientId);
         if (cid === log.observerId) throw new IntervalUnsupported('acks of local interval ops');
@@ -211,4 +466,4 @@ class IntervalCollections {
     }
 }
 
-module.exports = { IntervalCollections, IntervalUnsupported, IntervalType };
+module.exports = { IntervalCollections, IntervalUnsupported, IntervalType, UsageError, refKey, cmpKey };

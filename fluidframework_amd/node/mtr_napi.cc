@@ -387,6 +387,46 @@ napi_value GetLeaves(napi_env env, napi_callback_info info) {
     return r;
 }
 
+// getRefKeys(h, doc) -> Int32Array [position, MTR_REF_ST_* bits, compare key, offset] per local reference
+// (mtr_get_ref_keys): a live interval collection's order (SequenceInterval.compare, intervalCollection.ts:505-539)
+napi_value GetRefKeys(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    const int64_t n = mtr_get_ref_keys(e, doc, nullptr, 0);
+    if (n < 0) return throw_engine(env, "mtr_get_ref_keys");
+    void* data = nullptr;
+    napi_value ab, r;
+    NAPI_CALL(env, napi_create_arraybuffer(env, size_t(n) * 16, &data, &ab));
+    if (n > 0 && mtr_get_ref_keys(e, doc, static_cast<int32_t*>(data), 4 * n) != n)
+        return throw_engine(env, "mtr_get_ref_keys");
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, size_t(4 * n), ab, 0, &r));
+    return r;
+}
+
+// getViewLength(h, doc, refSeq, client) -> nodeLength(root) at that view (mtr_get_containing_segment past the end);
+// this client's own short id at its currentSeq is getLength (markers count 1)
+napi_value GetViewLength(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    uint32_t doc = 0;
+    int32_t ref = 0, client = 0;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[1], &doc));
+    NAPI_CALL(env, napi_get_value_int32(env, argv[2], &ref));
+    NAPI_CALL(env, napi_get_value_int32(env, argv[3], &client));
+    mtr_segment_info si;
+    if (mtr_get_containing_segment(e, doc, INT32_MAX, ref, client, &si, nullptr, 0) != MTR_OK)
+        return throw_engine(env, "mtr_get_containing_segment");
+    napi_value r;
+    NAPI_CALL(env, napi_create_int32(env, si.start, &r));
+    return r;
+}
+
 // getRefInfo(h, doc, id) -> [leaf, offset, refType, held] (LocalReference.getSegment/getOffset, localReference.ts:106-112)
 napi_value GetRefInfo(napi_env env, napi_callback_info info) {
     napi_value argv[3];
@@ -581,7 +621,8 @@ napi_value Init(napi_env env, napi_value exports) {
                {"getDeltas", GetDeltas},       {"submitRunAsync", SubmitRunAsync},
                {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment},
                {"getProps", GetProps}, {"getRefPositions", GetRefPositions}, {"getRefInfo", GetRefInfo},
-               {"getRefStates", GetRefStates}, {"getLeaves", GetLeaves}};
+               {"getRefStates", GetRefStates}, {"getLeaves", GetLeaves}, {"getRefKeys", GetRefKeys},
+               {"getViewLength", GetViewLength}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||

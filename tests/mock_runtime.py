@@ -53,6 +53,9 @@ class OracleExecutor:
     def props(self, d, ref):
         return self.docs[d].regen_props(ref)
 
+    def summary(self, batch, d):
+        return self.docs[d].summarize(batch, d)
+
 
 class Runtime:
     """MockContainerRuntime(ForReconnection) of one SharedString."""

@@ -448,6 +448,26 @@ def test_propagates_delete_op(kind):  # :733-774
     assert_intervals(s2, c2, [])
 
 
+@pytest.mark.parametrize("kind", EXECUTORS)
+def test_can_round_trip_intervals(kind):  # :776-811
+    from fixtures import blob_names
+
+    f, s1, _, _, _ = two(kind)
+    s1.insert_text(0, "ABCDEF")
+    c1 = s1.get_interval_collection("test")
+    iid = c1.add(2, 2, SLIDE).id()
+    f.process_all()
+    blobs = f.session.summary(s1.doc)
+    header = s1.interval_header().decode()
+    g = factory(kind)
+    s3 = g.session.client("3")
+    s3.log.load(dict(zip(blob_names(len(blobs), True), [b.decode() for b in blobs])), "3", g.session.it, header=header)
+    c3 = s3.get_interval_collection("test")
+    assert c1.positions(c1.get_interval_by_id(iid)) == (2, 2)
+    assert c3.positions(c3.get_interval_by_id(iid)) == (2, 2)
+    assert s3.get_text() == "ABCDEF"
+
+
 def comparator(kind):
     f, s1, s2, _, _ = two(kind)
     s1.insert_text(0, "ABCDEFG")

@@ -538,3 +538,13 @@ def test_intervals_through_node_host(tmp_path):
         assert r["header"] == s["want"]
         if "text" in s:
             assert r["text"] == s["text"]
+
+
+@pytest.mark.gpu
+def test_interval_live_ops_through_node_host():
+    """A collaborating client's own interval ops (add / change / changeProperties / delete, their acks, reconnect
+    rebasing) through the Node host, N-API -> C ABI -> HIP: known answers of intervalCollection.spec.ts (the same cases
+    tests/test_interval_live.py runs through the Python host)."""
+    _addon()
+    res = json.loads(_node([os.path.join(HERE, "node", "interval_live.js")], timeout=600))
+    assert res and all(v == "ok" for v in res.values()), res
