@@ -447,7 +447,7 @@ def main(argv=None):
                    "dependent LDS round trips, ballots and scalar control per op); waves per SIMD are "
                    "capped by VGPRs and LDS per document. HBM sees only stage-in/out and arenas "
                    "(counter_hbm_gbs), so the HBM roofline is the flat-pass B_op model's, not the traffic's",
-        "kernel": "mtr::apply_pair_kernel" if matrix else "mtr::apply_kernel",
+        "kernel": "mtr::apply_pair2_kernel" if matrix else "mtr::apply_kernel",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",

@@ -95,9 +95,15 @@ def build_engine(force=False, verbose=False, prof=False, variant=None, extra=())
         hdrs = [d for d in deps if d.endswith(".h")]
         flag_file = os.path.join(objdir, "flags.txt")
         same_flags = os.path.exists(flag_file) and open(flag_file).read() == " ".join(flags)
+        reuse = variant and os.environ.get("MTR_REUSE_VARIANTS") == "1"
         for src, obj, extra in units:
             if same_flags and not force and not _stale(obj, [src] + hdrs):
                 continue  # (per translation unit: an edit of one .hip recompiles that unit only)
+            if reuse and "apply_variants" in obj:  # (a C3 experiment: the runtime-layout kernels from the main build)
+                import shutil
+
+                shutil.copy(os.path.join(HERE, "build", os.path.basename(obj)), obj)
+                continue
             cmd = flags + extra + ["-Rpass-analysis=kernel-resource-usage", "-c", "-o", obj, src]
             if verbose:
                 print(" ".join(cmd))

@@ -34,6 +34,20 @@
 #include "../../include/mtr_types.h"
 
 #define MTR_DI __device__ __forceinline__
+// Rare, large paths (text-arena collection, snapshot loads, the scour fallback) as out-of-line calls: an experiment
+// switch, off -- the calls take the document structs by reference, which puts them on the scratch stack (r05: 644
+// scratch accesses in the CAP-224 kernel against 221 -> 44 SGPRs spilled)
+#ifndef MTR_COLD_NOINLINE
+#define MTR_COLD_NOINLINE 0
+#endif
+#if MTR_COLD_NOINLINE
+#define MTR_COLD __device__ __attribute__((noinline))
+#else
+#define MTR_COLD MTR_DI
+#endif
+#ifndef MTR_UNSWITCH
+#define MTR_UNSWITCH 1
+#endif
 
 namespace mtr {
 
@@ -560,18 +574,22 @@ struct Eng {
     static MTR_DI int vis_len(const D& L, int i, const View& v, int newlen, int minseq, bool valid = true) {
         return vis_hot(L, ld_hot(L, i), i, v, newlen, minseq, valid);
     }
+    template <int LOC = -1, int NL = -1>
     static MTR_DI int vis_hot(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
-        const int r = vis_leaf(L, h, i, v, newlen, minseq, valid);
+        const int r = vis_leaf<LOC, NL>(L, h, i, v, newlen, minseq, valid);
         if constexpr (G) return r | vp_bit(h.meta, 25);  // a hole slot (M_DEL) is no leaf (Eng::spread)
         return r;
     }
-    static MTR_DI int vis_leaf(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
+    // (LOC / NL >= 0: v.local / newlen known at compile time -- the remote view's scans carry no local branch)
+    template <int LOC = -1, int NL = -1>
+    static MTR_DI int vis_leaf(const D& L, const Hot& h, int i, const View& v, int newlen_, int minseq, bool valid) {
         static_assert(M_DEL == 1u << 25 && M_OVERLAP == 1u << 21, "vis_hot / vis_leaf bit positions");
         const int len = h.len;
         const int rseq = h.rseq;
         const uint32_t m = h.meta;
         const int seq = h.seq;
-        if (v.local) {  // localNetLength, mergeTree.ts:613-634 (a uniform branch)
+        const int newlen = NL >= 0 ? NL : newlen_;
+        if (LOC >= 0 ? LOC != 0 : v.local != 0) {  // localNetLength, mergeTree.ts:613-634 (a uniform branch)
             const bool removed = rseq != RNONE;
             const int rl = newlen ? 0 : (rseq > minseq ? 0 : -1);
             return removed ? rl : len;
@@ -666,6 +684,17 @@ struct Eng {
             wsync();
             return;
         }
+        // (the remote view with the default length rules -- every sequenced op of another client -- gets a loop
+        // without the uniform local / new-length branches)
+        if (MTR_UNSWITCH && !v.local && !newlen) prefix_lds<0, 0>(L, s, v, 0);
+        else prefix_lds<-1, -1>(L, s, v, newlen);
+        wsync();
+    }
+    template <int LOC, int NL>
+    static MTR_DI void prefix_lds(D& L, const St& s, const View& v, int newlen) {
+        const int S = s.nseg;
+        const int ln = lane_id();
+        int carry = 0;
         Hot h = S > 0 ? ld_hot(L, ln) : Hot{};  // software-pipelined: loaded one round ahead
         for (int base = 0; base < S; base += 64) {
             // every lane evaluates (reads past the last leaf stay inside the LDS allocation);
@@ -674,7 +703,7 @@ struct Eng {
             const int i = base + ln;
             const Hot cur = h;
             if (base + 64 < S) h = ld_hot(L, i + 64);
-            const int x0 = vis_hot(L, cur, i, v, newlen, s.minseq, i < S);
+            const int x0 = vis_hot<LOC, NL>(L, cur, i, v, newlen, s.minseq, i < S);
             const int in = vp_lt(i, S);
             const int x = x0 & in;
             const int inc = wave_incl_scan(max(x, 0));
@@ -683,7 +712,6 @@ struct Eng {
             L.E[vp_sel(in, i, S)] = (carry + inc) | (x & int(0x80000000u));
             carry += rdlane(inc, 63);
         }
-        wsync();
     }
 
     // ---- two-level view scan (HBM-resident documents with hole slots, s.chunked)
@@ -3094,7 +3122,7 @@ struct Eng {
 
     // Semi-space compaction of the text arena: copy every leaf's text into the other half in
     // leaf order (prefix scan of lengths), then switch halves.
-    static MTR_DI void text_gc(D& L, const KParams& P, St& s) {
+    static MTR_COLD void text_gc(D& L, const KParams& P, St& s) {
         PROF(P_TEXTGC);
         text_flush(L);
         const int S = s.nseg;
@@ -3289,7 +3317,7 @@ struct Eng {
     // scourNode (zamboni.ts:122-193) over the child blocks in [cs, ce): a new child block starts at
     // every leaf with bnd >= 1.  Marks M_DEL; returns #kept (used for a single block).  The leaves
     // are read 64 at a time into registers and visited in order by readlane.
-    static MTR_DI int scour_range(D& L, const KParams& P, St& s, int cs, int ce) {
+    static MTR_COLD int scour_range(D& L, const KParams& P, St& s, int cs, int ce) {
         const int minseq = s.minseq;
         int prev = -1, kept = 0, plen = 0;
         uint32_t pmeta = 0, pprops = 0, ptext = 0;
@@ -4005,7 +4033,7 @@ struct Eng {
     // ------------------------------------------------------------ snapshot load
     // merge info of a snapshot segment on leaf i (SnapshotLoader.specToSegment, snapshotLoader.ts:88-128):
     // removedSeq, and removedClientIds as first remover + newest-first cons list of the others
-    static MTR_DI void set_merge_info(D& L, const KParams& P, St& s, int i, const mtr_op& op, const mtr_doc_desc& dd) {
+    static MTR_COLD void set_merge_info(D& L, const KParams& P, St& s, int i, const mtr_op& op, const mtr_doc_desc& dd) {
         if (op.ref_seq >= 0) L.rseq[i] = op.ref_seq;
         const int nrem = op.min_seq;
         if (nrem > 0) {
@@ -4033,7 +4061,7 @@ struct Eng {
     }
 
     // one header segment appended in order; the block structure is built by finish_load
-    static MTR_DI void load_leaf(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd) {
+    static MTR_COLD void load_leaf(D& L, const KParams& P, St& s, const mtr_op& op, const mtr_doc_desc& dd) {
         if (s.collab) {  // "Trying to reload from segments while collaborating!"
             s.status = MTR_ERR_ASSERT | 0x049;
             return;
@@ -4083,7 +4111,7 @@ struct Eng {
     // the loop's 64-record window hold (lane t: the 8 words of record t): one lane per segment, as
     // load_leaf + set_merge_info would append them one by one.  Returns how many were appended (0: the
     // record at t0 takes the one-by-one path: a marker, props, removers, or room running short).
-    static MTR_DI int load_run(D& L, const KParams& P, St& s, const uint32_t (&ow)[8], int t0, int tend,
+    static MTR_COLD int load_run(D& L, const KParams& P, St& s, const uint32_t (&ow)[8], int t0, int tend,
                                gptr<const uint16_t> btext) {
         PROF(P_LOAD);
         const int ln = lane_id();
@@ -4121,7 +4149,7 @@ struct Eng {
 
     // MergeTree.reloadFromSegments (mergeTree.ts:678-728): MaxNodesInBlock - 1 = 7 children per block,
     // built bottom-up, so leaf i starts a level-l block iff 7^l divides i; leaf 0 starts every level
-    static MTR_DI void finish_load(D& L, St& s) {
+    static MTR_COLD void finish_load(D& L, St& s) {
         PROF(P_LOAD);
         const int S = s.nseg;
         int H = 1;
