@@ -3054,7 +3054,9 @@ struct Eng {
             }
             L.pc_on = pos < total;
             L.pc_dst = dst + uint32_t(pos);
-            L.pc_val = t[src];
+            // (lanes past the chain's end load unit 0 of this document's arena: their computed source can lie past
+            // the last document's allocation)
+            L.pc_val = t[uint32_t(vp_sel(vp_lt(pos, total), int(src), 0))];
             L.pc_any = 1;
             return;
         }

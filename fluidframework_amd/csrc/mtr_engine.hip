@@ -107,6 +107,7 @@ struct mtr_engine {
     bool pend_seen = false;           // a batch since mtr_reset held local ops while collaborating or acks:
                                       // documents may hold pending segments, so every launch is an X kernel
     DevBuf<uint32_t> pend;            // [doc][kPendRing][4] pending SegmentGroups (allocated on first use)
+    int dev_lds = 0;                  // the device's LDS per workgroup (bytes; 0 = unknown)
     bool refs_seen = false;           // a batch since mtr_reset created local references: they follow splits,
                                       // appends and removals in the X kernels only, so every launch is one
     DevBuf<uint32_t> refs;            // [doc][3][ref_slots] local references (allocated on first use)
@@ -307,11 +308,12 @@ mtr_engine* mtr_engine_create(const mtr_options* opt, int device, uint32_t max_d
         return nullptr;
     }
     {  // HBM-resident launches (and the query kernels) still keep per-chunk rows in LDS: about segcap / 8
-       // bytes, twice for a matrix pair -- a capacity whose rows exceed the device's LDS is refused here
-       // rather than failing every later launch with a generic HIP error
+       // bytes (twice for a matrix pair: mtr_set_matrix checks that) -- a capacity whose rows exceed the device's
+       // LDS is refused here rather than failing every later launch with a generic HIP error
         int dev_lds = 0;
         if (hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) dev_lds = 0;
-        const size_t need = 2 * ((lds_bytes_global_mode(int(c.max_segments)) + 15) & ~size_t(15));
+        e->dev_lds = dev_lds;
+        const size_t need = (lds_bytes_global_mode(int(c.max_segments)) + 15) & ~size_t(15);
         if (dev_lds > 0 && need > size_t(dev_lds)) {
             set_err("mtr_engine_create: max_segments " + std::to_string(c.max_segments) + " needs " +
                     std::to_string(need) + " bytes of LDS in HBM-resident mode (device: " + std::to_string(dev_lds) + ")");
@@ -578,6 +580,15 @@ int mtr_set_matrix(mtr_engine* e, uint32_t rows_doc, uint32_t cols_doc) {
         e->h_kind[rows_doc] || e->h_kind[cols_doc]) {
         set_err("mtr_set_matrix: bad or already paired documents");
         return MTR_ERR_BAD_OP;
+    }
+    {  // a pair's HBM-resident launches hold two documents' chunk rows in LDS
+        const size_t need = 2 * ((lds_bytes_global_mode(int(e->caps.max_segments)) + 15) & ~size_t(15));
+        if (e->dev_lds > 0 && need > size_t(e->dev_lds)) {
+            set_err("mtr_set_matrix: max_segments " + std::to_string(e->caps.max_segments) + " needs " +
+                    std::to_string(need) + " bytes of LDS for a matrix pair in HBM-resident mode (device: " +
+                    std::to_string(e->dev_lds) + ")");
+            return MTR_ERR_CAPACITY;
+        }
     }
     e->h_kind[rows_doc] = 1;
     e->h_kind[cols_doc] = 2;

@@ -614,10 +614,8 @@ def _endpoint(states: list, ref: int, from_op: bool) -> int:
     seg, held, removed = st & abi.REF_ST_SEGMENT, st & abi.REF_ST_HELD, st & abi.REF_ST_REMOVED
     if seg and held and not removed and pos >= 0:
         return pos
-    if not seg and from_op:
-        return abi.DETACHED_POSITION  # no segment: smaller than any (referencePositions.ts:119)
-    if not seg:
-        raise IntervalUnsupported("an endpoint created without an op has no segment (the reference throws)")
+    if not seg:  # no segment (created detached by an op, or slid off the string): smaller than any
+        return abi.DETACHED_POSITION  # (referencePositions.ts:119); a local creation without one throws first
     raise IntervalUnsupported("an interval endpoint on a removed segment, or dropped by its segment")
 
 

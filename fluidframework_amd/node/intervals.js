@@ -395,8 +395,7 @@ class Collection {
         const pos = (ref, fromOp) => {
             const p = states[2 * ref], st = states[2 * ref + 1];
             if ((st & REF_ST.SEGMENT) && (st & REF_ST.HELD) && !(st & REF_ST.REMOVED) && p >= 0) return p;
-            if (!(st & REF_ST.SEGMENT) && fromOp) return -1;
-            if (!(st & REF_ST.SEGMENT)) throw new IntervalUnsupported('an endpoint created without an op has no segment');
+            if (!(st & REF_ST.SEGMENT)) return -1;  // no segment (an op's detached endpoint, or slid off): first
             throw new IntervalUnsupported('an interval endpoint on a removed segment, or dropped by its segment');
         };
         const keyed = Array.from(this.byId.values(), (iv) => [pos(iv.start, iv.kind === 'op'), pos(iv.end, iv.kind === 'op'), iv]);

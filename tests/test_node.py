@@ -49,7 +49,8 @@ def test_addon_loads_and_fails_loudly_without_a_gpu():
     assert json.loads(lines[0]) == sorted(["createEngine", "submitRun", "summarize", "getSummary", "getText",
                                            "docStatus", "stats", "reset", "setMatrix", "getDeltas",
                                            "submitRunAsync", "summarizeAsync", "getContainingSegment", "getProps",
-                                           "getRefPositions", "getRefInfo", "getRefStates", "getLeaves"])
+                                           "getRefPositions", "getRefInfo", "getRefStates", "getLeaves",
+                                           "getRefKeys", "getViewLength"])
     if lines[1] != "ENGINE":  # no HIP device here: construction must throw, never fall back
         assert lines[1].startswith("ERR mtr_engine_create")
 
