@@ -48,24 +48,26 @@ def kernel_resources(stderr_texts):
     return res
 
 
-# HBM-resident apply kernels (apply_kernel<true, ...>, apply_pair_kernel<true, ...>) must not spill VGPRs, and the
-# lean one (CAP = -1: C5's kernel) must use no scratch at all.  A round-3 build whose lean HBM kernel spilled
-# produced wrong views; the main build refuses one.  (The X / delta / record-mode HBM
-# kernels keep a few private arrays in scratch -- dynamically indexed stack arrays, not spills.)
-_HBM_KERNELS = re.compile(r"^_ZN3mtr(12apply_kernel|17apply_pair_kernel)ILb1E")
+# No apply kernel may spill VGPRs (apply_kernel / apply_pair_kernel / apply_pair2_kernel, LDS- and HBM-resident), and
+# the lean HBM-resident one (CAP = -1: C5's kernel) must use no scratch at all.  A round-3 build whose lean HBM kernel
+# spilled produced wrong views; the main build refuses one.  (The X / delta / record-mode
+# kernels keep some scratch that is no spill: the call frames of their out-of-line rare paths -- regenerate, normalize,
+# props_apply_serial, props_restore -- whose by-reference document structs live on the stack, and a few dynamically
+# indexed private arrays)
+_APPLY_KERNELS = re.compile(r"^_ZN3mtr(12apply_kernel|17apply_pair_kernel|18apply_pair2_kernel)I")
 _HBM_LEAN = re.compile(r"^_ZN3mtr12apply_kernelILb1ELin1E")
 
 
 def check_no_scratch(res, strict=True):
     bad = {}
     for k, v in res.items():
-        if not _HBM_KERNELS.match(k):
+        if not _APPLY_KERNELS.match(k):
             continue
         scratch, vspill = v.get("ScratchSize [bytes/lane]", 0), v.get("VGPRs Spill", 0)
         if vspill or (_HBM_LEAN.match(k) and scratch):
             bad[k] = (scratch, vspill)
     if bad:
-        msg = "HBM-resident apply kernels spill: " + ", ".join(
+        msg = "apply kernels spill VGPRs: " + ", ".join(
             f"{k} (scratch {a} B/lane, {b} VGPRs spilled)" for k, (a, b) in sorted(bad.items()))
         if strict:
             raise RuntimeError(msg)

@@ -5259,8 +5259,15 @@ struct Eng {
 #ifndef MTR_WPE_G
 #define MTR_WPE_G 1
 #endif
+// (the LDS-resident kernels with the rare records compiled in -- CAP = 0: local ops, references, intervals,
+// reconnect, record mode -- run small batches of live clients: they take a SIMD's registers too, so their extra
+// state stays in registers (AGPRs when it must) instead of spilling to scratch)
+#ifndef MTR_WPE_X
+#define MTR_WPE_X 1
+#endif
 template <bool G, int CAP = 0, bool DL = false, bool GN = false>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G ? MTR_WPE_G : MTR_WPE))) apply_kernel(KParams P) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G ? MTR_WPE_G : (CAP == 0 ? MTR_WPE_X : MTR_WPE))))
+apply_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];

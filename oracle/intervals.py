@@ -274,6 +274,43 @@ class RedBlackTree:
         n.size = self.size_of(n.left) + self.size_of(n.right) + 1
         return n
 
+    def floor(self, key):
+        """rbTree.ts:441-462: the largest node comparing <= key (None when none)."""
+        n, best = self.root, None
+        while n is not None:
+            c = self.compare(key, n.key)
+            if c == 0:
+                return n
+            if c < 0:
+                n = n.left
+            else:
+                best, n = n, n.right
+        return best
+
+    def ceil(self, key):
+        """rbTree.ts:464-488: the smallest node comparing >= key (None when none)."""
+        n, best = self.root, None
+        while n is not None:
+            c = self.compare(key, n.key)
+            if c == 0:
+                return n
+            if c > 0:
+                n = n.right
+            else:
+                best, n = n, n.left
+        return best
+
+    def nodes(self):
+        out, stack, n = [], [], self.root
+        while stack or n is not None:
+            while n is not None:
+                stack.append(n)
+                n = n.left
+            n = stack.pop()
+            out.append(n)
+            n = n.right
+        return out
+
     def keys(self):
         out, stack, n = [], [], self.root
         while stack or n is not None:
@@ -478,6 +515,34 @@ class _Collection:
         if INTERVAL_ID not in iv.props:
             raise OracleUnsupported("uuid()")
         self.add(iv)
+
+    # ---- queries (LocalIntervalCollection, :946-992) of a transient interval (createSequenceInterval with
+    # IntervalType.Transient: Transient references at the local view)
+    def transient(self, start, end) -> SequenceInterval:
+        s = self.o.log.create_ref(int(start), abi.REFTYPE_TRANSIENT)
+        t = self.o.log.create_ref(int(end), abi.REFTYPE_TRANSIENT)
+        self.o.flush()
+        return SequenceInterval(s, t, TRANSIENT, {}, "transient")
+
+    def previous_interval(self, pos):
+        """previousInterval (:966-978): endIntervalTree.floor(transient) -> its data"""
+        n = self.end_tree.floor(self.transient(pos, pos))
+        return None if n is None else n.data
+
+    def next_interval(self, pos):
+        """nextInterval (:980-992): endIntervalTree.ceil(transient) -> its data"""
+        n = self.end_tree.ceil(self.transient(pos, pos))
+        return None if n is None else n.data
+
+    def find_overlapping(self, start, end):
+        """findOverlappingIntervals (:950-964): the tree's gather of SequenceInterval.overlaps (:544-549); the
+        augmentation (union of the subtree, intervalTree.ts:163-177) only prunes subtrees without a match, so the
+        in-order filter gives the same list."""
+        if end < start or self.tree.is_empty():
+            return []
+        t = self.transient(start, end)
+        return [iv for iv in self.tree.keys()
+                if self.o.compare_refs(iv.start, t.end) <= 0 and self.o.compare_refs(iv.end, t.start) >= 0]
 
     def serialize(self):
         """LocalIntervalCollection.serialize (:1105-1112) with compressInterval (:139-151)."""
