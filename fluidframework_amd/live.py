@@ -60,9 +60,10 @@ class EngineExecutor:
 class LiveSession:
     """Clients of one document family on one executor: `sync()` applies every client's queued records."""
 
-    def __init__(self, executor, interner: Interner | None = None):
+    def __init__(self, executor, interner: Interner | None = None, legacy: bool = False):
         self.ex = executor
         self.it = interner or Interner()
+        self.legacy = legacy          # the legacy summary format (newMergeTreeSnapshotFormat !== true): catch-up ops
         self.clients: list[SharedStringClient] = []
         self.deltas: dict[int, np.ndarray] = {}
 
@@ -79,6 +80,8 @@ class LiveSession:
         for c in self.clients:
             if b.docs[c.doc]["op_count"]:
                 self.deltas[c.doc] = self.ex.deltas(c.doc)
+                if c.log.pending:
+                    c.log.resolve(self.deltas[c.doc])
 
 
     def summary(self, doc: int) -> list[bytes]:
@@ -96,7 +99,7 @@ class SharedStringClient:
         self.session = session
         self.doc = doc
         self.name = name
-        self.log = SequenceLog(legacy=False)
+        self.log = SequenceLog(legacy=session.legacy)
         self.log.intervals = IntervalCollections()
         self.submit_fn: Callable[[Any, Any], None] | None = None
         self.lseq = 0                 # collabWindow.localSeq as this host counts it (every local op, interval ops too)
@@ -195,6 +198,13 @@ class SharedStringClient:
 
         h = self.log.intervals.serialize(self.ref_keys(), self.current_seq, live=True)
         return None if h is None else to_utf8(h)
+
+    def summary(self) -> list[bytes]:
+        """summarizeCore's merge-tree blobs (the engine's summary of this document) plus, in the legacy format, the
+        ``catchupOps`` blob of the messages since the MSN (summarizeMergeTree, sequence.ts:675-695)."""
+        blobs = self.session.summary(self.doc)
+        cu = self.log.catchup_blob()
+        return blobs + ([cu] if cu is not None else [])
 
     def local_reference_position(self, ref: int) -> int:
         return self.ref_keys()[ref][0]

@@ -670,10 +670,15 @@ function opsFromDeltas(members, opIndex, byOp) {
 class CatchUpLog {
     constructor() { this.stash = []; this.pending = []; }
     /** After log.message(msg) queued the message's records from op index `lo` on. */
-    add(msg, log, lo) {
+    add(msg, log, lo, own) {
         const copy = JSON.parse(JSON.stringify(msg));  // parseHandles (sequence.ts:698)
         if (typeof copy.contents === 'string') copy.contents = JSON.parse(copy.contents);
-        if (copy.referenceSequenceNumber !== copy.sequenceNumber - 1) {
+        if (own && copy.referenceSequenceNumber !== copy.sequenceNumber - 1) {
+            // an ack raises no "delta" event (ackPendingSegment, mergeTree.ts:1283-1323): transformOps collects
+            // nothing and the stashed copy is createGroupOp() of no ops (sequence.ts:697-725, opBuilder.ts:102-107)
+            copy.referenceSequenceNumber = copy.sequenceNumber - 1;
+            copy.contents = { ops: [], type: 3 };
+        } else if (copy.referenceSequenceNumber !== copy.sequenceNumber - 1) {
             const members = copy.contents.type === 3 ? copy.contents.ops : [copy.contents];
             const opIndex = members.map((_, i) => {
                 const r = log.ops[lo + i];
@@ -917,9 +922,6 @@ class BatchReplayClient {
     }
     applyMsg(msg, local, localOpMetadata) {
         const own = local || (msg.type === 'op' && String(msg.clientId) === this.log.observerId);
-        if (own && !this.engine.options.snapshotV1) {
-            throw new UnsupportedError("this client's own message in the legacy catch-up format");
-        }
         if (msg.type === 'op' && this.log.collaborating && this.log.intervals !== undefined) {
             const c = typeof msg.contents === 'string' ? JSON.parse(msg.contents) : msg.contents;
             if (c && c.type === 'act' && (own || this.log.intervals.live)) {  // a live client's interval op
@@ -929,7 +931,7 @@ class BatchReplayClient {
             }
         }
         this._queue(() => {
-            if (!this.engine.options.snapshotV1 && msg.type === 'op' &&
+            if (!this.engine.options.snapshotV1 && msg.type === 'op' && !own &&
                 msg.referenceSequenceNumber !== msg.sequenceNumber - 1) {
                 let c = msg.contents;
                 if (typeof c === 'string') c = JSON.parse(c);
@@ -945,7 +947,7 @@ class BatchReplayClient {
             this.log.message(msg, this.engine.interner, local);
             // (an interval op is handled by the collections and kept by no catch-up list, sequence.ts:636-645)
             if (!this.engine.options.snapshotV1 && msg.type === 'op' && this.log.currentSeq === msg.sequenceNumber) {
-                this.engine.catchUps[this.doc].add(msg, this.log, lo);
+                this.engine.catchUps[this.doc].add(msg, this.log, lo, !!own);
             }
         });
         this.currentSeq = this.log.currentSeq;

@@ -204,10 +204,22 @@ class SequenceLog(DocLog):
         if msg.get("type") != "op" or not self.legacy:
             super().message(msg, interner)
             return
-        if msg.get("clientId") == self.observer_id:
-            # an ack fires no delta event (ackPendingSegment, mergeTree.ts:1283-1322): the catch-up
-            # transform of a lagging own message is not built
-            raise Unsupported("this client's own message in the legacy catch-up format")
+        own = self.collaborating and msg.get("clientId") == self.observer_id
+        if own:
+            # applyMsg(msg, local = true) acks the pending segments (client.ts:858-875), which raises a
+            # "maintenance" event and no "delta" event (ackPendingSegment, mergeTree.ts:1283-1323): a lagging own
+            # message's transformOps listener collects nothing, so its stashed copy is createGroupOp() of no ops
+            # (sequence.ts:697-725, opBuilder.ts:102-107)
+            super().message(msg, interner)
+            stash = copy.deepcopy(msg)
+            seq = int(msg["sequenceNumber"])
+            if int(msg["referenceSequenceNumber"]) != seq - 1:
+                stash["referenceSequenceNumber"] = seq - 1
+                stash["contents"] = {"ops": [], "type": 3}
+            elif isinstance(stash.get("contents"), str):
+                stash["contents"] = parse(stash["contents"])
+            self._keep(stash, msg)
+            return
         if int(msg["referenceSequenceNumber"]) != int(msg["sequenceNumber"]) - 1:
             c = msg["contents"]
             c = parse(c) if isinstance(c, str) else c
@@ -242,6 +254,10 @@ class SequenceLog(DocLog):
             # {...message, referenceSequenceNumber: seq - 1, contents} keeps the key order
             stash["referenceSequenceNumber"] = seq - 1
             self.pending.append((stash, members, op_index))
+        self._keep(stash, msg)
+
+    def _keep(self, stash: dict, msg: dict) -> None:
+        """messagesSinceMSNChange.push + the GC every once in a while (sequence.ts:727-735)."""
         self.stash.append(stash)
         if len(self.stash) > _GC_SPAN and self.stash[_GC_SPAN]["sequenceNumber"] < msg["minimumSequenceNumber"]:
             self.min_seq_changed(int(msg["minimumSequenceNumber"]))

@@ -24,10 +24,10 @@ _ids = itertools.count(1)
 class OracleExecutor:
     """The CPU oracle as a live session's executor (one OracleDoc per client) -- the checker only."""
 
-    def __init__(self):
+    def __init__(self, legacy: bool = False):
         from oracle.oracle import OracleDoc, options
 
-        self._mk = lambda: OracleDoc(options())
+        self._mk = lambda: OracleDoc(options(snapshot_v1=not legacy))
         self.docs: list = []
 
     def apply(self, batch) -> None:
@@ -120,8 +120,8 @@ class Runtime:
 class Factory:
     """MockContainerRuntimeFactory(ForReconnection): the sequencer."""
 
-    def __init__(self, executor=None):
-        self.session = LiveSession(executor if executor is not None else OracleExecutor())
+    def __init__(self, executor=None, legacy: bool = False):
+        self.session = LiveSession(executor if executor is not None else OracleExecutor(legacy), legacy=legacy)
         self.seq = 0
         self.min_seq: dict[str, int] = {}
         self.messages: list[dict] = []

@@ -549,3 +549,24 @@ def test_interval_live_ops_through_node_host():
     _addon()
     res = json.loads(_node([os.path.join(HERE, "node", "interval_live.js")], timeout=600))
     assert res and all(v == "ok" for v in res.values()), res
+
+
+@pytest.mark.gpu
+def test_live_legacy_catchup_through_node_host(tmp_path):
+    """Legacy-format collaborating clients (own acked messages in the catch-up list, sequence.ts:697-736 with
+    local = true) through the Node host: every client's summary blobs (header, body, catchupOps) equal the
+    oracle-driven Python host's on the same script (tests/test_catchup_live.py)."""
+    from mock_runtime import OracleExecutor
+    from test_catchup_live import farm_script, replay
+
+    _addon()
+    script = farm_script(3)
+    f = tmp_path / "script.json"
+    f.write_text(json.dumps(script))
+    res = json.loads(_node([os.path.join(HERE, "node", "catchup_live.js"), str(f)], timeout=600))
+    _, want = replay(OracleExecutor(legacy=True), script)
+    assert res["texts"] == [r.dds.get_text() for r in want]
+    for got, r in zip(res["summaries"], want):
+        exp = r.dds.summary()
+        assert got[0][0] == "header" and got[-1][0] == "catchupOps"
+        assert [v.encode() for _, v in got] == exp
