@@ -18,9 +18,6 @@ import json
 
 from fluidframework_amd.live import LiveSession
 
-_ids = itertools.count(1)
-
-
 class OracleExecutor:
     """The CPU oracle as a live session's executor (one OracleDoc per client) -- the checker only."""
 
@@ -108,7 +105,7 @@ class Runtime:
                 self.process(m)
             self.pending_remote = []
             self.csn = 0
-            self.client_id = f"reconnected-{next(_ids)}"
+            self.client_id = f"reconnected-{next(self.factory.ids)}"
             msgs, self.pending = self.pending, []
             for contents, meta, _ in msgs:
                 self.dds.resubmit(contents, meta)
@@ -126,6 +123,7 @@ class Factory:
         self.min_seq: dict[str, int] = {}
         self.messages: list[dict] = []
         self.runtimes: list[Runtime] = []
+        self.ids = itertools.count(1)  # (per factory: two replays of one script name their clients alike)
 
     def runtime(self, name: str) -> Runtime:
         r = Runtime(self, name)

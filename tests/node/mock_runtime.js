@@ -8,8 +8,6 @@
 const path = require('path');
 const { BatchReplayEngine } = require(path.join(__dirname, '..', '..', 'fluidframework_amd', 'node', 'index.js'));
 
-let reconnects = 0;
-
 class Runtime {  // MockContainerRuntime(ForReconnection) + the SharedString around one BatchReplayClient
     constructor(factory, name) {
         this.factory = factory; this.clientId = name; this.csn = 0; this.lastSeq = 0;
@@ -45,7 +43,7 @@ class Runtime {  // MockContainerRuntime(ForReconnection) + the SharedString aro
             for (const m of this.pendingRemote) this.process(m);
             this.pendingRemote = [];
             this.csn = 0;
-            this.clientId = 'reconnected-' + (++reconnects);
+            this.clientId = 'reconnected-' + (++this.factory.reconnects);
             const msgs = this.pending;
             this.pending = [];
             for (const [contents, meta] of msgs) {
@@ -73,7 +71,7 @@ class Runtime {  // MockContainerRuntime(ForReconnection) + the SharedString aro
 }
 
 class Factory {  // MockContainerRuntimeFactory(ForReconnection)
-    constructor(options) { this.engine = new BatchReplayEngine(4, options); this.lastMsn = 0; this.seq = 0; this.minSeq = new Map(); this.messages = []; this.rts = []; }
+    constructor(options) { this.engine = new BatchReplayEngine(4, options); this.lastMsn = 0; this.reconnects = 0; this.seq = 0; this.minSeq = new Map(); this.messages = []; this.rts = []; }
     runtime(name) { const r = new Runtime(this, name); this.rts.push(r); return r; }
     push(msg) {
         if (msg.clientId && !this.minSeq.has(msg.clientId)) this.minSeq.set(msg.clientId, msg.referenceSequenceNumber);
