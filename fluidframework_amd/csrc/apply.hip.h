@@ -187,6 +187,7 @@ struct DocHdr {
     int32_t pfree;         // free list of pending-membership cells (first cell + 1, 0 = empty)
     int32_t lastnorm;      // Client.lastNormalizationRefSeq (client.ts:910): currentSeq of the last normalization
     int32_t nrefs;         // local references created (Eng::ref_create): ids 0 .. nrefs - 1
+    int32_t tfree;         // matrix vectors: tracking ids on the free stack (Eng::tid_free)
 };
 
 // 32-bit SoA fields per leaf kept in HBM and LDS
@@ -260,6 +261,8 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
        // the tail (deltas, zamboni, updateSeqNumbers)
        P_LOAD, P_PRE, P_VIEW, P_POST,
        P_NSUP, P_NDCH,  // counts: superchunks with events after refSeq, their chunks with such events
+       P_HELPER,        // the team's helper waves: cycles in the passes handed to them
+       P_SINK,          // (a slot nothing reads)
        P_COUNT };
 
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
@@ -439,10 +442,19 @@ constexpr size_t kScBytes = kScOnly + ((sizeof(mtr_synth_state) + 15) & ~size_t(
 __host__ __device__ inline size_t lds_bytes(int cap, int lhcap, bool gen = true) {
     return size_t(cap) * 4 * 8 + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
 }
-// (HBM-resident documents: Sc, the generator state, six superchunk rows, prefix2's chunk list and two
-// words per 64 slots)
+// HBM-resident documents run on a team of MTR_GW waves (one workgroup per document): wave 0 applies the ops, the
+// others wait at the workgroup barrier for the passes it hands out (Eng::team_*).  The team's mailbox: the task and
+// its arguments, then one result slot per wave.
+#ifndef MTR_GW
+#define MTR_GW 2
+#endif
+constexpr int kTeamInts = 64;  // (task + 15 argument words, then two step-parity rows of 4 result words per wave)
+constexpr size_t kTeamBytes = 4 * kTeamInts;
+// (HBM-resident documents: Sc, the generator state, the team's mailbox, six superchunk rows, prefix2's chunk list
+// and two words per 64 slots)
 __host__ __device__ inline size_t lds_bytes_global_mode(int segcap) {
-    return kScBytes + ((size_t(4) * (6 * sup_rows(segcap) + kListCap + 2 * (segcap / 64 + 1)) + 15) & ~size_t(15));
+    return kScBytes + kTeamBytes +
+           ((size_t(4) * (6 * sup_rows(segcap) + kListCap + 2 * (segcap / 64 + 1)) + 15) & ~size_t(15));
 }
 
 // Phase timers (builds with -DMTR_PROF only): lane-0 clock cycles per phase, summed over
@@ -868,13 +880,91 @@ struct Eng {
             wsync();
         }
     }
+    // ---- the team: an HBM-resident document's workgroup of MTR_GW waves.  Wave 0 runs the document; a pass it
+    // hands out is posted in the mailbox (task word + arguments), and the waves meet at the workgroup barrier
+    // twice: once to start (the helpers wait there between passes) and once when every wave's share is done.
+    enum { T_EXIT = 1, T_DIRTY = 2, T_PARENT = 3, T_PREFIX = 4 };
+    static_assert(16 + 2 * 4 * MTR_GW <= kTeamInts, "the team's mailbox holds two rows of results per wave");
+    static MTR_DI int team_n() {
+        if constexpr (G) return int(blockDim.x) >> 6;
+        return 1;
+    }
+    static MTR_DI lptr<int> tbox(const D& L) { return L.sx - kTeamInts; }
+    // wave 0: post task `t` (the arguments were written by lane 0 before) and start the team
+    static MTR_DI void team_start(const D& L, int t) {
+        if (lane_id() == 0) tbox(L)[0] = t;
+        __syncthreads();
+    }
+    // the helper waves (w >= 1): wait for passes until wave 0 posts T_EXIT
+    static MTR_DI void team_helper(char* smem, const KParams& P, uint32_t d, int w) {
+        if constexpr (G) {
+            D L;
+            carve_ptrs(L, smem, P, d);
+            const int W = team_n();
+            for (;;) {
+                __syncthreads();
+                const lptr<int> b = tbox(L);
+                const int t = uni(b[0]);
+                if (t != T_DIRTY && t != T_PREFIX && t != T_PARENT) break;  // T_EXIT
+                {
+#ifdef MTR_PROF
+                    ProfScope _prof_helper(L.sc, P_HELPER);  // (the pass, not the wait at its end)
+#endif
+                    View v;
+                    v.ref = uni(b[2]);
+                    v.client = uniu(uint32_t(b[3]));
+                    v.local = uni(b[4]);
+                    if (t == T_DIRTY) {
+                        dirty_part(L, v, uni(b[5]), uni(b[6]), uni(b[7]), uni(b[1]), w, W, dlist(L), true);
+                    } else if (t == T_PREFIX) {
+                        (void)prefix2_part(L, v, uni(b[5]), uni(b[6]), uni(b[7]), uni(b[1]), w, W);
+                    } else {
+                        int ps, pe, cnt;
+                        parent_part(L, uni(b[1]), uni(b[2]), uni(b[3]), w, W, ps, pe, cnt);
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+    static MTR_DI void team_exit(char* smem) {
+        if constexpr (G) {
+            if (team_n() > 1) {
+                if (lane_id() == 0) ((lptr<int>)(smem + kScBytes))[0] = T_EXIT;
+                __syncthreads();
+            }
+        }
+    }
     // view lengths of the listed chunks (dlist[0, n)) into ch_x, their change from the local lengths into
-    // their superchunks' sup_dlen
+    // their superchunks' sup_dlen (a team of waves takes the rounds of 64 chunks in turn)
     static MTR_DI void dirty_chunks(D& L, const St& s, const View& v, int newlen, int n) {
         PROF(P_PFSUM);  // (the listed chunks' evaluation; P_PFDIRTY: the unlisted ones inside it)
-        const int S = s.nseg, ln = lane_id();
-        const lptr<int> lst = dlist(L), cx = ch_x(L), sd = sup_dlen(L);
-        for (int e0 = 0; e0 < n; e0 += 64) {  // one lane per chunk: its whole record in one round of loads
+        const int W = team_n();
+        if (W > 1 && n > 64) {
+            const lptr<int> b = tbox(L);
+            if (lane_id() == 0) {
+                b[1] = n;
+                b[2] = v.ref;
+                b[3] = int(v.client);
+                b[4] = v.local;
+                b[5] = newlen;
+                b[6] = s.minseq;
+                b[7] = s.nseg;
+            }
+            team_start(L, T_DIRTY);
+            dirty_part(L, v, newlen, s.minseq, s.nseg, n, 0, W, dlist(L), true);
+            __syncthreads();
+            return;
+        }
+        dirty_part(L, v, newlen, s.minseq, s.nseg, n, 0, 1, dlist(L), false);
+        wsync();
+    }
+    // wave w of W: rounds w, w + W, ... of the listed chunks
+    static MTR_DI void dirty_part(D& L, const View& v, int newlen, int minseq, int S, int n, int w, int W,
+                                  lptr<int> lst, bool atomic) {
+        const int ln = lane_id();
+        const lptr<int> cx = ch_x(L), sd = sup_dlen(L);
+        for (int e0 = 64 * w; e0 < n; e0 += 64 * W) {  // one lane per chunk: its whole record in one round of loads
             const int e = e0 + ln;
             const int c = lst[min(e, n - 1)];
             const gptr<int> r = cs_rec(L, c);
@@ -897,14 +987,15 @@ struct Eng {
             for (int j = 0; j < kChunkList; j++) {
                 const bool on = listed && j < h.w;
                 const Hot hj{hv[j].x, hv[j].y, hv[j].z, uint32_t(hv[j].w)};
-                const int x0 = vis_hot(L, hj, on ? slt[j] : 0, v, newlen, s.minseq, on);
+                const int x0 = vis_hot(L, hj, on ? slt[j] : 0, v, newlen, minseq, on);
                 sum += on ? max(x0, 0) : 0;
             }
             int vl = sum;
             uint64_t um = __ballot(e < n && !listed);
 #ifdef MTR_PROF
-            if (ln == 0) L.sc->prof[P_NDIRTY] += (unsigned long long)__popcll(um);
-            ProfScope _prof_dirty(L.sc, P_PFDIRTY);
+            const bool lead = (threadIdx.x >> 6) == 0;  // (wave 0; the helpers' time is P_HELPER)
+            if (ln == 0 && lead) L.sc->prof[P_NDIRTY] += (unsigned long long)__popcll(um);
+            ProfScope _prof_dirty(L.sc, lead ? P_PFDIRTY : P_SINK);
 #endif
             while (um) {  // more than kChunkList leaves in the window: the chunk's leaves, GK chunks at a time
                 int lq[GK];
@@ -920,7 +1011,7 @@ struct Eng {
                 for (int g = 0; g < GK; g++) {
                     if (lq[g] < 0) break;
                     const int i = rdlane(c, lq[g]) * 64 + ln;
-                    const int x0 = vis_hot(L, hw[g], i, v, newlen, s.minseq, i < S);
+                    const int x0 = vis_hot(L, hw[g], i, v, newlen, minseq, i < S);
                     const int tot = rdlane(wave_incl_scan(i < S ? max(x0, 0) : 0), 63);
                     if (ln == lq[g]) vl = tot;
                 }
@@ -936,9 +1027,13 @@ struct Eng {
             const uint64_t starts = __ballot(ln == 0 || key != kprev);
             const int first = last_lane(starts & ((uint64_t(2) << ln) - 1));
             const int base = __shfl(inc, first) - __shfl(dv, first);
-            if (e < n && (ln == 63 || knext != key)) sd[key] += inc - base;
+            if (e < n && (ln == 63 || knext != key)) {
+                if (atomic)  // (another wave may hold chunks of the same superchunk)
+                    __hip_atomic_fetch_add(&sd[key], inc - base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    sd[key] += inc - base;
+            }
         }
-        wsync();
     }
     // the view's superchunk lengths and their inclusive prefix in sup_pre; returns the view's total length.
     // need < INT32_MAX: the caller reads the view only up to position need - 1 (its searches stop at the first
@@ -953,6 +1048,22 @@ struct Eng {
         if (ln == 0) {
             L.sc->sepoch = ep;
             L.sc->vref = v.local ? INT32_MAX : v.ref;  // (a local view: every chunk shows its local length)
+        }
+        if (team_n() > 1 && !v.local) {  // the team lists and evaluates the superchunks' chunks with later events
+            const lptr<int> b = tbox(L);
+            if (ln == 0) {
+                b[1] = need;
+                b[2] = v.ref;
+                b[3] = int(v.client);
+                b[4] = v.local;
+                b[5] = newlen;
+                b[6] = s.minseq;
+                b[7] = s.nseg;
+            }
+            team_start(L, T_PREFIX);
+            const int total = prefix2_part(L, v, newlen, s.minseq, s.nseg, need, 0, team_n());
+            __syncthreads();
+            return total;
         }
         const lptr<int> sl = sup_len(L), se = sup_ev(L), sd = sup_dlen(L), spre = sup_pre(L), ce = ch_ev(L),
                         lst = dlist(L);
@@ -1007,6 +1118,75 @@ struct Eng {
             const bool reached = __ballot(q < ns && carry + inc - slen >= need) != 0;
             carry += rdlane(inc, 63);
             if (reached) break;  // (the whole batch is complete)
+        }
+        wsync();
+        return carry;
+    }
+    // prefix2 on a team of W waves (wave w): the superchunks with later events go in rounds of kTeamSup per wave
+    // -- wave w lists the dirty chunks of its kTeamSup consecutive ones (in rank order) into its own part of the
+    // list and evaluates them -- and after each round every wave checks, from the same LDS words, whether the
+    // superchunks done so far reach `need` (the bounded scan's stop, as prefix2's).  Returns the view's total
+    // (partial when bounded) on every wave; wave 0 writes sup_pre.
+#ifndef MTR_TEAM_SUP
+#define MTR_TEAM_SUP 12
+#endif
+    static constexpr int kTeamSup = MTR_TEAM_SUP;
+    // the index of the r-th set bit of m (m has more than r)
+    static MTR_DI int nth_set(uint64_t m, int r) {
+        const int ln = lane_id();
+        const bool mine = ((m >> ln) & 1) && __popcll(m & lanes_below()) == r;
+        return first_lane(__ballot(mine));
+    }
+    static MTR_DI int prefix2_part(D& L, const View& v, int newlen, int minseq, int S, int need, int w, int W) {
+        const int nch = (S + 63) >> 6, ns = (nch + 63) >> 6, ln = lane_id();
+        const lptr<int> sl = sup_len(L), se = sup_ev(L), sd = sup_dlen(L), spre = sup_pre(L), ce = ch_ev(L);
+        const int lcap = kListCap / W;
+        const lptr<int> lst = dlist(L) + w * lcap;
+        int carry = 0;
+        for (int b = 0; b < ns; b += 64) {
+            const int q = b + ln, qc = min(q, ns - 1);
+            const int sl0 = sl[qc], se0 = se[qc];
+            const uint64_t dq0 = __ballot(q < ns && se0 > v.ref);
+            if (w == 0 && ((dq0 >> ln) & 1)) sd[q] = 0;
+            __syncthreads();  // (the zeros before any wave adds)
+            const int nd = __popcll(dq0);
+            for (int r0 = 0; r0 < nd; r0 += kTeamSup * W) {
+                int n = 0;
+                const int r1 = min(r0 + (w + 1) * kTeamSup, nd);
+                for (int r = r0 + w * kTeamSup; r < r1; r++) {
+                    const int c = (b + nth_set(dq0, r)) * 64 + ln;
+                    const bool dirty = c < nch && ce[min(c, nch - 1)] > v.ref;
+                    const uint64_t dm = __ballot(dirty);
+                    if (dirty) lst[n + __popcll(dm & lanes_below())] = c;
+                    n += __popcll(dm);
+                    if (n > lcap - 64 || r + 1 == r1) {
+                        wsync();
+                        // (a superchunk's chunks are this wave's alone: plain adds)
+                        if (n) dirty_part(L, v, newlen, minseq, S, n, 0, 1, lst, false);
+                        n = 0;
+                    }
+                }
+                __syncthreads();
+                const int rn = r0 + kTeamSup * W;
+                if (need != INT32_MAX && rn < nd) {
+                    // superchunks [b, b + lim) are complete: stop when one of them starts at or after need
+                    const int lim = nth_set(dq0, rn);
+                    const bool in = q < ns && ln < lim;
+                    const int slen = in ? sl0 + (((dq0 >> ln) & 1) ? sd[q] : 0) : 0;
+                    const int inc = wave_incl_scan(slen);
+                    if (__ballot(in && carry + inc - slen >= need)) {
+                        if (w == 0 && in) spre[q] = carry + inc;
+                        wsync();
+                        return carry + rdlane(inc, 63);
+                    }
+                }
+            }
+            const int slen = q < ns ? sl0 + (((dq0 >> ln) & 1) ? sd[q] : 0) : 0;
+            const int inc = wave_incl_scan(slen);
+            if (w == 0 && q < ns) spre[q] = carry + inc;
+            const bool reached = __ballot(q < ns && carry + inc - slen >= need) != 0;
+            carry += rdlane(inc, 63);
+            if (reached) break;
         }
         wsync();
         return carry;
@@ -1630,6 +1810,103 @@ struct Eng {
     // documents, whose upper blocks can span thousands of slots).  The block's end is the first bnd >= level
     // after x: none lies between its start and x.
     static MTR_DI void parent_block(const D& L, const St& s, int x, int level, int& ps, int& pe, int& cnt) {
+        const int W = team_n();
+        if (W > 1) {  // the team walks W * GK rounds per direction per step
+            const lptr<int> b = tbox(L);
+            if (lane_id() == 0) {
+                b[1] = x;
+                b[2] = level;
+                b[3] = s.nseg;
+            }
+            team_start(L, T_PARENT);
+            parent_part(L, x, level, s.nseg, 0, W, ps, pe, cnt);
+            __syncthreads();
+            return;
+        }
+        parent_walk(L, s, x, level, ps, pe, cnt);
+    }
+    // wave w of a team of W: step t covers slots x - (t W + w) 64 GK - [0, 64 GK) backwards and x + 1 + (t W + w)
+    // 64 GK + [0, 64 GK) forwards; each wave posts {stop slot or -1, children up to it} per direction, and every
+    // wave combines the posts in wave order (the nearest stop wins) -- the same answers parent_walk gives
+    static MTR_DI void parent_part(const D& L, int x, int level, int S, int w, int W, int& ps, int& pe, int& cnt) {
+        const int ln = lane_id();
+        const lptr<int> b = tbox(L);
+        int c = 0;
+        bool bdone = false, fdone = false;
+        ps = 0;
+        pe = S;
+        for (int t = 0; !bdone || !fdone; t++) {
+            const int bb = x - (t * W + w) * 64 * GK, fb = x + 1 + (t * W + w) * 64 * GK;
+            uint32_t mb[GK], mf[GK];
+#pragma unroll
+            for (int q = 0; q < GK; q++) {
+                mb[q] = L.meta[max(bb - 64 * q - ln, 0)];
+                mf[q] = L.meta[max(min(fb + 64 * q + ln, S - 1), 0)];
+            }
+            int bs = -1, bc = 0, fs = -1, fc = 0;
+            if (!bdone) {
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = bb - 64 * q - ln;
+                    const bool child = bnd_of(mb[q]) >= level - 1;
+                    const uint64_t stop = __ballot((i <= 0) | (bnd_of(mb[q]) >= level));
+                    if (stop) {
+                        const int k = first_lane(stop);
+                        bs = max(0, bb - 64 * q - k);
+                        bc += __popcll(__ballot(child) & ((uint64_t(2) << k) - 1));
+                        break;
+                    }
+                    bc += __popcll(__ballot(child));
+                }
+            }
+            if (!fdone) {
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const int i = fb + 64 * q + ln;
+                    const uint64_t stop = __ballot((i >= S) | (bnd_of(mf[q]) >= level));
+                    const uint64_t ch = __ballot((i < S) & (bnd_of(mf[q]) >= level - 1));
+                    if (stop) {
+                        const int k = first_lane(stop);
+                        fs = fb + 64 * q + k;
+                        fc += __popcll(ch & ((uint64_t(1) << k) - 1));
+                        break;
+                    }
+                    fc += __popcll(ch);
+                }
+            }
+            // (rows alternate by step parity: a wave posts step t + 1 while another may still read step t)
+            const lptr<int> row = b + 16 + 4 * W * (t & 1);
+            if (ln == 0) {
+                row[4 * w] = bs;
+                row[4 * w + 1] = bc;
+                row[4 * w + 2] = fs;
+                row[4 * w + 3] = fc;
+            }
+            __syncthreads();
+            for (int u = 0; u < W; u++) {
+                if (!bdone) {
+                    const int s0 = uni(row[4 * u]);
+                    c += uni(row[4 * u + 1]);
+                    if (s0 >= 0) {
+                        ps = s0;
+                        bdone = true;
+                    }
+                }
+            }
+            for (int u = 0; u < W; u++) {
+                if (!fdone) {
+                    const int s0 = uni(row[4 * u + 2]);
+                    c += uni(row[4 * u + 3]);
+                    if (s0 >= 0) {
+                        pe = s0;
+                        fdone = true;
+                    }
+                }
+            }
+        }
+        cnt = c;
+    }
+    static MTR_DI void parent_walk(const D& L, const St& s, int x, int level, int& ps, int& pe, int& cnt) {
         const int S = s.nseg, ln = lane_id();
         int c = 0;
         bool bdone = false, fdone = false;
@@ -3210,16 +3487,35 @@ struct Eng {
     // groups"): a vector's leaves keep their tracking id in the props field (NONE32: never tracked; a permutation
     // segment has no properties) and the document's property arena holds the group bits per id (propused = ids)
     static MTR_DI uint32_t tbits(const D& L, uint32_t tid) { return tid == NONE32 ? 0u : uniu(L.gprop()[tid]); }
-    // a fresh id holding `bits` (wave-uniform; NONE32 when the arena is full: s.status)
+    // a fresh id holding `bits` (wave-uniform; NONE32 when the arena is full: s.status): the id freed last, else a
+    // new one.  The free stack grows down from the arena's top and a new id reserves its slot there, so a free
+    // always fits (ids: propused <= pcap / 2).
     static MTR_DI uint32_t tid_new(const D& L, const KParams& P, St& s, uint32_t bits) {
-        if (uint32_t(s.propused) >= uint32_t(P.pcap)) {
+        const int nf = uni(L.ghdr()->tfree);
+        uint32_t t;
+        if (nf > 0) {
+            t = uniu(L.gprop()[uint32_t(P.pcap) - uint32_t(nf)]);
+            if (lane_id() == 0) L.ghdr()->tfree = nf - 1;
+        } else if (2 * (uint32_t(s.propused) + 1u) > uint32_t(P.pcap)) {
             s.status = MTR_ERR_CAPACITY;
             return NONE32;
+        } else {
+            t = uint32_t(s.propused++);
         }
-        const uint32_t t = uint32_t(s.propused++);
         if (lane_id() == 0) L.gprop()[t] = bits;
         wsync();
         return t;
+    }
+    // the id of a segment zamboni unlinked or merged away goes back on the free stack (no leaf names it any more,
+    // and the host's groups dropped it: an unlinked segment was in none, a merged one's report unlinked it)
+    static MTR_DI void tid_free(const D& L, const KParams& P, uint32_t t) {
+        const int nf = uni(L.ghdr()->tfree);
+        if (lane_id() == 0) {
+            L.gprop()[uint32_t(P.pcap) - 1u - uint32_t(nf)] = t;
+            L.gprop()[t] = 0u;
+            L.ghdr()->tfree = nf + 1;
+        }
+        wsync();
     }
     // TrackingGroup.link (mergeTreeTracking.ts:41-46) of leaf i into the groups `bits`, reported in link order
     static MTR_DI void track_link(D& L, const KParams& P, St& s, int i, uint32_t bits) {
@@ -3365,6 +3661,7 @@ struct Eng {
                         wsync();
                         const uint32_t tk = rdlane(vt, t);
                         if (PM && tk != uint32_t(MTR_HANDLE_UNALLOCATED)) free_handles(L, s, int(tk), rdlane(vl, t));
+                        if (PM && rdlane(vp, t) != NONE32) tid_free(L, P, rdlane(vp, t));
                     }
                     prev = -1;
                 } else if (rdlane(vs, t) <= minseq) {
@@ -3380,6 +3677,7 @@ struct Eng {
                         }
                         if (PM && DL && L.dcap > 0 && tbits(L, pk))  // the appended segment leaves its groups
                             put_record(L, s, s.cur_op, int(pk), int(pprops), MTR_DELTA_TMERGE);
+                        if (PM && pk != NONE32) tid_free(L, P, pk);
                         if (PM) {
                             L.len[prev] = plen + lk;
                             wsync();
@@ -3525,6 +3823,10 @@ struct Eng {
                 const int l = first_lane(um);
                 free_handles(L, s, int(rdlane(vt, l)), rdlane(vl, l));
             }
+            // the tracking ids of the unlinked and the merged-away segments, in leaf order (their bits were read
+            // into vb above)
+            for (uint64_t fm = __ballot((unlink | link) && vp != NONE32); fm; fm &= fm - 1)
+                tid_free(L, P, rdlane(vp, first_lane(fm)));
         }
         const int kept = __popcll(__ballot(in & !pre & !unlink & !link));
         if (lm) {  // concatenate each chain's text behind its head (prev.append, textSegment.ts:99-103)
@@ -4454,6 +4756,31 @@ struct Eng {
         }
     }
 
+    // the HBM-resident layout's pointers alone (the team's helper waves: they write nothing carve sets up)
+    static MTR_DI void carve_ptrs(D& L, char* smem, const KParams& P, uint32_t d) {
+        if constexpr (G) {
+            const gptr<uint32_t> g = gp(P.seg) + size_t(d) * NF * P.segcap;
+            L.len = (A<int>)(g + F_LEN * P.segcap);
+            L.seq = (A<int>)(g + F_SEQ * P.segcap);
+            L.rseq = (A<int>)(g + F_RSEQ * P.segcap);
+            L.meta = (A<uint32_t>)(g + F_META * P.segcap);
+            L.text = (A<uint32_t>)(g + F_TEXT * P.segcap);
+            L.props = (A<uint32_t>)(g + F_PROPS * P.segcap);
+            L.uid = (A<uint32_t>)(g + F_UID * P.segcap);
+            const gptr<uint32_t> sx = gp(P.scratch) + size_t(d) * 2 * P.segcap;
+            L.E = (A<int>)(sx);
+            const gptr<uint32_t> gh = gp(P.heap) + size_t(d) * 2 * P.hcap;
+            L.hseq = (A<int>)(gh);
+            L.huid = (A<uint32_t>)(gh + P.hcap);
+            L.cap = P.segcap;
+            L.lhcap = P.hcap;
+            L.sc = (lptr<Sc>)(smem);
+            L.gst = (lptr<mtr_synth_state>)(smem + ((sizeof(Sc) + 15) & ~size_t(15)));
+            L.sx = (lptr<int>)(smem + kScBytes + kTeamBytes);
+            L.rtmask = P.rtab - 1;
+            L.dcap = 0;
+        }
+    }
     static MTR_DI void carve(D& L, char* smem, const KParams& P, uint32_t d) {
         if (G) {  // every array lives in the document's HBM slab
             const gptr<uint32_t> g = gp(P.seg) + size_t(d) * NF * P.segcap;
@@ -4473,7 +4800,7 @@ struct Eng {
             L.lhcap = P.hcap;
             L.sc = (lptr<Sc>)(smem);
             L.gst = (lptr<mtr_synth_state>)(smem + ((sizeof(Sc) + 15) & ~size_t(15)));
-            L.sx = (lptr<int>)(smem + kScBytes);
+            L.sx = (lptr<int>)(smem + kScBytes + kTeamBytes);
             for (int q = lane_id(); q < 2 * sup_rows(L.cap); q += 64) L.sx[sup_rows(L.cap) + q] = 0;  // fills, marks
             if (lane_id() == 0) L.sc->sepoch = 0;
         } else {
@@ -5266,12 +5593,23 @@ struct Eng {
 #define MTR_WPE_X 1
 #endif
 template <bool G, int CAP = 0, bool DL = false, bool GN = false>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(G ? MTR_WPE_G : (CAP == 0 ? MTR_WPE_X : MTR_WPE))))
-apply_kernel(KParams P) {
+__global__ void __launch_bounds__(G ? NT * MTR_GW : NT)
+    __attribute__((amdgpu_waves_per_eu(G ? MTR_WPE_G : (CAP == 0 ? MTR_WPE_X : MTR_WPE)))) apply_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
-    Eng<G, false, CAP, DL, GN>::run(smem, P, d);
+    using E = Eng<G, false, CAP, DL, GN>;
+    if constexpr (G) {  // an HBM-resident document's team (launched with MTR_GW waves, or one)
+        const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));  // (wave-uniform)
+        if (w > 0) {
+            E::team_helper(smem, P, d, w);
+            return;
+        }
+        E::run(smem, P, d);
+        E::team_exit(smem);
+        return;
+    }
+    E::run(smem, P, d);
 }
 
 // leaf capacities with a compile-time LDS layout (apply_kernel<false, CAP>, instantiated in

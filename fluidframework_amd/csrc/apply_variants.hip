@@ -34,6 +34,15 @@ static void go2(void (*k)(Args...), bool& attr, uint32_t grid, size_t lds, hipSt
     hipLaunchKernelGGL(k, dim3(grid), dim3(2 * NT), lds, st, args...);  // two waves per workgroup
 }
 
+template <class... Args>
+static void go_team(void (*k)(Args...), bool& attr, uint32_t grid, size_t lds, hipStream_t st, Args... args) {
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(MTR_GW * NT), lds, st, args...);  // an HBM-resident document's team
+}
+
 // one variant, instantiated only in the part that owns it (V % kVariantParts)
 template <int V>
 static bool try_variant(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region) {
@@ -43,7 +52,7 @@ static bool try_variant(int v, uint32_t grid, size_t lds, hipStream_t st, const 
         if constexpr (V == AV_LDS_X) go(apply_kernel<false>, attr, grid, lds, st, P);
         if constexpr (V == AV_HBM_X) go(apply_kernel<true>, attr, grid, lds, st, P);
         if constexpr (V == AV_LDS_LEAN) go(apply_kernel<false, -1>, attr, grid, lds, st, P);
-        if constexpr (V == AV_HBM_LEAN) go(apply_kernel<true, -1>, attr, grid, lds, st, P);
+        if constexpr (V == AV_HBM_LEAN) go_team(apply_kernel<true, -1>, attr, grid, lds, st, P);
         if constexpr (V == AV_LDS_DL) go(apply_kernel<false, 0, true>, attr, grid, lds, st, P);
         if constexpr (V == AV_HBM_DL) go(apply_kernel<true, 0, true>, attr, grid, lds, st, P);
         if constexpr (V == AV_LDS_GN) go(apply_kernel<false, 0, false, true>, attr, grid, lds, st, P);

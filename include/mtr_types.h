@@ -211,8 +211,10 @@ enum {
 
 /* Tracking groups (SharedMatrix undo: VectorUndoProvider, matrix/src/undoprovider.ts:17-127, on the merge-tree's
  * TrackingGroup, mergeTreeTracking.ts).  A PermutationVector segment a group tracks carries a tracking id (tid,
- * numbered per vector from 0 as segments become tracked, each split-off half of a tracked segment a new one) and
- * the bit set of the groups that hold it (up to 32 groups live per vector; the host maps groups to bits).  A
+ * numbered per vector from 0 as segments become tracked, each split-off half of a tracked segment a new one; the id
+ * of a segment zamboni unlinks or merges away is reused, the one freed last first, so a vector holds at most
+ * prop_words / 2 ids at once) and the bit set of the groups that hold it (up to 32 groups live per vector; the host
+ * maps groups to bits).  A
  * segment with a non-empty set is never unlinked by zamboni and merges only with a segment of the same set
  * (zamboni.ts:132, 156).  Records:
  *  - MTR_OP_LOCAL_INSERT / MTR_OP_LOCAL_REMOVE of a matrix vector with payload != 0: the op's delta segments (the

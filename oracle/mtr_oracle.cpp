@@ -285,6 +285,7 @@ class Tree {
     // tracking groups (SharedMatrix undo: matrix/src/undoprovider.ts) by bit, and the next tracking id
     TGroup tgroup[MTR_TRACK_GROUPS];
     int ntid = 0;
+    std::vector<int> freeTids;  // tracking ids of segments zamboni unlinked or merged away (the engine's free stack)
 
     Block* makeBlock() {
         blockPool.emplace_back();
@@ -477,7 +478,7 @@ class Tree {
         r->localRemovedSeq = s->localRemovedSeq;
         if (s->localRefs) refsSplit(s->localRefs, pos, r);  // mergeTreeNodes.ts:501-503
         if (!s->tgroups.empty()) {  // trackingCollection.copyTo (mergeTreeNodes.ts:500; mergeTreeTracking.ts:86-92)
-            r->tid = ntid++;
+            r->tid = newTid();
             for (TGroup* g : s->tgroups) tlink(g, r);
             if (recycleLog) deltas.push_back({curOpIndex, s->tid, r->tid, MTR_DELTA_TSPLIT});
         }
@@ -519,8 +520,16 @@ class Tree {
         return b;
     }
     // VectorUndoProvider.record (undoprovider.ts:30-85): an op's delta segment joins the groups of `bits`
+    // tracking ids are an engine artifact the reports and leaf lists carry (include/mtr_types.h "Tracking groups"):
+    // the one freed last is reused first, as the engine's free stack does (Eng::tid_new / tid_free)
+    int newTid() {
+        if (freeTids.empty()) return ntid++;
+        const int t = freeTids.back();
+        freeTids.pop_back();
+        return t;
+    }
     void trackLink(Seg* s, uint32_t bits) {
-        if (s->tid < 0) s->tid = ntid++;
+        if (s->tid < 0) s->tid = newTid();
         for (int b = 0; b < MTR_TRACK_GROUPS; b++)
             if (bits >> b & 1u) tlink(&tgroup[b], s);
         if (recycleLog) deltas.push_back({curOpIndex, s->tid, s->len, MTR_DELTA_TLINK});
@@ -1381,6 +1390,7 @@ class Tree {
                                 deltas.push_back({curOpIndex, s->start, s->len, MTR_DELTA_RECYCLE});
                             for (int h = 0; h < s->len; h++) freeHandle(s->start + h);
                         }
+                        if (s->tid >= 0) freeTids.push_back(s->tid);
                         s->parent = nullptr;
                     }
                     prev = nullptr;
@@ -1395,6 +1405,7 @@ class Tree {
                                 const std::vector<TGroup*> gs = s->tgroups;
                                 for (TGroup* g : gs) tunlink(g, s);
                             }
+                            if (s->tid >= 0) freeTids.push_back(s->tid);
                             refsAppend(prev, s);    // BaseSegment.append, mergeTreeNodes.ts:527-530 (before lengths)
                             prev->text += s->text;  // TextSegment.append textSegment.ts:99-103 (BaseSegment.append for perm)
                             prev->len += s->len;

@@ -37,7 +37,7 @@ class USession:
     """Clients of one matrix; `process_all` is MockContainerRuntimeFactory.processAllMessages (every submitted
     message sequenced in order and delivered to every client, its author's being the ACK)."""
 
-    def __init__(self, names, attached=True, engine=False):
+    def __init__(self, names, attached=True, engine=False, prop_words=1024):
         self.it = Interner()
         self.queue = []
         self.seq = 0
@@ -47,7 +47,7 @@ class USession:
             from fluidframework_amd.engine import Engine
 
             self.eng = Engine(2 * len(names), max_segments=4096, heap_entries=4096, text_units=1 << 14,
-                              prop_words=1024, remover_cells=4096, ops_per_launch=64)
+                              prop_words=prop_words, remover_cells=4096, ops_per_launch=64)
             for k in range(len(names)):
                 self.eng.set_matrix(2 * k, 2 * k + 1)
         self.batches = 0
@@ -369,11 +369,11 @@ def test_connected_two_clients(name):
 
 
 # ---------------------------------------------------------------- a farm
-def farm(seed, engine=False, rounds=12, per_round=5):
+def farm(seed, engine=False, rounds=12, per_round=5, prop_words=1024):
     """Two clients edit, undo and redo at random; every round's messages are sequenced and delivered; the clients
     converge after every round."""
     rng = random.Random(seed)
-    s = USession(["w1", "w2"], attached=True, engine=engine)
+    s = USession(["w1", "w2"], attached=True, engine=engine, prop_words=prop_words)
     t = Case(s, True)
     s.clients[0].m.insert_rows(0, 3)
     s.clients[0].m.insert_cols(0, 3)
@@ -433,3 +433,42 @@ def test_connected_two_clients_engine():
 @pytest.mark.parametrize("seed", range(4))
 def test_undo_farm_engine(seed):
     farm(seed, engine=True)
+
+
+# ---------------------------------------------------------------- tracking ids are reclaimed
+def _tid_watch(monkeypatch):
+    """per flush: the largest tracking id a leaf holds, and ids that left every leaf and came back (reused)"""
+    st = {"max": 0, "reuse": 0}
+    hist = {}
+    orig = USession.flush
+
+    def flush(self):
+        orig(self)
+        for c in self.clients:
+            for w in (0, 1):
+                tids = {int(x[3]) for x in c.doc.select(w).leaves() if int(x[3]) >= 0}
+                cur, gone = hist.get((c.k, w), (set(), set()))
+                st["reuse"] += len(tids & gone)
+                hist[(c.k, w)] = (tids, (gone | (cur - tids)) - tids)
+                if tids:
+                    st["max"] = max(st["max"], max(tids))
+
+    monkeypatch.setattr(USession, "flush", flush)
+    return st
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_tracking_ids_are_reused(seed, monkeypatch):
+    """A segment zamboni unlinks or merges away gives its tracking id back (the engine's free stack, mirrored by
+    the oracle): a long farm of edits, undos and redos keeps its ids within a few dozen while it hands out ~80-90."""
+    st = _tid_watch(monkeypatch)
+    farm(seed, rounds=60)
+    assert st["reuse"] > 20 and st["max"] < 36, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1])
+def test_undo_churn_in_a_small_arena(seed):
+    """The same long farms on the engine with a 72-word property arena (35 tracking ids): ids handed out beyond it
+    come from the free stack -- records, leaf lists and group lists equal the oracle's after every batch."""
+    farm(seed, engine=True, rounds=60, prop_words=72)
