@@ -263,6 +263,8 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
        P_NSUP, P_NDCH,  // counts: superchunks with events after refSeq, their chunks with such events
        P_HELPER,        // the team's helper waves: cycles in the passes handed to them
        P_SINK,          // (a slot nothing reads)
+       P_OVB, P_OVPB, P_NOVFB, P_NOVL,  // overflow_fix: the leaf block's bounds and count, the parent walks; counts:
+                                        // bounds outside the one-ballot window, loop rounds
        P_COUNT };
 
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
@@ -883,7 +885,7 @@ struct Eng {
     // ---- the team: an HBM-resident document's workgroup of MTR_GW waves.  Wave 0 runs the document; a pass it
     // hands out is posted in the mailbox (task word + arguments), and the waves meet at the workgroup barrier
     // twice: once to start (the helpers wait there between passes) and once when every wave's share is done.
-    enum { T_EXIT = 1, T_DIRTY = 2, T_PARENT = 3, T_PREFIX = 4 };
+    enum { T_EXIT = 1, T_DIRTY = 2, T_PARENT = 3, T_PREFIX = 4, T_PACK = 5 };
     static_assert(16 + 2 * 4 * MTR_GW <= kTeamInts, "the team's mailbox holds two rows of results per wave");
     static MTR_DI int team_n() {
         if constexpr (G) return int(blockDim.x) >> 6;
@@ -905,7 +907,7 @@ struct Eng {
                 __syncthreads();
                 const lptr<int> b = tbox(L);
                 const int t = uni(b[0]);
-                if (t != T_DIRTY && t != T_PREFIX && t != T_PARENT) break;  // T_EXIT
+                if (t != T_DIRTY && t != T_PREFIX && t != T_PARENT && t != T_PACK) break;  // T_EXIT
                 {
 #ifdef MTR_PROF
                     ProfScope _prof_helper(L.sc, P_HELPER);  // (the pass, not the wait at its end)
@@ -918,9 +920,11 @@ struct Eng {
                         dirty_part(L, v, uni(b[5]), uni(b[6]), uni(b[7]), uni(b[1]), w, W, dlist(L), true);
                     } else if (t == T_PREFIX) {
                         (void)prefix2_part(L, v, uni(b[5]), uni(b[6]), uni(b[7]), uni(b[1]), w, W);
-                    } else {
+                    } else if (t == T_PARENT) {
                         int ps, pe, cnt;
-                        parent_part(L, uni(b[1]), uni(b[2]), uni(b[3]), w, W, ps, pe, cnt);
+                        parent_part(L, uni(b[1]), uni(b[8]), uni(b[2]), uni(b[3]), w, W, ps, pe, cnt);
+                    } else {
+                        (void)pack_part(L, uni(b[1]), uni(b[2]), uni(b[3]), uni(b[4]), w, W);
                     }
                 }
                 __syncthreads();
@@ -1153,18 +1157,31 @@ struct Eng {
             for (int r0 = 0; r0 < nd; r0 += kTeamSup * W) {
                 int n = 0;
                 const int r1 = min(r0 + (w + 1) * kTeamSup, nd);
-                for (int r = r0 + w * kTeamSup; r < r1; r++) {
-                    const int c = (b + nth_set(dq0, r)) * 64 + ln;
-                    const bool dirty = c < nch && ce[min(c, nch - 1)] > v.ref;
-                    const uint64_t dm = __ballot(dirty);
-                    if (dirty) lst[n + __popcll(dm & lanes_below())] = c;
-                    n += __popcll(dm);
-                    if (n > lcap - 64 || r + 1 == r1) {
-                        wsync();
-                        // (a superchunk's chunks are this wave's alone: plain adds)
-                        if (n) dirty_part(L, v, newlen, minseq, S, n, 0, 1, lst, false);
-                        n = 0;
+                for (int r = r0 + w * kTeamSup; r < r1; r += 4) {  // four superchunks' newest events per LDS round
+                    int cq[4], eq[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        cq[k] = (b + nth_set(dq0, min(r + k, r1 - 1))) * 64 + ln;
+                        eq[k] = ce[min(cq[k], nch - 1)];
                     }
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        if (r + k >= r1) break;
+                        const bool dirty = cq[k] < nch && eq[k] > v.ref;
+                        const uint64_t dm = __ballot(dirty);
+                        if (dirty) lst[n + __popcll(dm & lanes_below())] = cq[k];
+                        n += __popcll(dm);
+                        if (n > lcap - 64) {
+                            wsync();
+                            // (a superchunk's chunks are this wave's alone: plain adds)
+                            dirty_part(L, v, newlen, minseq, S, n, 0, 1, lst, false);
+                            n = 0;
+                        }
+                    }
+                }
+                if (n) {
+                    wsync();
+                    dirty_part(L, v, newlen, minseq, S, n, 0, 1, lst, false);
                 }
                 __syncthreads();
                 const int rn = r0 + kTeamSup * W;
@@ -1810,25 +1827,31 @@ struct Eng {
     // documents, whose upper blocks can span thousands of slots).  The block's end is the first bnd >= level
     // after x: none lies between its start and x.
     static MTR_DI void parent_block(const D& L, const St& s, int x, int level, int& ps, int& pe, int& cnt) {
-        const int W = team_n();
-        if (W > 1) {  // the team walks W * GK rounds per direction per step
-            const lptr<int> b = tbox(L);
-            if (lane_id() == 0) {
-                b[1] = x;
-                b[2] = level;
-                b[3] = s.nseg;
-            }
-            team_start(L, T_PARENT);
-            parent_part(L, x, level, s.nseg, 0, W, ps, pe, cnt);
-            __syncthreads();
+        if (team_n() > 1) {  // the team walks W * GK rounds per direction per step
+            team_bounds(L, s, x, x + 1, level, ps, pe, cnt);
             return;
         }
         parent_walk(L, s, x, level, ps, pe, cnt);
     }
+    // the team's walk: the last slot <= xb and the first slot >= xf with bnd >= level (ps, pe), and the slots
+    // with bnd >= level - 1 in [ps, pe) -- xf > xb, no such slot in (xb, xf) -- counted in cnt
+    static MTR_DI void team_bounds(const D& L, const St& s, int xb, int xf, int level, int& ps, int& pe, int& cnt) {
+        const lptr<int> b = tbox(L);
+        if (lane_id() == 0) {
+            b[1] = xb;
+            b[2] = level;
+            b[3] = s.nseg;
+            b[8] = xf;
+        }
+        team_start(L, T_PARENT);
+        parent_part(L, xb, xf, level, s.nseg, 0, team_n(), ps, pe, cnt);
+        __syncthreads();
+    }
     // wave w of a team of W: step t covers slots x - (t W + w) 64 GK - [0, 64 GK) backwards and x + 1 + (t W + w)
     // 64 GK + [0, 64 GK) forwards; each wave posts {stop slot or -1, children up to it} per direction, and every
     // wave combines the posts in wave order (the nearest stop wins) -- the same answers parent_walk gives
-    static MTR_DI void parent_part(const D& L, int x, int level, int S, int w, int W, int& ps, int& pe, int& cnt) {
+    static MTR_DI void parent_part(const D& L, int x, int xf0, int level, int S, int w, int W, int& ps, int& pe,
+                                   int& cnt) {
         const int ln = lane_id();
         const lptr<int> b = tbox(L);
         int c = 0;
@@ -1836,7 +1859,7 @@ struct Eng {
         ps = 0;
         pe = S;
         for (int t = 0; !bdone || !fdone; t++) {
-            const int bb = x - (t * W + w) * 64 * GK, fb = x + 1 + (t * W + w) * 64 * GK;
+            const int bb = x - (t * W + w) * 64 * GK, fb = xf0 + (t * W + w) * 64 * GK;
             uint32_t mb[GK], mf[GK];
 #pragma unroll
             for (int q = 0; q < GK; q++) {
@@ -1977,6 +2000,22 @@ struct Eng {
     }
     // index of the n-th (0-based) leaf in [bs, be) with bnd >= minb, -1 if none
     static MTR_DI int nth_bnd(const D& L, int bs, int be, int minb, int n) {
+        if constexpr (G) {  // HBM: GK rounds of loads in flight per step
+            for (int base = bs; base < be; base += 64 * GK) {
+                uint32_t mq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) mq[q] = L.meta[min(base + 64 * q + lane_id(), be - 1)];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const bool t = (base + 64 * q + lane_id() < be) & (bnd_of(mq[q]) >= minb);
+                    const uint64_t m = __ballot(t);
+                    const int pc = __popcll(m);
+                    if (n < pc) return base + 64 * q + first_lane(__ballot(t && __popcll(m & lanes_below()) == n));
+                    n -= pc;
+                }
+            }
+            return -1;
+        }
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
             const uint32_t mi = L.meta[min(i, be - 1)];
@@ -2009,6 +2048,22 @@ struct Eng {
         return c;
     }
     static MTR_DI int nth_live(const D& L, int bs, int be, int n) {
+        if constexpr (G) {  // HBM: GK rounds of loads in flight per step
+            for (int base = bs; base < be; base += 64 * GK) {
+                uint32_t mq[GK];
+#pragma unroll
+                for (int q = 0; q < GK; q++) mq[q] = L.meta[min(base + 64 * q + lane_id(), be - 1)];
+#pragma unroll
+                for (int q = 0; q < GK; q++) {
+                    const bool t = (base + 64 * q + lane_id() < be) & !(mq[q] & M_DEL);
+                    const uint64_t m = __ballot(t);
+                    const int pc = __popcll(m);
+                    if (n < pc) return base + 64 * q + first_lane(__ballot(t && __popcll(m & lanes_below()) == n));
+                    n -= pc;
+                }
+            }
+            return -1;
+        }
         for (int base = bs; base < be; base += 64) {
             const int i = base + lane_id();
             const bool t = (i < be) & !(L.meta[min(i, be - 1)] & M_DEL);
@@ -2048,11 +2103,20 @@ struct Eng {
         PROF(P_OVERFLOW);
         int level = 1;
         int bs = hbs, be = hbe, cnt = -1;
-        if (bs < 0) block_bounds1_live(L, s, x, bs, be, cnt);
-        if (!(G && s.holes)) cnt = be - bs;
-        else if (cnt < 0) cnt = count_live(L, bs, be);  // (holes are no children)
+        {
+#ifdef MTR_PROF
+            ProfScope _prof_ovb(L.sc, P_OVB);
+#endif
+            if (bs < 0) block_bounds1_live(L, s, x, bs, be, cnt);
+            if (!(G && s.holes)) cnt = be - bs;
+            else if (cnt < 0) cnt = count_live(L, bs, be);  // (holes are no children)
+#ifdef MTR_PROF
+            if (cnt < 0 || hbs < 0) PROF_COUNT(P_NOVFB);
+#endif
+        }
         int xbs = bs;
         while (cnt >= kMaxNodesInBlock) {
+            PROF_COUNT(P_NOVL);
             int c5 = bs + kMaxNodesInBlock / 2;
             if (G && s.holes && level == 1) c5 = nth_live(L, bs, be, kMaxNodesInBlock / 2);
             if (level == 1 && x >= c5) xbs = c5;
@@ -2070,6 +2134,9 @@ struct Eng {
             level++;
             if constexpr (G) {
                 int nbs, nbe;
+#ifdef MTR_PROF
+                ProfScope _prof_ovpb(L.sc, P_OVPB);
+#endif
                 parent_block(L, s, bs, level, nbs, nbe, cnt);
                 bs = nbs;
                 be = nbe;
@@ -3408,21 +3475,30 @@ struct Eng {
         const int half = P.tcap / 2;
         const int dst0 = s.texthalf ? 0 : half;
         int carry = 0;
-        for (int base = 0; base < S; base += 64) {
-            const int i = base + lane_id();
-            int n = 0;
-            uint32_t src = 0;
-            if (i < S && !(L.meta[i] & M_MARKER)) {
-                n = L.len[i];
-                src = L.text[i];
+        constexpr int ZK = G ? GK : 1;  // (HBM: GK rounds of leaf fields in flight)
+        for (int base = 0; base < S; base += 64 * ZK) {
+            uint32_t mq[ZK], tq[ZK];
+            int lq[ZK];
+#pragma unroll
+            for (int q = 0; q < ZK; q++) {
+                const int ic = min(base + 64 * q + lane_id(), S - 1);
+                mq[q] = L.meta[ic];
+                lq[q] = L.len[ic];
+                tq[q] = L.text[ic];
             }
-            const int inc = wave_incl_scan(n);
-            const int off = dst0 + carry + inc - n;
-            if (i < S && !(L.meta[i] & M_MARKER)) {
-                copy_units(L, uint32_t(off), src, n);
-                L.text[i] = uint32_t(off);
+#pragma unroll
+            for (int q = 0; q < ZK; q++) {
+                const int i = base + 64 * q + lane_id();
+                const bool t = i < S && !(mq[q] & M_MARKER);
+                const int n = t ? lq[q] : 0;
+                const int inc = wave_incl_scan(n);
+                const int off = dst0 + carry + inc - n;
+                if (t) {
+                    copy_units(L, uint32_t(off), tq[q], n);
+                    L.text[i] = uint32_t(off);
+                }
+                carry += rdlane(inc, 63);
             }
-            carry += rdlane(inc, 63);
         }
         wsync();
         s.texthalf ^= 1;
@@ -3901,6 +3977,72 @@ struct Eng {
         return kept;
     }
 
+    // packParent's rebalancing of the level-l block [ps, pe) on an HBM-resident document (wave w of W): the
+    // wave lists the items of its part of the range (surviving leaves at l == 2, else surviving level-(l-2) block
+    // starts; at most 64), the waves post their counts, and each wave gives its items their new bnd marks -- the
+    // first `rem` of the c blocks get base + 1 items, item 0 keeps `top`.  Returns c, or -1 (nothing written)
+    // when a part holds more than 64 items: the caller's two passes take over.
+    static MTR_DI int pack_part(const D& L, int ps, int pe, int l, int top, int w, int W) {
+        const int ln = lane_id();
+        const int part = ((pe - ps + W - 1) / W + 63) & ~63;
+        const int lo = min(pe, ps + w * part), hi = min(pe, lo + part);
+        // the list: prefix2's chunk list (HBM-resident documents), else the scan array E, which is dead between
+        // the op's work and the next op's view scan
+        lptr<int> lst;
+        if constexpr (G) lst = dlist(L) + 64 * w;
+        else lst = L.E;
+        constexpr int ZK = G ? GK : 1;
+        int n = 0;
+        for (int wb = lo; wb < hi; wb += 64 * ZK) {
+            uint32_t mq[ZK];
+#pragma unroll
+            for (int q = 0; q < ZK; q++) mq[q] = L.meta[min(wb + 64 * q + ln, hi - 1)];
+#pragma unroll
+            for (int q = 0; q < ZK; q++) {
+                const int i = wb + 64 * q + ln;
+                const bool it = i < hi && !(mq[q] & M_DEL) && (l == 2 || bnd_of(mq[q]) >= l - 2);
+                const uint64_t mask = __ballot(it);
+                const int k = n + __popcll(mask & lanes_below());
+                if (it && k < 64) lst[k] = i;
+                n += __popcll(mask);
+            }
+        }
+        int T = n, off = 0;
+        if (W > 1) {
+            const lptr<int> row = tbox(L) + 16;
+            if (ln == 0) row[w] = n;
+            __syncthreads();
+            T = 0;
+            for (int u = 0; u < W; u++) {
+                const int nu = uni(row[u]);
+                if (u < w) off += nu;
+                T += nu;
+                if (nu > 64) T = -(1 << 20);
+            }
+        } else if (n > 64) {
+            T = -1;
+        }
+        if (T < 0) return -1;
+        if (T == 0) return 0;
+        const int c = max(1, min(kMaxNodesInBlock - 1, T / (kMaxNodesInBlock / 2)));
+        const int base = T / c;
+        const int rem = T % c;
+        const int big = rem * (base + 1);
+        wsync();
+        if (ln < n) {
+            const int i = lst[ln];
+            uint32_t m = L.meta[i];
+            const int item = off + ln;
+            const bool isStart = item < big ? item % (base + 1) == 0 : (item - big) % base == 0;
+            const int nb = item == 0 ? top : (isStart ? l - 1 : (l == 2 ? 0 : l - 2));
+            m = set_bnd(m, nb);
+            if (l == 2 && isStart) m = set_ns(m, NS_UNDEF);
+            L.meta[i] = m;
+        }
+        wsync();
+        return c;
+    }
+
     // zamboniSegments body for one popped LRU entry whose segment is leaf x
     // (zamboni.ts:33-58 + packParent zamboni.ts:63-120).  Returns the first leaf index at or
     // after which leaves may be marked for deletion (the caller compacts from there), or -1.
@@ -3947,8 +4089,13 @@ struct Eng {
                 int ps, pe;
                 {
                     PROF(P_FETCH);
-                    ps = block_start(L, cs, l);
-                    pe = block_end(L, s, ce - 1, l);
+                    if (G && team_n() > 1) {
+                        int cnt;
+                        team_bounds(L, s, cs, ce, l, ps, pe, cnt);
+                    } else {
+                        ps = block_start(L, cs, l);
+                        pe = block_end(L, s, ce - 1, l);
+                    }
                 }
                 const int top = bnd_of(uniu(L.meta[ps]));
                 cs = ps;
@@ -3964,6 +4111,27 @@ struct Eng {
                         scour_range(L, P, s, ps, pe);
                 }
                 // items: surviving leaves (l == 2) or surviving level-(l-2) block starts
+                {  // one pass lists them (at most 64 per wave), one round rebalances
+                    int c = -1;
+                    if (G && team_n() > 1) {
+                        const lptr<int> b = tbox(L);
+                        if (lane_id() == 0) {
+                            b[1] = ps;
+                            b[2] = pe;
+                            b[3] = l;
+                            b[4] = top;
+                        }
+                        team_start(L, T_PACK);
+                        c = pack_part(L, ps, pe, l, top, 0, team_n());
+                        __syncthreads();
+                    } else {
+                        c = pack_part(L, ps, pe, l, top, 0, 1);
+                    }
+                    if (c >= 0) {
+                        if (!(c < kMaxNodesInBlock / 2 && l < H)) break;
+                        continue;
+                    }
+                }
                 constexpr int ZK = G ? GK : 1;  // (HBM: GK rounds of loads in flight)
                 int T = 0;
                 uint32_t m1r = M_DEL;  // a one-round range keeps its meta words in registers
@@ -5650,16 +5818,20 @@ enum ApplyVariant {
     AV_PAIR_LDS, AV_PAIR_HBM, AV_PAIR_LDS_DL, AV_PAIR_HBM_DL, AV_PAIR_LDS_GN, AV_PAIR_HBM_GN, AV_PAIR2_LDS,
     AV_PAIR2_HBM, AV_COUNT
 };
-constexpr int kVariantParts = 5;
+constexpr int kVariantParts = 8;  // (two variants per part at most: the HBM-resident ones take minutes each)
 bool launch_variant_p0(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p1(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p2(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p3(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p4(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p5(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p6(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p7(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 inline bool launch_variant(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region = 0) {
     return launch_variant_p0(v, grid, lds, st, P, region) || launch_variant_p1(v, grid, lds, st, P, region) ||
            launch_variant_p2(v, grid, lds, st, P, region) || launch_variant_p3(v, grid, lds, st, P, region) ||
-           launch_variant_p4(v, grid, lds, st, P, region);
+           launch_variant_p4(v, grid, lds, st, P, region) || launch_variant_p5(v, grid, lds, st, P, region) ||
+           launch_variant_p6(v, grid, lds, st, P, region) || launch_variant_p7(v, grid, lds, st, P, region);
 }
 
 }  // namespace mtr
