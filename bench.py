@@ -439,6 +439,12 @@ def main(argv=None):
             per_gpu = value / max(1, world)  # (the counters are one GPU's)
             issue["salu_roofline"] = {"achieved": round(salu * per_gpu / 1e9, 1), "peak": SALU_PEAK / 1e9,
                                       "unit": "G SALU instr/s per GPU", "frac": round(salu * per_gpu / SALU_PEAK, 4)}
+            clk = pmc.get("clock_ghz_measured")
+            if clk:  # the same roofline at the clock the kernels ran at (GRBM_GUI_ACTIVE / 8 / duration)
+                pk = SALU_PEAK / 2.4 * clk
+                issue["salu_roofline"].update({"clock_ghz_nominal": 2.4, "clock_ghz_measured": round(clk, 3),
+                                               "peak_measured_clock": round(pk / 1e9, 1),
+                                               "frac_measured_clock": round(salu * per_gpu / pk, 4)})
     roofline = {
         "bound": "hbm",  # (the contract's vocabulary: the path's roofline is HBM; no MFMA -- what binds is in
         # `binding` and issue.salu_roofline)

@@ -19,7 +19,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ENGINE_SRC = ["mtr_engine.hip"]
 ENGINE_DEPS = ["apply.hip.h", "summary.hip.h", "mtr_engine.hip", "apply_caps.hip", "apply_variants.hip"]
 CAP_PARTS = 3  # kCapParts in apply.hip.h
-VARIANT_PARTS = 8  # kVariantParts in apply.hip.h
+VARIANT_PARTS = 16  # kVariantParts in apply.hip.h
 
 
 def _stale(target, deps):
@@ -102,8 +102,14 @@ def build_engine(force=False, verbose=False, prof=False, variant=None, extra=())
         # objects as they are -- for an edit whose effect is confined to those units' kernels)
         only = [x for x in os.environ.get("MTR_ONLY", "").split(",") if x]
         for src, obj, extra in units:
-            if only and os.path.exists(obj) and not any(x in os.path.basename(obj) for x in only):
-                continue
+            if only and not any(x in os.path.basename(obj) for x in only):
+                main_obj = os.path.join(HERE, "build", os.path.basename(obj))
+                if not os.path.exists(obj) and os.path.exists(main_obj):  # (a variant: the main build's object)
+                    import shutil
+
+                    shutil.copy(main_obj, obj)
+                if os.path.exists(obj):
+                    continue
             if same_flags and not force and not _stale(obj, [src] + hdrs):
                 continue  # (per translation unit: an edit of one .hip recompiles that unit only)
             if reuse and "apply_variants" in obj:  # (a C3 experiment: the runtime-layout kernels from the main build)

@@ -265,6 +265,9 @@ enum { P_OP = 0, P_PREFIX, P_SPLIT, P_SHIFT, P_INSERT, P_RANGE, P_ZAMBONI, P_ZBL
        P_SINK,          // (a slot nothing reads)
        P_OVB, P_OVPB, P_NOVFB, P_NOVL,  // overflow_fix: the leaf block's bounds and count, the parent walks; counts:
                                         // bounds outside the one-ballot window, loop rounds
+       P_SUPREF, P_PXLIST, P_PXEVAL, P_PXSYNC, P_NPXR,  // prefix2 (wave 0): stale superchunk figures, listing,
+                                                        // evaluation, barrier waits; count: team rounds
+       P_NWALK, P_NDRND, P_WALK,  // counts: remover-list walks (vis_leaf), dirty-chunk rounds; cycles in the walks
        P_COUNT };
 
 // Per-document pointers the op loop needs only now and then (text / property / remover arenas, delta
@@ -619,7 +622,13 @@ struct Eng {
         const int walk = (valid ? -1 : 0) & rem & ~first & vp_bit(m, 21) & after &
                          (newlen ? vp_lt(minseq, rseq) : vis);
         int inr = first;
-        if (__ballot(walk != 0)) inr |= -later_remover(L, i, walk != 0, v.client);
+        if (__ballot(walk != 0)) {
+#ifdef MTR_PROF
+            PROF_COUNT(P_NWALK);
+            ProfScope _prof_walk(L.sc, P_WALK);
+#endif
+            inr |= -later_remover(L, i, walk != 0, v.client);
+        }
         if (newlen) {  // mergeTree.ts:935-965
             const int live = vis & len;
             const int gone = live & ~(~after | inr);
@@ -969,6 +978,9 @@ struct Eng {
         const int ln = lane_id();
         const lptr<int> cx = ch_x(L), sd = sup_dlen(L);
         for (int e0 = 64 * w; e0 < n; e0 += 64 * W) {  // one lane per chunk: its whole record in one round of loads
+#ifdef MTR_PROF
+            if ((threadIdx.x >> 6) == 0) PROF_COUNT(P_NDRND);
+#endif
             const int e = e0 + ln;
             const int c = lst[min(e, n - 1)];
             const gptr<int> r = cs_rec(L, c);
@@ -1046,7 +1058,12 @@ struct Eng {
     // superchunks are not evaluated, sup_pre is valid up to there and the returned length is partial.
     static MTR_DI int prefix2(D& L, const St& s, const View& v, int newlen, int need = INT32_MAX) {
         PROF(P_PREFIX);
-        sup_refresh(L, s);
+        {
+#ifdef MTR_PROF
+            ProfScope _prof_sr(L.sc, P_SUPREF);
+#endif
+            sup_refresh(L, s);
+        }
         const int nch = (s.nseg + 63) >> 6, ns = (nch + 63) >> 6, ln = lane_id();
         const int ep = uni(L.sc->sepoch) + 1;
         if (ln == 0) {
@@ -1157,6 +1174,11 @@ struct Eng {
             for (int r0 = 0; r0 < nd; r0 += kTeamSup * W) {
                 int n = 0;
                 const int r1 = min(r0 + (w + 1) * kTeamSup, nd);
+#ifdef MTR_PROF
+                const bool lead = w == 0 && (threadIdx.x >> 6) == 0;
+                const long long _t_l = clock64();
+                if (lead) PROF_COUNT(P_NPXR);
+#endif
                 for (int r = r0 + w * kTeamSup; r < r1; r += 4) {  // four superchunks' newest events per LDS round
                     int cq[4], eq[4];
 #pragma unroll
@@ -1174,6 +1196,9 @@ struct Eng {
                         if (n > lcap - 64) {
                             wsync();
                             // (a superchunk's chunks are this wave's alone: plain adds)
+#ifdef MTR_PROF
+                            ProfScope _prof_ev(L.sc, lead ? P_PXEVAL : P_SINK);
+#endif
                             dirty_part(L, v, newlen, minseq, S, n, 0, 1, lst, false);
                             n = 0;
                         }
@@ -1181,9 +1206,19 @@ struct Eng {
                 }
                 if (n) {
                     wsync();
+#ifdef MTR_PROF
+                    ProfScope _prof_ev(L.sc, lead ? P_PXEVAL : P_SINK);
+#endif
                     dirty_part(L, v, newlen, minseq, S, n, 0, 1, lst, false);
                 }
+#ifdef MTR_PROF
+                if (lead) PROF_ADD(P_PXLIST, _t_l);  // (listing + evaluation; P_PXEVAL the latter)
+                const long long _t_s = clock64();
+#endif
                 __syncthreads();
+#ifdef MTR_PROF
+                if (lead) PROF_ADD(P_PXSYNC, _t_s);
+#endif
                 const int rn = r0 + kTeamSup * W;
                 if (need != INT32_MAX && rn < nd) {
                     // superchunks [b, b + lim) are complete: stop when one of them starts at or after need
@@ -4377,6 +4412,17 @@ struct Eng {
                     const bool bw = inw & (bnd_of(mw) >= 1);
                     const uint64_t sm = __ballot((w <= 0) | bw) & LO32;
                     const uint64_t em = __ballot((w >= S) | bw) & HI32;
+#ifdef MTR_DEBUG_INSERT  // (spill experiment: bw against a fresh load of the same meta words)
+                    {
+                        const uint32_t mw2 = __atomic_load_n((uint32_t*)&L.meta[wc], __ATOMIC_RELAXED);
+                        const uint64_t b1 = __ballot(bw), b2 = __ballot(inw & (bnd_of(mw2) >= 1));
+                        const uint64_t dm = __ballot(mw != mw2);
+                        if (b1 != b2 && lane_id() == 0)
+                            printf("MISMATCH op_begin %llu i %d ballot(bw) %llx fresh %llx meta-differs %llx\n",
+                                   (unsigned long long)dd.op_begin, i, (unsigned long long)b1, (unsigned long long)b2,
+                                   (unsigned long long)dm);
+                    }
+#endif
                     if (sm && em) {
                         const int bs = max(0, i - 31 + last_lane(sm));
                         const int be = i - 31 + first_lane(em);
@@ -5818,7 +5864,7 @@ enum ApplyVariant {
     AV_PAIR_LDS, AV_PAIR_HBM, AV_PAIR_LDS_DL, AV_PAIR_HBM_DL, AV_PAIR_LDS_GN, AV_PAIR_HBM_GN, AV_PAIR2_LDS,
     AV_PAIR2_HBM, AV_COUNT
 };
-constexpr int kVariantParts = 8;  // (two variants per part at most: the HBM-resident ones take minutes each)
+constexpr int kVariantParts = 16;  // (one variant per part: the HBM-resident ones take many minutes each)
 bool launch_variant_p0(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p1(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p2(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
@@ -5827,11 +5873,31 @@ bool launch_variant_p4(int v, uint32_t grid, size_t lds, hipStream_t st, const K
 bool launch_variant_p5(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p6(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 bool launch_variant_p7(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p8(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p9(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p10(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p11(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p12(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p13(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p14(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
+bool launch_variant_p15(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region);
 inline bool launch_variant(int v, uint32_t grid, size_t lds, hipStream_t st, const KParams& P, uint32_t region = 0) {
-    return launch_variant_p0(v, grid, lds, st, P, region) || launch_variant_p1(v, grid, lds, st, P, region) ||
-           launch_variant_p2(v, grid, lds, st, P, region) || launch_variant_p3(v, grid, lds, st, P, region) ||
-           launch_variant_p4(v, grid, lds, st, P, region) || launch_variant_p5(v, grid, lds, st, P, region) ||
-           launch_variant_p6(v, grid, lds, st, P, region) || launch_variant_p7(v, grid, lds, st, P, region);
+    return launch_variant_p0(v, grid, lds, st, P, region) ||
+           launch_variant_p1(v, grid, lds, st, P, region) ||
+           launch_variant_p2(v, grid, lds, st, P, region) ||
+           launch_variant_p3(v, grid, lds, st, P, region) ||
+           launch_variant_p4(v, grid, lds, st, P, region) ||
+           launch_variant_p5(v, grid, lds, st, P, region) ||
+           launch_variant_p6(v, grid, lds, st, P, region) ||
+           launch_variant_p7(v, grid, lds, st, P, region) ||
+           launch_variant_p8(v, grid, lds, st, P, region) ||
+           launch_variant_p9(v, grid, lds, st, P, region) ||
+           launch_variant_p10(v, grid, lds, st, P, region) ||
+           launch_variant_p11(v, grid, lds, st, P, region) ||
+           launch_variant_p12(v, grid, lds, st, P, region) ||
+           launch_variant_p13(v, grid, lds, st, P, region) ||
+           launch_variant_p14(v, grid, lds, st, P, region) ||
+           launch_variant_p15(v, grid, lds, st, P, region);
 }
 
 }  // namespace mtr

@@ -473,7 +473,9 @@ PROFILE_KEYS = ["op", "prefix", "split", "shift", "insert", "range", "zamboni", 
                 "text_gc", "loadstore", "text_copy", "update_seq", "n_zblock", "n_compact", "scour1", "pack", "nlq",
                 "pmatch", "tappend", "heap", "overflow", "n_pack", "n_merge", "n_pmatch", "n_nlq", "split1", "ins1",
                 "fetch", "x1", "x2", "pf_sum", "pf_dirty", "materialize", "csum", "n_chunks", "n_listed", "n_dirty", "spread", "chunk_of", "n_spread",
-                "load", "pre", "view", "post", "n_sup", "n_dch", "helper", "sink"]
+                "load", "pre", "view", "post", "n_sup", "n_dch", "helper", "sink",
+                "ovf_bounds", "ovf_parent", "n_ovf_nowin", "n_ovf_rounds", "sup_refresh", "px_list_eval", "px_eval",
+                "px_sync", "n_px_rounds", "n_walk", "n_dirty_rounds", "walk"]
 
 
 def caps_for(batch, margin=1.25):

@@ -22,12 +22,18 @@ if not a.launches:  # the bench line of the kernel-trace run names the launches 
         if line.startswith("{"):
             a.launches = json.loads(line)["roofline"]["launches_per_step"]
 per = collections.Counter()
+clock = []  # GHz per dispatch: GRBM_GUI_ACTIVE (8 XCDs' sum) / 8 / the dispatch's duration in ns
 for f in sorted(glob.glob(os.path.join(a.dir, "*", "*_counter_collection.csv"))):
     d = collections.defaultdict(dict)
+    dur = {}
     for r in csv.DictReader(open(f)):
         if a.kernel in r["Kernel_Name"]:
             d[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+            dur[int(r["Dispatch_Id"])] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     ids = sorted(d)[-a.launches:]
+    for i in ids:
+        if "GRBM_GUI_ACTIVE" in d[i] and dur.get(i, 0) > 0:
+            clock.append(d[i]["GRBM_GUI_ACTIVE"] / 8.0 / dur[i])
     for i in ids:
         for k, v in d[i].items():
             per[k] += v / len(ids)
@@ -49,6 +55,9 @@ if "SQ_LDS_BANK_CONFLICT" in per and "SQ_LDS_IDX_ACTIVE" in per:
 if "SQ_WAVES" in per and "SQ_INSTS_VALU" in per:
     ops_per_launch = a.docs * a.ops / a.launches
     out["insts_per_op"] = {k[9:].lower(): per[k] / ops_per_launch for k in per if k.startswith("SQ_INSTS_")}
+if clock:
+    out["clock_ghz_measured"] = sum(clock) / len(clock)
+    out["note_clock"] = "GRBM_GUI_ACTIVE / 8 XCDs / dispatch duration, averaged over the same launches"
 if "SQ_WAVE_CYCLES" in per:
     wc = per["SQ_WAVE_CYCLES"]
     out["wait_any_frac"] = per.get("SQ_WAIT_ANY", 0) / wc
