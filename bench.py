@@ -102,12 +102,12 @@ def parse(argv=None):
                     help="multi-rank runs: nccl (= RCCL over xGMI); gloo only for the CPU tests' stub engine")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=None,
-                    help="PMC summary of this config (default: profiles/traffic_r04.json for C3, traffic_r04_c5.json "
-                         "for C5, traffic_r04_c4.json for C4, traffic_r04_c2.json for C2, traffic_r01.json else)")
+                    help="PMC summary of this config (default: profiles/traffic_r05.json for C3, traffic_r05_c5.json "
+                         "for C5, traffic_r05_c4.json for C4, traffic_r05_c2.json for C2, traffic_r01.json else)")
     a = ap.parse_args(argv)
     if a.traffic_file is None:
-        name = {"C2": "traffic_r04_c2.json", "C3": "traffic_r04.json", "C4": "traffic_r04_c4.json",
-                "C5": "traffic_r04_c5.json"}.get(
+        name = {"C2": "traffic_r05_c2.json", "C3": "traffic_r05.json", "C4": "traffic_r05_c4.json",
+                "C5": "traffic_r05_c5.json"}.get(
             a.config, "traffic_r01.json")
         a.traffic_file = os.path.join(ROOT, "profiles", name)
     for k, v in PRESETS[a.config].items():
