@@ -592,14 +592,18 @@ struct Eng {
         return vis_hot(L, ld_hot(L, i), i, v, newlen, minseq, valid);
     }
     template <int LOC = -1, int NL = -1>
-    static MTR_DI int vis_hot(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid) {
-        const int r = vis_leaf<LOC, NL>(L, h, i, v, newlen, minseq, valid);
+    static MTR_DI int vis_hot(const D& L, const Hot& h, int i, const View& v, int newlen, int minseq, bool valid,
+                              gptr<const int> slotp = nullptr) {
+        const int r = vis_leaf<LOC, NL>(L, h, i, v, newlen, minseq, valid, slotp);
         if constexpr (G) return r | vp_bit(h.meta, 25);  // a hole slot (M_DEL) is no leaf (Eng::spread)
         return r;
     }
     // (LOC / NL >= 0: v.local / newlen known at compile time -- the remote view's scans carry no local branch)
+    // (slotp: where the leaf's slot is read when its remover list must be walked -- a chunk record's slot list --
+    // instead of i)
     template <int LOC = -1, int NL = -1>
-    static MTR_DI int vis_leaf(const D& L, const Hot& h, int i, const View& v, int newlen_, int minseq, bool valid) {
+    static MTR_DI int vis_leaf(const D& L, const Hot& h, int i, const View& v, int newlen_, int minseq, bool valid,
+                               gptr<const int> slotp = nullptr) {
         static_assert(M_DEL == 1u << 25 && M_OVERLAP == 1u << 21, "vis_hot / vis_leaf bit positions");
         const int len = h.len;
         const int rseq = h.rseq;
@@ -627,7 +631,8 @@ struct Eng {
             PROF_COUNT(P_NWALK);
             ProfScope _prof_walk(L.sc, P_WALK);
 #endif
-            inr |= -later_remover(L, i, walk != 0, v.client);
+            const int iw = slotp ? (walk != 0 ? *slotp : 0) : i;
+            inr |= -later_remover(L, iw, walk != 0, v.client);
         }
         if (newlen) {  // mergeTree.ts:935-965
             const int live = vis & len;
@@ -977,34 +982,51 @@ struct Eng {
                                   lptr<int> lst, bool atomic) {
         const int ln = lane_id();
         const lptr<int> cx = ch_x(L), sd = sup_dlen(L);
-        for (int e0 = 64 * w; e0 < n; e0 += 64 * W) {  // one lane per chunk: its whole record in one round of loads
+        // one lane per chunk: its record's head and visibility fields in one round of loads, issued a round ahead
+        // (the slot list is read only by a lane whose leaf needs its remover list walked)
+        int cn = 0;
+        v4i hn = v4i{0, 0, 0, 0}, hvn[kChunkList];
+        if (64 * w < n) {
+            cn = lst[min(64 * w + ln, n - 1)];
+            const gptr<int> r = cs_rec(L, cn);
+            hn = ld4(r);
+#pragma unroll
+            for (int j = 0; j < kChunkList; j++) hvn[j] = ld4(r + 4 + 4 * j);
+        }
+        for (int e0 = 64 * w; e0 < n; e0 += 64 * W) {
 #ifdef MTR_PROF
             if ((threadIdx.x >> 6) == 0) PROF_COUNT(P_NDRND);
 #endif
             const int e = e0 + ln;
-            const int c = lst[min(e, n - 1)];
+            const int c = cn;
             const gptr<int> r = cs_rec(L, c);
-            const v4i h = ld4(r);
+            const v4i h = hn;
             v4i hv[kChunkList];
 #pragma unroll
-            for (int j = 0; j < kChunkList; j++) hv[j] = ld4(r + 4 + 4 * j);
-            int slt[kChunkList];
+            for (int j = 0; j < kChunkList; j++) hv[j] = hvn[j];
+            if (e0 + 64 * W < n) {  // (uniform) the next round's records
+                cn = lst[min(e0 + 64 * W + ln, n - 1)];
+                const gptr<int> rn = cs_rec(L, cn);
+                hn = ld4(rn);
 #pragma unroll
-            for (int j = 0; j < kChunkList; j += 4) {
-                const v4i sj = ld4(r + 4 + 4 * kChunkList + j);
-                slt[j] = sj.x;
-                slt[j + 1] = sj.y;
-                slt[j + 2] = sj.z;
-                slt[j + 3] = sj.w;
+                for (int j = 0; j < kChunkList; j++) hvn[j] = ld4(rn + 4 + 4 * j);
             }
             const bool listed = e < n && h.w <= kChunkList;
             int sum = h.z;
+            // (the wave's longest list bounds the tests: a chunk holds a few window leaves, its record up to 12)
+            int jm = listed ? h.w : 0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) jm = max(jm, __shfl_xor(jm, o));
+            jm = __builtin_amdgcn_readfirstlane(jm);
 #pragma unroll
             for (int j = 0; j < kChunkList; j++) {
-                const bool on = listed && j < h.w;
-                const Hot hj{hv[j].x, hv[j].y, hv[j].z, uint32_t(hv[j].w)};
-                const int x0 = vis_hot(L, hj, on ? slt[j] : 0, v, newlen, minseq, on);
-                sum += on ? max(x0, 0) : 0;
+                if (j < jm) {  // (a uniform skip; no break: the record stays in registers)
+                    const bool on = listed && j < h.w;
+                    const Hot hj{hv[j].x, hv[j].y, hv[j].z, uint32_t(hv[j].w)};
+                    const int x0 =
+                        vis_hot(L, hj, 0, v, newlen, minseq, on, (gptr<const int>)(r + 4 + 4 * kChunkList + j));
+                    sum += on ? max(x0, 0) : 0;
+                }
             }
             int vl = sum;
             uint64_t um = __ballot(e < n && !listed);
