@@ -443,9 +443,10 @@ __device__ bool props_match(PA gprop, PB val_eq, uint32_t a, uint32_t b) {
 // LDS scratch: Sc, plus the generator state in record-mode launches only
 constexpr size_t kScOnly = (sizeof(Sc) + 15) & ~size_t(15);
 constexpr size_t kScBytes = kScOnly + ((sizeof(mtr_synth_state) + 15) & ~size_t(15));
-// LDS bytes of a launch with leaf capacity cap and heap capacity lhcap (8 leaf arrays + heap)
-__host__ __device__ inline size_t lds_bytes(int cap, int lhcap, bool gen = true) {
-    return size_t(cap) * 4 * 8 + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
+// LDS bytes of a launch with leaf capacity cap and heap capacity lhcap (8 leaf arrays + heap; 7 for a matrix vector
+// of apply_pair2_kernel, which keeps no props array: Eng::NOPROPS)
+__host__ __device__ inline size_t lds_bytes(int cap, int lhcap, bool gen = true, int arrays = 8) {
+    return size_t(cap) * 4 * size_t(arrays) + size_t(lhcap) * 4 * 2 + (gen ? kScBytes : kScOnly);
 }
 // HBM-resident documents run on a team of MTR_GW waves (one workgroup per document): wave 0 applies the ops, the
 // others wait at the workgroup barrier for the passes it hands out (Eng::team_*).  The team's mailbox: the task and
@@ -502,6 +503,16 @@ struct Eng {
     // are compiled into the runtime-capacity and matrix instantiations only; the host launches those for a
     // batch holding any (mtr_submit's op scan), so the fixed-capacity replay kernels carry none of it
     static constexpr bool X = CAP == 0 || PM;
+    // a matrix vector in an LDS launch of apply_pair2_kernel (remote messages only: no tracking ids, every props
+    // field NONE32) keeps no props array in LDS -- 28 bytes a leaf instead of 32
+    static constexpr bool NOPROPS = PM && CAP == -2;
+    static MTR_DI uint32_t pget(const Doc<G>& L, int i) {
+        if constexpr (NOPROPS) return NONE32;
+        else return L.props[i];
+    }
+    static MTR_DI void pset(const Doc<G>& L, int i, uint32_t v) {
+        if constexpr (!NOPROPS) L.props[i] = v;
+    }
     template <class T>
     using A = typename D::template A<T>;
 
@@ -1409,7 +1420,7 @@ struct Eng {
                 out[5] = L.rseq[i] == RNONE ? -1 : L.rseq[i];
                 out[6] = (m & M_MARKER) ? 1 : 0;
                 out[7] = int(L.text[i]);
-                out[8] = L.props[i] == NONE32 ? -1 : int(L.props[i] & PN_MASK);
+                out[8] = pget(L, i) == NONE32 ? -1 : int(pget(L, i) & PN_MASK);
                 out[9] = before;
                 int groups = 0;  // segmentGroups.size: the leaf's pending cells (key cells are no group)
                 if (m & M_PEND)
@@ -1605,7 +1616,7 @@ struct Eng {
                     act[q] = hq > at && i < hq;
                     const int ic = max(min(i, S - 1), 0);
                     a0[q] = L.len[ic]; a1[q] = L.seq[ic]; a2[q] = L.rseq[ic]; a8[q] = L.E[ic];
-                    a3[q] = L.meta[ic]; a4[q] = L.text[ic]; a5[q] = L.props[ic]; a7[q] = L.uid[ic];
+                    a3[q] = L.meta[ic]; a4[q] = L.text[ic]; a5[q] = pget(L, ic); a7[q] = L.uid[ic];
                 }
                 wsync();
 #pragma unroll
@@ -1613,7 +1624,7 @@ struct Eng {
                     const int i = max(at, hi - 64 * q - 64) + lane_id();
                     if (act[q]) {
                         L.len[i + 1] = a0[q]; L.seq[i + 1] = a1[q]; L.rseq[i + 1] = a2[q]; L.meta[i + 1] = a3[q];
-                        L.text[i + 1] = a4[q]; L.props[i + 1] = a5[q]; L.uid[i + 1] = a7[q]; L.E[i + 1] = a8[q];
+                        L.text[i + 1] = a4[q]; pset(L, i + 1, a5[q]); L.uid[i + 1] = a7[q]; L.E[i + 1] = a8[q];
                         if (s.chunked) hint(L, a7[q], i + 1);
                     }
                 }
@@ -1627,11 +1638,11 @@ struct Eng {
             const bool act = i < hi;
             const int ic = min(i, S - 1);  // (unconditional loads: no divergent branch around them)
             const int a0 = L.len[ic], a1 = L.seq[ic], a2 = L.rseq[ic], a8 = L.E[ic];
-            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = L.props[ic], a7 = L.uid[ic];
+            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = pget(L, ic), a7 = L.uid[ic];
             wsync();
             if (act) {
                 L.len[i + 1] = a0; L.seq[i + 1] = a1; L.rseq[i + 1] = a2; L.meta[i + 1] = a3; L.text[i + 1] = a4;
-                L.props[i + 1] = a5; L.uid[i + 1] = a7; L.E[i + 1] = a8;
+                pset(L, i + 1, a5); L.uid[i + 1] = a7; L.E[i + 1] = a8;
             }
             wsync();
         }
@@ -1653,7 +1664,7 @@ struct Eng {
                 for (int q = 0; q < GK; q++) {
                     const int ic = min(lo + 64 * q + lane_id(), S - 1);
                     a0[q] = L.len[ic]; a1[q] = L.seq[ic]; a2[q] = L.rseq[ic];
-                    a3[q] = L.meta[ic]; a4[q] = L.text[ic]; a5[q] = L.props[ic]; a7[q] = L.uid[ic];
+                    a3[q] = L.meta[ic]; a4[q] = L.text[ic]; a5[q] = pget(L, ic); a7[q] = L.uid[ic];
                 }
                 wsync();
 #pragma unroll
@@ -1664,7 +1675,7 @@ struct Eng {
                     if (keep) {
                         const int d = base + __popcll(km & lanes_below());
                         L.len[d] = a0[q]; L.seq[d] = a1[q]; L.rseq[d] = a2[q]; L.meta[d] = a3[q];
-                        L.text[d] = a4[q]; L.props[d] = a5[q]; L.uid[d] = a7[q];
+                        L.text[d] = a4[q]; pset(L, d, a5[q]); L.uid[d] = a7[q];
                     }
                     base += __popcll(km);
                 }
@@ -1679,14 +1690,14 @@ struct Eng {
             const bool act = i < S;
             const int ic = min(i, S - 1);
             const int a0 = L.len[ic], a1 = L.seq[ic], a2 = L.rseq[ic];
-            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = L.props[ic], a7 = L.uid[ic];
+            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = pget(L, ic), a7 = L.uid[ic];
             const bool keep = act & !(a3 & M_DEL);
             const uint64_t km = __ballot(keep);
             wsync();
             if (keep) {
                 const int d = base + __popcll(km & lanes_below());
                 L.len[d] = a0; L.seq[d] = a1; L.rseq[d] = a2; L.meta[d] = a3;
-                L.text[d] = a4; L.props[d] = a5; L.uid[d] = a7;
+                L.text[d] = a4; pset(L, d, a5); L.uid[d] = a7;
             }
             base += __popcll(km);
             wsync();
@@ -1713,7 +1724,7 @@ struct Eng {
         L.seq[i] = 0;
         L.rseq[i] = 0;
         L.uid[i] = NONE32;
-        L.props[i] = NONE32;
+        pset(L, i, NONE32);
         L.text[i] = uint32_t(MTR_HANDLE_UNALLOCATED);
     }
     static MTR_DI void holeify(D& L, St& s, int from, int to) {
@@ -1756,12 +1767,12 @@ struct Eng {
             const bool in = i >= 0;
             const int ic = max(i, 0);
             const int a0 = L.len[ic], a1 = L.seq[ic], a2 = L.rseq[ic];
-            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = L.props[ic], a7 = L.uid[ic];
+            const uint32_t a3 = L.meta[ic], a4 = L.text[ic], a5 = pget(L, ic), a7 = L.uid[ic];
             wsync();
             if (in) {
                 const int d = i + i / (kGapEvery - 1);
                 L.len[d] = a0; L.seq[d] = a1; L.rseq[d] = a2; L.meta[d] = a3;
-                L.text[d] = a4; L.props[d] = a5; L.uid[d] = a7;
+                L.text[d] = a4; pset(L, d, a5); L.uid[d] = a7;
                 if (L.gumap()) hint(L, a7, d);
             }
             wsync();
@@ -2945,8 +2956,8 @@ struct Eng {
                     if (live) L.rseq[i] = 0;
                 }
             } else if (type == MTR_OP_ANNOTATE) {
-                const uint32_t np = props_restore(L, P, s, uniu(L.props[i]), oldp, pp, (comb & 7u) == MTR_COMB_REWRITE);
-                if (lane_id() == 0) L.props[i] = np;
+                const uint32_t np = props_restore(L, P, s, uniu(pget(L, i)), oldp, pp, (comb & 7u) == MTR_COMB_REWRITE);
+                if (lane_id() == 0) pset(L, i, np);
             } else {
                 s.status = MTR_ERR_BAD_OP;
                 break;
@@ -2963,7 +2974,7 @@ struct Eng {
         uint32_t meta, text, props, uid;
     };
     static MTR_DI LeafRec leaf_ld(const D& L, int i) {
-        return LeafRec{L.len[i], L.seq[i], L.rseq[i], L.meta[i], L.text[i], L.props[i], L.uid[i]};
+        return LeafRec{L.len[i], L.seq[i], L.rseq[i], L.meta[i], L.text[i], pget(L, i), L.uid[i]};
     }
     // a leaf's data into slot i; the slot keeps its tree-structure bits (leaf-block bounds, needsScour):
     // assignChild puts the segment at the (parent, index) place (mergeTree.ts:2303-2308)
@@ -2974,7 +2985,7 @@ struct Eng {
         L.rseq[i] = x.rseq;
         L.meta[i] = (x.meta & ~kPlace) | (L.meta[i] & kPlace);
         L.text[i] = x.text;
-        L.props[i] = x.props;
+        pset(L, i, x.props);
         L.uid[i] = x.uid;
     }
     // normalizeAdjacentSegments (mergeTree.ts:2231-2331) on the run of leaves in slots [a, b) (holes
@@ -3170,7 +3181,7 @@ struct Eng {
                 off += ln;
                 if (!emit) continue;
                 if constexpr (DL) {
-                    const uint32_t pr = uniu(L.props[j]);
+                    const uint32_t pr = uniu(pget(L, j));
                     const int ref = (type == MTR_OP_INSERT && pr != NONE32) ? int(pr & PN_MASK) : -1;
                     put_record(L, s, gidx, before, ln, uint32_t(MTR_DELTA_REGEN + type));
                     put_record(L, s, gidx, type == MTR_OP_INSERT ? here : 0, ref, MTR_DELTA_REGEN_X);
@@ -3652,11 +3663,11 @@ struct Eng {
     }
     // TrackingGroup.link (mergeTreeTracking.ts:41-46) of leaf i into the groups `bits`, reported in link order
     static MTR_DI void track_link(D& L, const KParams& P, St& s, int i, uint32_t bits) {
-        uint32_t t = uniu(L.props[i]);
+        uint32_t t = uniu(pget(L, i));
         if (t == NONE32) {
             t = tid_new(L, P, s, bits);
             if (t == NONE32) return;
-            if (lane_id() == 0) L.props[i] = t;
+            if (lane_id() == 0) pset(L, i, t);
         } else if (lane_id() == 0) {
             L.gprop()[t] = L.gprop()[t] | bits;
         }
@@ -3692,10 +3703,10 @@ struct Eng {
         for (int base = 0; base < s.nseg && at < 0; base += 64) {
             const int i = base + lane_id();
             const int ic = min(i, s.nseg - 1);
-            const uint64_t hit = __ballot(i < s.nseg && !(L.meta[ic] & M_DEL) && L.props[ic] == src);
+            const uint64_t hit = __ballot(i < s.nseg && !(L.meta[ic] & M_DEL) && pget(L, ic) == src);
             if (hit) at = base + first_lane(hit);
         }
-        const uint32_t dt = uniu(L.props[dst]);
+        const uint32_t dt = uniu(pget(L, dst));
         if (at < 0 || at == dst || dt == NONE32) {
             s.status = MTR_ERR_BAD_OP;
             return;
@@ -3717,7 +3728,7 @@ struct Eng {
         for (int base = 0; base < s.nseg && at < 0; base += 64) {
             const int i = base + lane_id();
             const int ic = min(i, s.nseg - 1);
-            const uint64_t hit = __ballot(i < s.nseg && !(L.meta[ic] & M_DEL) && L.props[ic] == t);
+            const uint64_t hit = __ballot(i < s.nseg && !(L.meta[ic] & M_DEL) && pget(L, ic) == t);
             if (hit) at = base + first_lane(hit);
         }
         if (at < 0) return -1;
@@ -3756,7 +3767,7 @@ struct Eng {
             const int i = base + lane_id();
             const int ic = min(i, ce - 1);
             uint32_t vm = L.meta[ic];
-            const uint32_t vp = L.props[ic], vt = L.text[ic];
+            const uint32_t vp = pget(L, ic), vt = L.text[ic];
             const int vr = L.rseq[ic], vs = L.seq[ic], vl = L.len[ic];
             if (i >= ce) vm = M_DEL;
             {  // merge candidates whose trailing-newline bit is unknown: one HBM round trip
@@ -3890,7 +3901,7 @@ struct Eng {
         const int minseq = s.minseq;
         const int ln = lane_id();
         const int ic = in ? i : min(cs, clamp);
-        const uint32_t vm0 = L.meta[ic], vp = L.props[ic], vt = L.text[ic];
+        const uint32_t vm0 = L.meta[ic], vp = pget(L, ic), vt = L.text[ic];
         const int vr0 = L.rseq[ic], vs = L.seq[ic], vl0 = L.len[ic];
         const uint32_t vu = X ? L.uid[ic] : 0u;  // (local references follow appends)
         uint32_t vm = in ? vm0 : M_DEL;
@@ -4304,7 +4315,7 @@ struct Eng {
         const bool in = jj < S;
         const int jc = min(jj, S - 1);  // unconditional (clamped) loads
         const int ej0 = L.E[jc], ep = L.E[max(jc - 1, 0)];
-        const uint32_t mj = L.meta[jc], tj = L.text[jc], pj = L.props[jc], uj = L.uid[jc];
+        const uint32_t mj = L.meta[jc], tj = L.text[jc], pj = pget(L, jc), uj = L.uid[jc];
         const int lj = L.len[jc], sqj = L.seq[jc], rsj = L.rseq[jc];
         const int vj = ev(ej0, jc > 0 ? ep : 0);
         const int ej = ej0 & EMASK;
@@ -4332,7 +4343,7 @@ struct Eng {
                 L.text[r] = t0 == uint32_t(MTR_HANDLE_UNALLOCATED) ? t0 : t0 + uint32_t(off);
             }
             // (a matrix vector's props field is a tracking id: a tracked leaf's right half gets one of its own)
-            L.props[r] = (PM && rdlane(pj, jl) != NONE32) ? track_split(L, P, s, rdlane(pj, jl)) : rdlane(pj, jl);
+            pset(L, r, (PM && rdlane(pj, jl) != NONE32) ? track_split(L, P, s, rdlane(pj, jl)) : rdlane(pj, jl));
             const uint32_t ur = uint32_t(s.uidnext++);
             L.uid[r] = ur;
             if (G && s.chunked && lane_id() == 0) hint(L, ur, r);
@@ -4552,7 +4563,7 @@ struct Eng {
         if (!marker && !PM) s.textused = t0 + len;
         uint32_t pr = NONE32;
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
-        L.props[slot] = pr;
+        pset(L, slot, pr);
         L.uid[slot] = uint32_t(s.uidnext++);
         if (G && s.chunked && lane_id() == 0) hint(L, uint32_t(s.uidnext - 1), slot);
         if (X && marker && op.payload2 != 0) {  // mapIdToSegment (mergeTree.ts:1655-1662)
@@ -4636,7 +4647,7 @@ struct Eng {
         L.text[i] = (marker || PM) ? op.payload : uint32_t(t0);
         uint32_t pr = NONE32;
         if ((op.flags & MTR_F_PROPS) && op.pos2 >= 0) pr = props_apply(L, P, s, NONE32, uint32_t(op.pos2));
-        L.props[i] = pr;
+        pset(L, i, pr);
         L.uid[i] = uint32_t(s.uidnext++);
         if (X && marker && op.payload2 != 0) {  // reloadFromSegments' blockUpdate maps live markers (mergeTree.ts:297-306)
             if (lane_id() == 0 && !mk_set(L, op.payload2 - 1, uint32_t(s.uidnext - 1))) s.status = MTR_ERR_CAPACITY;
@@ -4677,7 +4688,7 @@ struct Eng {
             L.rseq[i] = int(ow[2]) >= 0 ? int(ow[2]) : RNONE;
             L.meta[i] = enc_client(int(int16_t(ow[0] >> 16))) | M_NLQ | ((fl & MTR_F_NOREF) ? M_NOREF : 0u);
             L.text[i] = t;
-            L.props[i] = NONE32;
+            pset(L, i, NONE32);
             L.uid[i] = uint32_t(s.uidnext + (ln - t0));
         }
         wsync();
@@ -4784,7 +4795,7 @@ struct Eng {
                     s.rmused += nov;
                 } else {
                     // one new property set per distinct old set in the round (memoized addProperties)
-                    const uint32_t old = act ? L.props[j] : 0u;
+                    const uint32_t old = act ? pget(L, j) : 0u;
                     uint64_t pend = am;
                     if (X && !pending) {  // leaves with pending local annotates: one filtered set each
                         uint64_t pm = __ballot(act && (mj & (M_PEND | M_ZOMB)));
@@ -4795,7 +4806,7 @@ struct Eng {
                             const PropRes r = props_apply_serial(L, P, s.propused, rdlane(old, l), pp, comb, pl);
                             s.propused = uni(r.propused);
                             if (uni(r.status) != MTR_OK) s.status = uni(r.status);
-                            if (ln == l) L.props[j] = uniu(r.dst);
+                            if (ln == l) pset(L, j, uniu(r.dst));
                             wsync();
                         }
                     }
@@ -4804,7 +4815,7 @@ struct Eng {
                         const bool mine = act && old == o && (!X || ((pend >> ln) & 1));
                         const uint64_t sel = __ballot(mine);
                         const uint32_t nw = props_apply(L, P, s, o, pp, comb);
-                        if (mine) L.props[j] = nw;
+                        if (mine) pset(L, j, nw);
                         pend &= ~sel;
                     }
                     if (dl && act) {  // every annotated segment is a delta segment
@@ -4922,7 +4933,7 @@ struct Eng {
                 L.rseq[i] = int(g[F_RSEQ * cs + i]);
                 L.meta[i] = g[F_META * cs + i];
                 L.text[i] = g[F_TEXT * cs + i];
-                L.props[i] = g[F_PROPS * cs + i];
+                pset(L, i, g[F_PROPS * cs + i]);
                 L.uid[i] = g[F_UID * cs + i];
             }
             const int hn = s.heapn;
@@ -4949,7 +4960,7 @@ struct Eng {
                 g[F_RSEQ * cs + i] = uint32_t(L.rseq[i]);
                 g[F_META * cs + i] = L.meta[i];
                 g[F_TEXT * cs + i] = L.text[i];
-                g[F_PROPS * cs + i] = L.props[i];
+                g[F_PROPS * cs + i] = pget(L, i);
                 g[F_UID * cs + i] = L.uid[i];
             }
             const int hn = s.heapn;
@@ -5052,7 +5063,8 @@ struct Eng {
             L.rseq = (A<int>)(take(4 * size_t(cap)));
             L.meta = (A<uint32_t>)(take(4 * size_t(cap)));
             L.text = (A<uint32_t>)(take(4 * size_t(cap)));
-            L.props = (A<uint32_t>)(take(4 * size_t(cap)));
+            if constexpr (NOPROPS) L.props = (A<uint32_t>)(p);  // (never read: pget / pset)
+            else L.props = (A<uint32_t>)(take(4 * size_t(cap)));
             L.uid = (A<uint32_t>)(take(4 * size_t(cap)));
             L.E = (A<int>)(take(4 * size_t(cap)));
             L.hseq = (A<int>)(take(4 * size_t(lhcap)));
@@ -5874,7 +5886,7 @@ __global__ void __launch_bounds__(2 * NT) __attribute__((amdgpu_waves_per_eu(1, 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (blockIdx.x >= P.n_launch) return;
     const uint32_t d = P.doc_list[blockIdx.x];
-    Eng<G, true, 0, false, false>::run_pair2(smem, pair_region, P, d);
+    Eng<G, true, G ? 0 : -2, false, false>::run_pair2(smem, pair_region, P, d);
 }
 constexpr size_t kPair2Xch = 64;  // bytes behind the two regions: run_pair2's exchange words
 

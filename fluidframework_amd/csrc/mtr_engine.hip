@@ -823,6 +823,8 @@ static int run_impl(mtr_engine* e, int gen) {
                 if (!Q.gen && !Q.doff && !e->has_ext && !e->pend_seen && !pair1 &&
                     lds + kPair2Xch <= size_t(std::max(dev_lds, 0))) {
                     av = Q.global_mode ? AV_PAIR2_HBM : AV_PAIR2_LDS;
+                    // (an LDS pair2 launch keeps no props arrays: remote messages only, Eng::NOPROPS)
+                    if (!Q.global_mode) lds = 2 * ((lds_bytes(cap, lhcap, false, 7) + 15) & ~size_t(15));
                     lds += kPair2Xch;
                 }
             } else if (Q.gen) {  // record mode: the generating instantiation
