@@ -779,8 +779,11 @@ static int run_impl(mtr_engine* e, int gen) {
             if (cap > P.segcap) cap = P.segcap;
             // LRU heap: what the class holds now plus room for this launch's pushes; a document that
             // could overflow it stops before the op and asks for more (DocHdr.heap_need)
-            int lhcap = std::min<int>(P.hcap, std::max(cap / 8, tight ? round32(maxheap + slack + 8)
-                                                                       : round64(maxheap + 2 * k + 8)));
+            // (matrix pairs replaying remote messages: a smaller floor -- a document whose op could overflow the heap
+            // yields before it like any other, and two matrices of the larger classes then fit one CU's LDS)
+            int lhcap = std::min<int>(P.hcap, pair && !P.gen ? std::max(cap / 16, round32(maxheap + 2 * k + 8))
+                                               : std::max(cap / 8, tight ? round32(maxheap + slack + 8)
+                                                                         : round64(maxheap + 2 * k + 8)));
             size_t lds = lds_bytes(cap, lhcap, P.gen != 0);
             if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             KParams Q = P;
