@@ -681,6 +681,11 @@ static int run_impl(mtr_engine* e, int gen) {
         const char* v = std::getenv("MTR_SLACK");
         return v ? std::max(0, std::atoi(v)) : -1;
     }();
+    // the LRU heap's floor in a yielding (tight) launch: cap / heap_div entries (tuning knob MTR_HEAP_DIV)
+    static const int heap_div = [] {
+        const char* v = std::getenv("MTR_HEAP_DIV");
+        return v ? std::max(1, std::atoi(v)) : 8;
+    }();
     // Independent document groups (tuning knob MTR_GROUPS, 1..kLanes): each group runs its own round loop
     // (classify -> one launch per size class -> classify ...) on its own streams, so one group's launches fill
     // the device while another's last documents of a round finish (a round is quantised by how many of its
@@ -782,8 +787,9 @@ static int run_impl(mtr_engine* e, int gen) {
             // (matrix pairs replaying remote messages: a smaller floor -- a document whose op could overflow the heap
             // yields before it like any other, and two matrices of the larger classes then fit one CU's LDS)
             int lhcap = std::min<int>(P.hcap, pair && !P.gen ? std::max(cap / 16, round32(maxheap + 2 * k + 8))
-                                               : std::max(cap / 8, tight ? round32(maxheap + slack + 8)
-                                                                         : round64(maxheap + 2 * k + 8)));
+                                               : std::max(cap / (tight ? heap_div : 8),
+                                                          tight ? round32(maxheap + slack + 8)
+                                                                : round64(maxheap + 2 * k + 8)));
             size_t lds = lds_bytes(cap, lhcap, P.gen != 0);
             if (pair) lds = 2 * ((lds + 15) & ~size_t(15));
             KParams Q = P;
