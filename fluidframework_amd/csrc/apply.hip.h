@@ -5868,9 +5868,10 @@ bool launch_fixed_cap_p0(int cap, uint32_t grid, size_t lds, hipStream_t st, con
 bool launch_fixed_cap_p1(int cap, uint32_t grid, size_t lds, hipStream_t st, const KParams& P);
 bool launch_fixed_cap_p2(int cap, uint32_t grid, size_t lds, hipStream_t st, const KParams& P);
 #define MTR_FIXED_CAPS(X) \
-    X(64) X(96) X(128) X(160) X(192) X(224) X(256) X(288) X(320) X(352) X(384) X(416) X(448) X(480) X(512) X(576) X(640) \
-    X(704) X(768) X(832) X(896) X(960) X(1024) X(1088) X(1152) X(1216) X(1280) X(1344) X(1408) X(1472) X(1536)
-// (above 512 leaves the fixed capacities step by 64: a yielding launch's capacity is rounded up to one of them,
+    X(64) X(96) X(128) X(160) X(192) X(224) X(256) X(288) X(320) X(352) X(384) X(416) X(448) X(480) X(512) X(544) \
+    X(576) X(608) X(640) X(672) X(704) X(736) X(768) X(800) X(832) X(864) X(896) X(928) X(960) X(992) X(1024) X(1088) \
+    X(1152) X(1216) X(1280) X(1344) X(1408) X(1472) X(1536)
+// (above 1,024 leaves the fixed capacities step by 64: a yielding launch's capacity is rounded up to one of them,
 // mtr_engine.hip's class loop)
 
 // SharedMatrix pairs: one wave applies a matrix's op list to its two PermutationVectors, each with

@@ -781,8 +781,8 @@ static int run_impl(mtr_engine* e, int gen) {
             // does not yield and wait for a round of its own)
             const int slack = slack_env >= 0 ? slack_env : (few_docs ? k + 8 : 8);
             int cap = tight ? round32(maxseg + slack + 8) : round64(maxseg + 2 * k + 8);
-            // (a yielding launch above 512 leaves: the next multiple of 64, a capacity with a compile-time layout)
-            if (tight && cap > 512 && cap <= 1536) cap = round64(cap);
+            // (a yielding launch above 1,024 leaves: the next multiple of 64, a capacity with a compile-time layout)
+            if (tight && cap > 1024 && cap <= 1536) cap = round64(cap);
             if (cap > P.segcap) cap = P.segcap;
             // LRU heap: what the class holds now plus room for this launch's pushes; a document that
             // could overflow it stops before the op and asks for more (DocHdr.heap_need)
