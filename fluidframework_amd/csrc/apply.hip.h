@@ -5067,10 +5067,11 @@ struct Eng {
             else L.props = (A<uint32_t>)(take(4 * size_t(cap)));
             L.uid = (A<uint32_t>)(take(4 * size_t(cap)));
             L.E = (A<int>)(take(4 * size_t(cap)));
-            L.hseq = (A<int>)(take(4 * size_t(lhcap)));
-            L.huid = (A<uint32_t>)(take(4 * size_t(lhcap)));
+            // (Sc ahead of the heap: with a compile-time capacity its address is a constant, not an SGPR)
             L.sc = (lptr<Sc>)(take(sizeof(Sc)));
             L.gst = (lptr<mtr_synth_state>)(GN ? take(sizeof(mtr_synth_state)) : p);
+            L.hseq = (A<int>)(take(4 * size_t(lhcap)));
+            L.huid = (A<uint32_t>)(take(4 * size_t(lhcap)));
             L.sx = (lptr<int>)(p);
             L.cap = cap;
             L.lhcap = lhcap;
