@@ -492,9 +492,11 @@ def main(argv=None):
             "achieved_span": round(b2_step / apply_s / 1e9, 2) if apply_s > 0 else 0.0,
             "frac_span": round(b2_step / apply_s / 1e9 / HBM_PEAK_GBS, 4) if apply_s > 0 else 0.0,
             "algorithmic_bytes_per_launch": b2_launch,
-            "limiter": "per-wave latency: one wave per document (about one per SIMD at C5), each op a chain of "
-                       "dependent HBM round trips (superchunk/chunk figures in LDS, records of chunks with later "
-                       "events, the op's leaf region) and scalar control; the scalar unit is shared by the CU's waves",
+            "limiter": "per-document latency: a two-wave workgroup per document (wave 0 applies the ops in order, "
+                       "wave 1 takes halves of the view scan's superchunk rounds, the dirty-chunk evaluation, the "
+                       "block walks and packParent), each op a chain of dependent HBM round trips (superchunk/chunk "
+                       "figures in LDS, records of chunks with later events, the op's leaf region) and scalar "
+                       "control; the scalar unit is shared by the CU's waves",
         })
 
     e2e = None
