@@ -7,7 +7,8 @@ Inputs are recorded on the device before the timed region (record mode of the en
 include/mtr_synth.h), so the timed region starts with every op log resident in HBM.
 
 Single GPU:   python bench.py
-Multi GPU:    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Multi GPU:    python bench.py --gpus N        (bench.py starts the N rank processes itself, one per GPU)
+         or:  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 Documents are sharded over ranks.  Default strong scaling: `--docs` is the node's total (C3: 100k
 documents split into contiguous equal ranges -- the LPT assignment for documents of one recipe);
 `--scaling weak` gives every rank its own `--docs`.  The only collective is the final RCCL reduction of
@@ -100,7 +101,12 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="default: every host core this job may use")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="multi-rank runs: nccl (= RCCL over xGMI); gloo only for the CPU tests' stub engine")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the CPU baseline (N=1) and the per-rank oracle sample (N>1)")
+    ap.add_argument("--rank-sample-docs", type=int, default=0,
+                    help="N>1: documents of its own shard each rank checks against the oracle after the timed "
+                         "region (default: about 4M messages' worth; one per host thread for C5)")
+    ap.add_argument("--master-port", type=int, default=0, help="--gpus N launcher: rendezvous port (default: a free one)")
     ap.add_argument("--traffic-file", default=None,
                     help="PMC summary of this config (default: profiles/traffic_r05.json for C3, traffic_r05_c5.json "
                          "for C5, traffic_r05_c4.json for C4, traffic_r05_c2.json for C2, traffic_r01.json else)")
@@ -120,7 +126,7 @@ def parse(argv=None):
     return a
 
 
-def end_to_end(eng, n, steps, messages, matrix, hashes):
+def end_to_end(eng, n, steps, messages, matrix, hashes, barrier=lambda: None):
     """SURVEY.md 8d's end-to-end time: the host hands the op logs over (one upload from page-locked
     memory), the engine applies and summarizes, and every blob of every document lands in host memory
     (one bulk download, mtr_get_summaries).  The op logs are the recorded ones, downloaded once
@@ -137,6 +143,7 @@ def end_to_end(eng, n, steps, messages, matrix, hashes):
     out = pinned(int(eng.summary_bytes()) + 8 * n + 4096, "u1")
     times, parts = [], []
     for i in range(steps + 1):  # the first is untimed (warm)
+        barrier()  # (N > 1: the ranks start each step together; the slowest rank's time is the node's)
         t0 = _t.perf_counter()
         eng.reset()
         eng.submit(hb)
@@ -251,13 +258,113 @@ def _bulk_record(buf, off, d):
     return Engine.split_record(buf, int(off[d]), int(off[d + 1]))
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(a, argv) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script, one per GPU, and wait for them.
+
+    The parent makes no HIP call (it imports neither torch nor the engine), so every rank initialises its own
+    device from scratch.  Rank r gets RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free
+    MASTER_PORT, exactly what torch.distributed.run would set; rank 0 writes to this process's stdout (its JSON
+    line is the run's line), the other ranks' stdout goes to stderr.  A rank that fails ends the others after a
+    grace period (they would wait in a collective).  Returns the worst exit status.  The shape follows the
+    reference's replay driver, which forks one worker per shard of the files and joins them
+    (packages/test/snapshots/src/replayMultipleFiles.ts:355-410)."""
+    import signal
+    import subprocess
+
+    port = a.master_port or _free_port()
+    try:
+        err_fd = sys.stderr.fileno()
+    except (AttributeError, OSError, ValueError):
+        err_fd = subprocess.DEVNULL
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MTR_BENCH_LAUNCHER="bench.py")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else err_fd, start_new_session=True))
+    rcs = [None] * len(procs)
+    failed_at = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0) and failed_at is None:
+                    failed_at = time.time()
+                    print(f"bench.py launcher: rank {i} exited with status {rcs[i]}", file=sys.stderr, flush=True)
+        if failed_at is not None and time.time() - failed_at > 30:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    os.killpg(p.pid, signal.SIGKILL)  # (the rank's own process group: start_new_session)
+                    rcs[i] = p.wait()
+        time.sleep(0.2)
+    bad = [rc for rc in rcs if rc]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+
+
+def _engine_class():
+    """The engine the bench drives: fluidframework_amd.engine.Engine (the HIP engine).  MTR_BENCH_STUB_ENGINE =
+    "module:Class" substitutes a stub for the CPU tests of the multi-rank plumbing (tests/bench_stub.py); the line
+    then says `"engine": "stub"`, so such a run can never pass for a measurement."""
+    spec = os.environ.get("MTR_BENCH_STUB_ENGINE")
+    if spec:
+        import importlib
+
+        mod, cls = spec.split(":")
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        return getattr(importlib.import_module(mod), cls), "stub"
+    from fluidframework_amd.engine import Engine
+
+    return Engine, "hip"
+
+
+def rank_sample(a, eng, n, ops, grow, matrix, hashes, fixture_batch, threads):
+    """N > 1: the checker leg of one rank.  After the timed region the oracle replays a bounded sample of this
+    rank's own documents (the first of its shard) and compares their summary digests with the engine's; the
+    counts are summed over ranks into the line's bit_exact_sample.  Not a baseline: nothing here is timed."""
+    from oracle.oracle import replay_batch, replay_matrix_batch
+
+    k = min(n, a.rank_sample_docs or (threads if grow else max(1, 4_000_000 // max(1, ops))))
+    if fixture_batch is not None:
+        k, sample = n, fixture_batch
+    elif matrix:
+        sample = eng.download_matrix(0, k)
+    else:
+        sample = eng.download(0, k)
+    if matrix:
+        _, oh, ost = replay_matrix_batch(sample, 0, k, threads)
+        eq = int((oh == hashes[:2 * k]).reshape(k, 2).all(axis=1).sum())
+    else:
+        _, oh, ost = replay_batch(sample, 0, k, threads)
+        eq = int((oh == hashes[:k]).sum())
+    return {"checked_docs": int(k), "equal": eq, "oracle_errors": int((ost != 0).sum())}
+
+
 def main(argv=None):
     a = parse(argv)
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be at least 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:  # no launcher around us: be it (before any HIP call)
+        return launch(a, sys.argv[1:] if argv is None else argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but the launcher started {world} ranks (WORLD_SIZE): refusing to report "
+                         f"a {world}-GPU run as a {a.gpus}-GPU one")
     dist = None
     reduce_device = f"cuda:{local}"
+    comm_world = 1
     if world > 1:
         import torch
         import torch.distributed as dist_mod
@@ -268,9 +375,12 @@ def main(argv=None):
             reduce_device = "cpu"
         dist_mod.init_process_group(a.dist_backend)
         dist = dist_mod
+        comm_world = dist.get_world_size()
+        if comm_world != a.gpus:
+            raise SystemExit(f"--gpus {a.gpus} but the process group holds {comm_world} ranks")
 
     from fluidframework_amd import shard
-    from fluidframework_amd.engine import Engine
+    Engine, engine_kind = _engine_class()
     from fluidframework_amd.synth import make_cfg, tables
 
     n, ops = a.docs, a.ops
@@ -379,17 +489,40 @@ def main(argv=None):
     hashes = eng.hashes(2 * n if matrix else n)
     messages = n * ops if fixture_text is None else fixture_msgs
     run_digest = shard.digest(hashes)
-    if dist is not None:  # the only collective: counters + summary digests over RCCL/xGMI
-        r = shard.reduce_run(dist, reduce_device, elapsed, messages, int(st["bad_docs"]), run_digest)
+    # (after the timed region) N > 1: every rank checks a sample of its own shard against the oracle
+    sample_counts = [0, 0, 0]
+    if world > 1 and not a.no_cpu_baseline:
+        threads = max(1, host_cores() // max(1, local_world))
+        rs = rank_sample(a, eng, n, ops, grow, matrix, hashes, fixture_batch if fixture_text is not None else None,
+                         threads)
+        sample_counts = [rs["checked_docs"], rs["equal"], rs["oracle_errors"]]
+    e2e = None
+    if a.e2e_steps > 0 and fixture_text is None and not grow:
+        e2e = end_to_end(eng, n, a.e2e_steps, messages, matrix, hashes, barrier=barrier)
+    if dist is not None:  # the only collectives: counters + summary digests over RCCL/xGMI
+        r = shard.reduce_run(dist, reduce_device, elapsed, messages, int(st["bad_docs"]), run_digest,
+                             extra=sample_counts)
         elapsed, total_messages, bad, run_digest = r["elapsed"], float(r["messages"]), float(r["bad_docs"]), r["digest"]
+        sample_counts = r["extra"]
+        if e2e is not None:  # the slowest rank's end-to-end step times the node
+            keys = ("ms_per_step", "upload_ms", "apply_summarize_ms", "download_ms")
+            mx = shard.reduce_max(dist, reduce_device, [e2e[k] for k in keys])
+            e2e.update({k: round(v, 3) for k, v in zip(keys, mx)})
+            e2e["value"] = round(total_messages / (e2e["ms_per_step"] / 1000.0), 1)
+            e2e["ranks"] = world
     else:
         total_messages = float(messages)
         bad = float(st["bad_docs"])
+    sample_bad = world > 1 and (sample_counts[1] != sample_counts[0] or sample_counts[2])
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
-        return
+        if sample_bad:
+            raise SystemExit(1)
+        return 0
+    if sample_bad:
+        raise SystemExit(f"summaries differ from the CPU oracle on the ranks' samples: {sample_counts}")
 
     ms_per_step = 1000.0 * elapsed / a.steps
     value = total_messages * a.steps / elapsed
@@ -499,12 +632,12 @@ def main(argv=None):
                        "control; the scalar unit is shared by the CU's waves",
         })
 
-    e2e = None
-    if a.e2e_steps > 0 and world == 1 and fixture_text is None and not grow:
-        e2e = end_to_end(eng, n, a.e2e_steps, messages, matrix, hashes)
-
     cpu = None
     bit_exact = {"checked_docs": 0, "equal": 0}
+    if world > 1:
+        bit_exact = {"checked_docs": sample_counts[0], "equal": sample_counts[1], "oracle_errors": sample_counts[2],
+                     "ranks": world, "note": "each rank replayed the first documents of its own shard on the oracle "
+                                             "after the timed region; counts summed over ranks"}
     if not a.no_cpu_baseline and world == 1:
         cpu, bit_exact = cpu_baseline(a, eng, n, ops, grow, matrix, hashes, fixture_batch if fixture_text is not None
                                       else None, messages)
@@ -513,6 +646,9 @@ def main(argv=None):
         "value": round(value, 1),
         "unit": "ops/s",
         "n_gpus": world,
+        "rccl_world_size": comm_world if dist is not None else None,
+        "launcher": os.environ.get("MTR_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else None),
+        "engine": engine_kind,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
@@ -559,7 +695,8 @@ def main(argv=None):
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -71,14 +71,25 @@ def limbs_digest(limbs) -> int:
     return sum(int(x) << (16 * q) for q, x in enumerate(limbs)) & MASK64
 
 
-def reduce_run(dist, device, elapsed: float, messages: int, bad_docs: int, run_digest: int) -> dict:
-    """Reduce one bench run over ranks: max elapsed, summed messages / bad documents / digest."""
+def reduce_run(dist, device, elapsed: float, messages: int, bad_docs: int, run_digest: int, extra=()) -> dict:
+    """Reduce one bench run over ranks: max elapsed, summed messages / bad documents / digest, and the sums
+    of `extra` (integer counters, e.g. the ranks' oracle-sample counts)."""
     import torch
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    s = torch.tensor([messages, bad_docs] + digest_limbs(run_digest), dtype=torch.int64, device=device)
+    extra = [int(x) for x in extra]
+    s = torch.tensor([messages, bad_docs] + digest_limbs(run_digest) + extra, dtype=torch.int64, device=device)
     dist.all_reduce(s, op=dist.ReduceOp.SUM)
     v = s.tolist()
     return {"elapsed": float(t.item()), "messages": int(v[0]), "bad_docs": int(v[1]),
-            "digest": limbs_digest(v[2:6])}
+            "digest": limbs_digest(v[2:6]), "extra": [int(x) for x in v[6:]]}
+
+
+def reduce_max(dist, device, values) -> list[float]:
+    """Element-wise max over ranks of a few floats (e.g. the end-to-end step's phase times)."""
+    import torch
+
+    t = torch.tensor([float(x) for x in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
