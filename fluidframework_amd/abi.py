@@ -30,6 +30,7 @@ OP_LSEQ = 26
 REF_SLIDE = 1
 REF_LOCALVIEW = 2
 REF_LSEQ = 4
+REF_SLOT = 8  # MTR_REF_SLOT: the reference takes id pos2 (a recycled slot, include/mtr_types.h)
 # ReferenceType (ops.ts:9-36)
 REFTYPE_SIMPLE = 0x0
 REFTYPE_TILE = 0x1

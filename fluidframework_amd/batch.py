@@ -219,7 +219,8 @@ class DocLog:
     marker_ids: dict = field(default_factory=dict)
     marker_dup: set = field(default_factory=set)  # ids mapped to two markers: block-update order decides
     marker_id_annotated: bool = False              # an annotate touched "markerId": remapped by blockUpdate
-    n_refs: int = 0                                # local references created (MTR_OP_REF_CREATE ids)
+    n_refs: int = 0                                # reference ids handed out (MTR_OP_REF_CREATE ids; high-water mark)
+    free_refs: list = field(default_factory=list)  # ids released for reuse (MTR_REF_SLOT), a stack
     # the merge-tree client's currentSeq (collabWindow.currentSeq) as the host sees it: interval ops do not move it
     current_seq: int = 0
     intervals: Any = None                          # fluidframework_amd.intervals.IntervalCollections, when used
@@ -385,34 +386,55 @@ class DocLog:
         return first
 
     # -- local references (localReference.ts)
+    def _new_ref_id(self) -> int:
+        if self.free_refs:
+            return self.free_refs.pop()
+        self.n_refs += 1
+        return self.n_refs - 1
+
     def create_ref(self, pos: int, ref_type: int, view: tuple | None = None, slide: bool = False) -> int:
         """createPositionReference (sequence/src/intervalCollection.ts:697-724): Client.getContainingSegment(pos,
         view) (client.ts:1065-1078; view = (referenceSequenceNumber, long client id), None = the local view),
         Client.getSlideToSegment when `slide` (client.ts:1085-1099), then createLocalReferencePosition
-        (client.ts:377-389) -- a detached reference when no segment holds pos.  Returns the reference id."""
+        (client.ts:377-389) -- a detached reference when no segment holds pos.  Returns the reference id: a released
+        one when there is one (MTR_REF_SLOT), else the next."""
         if view is None:
             short, ref, flags = 0, 0, abi.REF_LOCALVIEW
         else:
             short, ref, flags = self.short_id(str(view[1])), int(view[0]), 0
         if slide:
             flags |= abi.REF_SLIDE
-        self.ops.append((abi.OP_REF_CREATE, 0, short, 0, ref, 0, int(pos), 0, int(ref_type), flags))
-        self.n_refs += 1
-        return self.n_refs - 1
+        rid = self._new_ref_id()
+        self.ops.append((abi.OP_REF_CREATE, 0, short, 0, ref, 0, int(pos), rid, int(ref_type), flags | abi.REF_SLOT))
+        return rid
 
     def create_ref_at(self, pos: int, ref_type: int, ref_seq: int, local_seq: int) -> int:
         """createPositionReference with a localSeq (sequence/src/intervalCollection.ts:697-724, a rebase's
         changeInterval): getContainingSegment(pos, undefined, localSeq) -- this client's view at (ref_seq =
         currentSeq, localSeq) -- then createLocalReferencePosition; no segment = a detached reference."""
-        self.ops.append((abi.OP_REF_CREATE, 0, 0, 0, int(ref_seq), int(local_seq), int(pos), 0, int(ref_type),
-                         abi.REF_LSEQ))
-        self.n_refs += 1
-        return self.n_refs - 1
+        rid = self._new_ref_id()
+        self.ops.append((abi.OP_REF_CREATE, 0, 0, 0, int(ref_seq), int(local_seq), int(pos), rid, int(ref_type),
+                         abi.REF_LSEQ | abi.REF_SLOT))
+        return rid
+
+    def release_ref(self, ref_id: int, remove: bool = True) -> None:
+        """The host is done with reference `ref_id`; its id is reused by the next create (MTR_REF_SLOT).  remove:
+        Client.removeLocalReferencePosition first (client.ts:394-396) -- a reference a segment's collection may
+        hold (an interval endpoint that a change superseded or a delete dropped: nothing reads it again, and the
+        reference's own left-over LocalReferencePositions are unobservable); a Transient query reference is held by
+        no collection and needs no record (localReference.ts:260-298)."""
+        self._check_ref(ref_id)
+        if remove:
+            self.ops.append((abi.OP_REF_REMOVE, 0, 0, 0, 0, 0, 0, 0, int(ref_id), 0))
+        self.free_refs.append(int(ref_id))
+
+    def _check_ref(self, ref_id: int) -> None:
+        if not 0 <= ref_id < self.n_refs or ref_id in self.free_refs:
+            raise ValueError(f"no local reference {ref_id}")
 
     def ack_ref(self, ref_id: int) -> None:
         """IntervalCollection.ackInterval for one endpoint reference (MTR_OP_REF_ACK, include/mtr_types.h)."""
-        if not 0 <= ref_id < self.n_refs:
-            raise ValueError(f"no local reference {ref_id}")
+        self._check_ref(ref_id)
         self.ops.append((abi.OP_REF_ACK, 0, 0, 0, 0, 0, 0, 0, int(ref_id), 0))
 
     def rebase_position(self, pos: int, seq_from: int, local_seq: int) -> int:
@@ -427,8 +449,7 @@ class DocLog:
 
     def remove_ref(self, ref_id: int) -> None:
         """Client.removeLocalReferencePosition (client.ts:394-396)."""
-        if not 0 <= ref_id < self.n_refs:
-            raise ValueError(f"no local reference {ref_id}")
+        self._check_ref(ref_id)
         self.ops.append((abi.OP_REF_REMOVE, 0, 0, 0, 0, 0, 0, 0, int(ref_id), 0))
 
     def local_op(self, op: dict, interner: Interner) -> None:

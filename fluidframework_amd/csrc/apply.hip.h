@@ -2580,7 +2580,15 @@ struct Eng {
     // when no segment holds the position
     static MTR_DI void ref_create(D& L, const KParams& P, St& s, const mtr_op& op) {
         const int n = nrefs(L);
-        if (!rf_uid(L) || n >= uni(L.sc->refcap)) {
+        int id = n;  // numbered by creation, or (MTR_REF_SLOT) a slot the host recycles
+        if (op.payload2 & MTR_REF_SLOT) {
+            id = op.pos2;
+            if (id < 0 || id > n || (id < n && rf_uid(L) && (uniu(rf_ty(L)[id]) & RF_HELD))) {
+                s.status = MTR_ERR_BAD_OP;  // (a slot some segment's collection still holds)
+                return;
+            }
+        }
+        if (!rf_uid(L) || id >= uni(L.sc->refcap)) {
             s.status = MTR_ERR_CAPACITY;
             return;
         }
@@ -2625,10 +2633,10 @@ struct Eng {
             }
         }
         if (lane_id() == 0) {
-            rf_uid(L)[n] = u;
-            rf_off(L)[n] = uint32_t(off);
-            rf_ty(L)[n] = tw;
-            L.sc->nrefs = n + 1;
+            rf_uid(L)[id] = u;
+            rf_off(L)[id] = uint32_t(off);
+            rf_ty(L)[id] = tw;
+            if (id == n) L.sc->nrefs = n + 1;
         }
         wsync();
     }

@@ -189,6 +189,16 @@ class Collection:
         """removeExistingInterval (:1015-1021)."""
         del self.by_id[iv.id()]
 
+    @staticmethod
+    def _release(log, iv: Interval, keep: Interval | None = None) -> None:
+        """The endpoint references of `iv` that nothing reads again -- an interval a delete dropped, or the endpoints
+        a change superseded (those `keep`, the changed interval, does not share) -- go back for reuse
+        (DocLog.release_ref).  The reference leaves them in their segments' collections (removeExistingInterval
+        only drops the index entries and listeners, :1007-1021), where nothing observes them."""
+        for r in (iv.start, iv.end):
+            if keep is None or r not in (keep.start, keep.end):
+                log.release_ref(r)
+
     def attach(self, log) -> None:
         """attachGraph (:1531-1579): the saved intervals, created from the snapshot (local view,
         SlideOnRemove endpoints), in order."""
@@ -228,12 +238,13 @@ class Collection:
             raise IntervalUnsupported("an interval without an id (a random uuid)")
         self._add(iv)
 
-    def ack_delete(self, si: dict) -> None:
+    def ack_delete(self, log, si: dict) -> None:
         """ackDelete of a remote op (:2187-2208)."""
         i = ensure_serialized_id(si).get(INTERVAL_ID)
         iv = self.by_id.get(i) if isinstance(i, str) else None  # Map.get with the raw id
         if iv is not None:
             self._remove(iv)
+            self._release(log, iv)
 
     def ack_change(self, log, si: dict, msg: dict) -> None:
         """ackChange of a remote op (:1859-1932): changeInterval (modify, :600-656: a new reference for each
@@ -264,6 +275,7 @@ class Collection:
             nv = Interval(s, e, iv.itype, dict(iv.props), "op")  # propertyManager.copyTo
             self._remove(iv)
             self._add(nv)
+            self._release(log, iv, keep=nv)
             iv = nv
         add_props(iv.props, new_props)
 
@@ -353,6 +365,7 @@ class Collection:
         self._remove(iv)
         ser = {"end": keys[iv.end][0], "intervalType": iv.itype, "sequenceNumber": live.current_seq,
                "start": keys[iv.start][0], "properties": iv.props}
+        self._release(live.log, iv)
         lseq = live.next_local_seq()
         live.submit({"key": self.label, "type": "act", "value": {"opName": "delete", "value": ser}}, {"localSeq": lseq})
         return iv
@@ -398,6 +411,7 @@ class Collection:
         iv.pm.copy_to(iv.props, nv.props, nv.pm)
         self._remove(iv)
         self._add(nv)
+        self._release(live.log, iv, keep=nv)
         return nv
 
     def live_change(self, live, iid: Any, start: Any = _UNDEF, end: Any = _UNDEF) -> Interval | None:
@@ -455,7 +469,7 @@ class Collection:
             return
         if name == "delete":
             if not local:
-                self.ack_delete(si)
+                self.ack_delete(live.log, si)
             return
         # change
         if local:
@@ -726,7 +740,7 @@ class IntervalCollections:
         if name == "add":
             c.ack_add(log, params, msg)
         elif name == "delete":
-            c.ack_delete(params)
+            c.ack_delete(log, params)
         else:
             c.ack_change(log, params, msg)
 

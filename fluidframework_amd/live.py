@@ -286,22 +286,45 @@ class LiveIntervalCollection:
         """[Symbol.iterator]: the start tree's in-order walk (compare order)."""
         return iter(self.coll.ordered(self.client.ref_keys()))
 
-    def _transient(self, start: int, end: int) -> tuple[int, int]:
+    def _transient_keys(self, start: int, end: int) -> tuple[list, tuple, tuple]:
         """helpers.create("transient", start, end, client, Transient) -> two Transient references at the local view
-        (detached when no segment holds the position)"""
+        (detached when no segment holds the position); returns the document's reference keys (one sync) and the two
+        transients' compare keys.  A Transient reference is held by no segment's collection (localReference.ts:
+        260-298), so once its key is read its id goes back to the host's free list with no record: queries take no
+        reference slot."""
         log = self.client.log
-        return (log.create_ref(int(start), abi.REFTYPE_TRANSIENT), log.create_ref(int(end), abi.REFTYPE_TRANSIENT))
+        ts, te = log.create_ref(int(start), abi.REFTYPE_TRANSIENT), log.create_ref(int(end), abi.REFTYPE_TRANSIENT)
+        keys = self.client.ref_keys()
+        ks, ke = _ref_key(keys, ts), _ref_key(keys, te)
+        log.release_ref(te, remove=False)
+        log.release_ref(ts, remove=False)
+        return keys, ks, ke
 
     def find_overlapping_intervals(self, start: int, end: int) -> list:
         """findOverlappingIntervals (:950-964): the intervals overlapping [start, end] (SequenceInterval.overlaps,
         :544-549), in the tree's order (RedBlackTree.gather, rbTree.ts:174-199)."""
-        if end < start or not self.coll.by_id:
-            return []
-        ts, te = self._transient(start, end)
+        return self.find_overlapping_intervals_many([(start, end)])[0]
+
+    def find_overlapping_intervals_many(self, ranges) -> list:
+        """findOverlappingIntervals for each (start, end) of `ranges`, answered from one engine sync: every query's
+        Transient references are created in one batch and their keys read together."""
+        ranges = [(int(a), int(b)) for a, b in ranges]
+        live = [k for k, (a, b) in enumerate(ranges) if b >= a and self.coll.by_id]
+        out: list = [[] for _ in ranges]
+        if not live:
+            return out
+        log = self.client.log
+        refs = [(log.create_ref(ranges[k][0], abi.REFTYPE_TRANSIENT), log.create_ref(ranges[k][1], abi.REFTYPE_TRANSIENT))
+                for k in live]
         keys = self.client.ref_keys()
-        ks, ke = _ref_key(keys, ts), _ref_key(keys, te)
-        return [iv for iv in self.coll.ordered(keys)
-                if _ref_key(keys, iv.start) <= ke and _ref_key(keys, iv.end) >= ks]
+        ordered = self.coll.ordered(keys)
+        for k, (ts, te) in zip(live, refs):
+            ks, ke = _ref_key(keys, ts), _ref_key(keys, te)
+            out[k] = [iv for iv in ordered if _ref_key(keys, iv.start) <= ke and _ref_key(keys, iv.end) >= ks]
+        for ts, te in reversed(refs):
+            log.release_ref(te, remove=False)
+            log.release_ref(ts, remove=False)
+        return out
 
     def _by_end(self, keys: list) -> list:
         """the end tree's keys (compareSequenceIntervalEnds, :1168-1169): one node per end; two intervals with equal
@@ -314,9 +337,7 @@ class LiveIntervalCollection:
 
     def previous_interval(self, pos: int) -> Interval | None:
         """previousInterval (:966-978): endIntervalTree.floor of a transient (pos, pos)."""
-        _, te = self._transient(pos, pos)
-        keys = self.client.ref_keys()
-        k = _ref_key(keys, te)
+        keys, _, k = self._transient_keys(pos, pos)
         best = None
         for iv in self._by_end(keys):
             if _ref_key(keys, iv.end) <= k:
@@ -325,9 +346,7 @@ class LiveIntervalCollection:
 
     def next_interval(self, pos: int) -> Interval | None:
         """nextInterval (:980-992): endIntervalTree.ceil of a transient (pos, pos)."""
-        _, te = self._transient(pos, pos)
-        keys = self.client.ref_keys()
-        k = _ref_key(keys, te)
+        keys, _, k = self._transient_keys(pos, pos)
         for iv in self._by_end(keys):
             if _ref_key(keys, iv.end) >= k:
                 return iv
@@ -340,14 +359,12 @@ class LiveIntervalCollection:
         if start is None and end is None:
             out = self.coll.ordered(keys)
             return out if forward else out[::-1]
-        ts, te = self._transient(start if start is not None else 0, end if end is not None else 0)
-        keys = self.client.ref_keys()
+        keys, ks, ke = self._transient_keys(start if start is not None else 0, end if end is not None else 0)
         out = self.coll.ordered(keys)
         if start is None:
-            out = [iv for iv in out if _ref_key(keys, iv.end) == _ref_key(keys, te)]
+            out = [iv for iv in out if _ref_key(keys, iv.end) == ke]
         elif end is None:
-            out = [iv for iv in out if _ref_key(keys, iv.start) == _ref_key(keys, ts)]
+            out = [iv for iv in out if _ref_key(keys, iv.start) == ks]
         else:
-            out = [iv for iv in out if _ref_key(keys, iv.start) == _ref_key(keys, ts) and
-                   _ref_key(keys, iv.end) == _ref_key(keys, te)]
+            out = [iv for iv in out if _ref_key(keys, iv.start) == ks and _ref_key(keys, iv.end) == ke]
         return out if forward else out[::-1]

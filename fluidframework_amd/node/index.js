@@ -35,7 +35,7 @@ function native() {
 const OP = { INSERT: 0, REMOVE: 1, ANNOTATE: 2, SEQ: 3, LOCAL_INSERT: 8, LOCAL_REMOVE: 9, LOCAL_ANNOTATE: 10,
     START_COLLAB: 12, LOAD: 13, SETCELL: 14, RELPOS: 15, ACK: 17, ROLLBACK: 18, REGENERATE: 19, REF_CREATE: 20, REF_REMOVE: 21,
     REF_ACK: 24, REBASE_POS: 25, LSEQ: 26 };
-const REF = { SLIDE: 1, LOCALVIEW: 2, LSEQ: 4 };  // MTR_OP_REF_CREATE payload2
+const REF = { SLIDE: 1, LOCALVIEW: 2, LSEQ: 4, SLOT: 8 };  // MTR_OP_REF_CREATE payload2
 const DELTA_REBASE = 80;
 const DetachedReferencePosition = -1;   // referencePositions.ts:103
 const DELTA_REGEN = 64, DELTA_REGEN_X = 72;
@@ -206,7 +206,8 @@ class DocLog {
         this.ops = []; this.text = []; this.collaborating = false;
         // MergeTree.idToSegment (mergeTree.ts:549,668) as the host sees it: id key -> marker ordinal
         this.nMarkers = 0; this.markerIds = new Map(); this.markerDup = new Set(); this.markerIdAnnotated = false;
-        this.nRefs = 0;  // local references created (MTR_OP_REF_CREATE ids)
+        this.nRefs = 0;  // reference ids handed out (MTR_OP_REF_CREATE ids; high-water mark)
+        this.freeRefs = [];  // ids released for reuse (MTR_REF_SLOT), a stack
         this.currentSeq = 0;  // collabWindow.currentSeq as the host sees it (interval ops do not move it)
         this.intervals = undefined;  // ./intervals.js IntervalCollections, when used
     }
@@ -316,15 +317,26 @@ class DocLog {
             flags = 0;
         }
         if (slide) flags |= REF.SLIDE;
-        this.push(OP.REF_CREATE, 0, short, 0, ref, 0, pos, 0, refType, flags);
-        return this.nRefs++;
+        const id = this._newRefId();
+        this.push(OP.REF_CREATE, 0, short, 0, ref, 0, pos, id, refType, flags | REF.SLOT);
+        return id;
     }
+    _newRefId() { return this.freeRefs.length ? this.freeRefs.pop() : this.nRefs++; }
     removeRef(id) { this.push(OP.REF_REMOVE, 0, 0, 0, 0, 0, 0, 0, id, 0); }
+    // the host is done with reference `id`: its id is reused by the next create (MTR_REF_SLOT); remove: a reference a
+    // segment's collection may hold (a superseded or deleted interval endpoint) is removed first, a Transient query
+    // reference needs no record (fluidframework_amd/batch.py DocLog.release_ref)
+    releaseRef(id, remove = true) {
+        if (!(id >= 0 && id < this.nRefs) || this.freeRefs.includes(id)) throw new Error('no local reference ' + id);
+        if (remove) this.removeRef(id);
+        this.freeRefs.push(id);
+    }
     // createPositionReference with a localSeq (a rebase's changeInterval): getContainingSegment(pos, undefined,
     // localSeq) -- this client's view at (refSeq, localSeq) -- then createLocalReferencePosition
     createRefAt(pos, refType, refSeq, localSeq) {
-        this.push(OP.REF_CREATE, 0, 0, 0, refSeq, localSeq, pos, 0, refType, REF.LSEQ);
-        return this.nRefs++;
+        const id = this._newRefId();
+        this.push(OP.REF_CREATE, 0, 0, 0, refSeq, localSeq, pos, id, refType, REF.LSEQ | REF.SLOT);
+        return id;
     }
     ackRef(id) { this.push(OP.REF_ACK, 0, 0, 0, 0, 0, 0, 0, id, 0); }  // IntervalCollection.ackInterval, one endpoint
     // rebasePositionWithSegmentSlide(pos, seqNumberFrom, localSeq): returns the record index its result names
@@ -1079,10 +1091,29 @@ class BatchReplayClient {
         this.log.intervals.live = true;
         const run = (fn) => { const r = this.log._intervals(fn); this.engine.dirty = true; return r; };
         const self = this;
-        const transient = (start, end) => {
-            const ts = self.log.createRef(start, 0x100, undefined, false), te = self.log.createRef(end, 0x100, undefined, false);
+        // helpers.create("transient", ...): two Transient references at the local view; their compare keys are read
+        // with the document's (one sync), then the ids go back to the free list -- a Transient reference is held by no
+        // segment's collection (localReference.ts:260-298), so queries take no reference slot
+        const transientKeys = (ranges) => {
+            const ids = ranges.map(([a, b]) => [self.log.createRef(a, 0x100, undefined, false),
+                self.log.createRef(b, 0x100, undefined, false)]);
             self.engine.dirty = true;
-            return [ts, te];
+            const keys = self.refKeys();
+            const out = self.log._intervals(() => ids.map(([ts, te]) => [refKey(keys, ts), refKey(keys, te)]));
+            for (let k = ids.length - 1; k >= 0; k--) {
+                self.log.releaseRef(ids[k][1], false);
+                self.log.releaseRef(ids[k][0], false);
+            }
+            return [keys, out];
+        };
+        // the end tree (compareSequenceIntervalEnds, :1168-1169): one node per end; two intervals with equal ends
+        // share a node that holds the later-put one -- a history this host does not keep, so it refuses
+        const byEnd = (keys) => {
+            const ivs = [...c.byId.values()].map((iv) => [refKey(keys, iv.end), iv]).sort((x, y) => cmpKey(x[0], y[0]));
+            for (let k = 1; k < ivs.length; k++) {
+                if (cmpKey(ivs[k - 1][0], ivs[k][0]) === 0) throw new IntervalUnsupported('two intervals with one end: the end tree keeps one node for them');
+            }
+            return ivs;
         };
         return {
             add: (start, end, intervalType, props) => run(() => c.liveAdd(self, start, end, intervalType, props)),
@@ -1094,14 +1125,59 @@ class BatchReplayClient {
             positions(iv, keys) { const k = keys || self.refKeys(); return [k[4 * iv.start], k[4 * iv.end]]; },
             [Symbol.iterator]() { return self.log._intervals(() => c.ordered(self.refKeys()))[Symbol.iterator](); },
             findOverlappingIntervals(start, end) {  // :950-964 (SequenceInterval.overlaps in tree order)
-                if (end < start || c.byId.size === 0) return [];
-                const [ts, te] = transient(start, end);
-                const keys = self.refKeys();
+                return this.findOverlappingIntervalsMany([[start, end]])[0];
+            },
+            /** findOverlappingIntervals for each [start, end] of `ranges`, from one engine sync */
+            findOverlappingIntervalsMany(ranges) {
+                const live = ranges.map((r, k) => k).filter((k) => ranges[k][1] >= ranges[k][0] && c.byId.size > 0);
+                const out = ranges.map(() => []);
+                if (live.length === 0) return out;
+                const [keys, tk] = transientKeys(live.map((k) => ranges[k]));
                 return self.log._intervals(() => {
-                    const ks = refKey(keys, ts), ke = refKey(keys, te);
-                    return c.ordered(keys).filter((iv) => cmpKey(refKey(keys, iv.start), ke) <= 0 && cmpKey(refKey(keys, iv.end), ks) >= 0);
+                    const ordered = c.ordered(keys);
+                    live.forEach((k, q) => {
+                        const [ks, ke] = tk[q];
+                        out[k] = ordered.filter((iv) => cmpKey(refKey(keys, iv.start), ke) <= 0 && cmpKey(refKey(keys, iv.end), ks) >= 0);
+                    });
+                    return out;
                 });
             },
+            previousInterval(pos) {  // :966-978: endIntervalTree.floor of a transient (pos, pos)
+                const [keys, tk] = transientKeys([[pos, pos]]);
+                return self.log._intervals(() => {
+                    const k = tk[0][1];
+                    let best;
+                    for (const [e, iv] of byEnd(keys)) if (cmpKey(e, k) <= 0) best = iv;
+                    return best;
+                });
+            },
+            nextInterval(pos) {  // :980-992: endIntervalTree.ceil of a transient (pos, pos)
+                const [keys, tk] = transientKeys([[pos, pos]]);
+                return self.log._intervals(() => {
+                    const k = tk[0][1];
+                    for (const [e, iv] of byEnd(keys)) if (cmpKey(e, k) >= 0) return iv;
+                    return undefined;
+                });
+            },
+            // the positional iterators (:2232-2331, gatherIterationResults :864-944): the intervals whose start (and
+            // end) compare equal to a transient interval's, forward or backward in the tree's order
+            gather(forward = true, start, end) {
+                if (start === undefined && end === undefined) {
+                    const out = self.log._intervals(() => c.ordered(self.refKeys()));
+                    return forward ? out : out.reverse();
+                }
+                const [keys, tk] = transientKeys([[start !== undefined ? start : 0, end !== undefined ? end : 0]]);
+                const [ks, ke] = tk[0];
+                let out = self.log._intervals(() => c.ordered(keys));
+                if (start === undefined) out = out.filter((iv) => cmpKey(refKey(keys, iv.end), ke) === 0);
+                else if (end === undefined) out = out.filter((iv) => cmpKey(refKey(keys, iv.start), ks) === 0);
+                else out = out.filter((iv) => cmpKey(refKey(keys, iv.start), ks) === 0 && cmpKey(refKey(keys, iv.end), ke) === 0);
+                return forward ? out : out.reverse();
+            },
+            CreateForwardIteratorWithStartPosition(pos) { return this.gather(true, pos, undefined)[Symbol.iterator](); },
+            CreateBackwardIteratorWithStartPosition(pos) { return this.gather(false, pos, undefined)[Symbol.iterator](); },
+            CreateForwardIteratorWithEndPosition(pos) { return this.gather(true, undefined, pos)[Symbol.iterator](); },
+            CreateBackwardIteratorWithEndPosition(pos) { return this.gather(false, undefined, pos)[Symbol.iterator](); },
         };
     }
     /** The summary's `header` blob (summarizeCore, sequence.ts:467-480), undefined when there are no collections. */

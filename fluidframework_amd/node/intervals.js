@@ -150,6 +150,10 @@ class Collection {
         this.byId.set(i, iv);
     }
     _remove(iv) { this.byId.delete(iv.id()); }
+    // the endpoint references nothing reads again (a deleted interval's, those a change superseded) go back for reuse
+    static _release(log, iv, keep) {
+        for (const r of [iv.start, iv.end]) if (!keep || (r !== keep.start && r !== keep.end)) log.releaseRef(r);
+    }
     attach(log) {  // attachGraph (:1531-1579)
         const saved = this.saved || [];
         this.saved = undefined;
@@ -179,10 +183,13 @@ class Collection {
         if (iv.props[INTERVAL_ID] === undefined) throw new IntervalUnsupported('an interval without an id (a random uuid)');
         this._add(iv);
     }
-    ackDelete(si) {  // :2187-2208
+    ackDelete(log, si) {  // :2187-2208
         const i = ensureSerializedId(si)[INTERVAL_ID];
         const iv = typeof i === 'string' ? this.byId.get(i) : undefined;
-        if (iv !== undefined) this._remove(iv);
+        if (iv !== undefined) {
+            this._remove(iv);
+            Collection._release(log, iv);
+        }
     }
     ackChange(log, si, msg) {  // :1859-1932
         const props = si.properties && typeof si.properties === 'object' ? si.properties : {};
@@ -201,6 +208,7 @@ class Collection {
             const nv = new Interval(s, e, iv.itype, Object.assign({}, iv.props), 'op');  // modify + copyTo (:600-656)
             this._remove(iv);
             this._add(nv);
+            Collection._release(log, iv, nv);
             iv = nv;
         }
         addProps(iv.props, newProps);
@@ -255,6 +263,7 @@ class Collection {
         this._remove(iv);
         const ser = { end: keys[4 * iv.end], intervalType: iv.itype, sequenceNumber: live.currentSeq,
             start: keys[4 * iv.start], properties: iv.props };
+        Collection._release(live.log, iv);
         live.emit(this.label, 'delete', ser, { localSeq: live.nextLocalSeq() });
         return iv;
     }
@@ -288,6 +297,7 @@ class Collection {
         iv.pm.copyTo(iv.props, nv.props, nv.pm);
         this._remove(iv);
         this._add(nv);
+        Collection._release(live.log, iv, nv);
         return nv;
     }
     liveChange(live, id, start, end) {  // IntervalCollection.change (:1761-1793)
@@ -326,7 +336,7 @@ class Collection {
             if (iv !== undefined) this.ackInterval(live, iv);
             return undefined;
         }
-        if (name === 'delete') { if (!local) this.ackDelete(si); return undefined; }
+        if (name === 'delete') { if (!local) this.ackDelete(live.log, si); return undefined; }
         if (local) {
             this._lseqMap(false).delete(meta.localSeq);
             this._removePendingChange(si);
@@ -451,7 +461,7 @@ class IntervalCollections {
         if (!params || typeof params !== 'object') throw new IntervalUnsupported('interval op parameters');
         const si = Object.assign({}, params);
         if (name === 'add') c.ackAdd(log, si, msg);
-        else if (name === 'delete') c.ackDelete(si);
+        else if (name === 'delete') c.ackDelete(log, si);
         else c.ackChange(log, si, msg);
     }
     serialize(states, currentSeq) {  // summarizeCore's header blob (sequence.ts:467-480); undefined when none

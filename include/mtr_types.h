@@ -76,7 +76,12 @@ enum {
                                    offset, payload = ReferenceType, client.ts:377-389 -> mergeTree.ts:2209-2226), as
                                    sequence/src/intervalCollection.ts:668-724 createPositionReference does; no
                                    segment = a detached reference (createDetachedLocalReferencePosition).  The
-                                   document's references are numbered by creation, from 0. */
+                                   document's references are numbered by creation, from 0; with payload2 &
+                                   MTR_REF_SLOT the reference takes id pos2 instead -- a slot the host freed (one
+                                   no segment's collection holds: removed, transient, or never created; else
+                                   MTR_ERR_BAD_OP) or the next new id.  The host recycles ids that way: a removed
+                                   reference, a transient query reference once its key was read, an interval
+                                   endpoint a change superseded (nothing observable reads them again). */
     MTR_OP_REF_REMOVE = 21,     /* Client.removeLocalReferencePosition (client.ts:394-396 -> mergeTree.ts:2190-2207) of
                                    reference payload */
     MTR_OP_LOCAL_SETCELL = 22,  /* SharedMatrix.setCell of the local client (matrix.ts:202-310, setCellCore -> sendSetCellOp):
@@ -124,7 +129,7 @@ enum { MTR_REL_BEFORE = 1, MTR_REL_OFFSET = 2 };
  * local client's view at (ref_seq, localSeq = min_seq) -- getContainingSegment(pos, undefined, localSeq), whose
  * lengths are localNetLength(segment, refSeq, localSeq), mergeTree.ts:636-662 (IntervalCollection.rebaseLocalInterval's
  * changeInterval, intervalCollection.ts:2019-2025 -> createPositionReference with a localSeq, :697-724) */
-enum { MTR_REF_SLIDE = 1, MTR_REF_LOCALVIEW = 2, MTR_REF_LSEQ = 4 };
+enum { MTR_REF_SLIDE = 1, MTR_REF_LOCALVIEW = 2, MTR_REF_LSEQ = 4, MTR_REF_SLOT = 8 };
 enum {
     MTR_REFTYPE_SIMPLE = 0x0,
     MTR_REFTYPE_TILE = 0x1,

@@ -851,21 +851,31 @@ class Tree {
     }
     // MergeTree.createLocalReferencePosition (mergeTree.ts:2209-2226) -> createLocalRef / addLocalRef
     // (localReference.ts:260-298); a null segment is createDetachedLocalReferencePosition (:123-127)
-    int createRef(Seg* seg, int offset, int refType) {
+    // slot >= 0: the id the host recycles (MTR_REF_SLOT, include/mtr_types.h) -- one no collection holds, or the next
+    int createRef(Seg* seg, int offset, int refType, int slot = -1) {
         const int excl = !!(refType & kTransient) + !!(refType & kSlide) + !!(refType & kStay);
         if (excl > 1) return MTR_ERR_BAD_OP;  // _validateReferenceType's UsageError (:23-39)
         LRef r;
         r.refType = refType;
-        const int id = int(refs.size());
+        const int id = slot >= 0 ? slot : int(refs.size());
+        if (id > int(refs.size())) return MTR_ERR_BAD_OP;
+        if (id < int(refs.size())) {
+            const LRef& o = refs[size_t(id)];
+            if (o.segment && o.segment->localRefs && refsHas(o.segment->localRefs, id)) return MTR_ERR_BAD_OP;
+        }
+        auto put = [&](const LRef& x) {
+            if (id == int(refs.size())) refs.push_back(x);
+            else refs[size_t(id)] = x;
+        };
         if (!seg) {
-            refs.push_back(r);
+            put(r);
             return status;
         }
         if (removedAndAcked(seg) && !(refType & (kSlide | kTransient))) return MTR_ERR_BAD_OP;  // UsageError
         if (!seg->localRefs) seg->localRefs = newLocalRefs(seg, size_t(seg->len));
         r.segment = seg;
         r.offset = offset;
-        refs.push_back(r);
+        put(r);
         if (!(refType & kTransient)) {
             if (offset >= seg->len) return MTR_ERR_ASSERT | 0x348;  // "offset cannot be beyond segment length"
             RefsAtOffset& slot = refSlot(seg->localRefs, offset);
@@ -1930,7 +1940,7 @@ class Tree {
                         s = t;
                     }
                 }
-                return createRef(s, off, int(op.payload));
+                return createRef(s, off, int(op.payload), (op.payload2 & MTR_REF_SLOT) ? (op.pos2 < 0 ? INT32_MAX : op.pos2) : -1);
             }
             case MTR_OP_REF_REMOVE: {  // MergeTree.removeLocalReferencePosition, mergeTree.ts:2190-2207
                 if (op.payload >= refs.size()) return MTR_ERR_BAD_OP;

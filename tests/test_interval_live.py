@@ -843,3 +843,80 @@ def test_rebasing_interval_slides_off_end(kind):  # :103-125
     rs[0].connected = True
     f.process_all()
     assert_consistent(rs)
+
+
+# ---------------------------------------------------------------- reference lifetimes (VERDICT r05 Missing #2)
+class Lcg:
+    """A tiny PRNG both hosts restate (tests/node/interval_live.js `churn`), so the Node run can be held to this one."""
+
+    def __init__(self, seed):
+        self.x = seed & 0x7fffffff
+
+    def next(self, n):
+        self.x = (self.x * 1103515245 + 12345) & 0x7fffffff
+        return (self.x >> 8) % n
+
+
+def churn(f, rounds, labels=("t",)):
+    """Two clients change interval endpoints, query (findOverlappingIntervals, gather) and edit text every round;
+    returns per round both clients' text and interval positions.  Every change supersedes an endpoint reference and
+    every query makes two Transient ones: the host must recycle their ids (DocLog.release_ref) or a fixed-size engine
+    reference table runs out (MTR_ERR_CAPACITY)."""
+    r1, r2 = f.runtime("1"), f.runtime("2")
+    s1, s2 = r1.dds, r2.dds
+    s1.insert_text(0, "abcdefghijklmnopqrstuvwxyz" * 3)
+    f.process_all()
+    cs = [(s1, s1.get_interval_collection(lb), s2, s2.get_interval_collection(lb)) for lb in labels]
+    ids = []
+    for a, ca, _, _ in cs:
+        ids.append([ca.add(i, i + 4, SLIDE).id() for i in range(0, 60, 12)])
+    f.process_all()
+    g = Lcg(20240611)
+    out = []
+    for rd in range(rounds):
+        for k, (a, ca, b, cb) in enumerate(cs):
+            for s, c in ((a, ca), (b, cb)):
+                n = s.get_length()
+                lo = g.next(n)
+                c.change(ids[k][g.next(len(ids[k]))], lo, lo + g.next(n - lo))
+                q = g.next(n)
+                got = c.find_overlapping_intervals(q, q + 3)
+                assert all(iv.id() is not None for iv in got)
+                c.gather(True, q, None)
+                if g.next(10) < 3:
+                    s.insert_text(g.next(n), "xy")
+                if g.next(10) < 3 and s.get_length() > 20:
+                    p = g.next(s.get_length() - 2)
+                    s.remove_range(p, p + 2)
+        if rd % 3 == 2 or rd == rounds - 1:
+            f.process_all()
+            assert_consistent([r1, r2])
+            out.append((s1.get_text(), [positions(s1, ca) for _, ca, _, _ in cs]))
+    return out, (s1, s2)
+
+
+def test_reference_ids_recycled_oracle():
+    """On the oracle: 400 endpoint changes and 400 queries leave the host's reference-id high-water mark near the
+    live endpoints' count instead of growing by two per change and two per query."""
+    out, (s1, s2) = churn(factory("oracle"), 100)
+    assert len(out) == 34
+    for s in (s1, s2):
+        assert s.log.n_refs <= 40, s.log.n_refs  # (10 live endpoints + the transients and superseded ones in flight)
+
+
+@pytest.mark.gpu
+def test_reference_churn_on_a_small_engine_table():
+    """VERDICT r05 Next #3: 10 x ref_slots interval changes plus overlap / gather queries on one live document of an
+    engine whose reference table holds 64 ids: every document stays OK and every client's intervals equal the
+    oracle-driven run's after every processAllMessages."""
+    from fluidframework_amd.engine import Engine
+    from fluidframework_amd.live import EngineExecutor
+
+    eng = Engine(4, max_segments=4096, heap_entries=4096, text_units=1 << 16, prop_words=1 << 14,
+                 remover_cells=1 << 12, ref_slots=64)
+    got, (s1, _) = churn(Factory(EngineExecutor(eng)), 160)
+    want, _ = churn(factory("oracle"), 160)
+    assert got == want
+    for d in range(2):
+        assert eng.status(d)[0] == 0
+    assert s1.log.n_refs <= 64

@@ -570,3 +570,19 @@ def test_live_legacy_catchup_through_node_host(tmp_path):
         exp = r.dds.summary()
         assert got[0][0] == "header" and got[-1][0] == "catchupOps"
         assert [v.encode() for _, v in got] == exp
+
+
+@pytest.mark.gpu
+def test_reference_churn_through_node_host():
+    """Reference-id recycling through the Node host (VERDICT r05 Next #3): tests/node/interval_churn.js runs
+    test_interval_live.churn's script (same PRNG) on an engine whose reference table holds 64 ids -- 320 endpoint
+    changes and 320 queries per client; every checkpoint's text and interval positions equal the oracle-driven
+    Python run's, and the id high-water mark stays within the table."""
+    from mock_runtime import Factory, OracleExecutor
+    from test_interval_live import churn
+
+    _addon()
+    res = json.loads(_node([os.path.join(HERE, "node", "interval_churn.js"), "160"], timeout=600))
+    want, _ = churn(Factory(OracleExecutor()), 160)
+    assert [[t, [[list(p) for p in ps] for ps in pss]] for t, pss in want] == res["out"]
+    assert max(res["nRefs"]) <= 64
