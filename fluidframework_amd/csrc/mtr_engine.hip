@@ -138,6 +138,16 @@ struct mtr_engine {
     std::vector<uint32_t> h_val_eq;  // host copy for export hashes
     int64_t out_total = 0;
     bool summarized = false;
+    // pipelined hand-over (mtr_submit_pipelined): the copy stream, per part its landing event, document range and
+    // op-scan bits (device, then page-locked host copy)
+    hipStream_t copy = nullptr;
+    std::vector<hipEvent_t> part_ev;
+    std::vector<uint32_t> part_lo;
+    uint32_t pipe_parts = 0;
+    DevBuf<int32_t> pflags;
+    int32_t* h_pflags = nullptr;
+    uint32_t h_pflags_n = 0;
+    DevBuf<mtr_doc_desc> pdocs;  // the descriptors as uploaded (part_ready_kernel enables them)
     // timing
     double t_apply = 0, t_summary = 0;
     double t_kernels = 0;  // sum of the apply launches' own durations (they overlap across lanes)
@@ -167,6 +177,27 @@ __global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_
             h[d].fail_op = 0;
         }
     }
+}
+
+// mtr_submit_pipelined: the documents [lo, hi) of part p have landed; enable them (copy the descriptor, op_count
+// last, after a fence: classify_kernel reads op_count and a launch the rest) unless the part's op scan found
+// records the pipelined path does not run (they then never start; mtr_run reports MTR_ERR_UNSUPPORTED)
+__global__ void part_ready_kernel(DocHdr* h, mtr_doc_desc* docs, const mtr_doc_desc* src, uint32_t lo, uint32_t hi,
+                                  const int32_t* flags) {
+    const uint32_t d = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= hi || *flags != 0) return;
+    mtr_doc_desc x = src[d];
+    h[d].op_cursor = 0;
+    h[d].dused = 0;
+    if (x.n_clients > MTR_MAX_CLIENTS && h[d].status == MTR_OK) {  // (cursor_reset_kernel's check)
+        h[d].status = MTR_ERR_UNSUPPORTED;
+        h[d].fail_op = 0;
+    }
+    const uint32_t cnt = x.op_count;
+    x.op_count = 0;
+    docs[d] = x;
+    __threadfence();
+    docs[d].op_count = cnt;
 }
 
 // bit 3: local-reference records (MTR_OP_REF_*, and an interval collection's MTR_OP_REBASE_POS / MTR_OP_LSEQ)
@@ -403,6 +434,15 @@ int mtr_engine_destroy(mtr_engine* e) {
             (void)hipStreamSynchronize(x);
             (void)hipStreamDestroy(x);
         }
+    for (auto& x : e->part_ev)
+        if (x) (void)hipEventDestroy(x);
+    e->pflags.release();
+    e->pdocs.release();
+    if (e->h_pflags) (void)hipHostFree(e->h_pflags);
+    if (e->copy) {
+        (void)hipStreamSynchronize(e->copy);
+        (void)hipStreamDestroy(e->copy);
+    }
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return 0;
@@ -528,6 +568,79 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
         cursor_reset_kernel<<<(b->n_docs + 255) / 256, 256, 0, e->stream>>>(e->hdr.p, e->docs.p, b->n_docs);
         HIPCHK(hipGetLastError());
     }
+    e->summarized = false;
+    return MTR_OK;
+}
+
+int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts) {
+    HIPCHK(hipSetDevice(e->device));
+    const uint32_t n = b->n_docs;
+    parts = std::min(parts, n);
+    // documents laid out in order (each one's records and text after the previous one's), no matrix pairs
+    bool plain = parts > 1 && n <= e->max_docs;
+    for (uint32_t d = 1; d < n && plain; d++)
+        plain = b->docs[d].op_begin >= b->docs[d - 1].op_begin + b->docs[d - 1].op_count &&
+                b->docs[d].text_base >= b->docs[d - 1].text_base + b->docs[d - 1].text_count;
+    for (uint32_t d = 0; d < n && plain && d < e->h_kind.size(); d++) plain = e->h_kind[d] == 0;
+    if (!plain) return mtr_submit(e, b);
+    e->n_docs = n;
+    uint32_t mx = 0;
+    for (uint32_t d = 0; d < n; d++) mx = std::max(mx, b->docs[d].op_count);
+    e->max_ops_per_doc = mx;
+    // the tables, as mtr_submit (small)
+    const size_t nkv = b->n_propops ? size_t(b->propop_off[b->n_propops]) * 2 : 0;
+    size_t ncl = 0;
+    for (uint32_t d = 0; d < n; d++) ncl = std::max<size_t>(ncl, size_t(b->docs[d].client_base) + b->docs[d].n_clients);
+    ncl += 1;
+    if (upload(e, e->propop_off, b->propop_off, size_t(b->n_propops) + 1) || upload(e, e->propop_kv, b->propop_kv, nkv) ||
+        upload(e, e->key_off, b->key_off, size_t(b->n_keys) + 1) ||
+        upload(e, e->key_bytes, b->key_bytes, b->n_keys ? size_t(b->key_off[b->n_keys]) : 0) ||
+        upload(e, e->key_index, b->key_index, b->n_keys) || upload(e, e->val_off, b->val_off, size_t(b->n_vals) + 1) ||
+        upload(e, e->val_bytes, b->val_bytes, b->n_vals ? size_t(b->val_off[b->n_vals]) : 0) ||
+        upload(e, e->val_eq, b->val_eq, b->n_vals) || upload(e, e->client_off, b->client_off, ncl) ||
+        upload(e, e->client_bytes, b->client_bytes, size_t(b->client_off[ncl - 1])) || upload(e, e->pdocs, b->docs, n))
+        return -1;
+    e->h_val_eq.assign(b->val_eq, b->val_eq + b->n_vals);
+    e->has_delta = false;
+    e->has_ext = e->pend_seen || e->refs_seen;
+    e->h_doff.assign(size_t(n) + 1, 0);
+    if (e->ops.ensure(b->n_ops) || e->btext.ensure(b->n_text) || e->docs.ensure(n) || e->pflags.ensure(parts)) return -1;
+    // every document starts disabled (op_count 0: classify_kernel passes it over) until its part has landed
+    HIPCHK(hipMemsetAsync(e->docs.p, 0, size_t(n) * sizeof(mtr_doc_desc), e->stream));
+    HIPCHK(hipMemsetAsync(e->pflags.p, 0, size_t(parts) * sizeof(int32_t), e->stream));
+    if (!e->copy) HIPCHK(hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking));
+    while (e->part_ev.size() < parts) {
+        hipEvent_t x;
+        HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        e->part_ev.push_back(x);
+    }
+    if (e->h_pflags_n < parts) {
+        if (e->h_pflags) HIPCHK(hipHostFree(e->h_pflags));
+        HIPCHK(hipHostMalloc((void**)&e->h_pflags, size_t(parts) * sizeof(int32_t), hipHostMallocDefault));
+        e->h_pflags_n = parts;
+    }
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));  // (the copy stream starts after the tables)
+    HIPCHK(hipStreamWaitEvent(e->copy, e->ev[0], 0));
+    e->part_lo.assign(size_t(parts) + 1, 0);
+    for (uint32_t p = 0; p <= parts; p++) e->part_lo[p] = uint32_t(uint64_t(n) * p / parts);
+    for (uint32_t p = 0; p < parts; p++) {
+        const uint32_t lo = e->part_lo[p], hi = e->part_lo[p + 1];
+        const mtr_doc_desc &a = b->docs[lo], &z = b->docs[hi - 1];
+        const uint64_t o0 = a.op_begin, o1 = std::min<uint64_t>(z.op_begin + z.op_count, b->n_ops);
+        const uint64_t t0 = a.text_base, t1 = std::min<uint64_t>(z.text_base + z.text_count, b->n_text);
+        if (o1 > o0) {
+            HIPCHK(hipMemcpyAsync(e->ops.p + o0, b->ops + o0, (o1 - o0) * sizeof(mtr_op), hipMemcpyHostToDevice, e->copy));
+            const uint64_t blocks = std::min<uint64_t>((o1 - o0 + 255) / 256, 4096);
+            op_scan_kernel<<<uint32_t(blocks), 256, 0, e->copy>>>(e->ops.p + o0, o1 - o0, e->pflags.p + p);
+        }
+        if (t1 > t0)
+            HIPCHK(hipMemcpyAsync(e->btext.p + t0, b->text + t0, (t1 - t0) * sizeof(uint16_t), hipMemcpyHostToDevice, e->copy));
+        part_ready_kernel<<<(hi - lo + 255) / 256, 256, 0, e->copy>>>(e->hdr.p, e->docs.p, e->pdocs.p, lo, hi, e->pflags.p + p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(e->h_pflags + p, e->pflags.p + p, sizeof(int32_t), hipMemcpyDeviceToHost, e->copy));
+        HIPCHK(hipEventRecord(e->part_ev[p], e->copy));
+    }
+    e->pipe_parts = parts;
     e->summarized = false;
     return MTR_OK;
 }
@@ -710,7 +823,10 @@ static int run_impl(mtr_engine* e, int gen) {
     // profiles/r04_sched_sweep.json)
     const int class_leaves = class_env > 0 ? class_env
                                            : (any_pair || (e->n_docs >= 4096u && e->n_docs <= 60000u) ? 128 : 64);
-    const int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
+    // (a pipelined hand-over: its parts still landing; a group takes whole parts)
+    const uint32_t PP = gen ? 0u : e->pipe_parts;
+    int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
+    if (PP) G = std::min<int>(G, int(PP));
     const int L = std::max(1, nlanes / G);  // lanes (streams) per group
     const size_t ncls = 1 + 3 * kAllClasses;
     if (e->cls.ensure(ncls * mtr_engine::kLanes) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
@@ -723,11 +839,20 @@ static int run_impl(mtr_engine* e, int gen) {
     struct Grp {
         uint32_t lo = 0, hi = 0;
         bool done = false;
+        uint32_t p_hi = 0, waited = 0;  // pipelined: the group's parts [waited .. p_hi) not yet waited for
     };
     std::vector<Grp> grp(static_cast<size_t>(G));
     for (int g = 0; g < G; g++) {
-        grp[size_t(g)].lo = uint32_t(uint64_t(e->n_docs) * uint64_t(g) / uint64_t(G));
-        grp[size_t(g)].hi = uint32_t(uint64_t(e->n_docs) * uint64_t(g + 1) / uint64_t(G));
+        Grp& gr = grp[size_t(g)];
+        if (PP) {
+            gr.waited = uint32_t(uint64_t(PP) * uint64_t(g) / uint64_t(G));
+            gr.p_hi = uint32_t(uint64_t(PP) * uint64_t(g + 1) / uint64_t(G));
+            gr.lo = e->part_lo[gr.waited];
+            gr.hi = e->part_lo[gr.p_hi];
+        } else {
+            gr.lo = uint32_t(uint64_t(e->n_docs) * uint64_t(g) / uint64_t(G));
+            gr.hi = uint32_t(uint64_t(e->n_docs) * uint64_t(g + 1) / uint64_t(G));
+        }
     }
     // the groups' lanes start after everything queued on the engine stream (the batch upload)
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
@@ -868,10 +993,17 @@ static int run_impl(mtr_engine* e, int gen) {
         }
         return 0;
     };
+    // pipelined: a group classifies again once the next of its parts has landed (its lane 0 waits for it)
+    auto wait_part = [&](int g) -> int {
+        Grp& gr = grp[size_t(g)];
+        HIPCHK(hipStreamWaitEvent(lane_stream(g, 0), e->part_ev[gr.waited], 0));
+        gr.waited++;
+        return 0;
+    };
     const size_t launches0 = size_t(e->launches);
     HIPCHK(hipEventRecord(e->ev[1], e->stream));  // (timing start: after the forks above)
     for (int g = 0; g < G; g++)
-        if (classify(g)) return -1;
+        if ((PP && wait_part(g)) || classify(g)) return -1;
     int left = G;
     bool stuck = false;
     while (left > 0) {
@@ -885,6 +1017,10 @@ static int run_impl(mtr_engine* e, int gen) {
             progressed = true;
             const int32_t* cls = e->h_cls + size_t(g) * ncls;
             if (cls[0] <= 0) {
+                if (PP && gr.waited < gr.p_hi) {  // more of the group's documents are still landing
+                    if (wait_part(g) || classify(g)) return -1;
+                    continue;
+                }
                 gr.done = true;
                 left--;
                 continue;
@@ -910,6 +1046,17 @@ static int run_impl(mtr_engine* e, int gen) {
         float kms = 0;
         HIPCHK(hipEventElapsedTime(&kms, e->kev[2 * q], e->kev[2 * q + 1]));
         e->t_kernels += kms;
+    }
+    if (PP) {  // the parts' op-scan bits: a part holding records the pipelined path does not run was not started
+        e->pipe_parts = 0;
+        HIPCHK(hipStreamSynchronize(e->copy));
+        for (uint32_t p = 0; p < PP; p++)
+            if (e->h_pflags[p]) {
+                set_err("mtr_submit_pipelined: documents " + std::to_string(e->part_lo[p]) + ".." +
+                        std::to_string(e->part_lo[p + 1]) + " hold records beyond remote ops (MTR_F_DELTA, local ops, "
+                        "local references or rare records); mtr_reset and submit the batch with mtr_submit");
+                return MTR_ERR_UNSUPPORTED;
+            }
     }
     if (stuck) {
         set_err("document exceeds the leaf capacity");

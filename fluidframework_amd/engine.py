@@ -57,6 +57,8 @@ def lib():
             getattr(L, name).restype = C.c_int
         L.mtr_submit.argtypes = [C.c_void_p, C.c_void_p]
         L.mtr_submit.restype = C.c_int
+        L.mtr_submit_pipelined.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
+        L.mtr_submit_pipelined.restype = C.c_int
         L.mtr_get_summary.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]
         L.mtr_get_summary.restype = C.c_int64
         L.mtr_summary_info.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
@@ -183,6 +185,13 @@ class Engine:
     def submit(self, batch):
         self._batch = batch  # keep host arrays alive until the copies completed
         self._check(lib().mtr_submit(self.h, C.addressof(batch.c)), "mtr_submit")
+
+    def submit_pipelined(self, batch, parts=16):
+        """mtr_submit_pipelined: the op records and text go over in `parts` document ranges on a copy stream and the
+        next run() starts each range as soon as it has landed (remote-op batches; see include/mtr.h).  The batch's
+        arrays should be page-locked (Engine.download(..., pinned_memory=True)) for the copies to overlap."""
+        self._batch = batch
+        self._check(lib().mtr_submit_pipelined(self.h, C.addressof(batch.c), int(parts)), "mtr_submit_pipelined")
 
     def run(self):
         self._check(lib().mtr_run(self.h), "mtr_run")

@@ -57,6 +57,17 @@ int mtr_reset(mtr_engine* e);
  * engine document i.  The batch's host arrays may be reused after mtr_sync. */
 int mtr_submit(mtr_engine* e, const mtr_batch* b);
 
+/* mtr_submit with the hand-over pipelined (SURVEY 8d's end-to-end path: a summarizer handing over sequenced
+ * remote messages).  The batch's document descriptors and tables are copied at once; its op records and text
+ * go over in `parts` document ranges on a copy stream, and the next mtr_run starts each range's documents as
+ * soon as their records have landed, so the upload overlaps the apply of the ranges before it.  Same results as
+ * mtr_submit + mtr_run.  The batch's host arrays must stay valid (and, for an overlapped copy, page-locked:
+ * mtr_host_alloc) until mtr_run returns.  Only the remote-op path is pipelined: a range holding MTR_F_DELTA,
+ * local-op, local-reference or rare records (op_scan) is not started, and mtr_run then returns
+ * MTR_ERR_UNSUPPORTED -- mtr_reset and submit that batch with mtr_submit.  Documents must be laid out in order
+ * (each document's op records and text after the previous one's); parts <= 1 is mtr_submit. */
+int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts);
+
 /* Apply the submitted ops (Client.applyMsg for each message, in order, per document). Async. */
 int mtr_run(mtr_engine* e);
 
