@@ -32,7 +32,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "sequenced ops applied/sec (whole node) over 100k docs, bit-exact summaries"
-PIPE_PARTS = 16  # document ranges of the end-to-end leg's pipelined hand-over
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: chip-level parameters)
 SALU_PEAK = 256 * 2.4e9  # scalar instructions per second: one SALU per CU per cycle at the 2.4 GHz peak clock
 
@@ -107,6 +106,8 @@ def parse(argv=None):
     ap.add_argument("--rank-sample-docs", type=int, default=0,
                     help="N>1: documents of its own shard each rank checks against the oracle after the timed "
                          "region (default: about 4M messages' worth; one per host thread for C5)")
+    ap.add_argument("--pipe-parts", type=int, default=16,
+                    help="end-to-end leg: document ranges of the pipelined hand-over (mtr_submit_pipelined)")
     ap.add_argument("--master-port", type=int, default=0, help="--gpus N launcher: rendezvous port (default: a free one)")
     ap.add_argument("--traffic-file", default=None,
                     help="PMC summary of this config (default: profiles/traffic_r05.json for C3, traffic_r05_c5.json "
@@ -127,7 +128,7 @@ def parse(argv=None):
     return a
 
 
-def end_to_end(eng, n, steps, messages, matrix, hashes, barrier=lambda: None):
+def end_to_end(eng, n, steps, messages, matrix, hashes, barrier=lambda: None, pipe_parts=16):
     """SURVEY.md 8d's end-to-end time: the host hands the op logs over (one upload from page-locked
     memory), the engine applies and summarizes, and every blob of every document lands in host memory
     (one bulk download, mtr_get_summaries).  The op logs are the recorded ones, downloaded once
@@ -175,7 +176,7 @@ def end_to_end(eng, n, steps, messages, matrix, hashes, barrier=lambda: None):
         barrier()
         t0 = _t.perf_counter()
         eng.reset()
-        eng.submit_pipelined(hb, PIPE_PARTS)
+        eng.submit_pipelined(hb, pipe_parts)
         eng.run()
         eng.summarize()
         eng.sync()
@@ -202,7 +203,7 @@ def end_to_end(eng, n, steps, messages, matrix, hashes, barrier=lambda: None):
         "ms_per_step": round(1000 * tp, 3),
         "upload_apply_summarize_ms": round(1000 * pdev, 3),
         "download_ms": round(1000 * pdown, 3),
-        "parts": PIPE_PARTS,
+        "parts": pipe_parts,
         "serial": {"value": round(messages / t, 1), "ms_per_step": round(1000 * t, 3), "upload_ms": round(1000 * up, 3),
                    "apply_summarize_ms": round(1000 * dev, 3), "download_ms": round(1000 * down, 3)},
         "upload_bytes": int(hb.ops.nbytes + hb.text.nbytes + hb.docs.nbytes),
@@ -528,7 +529,7 @@ def main(argv=None):
         sample_counts = [rs["checked_docs"], rs["equal"], rs["oracle_errors"]]
     e2e = None
     if a.e2e_steps > 0 and fixture_text is None and not grow:
-        e2e = end_to_end(eng, n, a.e2e_steps, messages, matrix, hashes, barrier=barrier)
+        e2e = end_to_end(eng, n, a.e2e_steps, messages, matrix, hashes, barrier=barrier, pipe_parts=a.pipe_parts)
     if dist is not None:  # the only collectives: counters + summary digests over RCCL/xGMI
         r = shard.reduce_run(dist, reduce_device, elapsed, messages, int(st["bad_docs"]), run_digest,
                              extra=sample_counts)
@@ -617,22 +618,25 @@ def main(argv=None):
                    "capped by VGPRs and LDS per document. HBM sees only stage-in/out and arenas "
                    "(counter_hbm_gbs), so the HBM roofline is the flat-pass B_op model's, not the traffic's",
         "kernel": "mtr::apply_pair2_kernel" if matrix else "mtr::apply_kernel",
-        "achieved": round(achieved, 2),
+        "achieved": round(achieved_span, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "frac": round(achieved_span / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "achieved_span": round(achieved_span, 2),
-        "frac_span": round(achieved_span / HBM_PEAK_GBS, 4),
-        "algorithmic_bytes_per_launch": b_launch,
-        "avg_launch_ms": kernel_ms / max(1, launches),
+        "per_launch": {"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                       "algorithmic_bytes_per_launch": b_launch, "avg_launch_ms": kernel_ms / max(1, launches),
+                       "note": "algorithmic bytes per launch / the launches' average duration (HIP events on each "
+                               "launch's stream; the rocprof kernel-trace average agrees): a round's launches overlap "
+                               "on 4 streams, so each runs stretched by the others and this figure double-counts "
+                               "that overlap"},
+        "algorithmic_bytes_per_step": b_step,
         "launches_per_step": launches_per_step,
         "apply_wall_ms_per_step": apply_ms / a.steps,
         "kernel_sum_ms_per_step": 1000.0 * kernel_s,
         "issue": issue,
-        "note": "frac = algorithmic bytes per launch / average launch duration (the prescribed per-launch "
-                "figure); frac_span = the step's algorithmic bytes / the apply span (launches of a round "
-                "overlap on 4 streams); traffic = PMC HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)",
+        "note": "achieved / frac = the step's algorithmic bytes / the step's apply span (the driver's clock: the launches "
+                "of a round overlap on 4 streams); per_launch = the same bytes per launch / the average launch "
+                "duration; traffic = PMC HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)",
         "model": "B_op = 16*S_d(t) + 32 + 2*L_ins (SURVEY.md 8d)" + (
             "; setCell: S_d = leaves of both vectors (two position resolutions)" if matrix else ""),
     }
@@ -644,17 +648,18 @@ def main(argv=None):
         b2_step = 8.0 / 6.0 * st["sum_leaves_before_op"] + (16.0 * 14 + 32.0) * messages + 2.0 * st["text_units_inserted"]
         b2_launch = b2_step / launches_per_step
         achieved2 = b2_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        roofline["flat_pass"] = {k: roofline[k] for k in ("model", "achieved", "frac", "achieved_span", "frac_span",
-                                                          "algorithmic_bytes_per_launch")}
+        roofline["flat_pass"] = {k: roofline[k] for k in ("model", "achieved", "frac", "per_launch",
+                                                          "algorithmic_bytes_per_step")}
+        a2_span = b2_step / apply_s / 1e9 if apply_s > 0 else 0.0
         roofline.update({
             "model": "B_op2 = 8*#blocks + 16*(leaf records in <= 2 touched leaf blocks) + 32 + 2*L_ins; "
                      "#blocks ~ S/6 (reloadFromSegments' 7-per-block layout and its splits), 2 leaf blocks = 14 "
                      "records (SURVEY.md 8d, two-level)",
-            "achieved": round(achieved2, 2),
-            "frac": round(achieved2 / HBM_PEAK_GBS, 4),
-            "achieved_span": round(b2_step / apply_s / 1e9, 2) if apply_s > 0 else 0.0,
-            "frac_span": round(b2_step / apply_s / 1e9 / HBM_PEAK_GBS, 4) if apply_s > 0 else 0.0,
-            "algorithmic_bytes_per_launch": b2_launch,
+            "achieved": round(a2_span, 2),
+            "frac": round(a2_span / HBM_PEAK_GBS, 4),
+            "per_launch": {"achieved": round(achieved2, 2), "frac": round(achieved2 / HBM_PEAK_GBS, 4),
+                           "algorithmic_bytes_per_launch": b2_launch, "avg_launch_ms": kernel_ms / max(1, launches)},
+            "algorithmic_bytes_per_step": b2_step,
             "limiter": "per-document latency: a two-wave workgroup per document (wave 0 applies the ops in order, "
                        "wave 1 takes halves of the view scan's superchunk rounds, the dirty-chunk evaluation, the "
                        "block walks and packParent), each op a chain of dependent HBM round trips (superchunk/chunk "

@@ -118,7 +118,8 @@ struct mtr_engine {
     DevBuf<unsigned long long> prof;  // phase-timer sums (-DMTR_PROF builds)
     DevBuf<int32_t> cls;              // size-class counters of one apply round (classify_kernel)
     DevBuf<uint32_t> dlist;           // [class][n_docs] document lists of one apply round
-    int32_t* h_cls = nullptr;         // pinned host copy of cls
+    int32_t* h_cls = nullptr;         // page-locked, mapped host copy of cls (written by words_kernel)
+    int32_t* d_cls = nullptr;         // (its device address)
     DevBuf<uint32_t> scratch;         // E/V arrays for HBM-resident (global-mode) launches
     DevBuf<mtr_synth_state> gstate;   // record mode generator state
     // SharedMatrix pairs (mtr_set_matrix): per document kind (0 SharedString, 1 rows vector, 2 cols
@@ -140,10 +141,12 @@ struct mtr_engine {
     bool summarized = false;
     // pipelined hand-over (mtr_submit_pipelined): the copy stream, per part its landing event, document range and
     // op-scan bits (device, then page-locked host copy)
-    hipStream_t copy = nullptr;
+    hipStream_t copy = nullptr;  // (= aux[kLanes - 2]: the last launch lane)
     std::vector<hipEvent_t> part_ev;
     std::vector<uint32_t> part_lo;
     uint32_t pipe_parts = 0;
+    uint32_t pipe_groups = 1;
+    uint32_t pipe_last = 0;    // the part uploaded last  // document groups of the pipelined run (their parts are uploaded alternately)
     DevBuf<int32_t> pflags;
     int32_t* h_pflags = nullptr;
     uint32_t h_pflags_n = 0;
@@ -177,6 +180,12 @@ __global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_
             h[d].fail_op = 0;
         }
     }
+}
+
+// dst[i] = src ? src[i] : 0 for i < n (one block): zeroing and reading back small counters without a DMA copy
+__global__ void words_kernel(int32_t* dst, const int32_t* src, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src ? src[i] : 0;
+    __threadfence_system();
 }
 
 // mtr_submit_pipelined: the documents [lo, hi) of part p have landed; enable them (copy the descriptor, op_count
@@ -439,10 +448,6 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->pflags.release();
     e->pdocs.release();
     if (e->h_pflags) (void)hipHostFree(e->h_pflags);
-    if (e->copy) {
-        (void)hipStreamSynchronize(e->copy);
-        (void)hipStreamDestroy(e->copy);
-    }
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return 0;
@@ -608,7 +613,10 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts) {
     // every document starts disabled (op_count 0: classify_kernel passes it over) until its part has landed
     HIPCHK(hipMemsetAsync(e->docs.p, 0, size_t(n) * sizeof(mtr_doc_desc), e->stream));
     HIPCHK(hipMemsetAsync(e->pflags.p, 0, size_t(parts) * sizeof(int32_t), e->stream));
-    if (!e->copy) HIPCHK(hipStreamCreateWithFlags(&e->copy, hipStreamNonBlocking));
+    // the copy stream is the last launch lane, which mtr_run leaves idle while parts are landing: a stream of its
+    // own would share a hardware queue with the engine stream (GPU_MAX_HW_QUEUES = 4 = the launch lanes), and the
+    // copies would then hold back every launch queued behind them there
+    e->copy = e->aux[mtr_engine::kLanes - 2];
     while (e->part_ev.size() < parts) {
         hipEvent_t x;
         HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
@@ -623,7 +631,12 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts) {
     HIPCHK(hipStreamWaitEvent(e->copy, e->ev[0], 0));
     e->part_lo.assign(size_t(parts) + 1, 0);
     for (uint32_t p = 0; p <= parts; p++) e->part_lo[p] = uint32_t(uint64_t(n) * p / parts);
-    for (uint32_t p = 0; p < parts; p++) {
+    // two document groups (mtr_run's default above 4,096 documents), each with half the parts: the upload
+    // alternates between them, so both start within the first two parts
+    e->pipe_groups = (n >= 4096u && parts >= 2) ? 2u : 1u;
+    const uint32_t half = (parts + 1) / 2;
+    for (uint32_t q = 0; q < parts; q++) {
+        const uint32_t p = e->pipe_groups == 2 ? ((q & 1) ? half + q / 2 : q / 2) : q;
         const uint32_t lo = e->part_lo[p], hi = e->part_lo[p + 1];
         const mtr_doc_desc &a = b->docs[lo], &z = b->docs[hi - 1];
         const uint64_t o0 = a.op_begin, o1 = std::min<uint64_t>(z.op_begin + z.op_count, b->n_ops);
@@ -641,6 +654,7 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts) {
         HIPCHK(hipEventRecord(e->part_ev[p], e->copy));
     }
     e->pipe_parts = parts;
+    e->pipe_last = e->pipe_groups == 2 ? ((parts & 1) ? half - 1 : parts - 1) : parts - 1;  // (uploaded last)
     e->summarized = false;
     return MTR_OK;
 }
@@ -815,7 +829,10 @@ static int run_impl(mtr_engine* e, int gen) {
     const bool few_docs = e->n_docs <= uint32_t(std::max(n_cu, 1));
     bool any_pair = false;
     for (uint32_t d = 0; d < e->n_docs && d < e->h_kind.size(); d++) any_pair = any_pair || e->h_kind[d] != 0;
-    const int g_want = groups_env > 0 ? groups_env : (e->n_docs >= 4096u && e->n_docs <= 60000u ? 2 : 1);
+    // (round 6: two groups at 100,000 documents too -- 424.4 M against 418.5 M ops/s on one box; the per-launch
+    // roofline figure that kept one group there is no longer the headline, the step span is; a pipelined hand-over
+    // keeps one group, whose lanes take the landing parts in order)
+    const int g_want = groups_env > 0 ? groups_env : (e->n_docs >= 4096u && !e->pipe_parts ? 2 : 1);
     // Default class width: 128 leaves for the batches that run two groups (4,096 to 60,000 documents) -- half the
     // launches per round of 64-leaf classes, which at those sizes cost more than the wider classes' LDS spread
     // (profiles/r04_class_sweep.json: 12,500 documents 379.0 M vs 341.4 M ops/s, 25,000 395.5 M vs 385.0 M);
@@ -826,15 +843,33 @@ static int run_impl(mtr_engine* e, int gen) {
     // (a pipelined hand-over: its parts still landing; a group takes whole parts)
     const uint32_t PP = gen ? 0u : e->pipe_parts;
     int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
-    if (PP) G = std::min<int>(G, int(PP));
+    if (PP) G = std::min<int>(int(e->pipe_groups), int(PP));
     const int L = std::max(1, nlanes / G);  // lanes (streams) per group
     const size_t ncls = 1 + 3 * kAllClasses;
     if (e->cls.ensure(ncls * mtr_engine::kLanes) || e->dlist.ensure(size_t(kAllClasses) * e->n_docs)) return -1;
-    if (!e->h_cls)
-        HIPCHK(hipHostMalloc((void**)&e->h_cls, ncls * mtr_engine::kLanes * sizeof(int32_t), hipHostMallocDefault));
+    if (!e->h_cls) {
+        HIPCHK(hipHostMalloc((void**)&e->h_cls, ncls * mtr_engine::kLanes * sizeof(int32_t),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void**)&e->d_cls, e->h_cls, 0));
+    }
+    // stream index of group g's lane l.  A pipelined run uses all four streams whatever MTR_LANES says: the last
+    // one is the copy stream, a launch lane again once every part has landed -- group 0's lanes are streams 0 (and 1
+    // with two groups), group 1's stream 2 and then 3; one group: streams 0-2, then 3
+    auto lane_si = [&](int g, int l) -> int {
+        if (PP && G == 2) return g == 0 ? l : 2 + l;
+        return PP ? l : g * L + l;
+    };
     auto lane_stream = [&](int g, int l) -> hipStream_t {
-        const int si = g * L + l;
+        const int si = lane_si(g, l);
         return si == 0 ? e->stream : e->aux[si - 1];
+    };
+    // the lanes group g launches on this round
+    auto lanes_of = [&](int g) -> int {
+        if (!PP) return L;
+        const int base = G == 2 ? (g == 0 ? 2 : 1) : int(mtr_engine::kLanes) - 1;
+        if (G == 2 && g == 0) return base;  // (the copy stream is group 1's second lane)
+        const hipError_t q = hipEventQuery(e->part_ev[e->pipe_last]);
+        return q == hipSuccess ? base + 1 : base;
     };
     struct Grp {
         uint32_t lo = 0, hi = 0;
@@ -844,9 +879,10 @@ static int run_impl(mtr_engine* e, int gen) {
     std::vector<Grp> grp(static_cast<size_t>(G));
     for (int g = 0; g < G; g++) {
         Grp& gr = grp[size_t(g)];
-        if (PP) {
-            gr.waited = uint32_t(uint64_t(PP) * uint64_t(g) / uint64_t(G));
-            gr.p_hi = uint32_t(uint64_t(PP) * uint64_t(g + 1) / uint64_t(G));
+        if (PP) {  // (mtr_submit_pipelined's split: two groups take [0, half) and [half, PP))
+            const uint32_t half = (PP + 1) / 2;
+            gr.waited = G == 2 && g == 1 ? half : 0u;
+            gr.p_hi = G == 2 && g == 0 ? half : PP;
             gr.lo = e->part_lo[gr.waited];
             gr.hi = e->part_lo[gr.p_hi];
         } else {
@@ -856,20 +892,26 @@ static int run_impl(mtr_engine* e, int gen) {
     }
     // the groups' lanes start after everything queued on the engine stream (the batch upload)
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
-    for (int g = 0; g < G; g++)
-        for (int l = 0; l < L; l++)
-            if (g * L + l > 0) HIPCHK(hipStreamWaitEvent(lane_stream(g, l), e->ev[0], 0));
+    if (PP) {
+        for (int si = 1; si < int(mtr_engine::kLanes); si++) HIPCHK(hipStreamWaitEvent(e->aux[si - 1], e->ev[0], 0));
+    } else {
+        for (int g = 0; g < G; g++)
+            for (int l = 0; l < L; l++)
+                if (g * L + l > 0) HIPCHK(hipStreamWaitEvent(lane_stream(g, l), e->ev[0], 0));
+    }
     // classify group g (on its first lane) and read its class counts back
     auto classify = [&](int g) -> int {
         Grp& gr = grp[size_t(g)];
         hipStream_t st = lane_stream(g, 0);
         int32_t* dcls = e->cls.p + size_t(g) * ncls;
-        HIPCHK(hipMemsetAsync(dcls, 0, ncls * sizeof(int32_t), st));
+        // (the counters are zeroed and read back by kernels, the read-back into mapped page-locked memory: a DMA
+        // copy would queue behind mtr_submit_pipelined's uploads on the copy engine)
+        words_kernel<<<1, 256, 0, st>>>(dcls, nullptr, int(ncls));
         const uint32_t n = gr.hi - gr.lo;
         classify_kernel<<<(n + 255) / 256, 256, 0, st>>>(e->hdr.p, e->docs.p, gr.lo, gr.hi, e->dkind.p, e->dpart.p,
                                                          dcls, e->dlist.p + size_t(kAllClasses) * gr.lo, class_leaves);
+        words_kernel<<<1, 256, 0, st>>>(e->d_cls + size_t(g) * ncls, dcls, int(ncls));
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(e->h_cls + size_t(g) * ncls, dcls, ncls * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipEventRecord(e->grp_cls[g], st));
         return 0;
     };
@@ -888,6 +930,7 @@ static int run_impl(mtr_engine* e, int gen) {
     // one round of group g: a launch per size class, spread over the group's lanes, joined on its first lane
     auto issue_round = [&](int g, bool& stuck) -> int {
         Grp& gr = grp[size_t(g)];
+        const int Lr = lanes_of(g);
         const int32_t* cls = e->h_cls + size_t(g) * ncls;
         const uint32_t n = gr.hi - gr.lo;
         const int k = std::min(K, cls[0]);
@@ -940,9 +983,9 @@ static int run_impl(mtr_engine* e, int gen) {
             Q.ops_this_launch = kk;
             Q.doc_list = e->dlist.p + size_t(kAllClasses) * gr.lo + size_t(c) * n;
             Q.n_launch = uint32_t(cnt);
-            const int lane = nl % L;
+            const int lane = nl % Lr;
             hipStream_t st = lane_stream(g, lane);
-            if (lane != 0 && nl < L) HIPCHK(hipStreamWaitEvent(st, e->grp_fork[g], 0));
+            if (lane != 0 && nl < Lr) HIPCHK(hipStreamWaitEvent(st, e->grp_fork[g], 0));
             const size_t q = size_t(e->launches);
             while (e->kev.size() < 2 * (q + 1)) {
                 hipEvent_t x;
@@ -986,8 +1029,8 @@ static int run_impl(mtr_engine* e, int gen) {
             e->launches++;
             nl++;
         }
-        for (int l = 1; l < std::min(nl, L); l++) {  // join the lanes
-            const int si = g * L + l;
+        for (int l = 1; l < std::min(nl, Lr); l++) {  // join the lanes
+            const int si = lane_si(g, l);
             HIPCHK(hipEventRecord(e->lane_done[si], lane_stream(g, l)));
             HIPCHK(hipStreamWaitEvent(st0, e->lane_done[si], 0));
         }
@@ -1034,8 +1077,8 @@ static int run_impl(mtr_engine* e, int gen) {
     }
     for (int g = 0; g < G; g++)
         if (g > 0) {  // join every group into the engine stream
-            HIPCHK(hipEventRecord(e->lane_done[g * L], lane_stream(g, 0)));
-            HIPCHK(hipStreamWaitEvent(e->stream, e->lane_done[g * L], 0));
+            HIPCHK(hipEventRecord(e->lane_done[lane_si(g, 0)], lane_stream(g, 0)));
+            HIPCHK(hipStreamWaitEvent(e->stream, e->lane_done[lane_si(g, 0)], 0));
         }
     HIPCHK(hipEventRecord(e->ev[2], e->stream));
     HIPCHK(hipEventSynchronize(e->ev[2]));

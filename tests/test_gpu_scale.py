@@ -219,14 +219,14 @@ def test_containing_segment_matches_oracle():
     assert n_checked > 400
 
 
-@pytest.mark.parametrize("parts", [2, 7, 64])
-def test_pipelined_submit_equals_serial_submit(parts):
+@pytest.mark.parametrize("n, parts", [(3000, 2), (3000, 64), (5000, 7), (5000, 16)])
+def test_pipelined_submit_equals_serial_submit(n, parts):
     """mtr_submit_pipelined (the end-to-end hand-over with the upload overlapped): the same summaries as
     mtr_submit + mtr_run, from the recorded op logs in page-locked memory, for part counts that do not divide the
     documents evenly; a pipelined batch can be followed by an ordinary one on the same engine."""
     from fluidframework_amd.synth import make_cfg, tables
 
-    n, ops = 3000, 300
+    ops = 300  # (5,000 documents: two document groups, whose parts are uploaded alternately)
     cfg = make_cfg(n, ops, writers=8, max_lag=32, seed=0x91be + parts)
     eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
                   prop_words=16384, remover_cells=4096, ops_per_launch=48)
