@@ -52,6 +52,7 @@ DELTA_TMERGE = 98
 TRACK_GROUPS = 32
 DELTA_REGEN_X = 72
 DELTA_REBASE = 80
+REBASE_NOSLIDE = 1  # MTR_OP_REBASE_POS payload2: SharedMatrix.rebasePosition (no slide)
 REL_BEFORE = 1
 REL_OFFSET = 2
 COMB_NONE, COMB_REWRITE, COMB_INCR, COMB_CONSENSUS, COMB_KEEP = 0, 1, 2, 3, 4

@@ -22,7 +22,7 @@ from typing import Any
 import numpy as np
 
 from . import abi
-from .batch import Interner, MatrixLog
+from .batch import Interner, MatrixLog, Unsupported
 from .engine import EngineError
 from .jsjson import js_stringify, parse, to_utf8
 
@@ -148,6 +148,8 @@ class CellMatrixLog(MatrixLog):
         self.ops_kind: dict[int, str] = {}    # record index of a local write before attaching (no pending entry)
         self.cell_undo: dict = {}             # record index of an undoable local write -> callback(rh, ch, old value)
         self.tracker = None                   # the undo provider's tracking groups (fluidframework_amd/undo.py)
+        # reconnect (reSubmitCore): per vector the last batch's MTR_DELTA_REGEN / _REGEN_X / _REBASE records
+        self.reconnect: dict = {"rows": [], "cols": []}
 
     def local_set_cell(self, row: int, col: int, value: Any) -> None:
         """SharedMatrix.setCell(row, col, value) of this client (local positions)."""
@@ -191,6 +193,7 @@ class CellMatrixLog(MatrixLog):
         """Apply the last batch's records (engine.deltas(rows doc), engine.deltas(cols doc)) in op
         order; within one op the rows records come first (a vector op touches one vector); the acks of local
         writes in this batch come between the records at their place in the message stream."""
+        self.reconnect = {"rows": [], "cols": []}
         recs = [(int(r["op"]), 0, i, r) for i, r in enumerate(rows)] + [(int(r["op"]), 1, i, r) for i, r in enumerate(cols)]
         recs += [(pos - 0.5, 2, i, None) for i, (pos, _) in enumerate(self.events)]
         recs.sort(key=lambda x: (x[0], x[1], x[2]))
@@ -207,6 +210,9 @@ class CellMatrixLog(MatrixLog):
                     self.pending.set_cell(a, b, None)
                 continue
             kind, a, b = int(r["kind"]), int(r["pos"]), int(r["len"])
+            if abi.DELTA_REGEN <= kind <= abi.DELTA_REGEN_X or kind == abi.DELTA_REBASE:  # reconnect (resubmit)
+                self.reconnect["cols" if which else "rows"].append((op, kind, a, b))
+                continue
             if kind in (abi.DELTA_TLINK, abi.DELTA_TSPLIT, abi.DELTA_TMERGE):  # tracking groups (undo.py)
                 if self.tracker is None:
                     raise ValueError("tracking records without an undo provider")
@@ -240,6 +246,63 @@ class CellMatrixLog(MatrixLog):
         self.cell_undo = {}
         if self.tracker is not None:
             self.tracker.batch_done()
+
+    # -- reconnect: SharedMatrix.reSubmitCore (matrix.ts:553-604)
+    def regenerate_vector(self, target: str, op: dict) -> int:
+        """PermutationVector.regeneratePendingOp (-> Client.regeneratePendingOp, client.ts:917-960) of the vector's
+        oldest pending op `op` (its contents): one MTR_OP_REGENERATE record per member on the rows or cols vector.
+        Returns the first record's index (its MTR_DELTA_REGEN records carry it)."""
+        tf = abi.F_COLS if target == "cols" else 0
+        members = op["ops"] if op.get("type") == 3 else [op]
+        first = len(self.ops)
+        for m in members:
+            t = m.get("type")
+            if t not in (0, 1):
+                raise Unsupported(f"regenerate of vector op type {t}")
+            self.ops.append((abi.OP_REGENERATE, abi.F_DELTA | tf, 0, -1, 0, 0, 0, 0, 0, t))
+        return first
+
+    def rebase_position(self, target: str, pos: int, ref_seq: int, local_seq: int) -> int:
+        """SharedMatrix.rebasePosition (matrix.ts:534-551) on the rows or cols vector: getContainingSegment(pos) at
+        (ref_seq, this client, local_seq), then findReconnectionPosition(segment, local_seq) + offset
+        (MTR_OP_REBASE_POS with MTR_REBASE_NOSLIDE).  Returns the record's index."""
+        tf = abi.F_COLS if target == "cols" else 0
+        self.ops.append((abi.OP_REBASE_POS, abi.F_DELTA | tf, 0, 0, int(ref_seq), int(local_seq), int(pos), 0, 0,
+                         abi.REBASE_NOSLIDE))
+        return len(self.ops) - 1
+
+    def _reconnect_records(self, target: str, first: int) -> list:
+        return [r for r in self.reconnect[target] if r[0] >= first]
+
+    def regenerated_vector_op(self, target: str, reset_op: dict, first: int) -> dict:
+        """The vector op regeneratePendingOp returns (resetPendingDeltaToOps, client.ts:708-800) from the records
+        of regenerate_vector's batch: a member per regenerated segment -- an insert's spec is the
+        PermutationSegment clone's [length, start] (permutationvector.ts:118-120), a remove its range -- and a GROUP
+        unless exactly one (createGroupOp, client.ts:959), with the op's target (submitVectorMessage,
+        matrix.ts:321-345)."""
+        members = reset_op["ops"] if reset_op.get("type") == 3 else [reset_op]
+        recs = self._reconnect_records(target, first)
+        ops = []
+        k = 0
+        while k < len(recs):
+            op, kind, a, b = recs[k]
+            if not abi.DELTA_REGEN <= kind < abi.DELTA_REGEN + 3 or k + 1 >= len(recs) or recs[k + 1][1] != abi.DELTA_REGEN_X:
+                raise ValueError("MTR_DELTA_REGEN without its MTR_DELTA_REGEN_X record")
+            t = kind - abi.DELTA_REGEN
+            if op - first >= len(members) or t != members[op - first].get("type"):
+                raise ValueError("regenerate record does not match the op")
+            start = int(np.int32(np.uint32(recs[k + 1][3] & 0xFFFFFFFF)))
+            ops.append({"pos1": a, "seg": [b, start], "type": 0} if t == 0 else {"pos1": a, "pos2": a + b, "type": 1})
+            k += 2
+        out = ops[0] if len(ops) == 1 else {"ops": ops, "type": 3}
+        return dict(out, target=target)
+
+    def rebased(self, target: str, idx: int) -> int:
+        """rebase_position's answer (-1: undefined, no segment)."""
+        for op, kind, a, _ in self.reconnect[target]:
+            if op == idx and kind == abi.DELTA_REBASE:
+                return a
+        raise ValueError(f"no rebase record for record {idx}")
 
     def cells_blob(self) -> bytes:
         """The ``cells`` blob of SharedMatrix.summarizeCore (matrix.ts:458-462):

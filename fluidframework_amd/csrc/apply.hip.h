@@ -2754,15 +2754,27 @@ struct Eng {
     }
     // IntervalCollection.rebasePositionWithSegmentSlide (intervalCollection.ts:1472-1505): the position an endpoint
     // created at op.pos1 in the view (op.ref_seq, this client, localSeq op.min_seq) has after a reconnect
+    // With MTR_REBASE_NOSLIDE it is SharedMatrix.rebasePosition (matrix.ts:534-551): the same getContainingSegment,
+    // then findReconnectionPosition(segment, localSeq) + offset with no slide; no segment = undefined (the
+    // detached position), which the resubmit skips
     static MTR_DI void rebase_pos(D& L, St& s, const mtr_op& op, int gidx) {
         int i = 0, before = 0;
+        const bool noslide = (op.payload2 & MTR_REBASE_NOSLIDE) != 0;
         find1_at(L, s, op.ref_seq, op.min_seq, op.pos1, i, before);
         if (op.pos1 < 0 || i >= s.nseg) {
+            if (noslide) {
+                if constexpr (DL) put_record(L, s, gidx, MTR_DETACHED_POSITION, 0, MTR_DELTA_REBASE);
+                return;
+            }
             s.status = MTR_ERR_ASSERT | 0x54e;  // "No segment found"
             return;
         }
         const int off = op.pos1 - before;
         int t = i, toff = off;
+        if (noslide) {
+            if constexpr (DL) put_record(L, s, gidx, pos_at(L, s, i, s.curseq, op.min_seq) + off, 0, MTR_DELTA_REBASE);
+            return;
+        }
         if (removed_acked(uni(L.rseq[i]))) {  // getSlideToSegment (client.ts:1085-1099)
             t = slide_target(L, s, i);
             toff = (t >= 0 && t < i) ? uni(L.len[t]) - 1 : 0;
@@ -3189,8 +3201,10 @@ struct Eng {
                 off += ln;
                 if (!emit) continue;
                 if constexpr (DL) {
-                    const uint32_t pr = uniu(pget(L, j));
-                    const int ref = (type == MTR_OP_INSERT && pr != NONE32) ? int(pr & PN_MASK) : -1;
+                    // (a PermutationSegment's clone keeps its start handle: the regenerated spec is [length, start])
+                    const uint32_t pr = PM ? uniu(L.text[j]) : uniu(pget(L, j));
+                    const int ref = PM ? (type == MTR_OP_INSERT ? int(pr) : -1)
+                                       : ((type == MTR_OP_INSERT && pr != NONE32) ? int(pr & PN_MASK) : -1);
                     put_record(L, s, gidx, before, ln, uint32_t(MTR_DELTA_REGEN + type));
                     put_record(L, s, gidx, type == MTR_OP_INSERT ? here : 0, ref, MTR_DELTA_REGEN_X);
                 }
@@ -5345,7 +5359,8 @@ struct Eng {
                 rollback(L, P, s, int(op.payload2), op.payload, uint32_t(op.pos1));
                 break;
             case MTR_OP_REGENERATE:  // Client.regeneratePendingOp (client.ts:917-960) of the oldest pending op
-                if (!X || !DL || PM || !s.collab) {
+                // (a matrix vector too: SharedMatrix.reSubmitCore, matrix.ts:553-570)
+                if (!X || !DL || !s.collab) {
                     s.status = MTR_ERR_BAD_OP;
                     break;
                 }
@@ -5413,8 +5428,8 @@ struct Eng {
                 if (!X || PM) s.status = MTR_ERR_BAD_OP;
                 else ref_ack(L, s, op.payload);
                 break;
-            case MTR_OP_REBASE_POS:  // IntervalCollection.rebasePositionWithSegmentSlide
-                if (!X || !DL || PM || !s.collab) s.status = MTR_ERR_BAD_OP;
+            case MTR_OP_REBASE_POS:  // IntervalCollection.rebasePositionWithSegmentSlide / SharedMatrix.rebasePosition
+                if (!X || !DL || !s.collab) s.status = MTR_ERR_BAD_OP;
                 else rebase_pos(L, s, op, gidx);
                 break;
             case MTR_OP_LSEQ:  // IntervalCollection.getNextLocalSeq: ++collabWindow.localSeq

@@ -541,6 +541,10 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b) {
                 flagged = true;
                 if (kind == 1) {
                     if (op.type == MTR_OP_SETCELL || op.type == MTR_OP_LOCAL_SETCELL) need[d] += 1;
+                    // (a vector's reconnect records: regenerate, two per member; rebasePosition, one)
+                    const uint32_t dv = (op.flags & MTR_F_COLS) && e->h_part[d] < b->n_docs ? e->h_part[d] : d;
+                    if (op.type == MTR_OP_REGENERATE) need[dv] += 2 * uint64_t(e->caps.max_segments);
+                    if (op.type == MTR_OP_REBASE_POS) need[dv] += 1;
                 } else if (op.type == MTR_OP_INSERT) {
                     need[d] += 1;
                 } else if (op.type == MTR_OP_REMOVE || op.type == MTR_OP_ANNOTATE) {

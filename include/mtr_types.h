@@ -109,6 +109,11 @@ enum {
                                    localSeq) + offset (client.ts:699-706), or DetachedReferencePosition; asserts 0x54e /
                                    0x54f.  Flag it MTR_F_DELTA: the result is one mtr_delta {op, position, 0,
                                    MTR_DELTA_REBASE} */
+    /* MTR_OP_REBASE_POS with payload2 & MTR_REBASE_NOSLIDE (a SharedMatrix vector, flagged MTR_F_COLS for cols):
+       SharedMatrix.rebasePosition (matrix.ts:534-551) -- no slide, no offset assert, and no segment gives
+       MTR_DETACHED_POSITION (undefined: the resubmit skips the write).  MTR_OP_REGENERATE on a matrix vector
+       (reSubmitCore, matrix.ts:553-570): its MTR_DELTA_REGEN_X record's second field is the segment's start
+       handle (the regenerated PermutationSegment spec is [length, start]). */
     MTR_OP_LSEQ = 26,           /* IntervalCollection.getNextLocalSeq (:1584-1590): ++collabWindow.localSeq -- an
                                    interval op takes a localSeq the merge-tree's later local ops count past */
     MTR_OP_RELPOS = 15          /* a relative position of the NEXT record (getValidOpRange, client.ts:527-545 ->
@@ -121,6 +126,9 @@ enum {
                                    a marker zamboni unlinked has position 0 (its parent is gone). A resolved
                                    position < 0 makes the document MTR_ERR_UNSUPPORTED. */
 };
+
+/* MTR_OP_REBASE_POS payload2 */
+enum { MTR_REBASE_NOSLIDE = 1 };
 
 /* MTR_OP_RELPOS payload2 */
 enum { MTR_REL_BEFORE = 1, MTR_REL_OFFSET = 2 };

@@ -1144,7 +1144,9 @@ class Tree {
             off += s->len;
             if (!emit) continue;
             uint32_t ref = 0xffffffffu;
-            if (type == MTR_OP_INSERT && s->hasProps) {
+            if (s->perm) {  // a PermutationSegment's clone keeps its start handle (the spec is [length, start])
+                if (type == MTR_OP_INSERT) ref = uint32_t(s->start);
+            } else if (type == MTR_OP_INSERT && s->hasProps) {
                 ref = uint32_t(regenProps.size());
                 regenProps.push_back({true, s->props});
             }
@@ -1981,6 +1983,21 @@ class Tree {
                 if (!collaborating) return MTR_ERR_BAD_OP;
                 int off = 0;
                 Seg* s = containingSegmentAt(op.pos1, op.ref_seq, op.min_seq, off);
+                if (op.payload2 & MTR_REBASE_NOSLIDE) {  // SharedMatrix.rebasePosition (matrix.ts:534-551)
+                    int res = MTR_DETACHED_POSITION;     // (no segment: undefined)
+                    if (s && op.pos1 >= 0) {  // findReconnectionPosition(segment, localSeq) + offset, no slide
+                        std::vector<Seg*> lv;
+                        leaves(root, lv);
+                        int before = 0;
+                        for (Seg* x : lv) {
+                            if (x == s) break;
+                            before += localNetLengthAt(x, currentSeq, op.min_seq);
+                        }
+                        res = before + off;
+                    }
+                    deltas.push_back({curOpIndex, res, 0, MTR_DELTA_REBASE});
+                    return status;
+                }
                 if (!s) return status = MTR_ERR_ASSERT | 0x54e;  // "No segment found"
                 Seg* t = getSlideToSegment(s);
                 int toff = off;

@@ -10,6 +10,7 @@ the minimum over every sender's latest referenceSequenceNumber, and hands each t
 the ACK).  The matrices' PermutationVectors and handle records run on the CPU oracle, or under -m gpu on the HIP
 engine's matrix kernels, where every batch's records and both vectors' segment lists must also equal the oracle's.
 """
+import itertools
 import json
 
 import numpy as np
@@ -29,16 +30,74 @@ class MClient:
 
     def __init__(self, s, name, k, attached=True):
         self.s, self.name, self.k = s, name, k
+        self.client_id = name
         self.log = CellMatrixLog()
         if attached:
             self.log.start_collab(name)
         self.doc = OracleDoc(options(), matrix=True)
         self.seq = 0
+        self.pending = []         # MockContainerRuntime's pending messages: (contents, metadata)
+        self.pending_remote = []  # messages sequenced while disconnected
+        self._connected = True
 
     def _vector(self, target, contents):
         self.log.local_vector_op(target, contents)
         if self.log.collaborating:
             self.s.submit(self, dict(contents, target=target))
+
+    # ---- MockContainerRuntimeForReconnection (runtime/test-runtime-utils/src/mocksForReconnection.ts:18-140)
+    def process(self, msg):
+        if not self._connected:
+            self.pending_remote.append(msg)
+            return
+        self.log.message(json.loads(json.dumps(msg)), self.s.it)
+        self.seq = msg["sequenceNumber"]
+        if msg["clientId"] == self.client_id:
+            self.pending.pop(0)
+
+    @property
+    def connected(self):
+        return self._connected
+
+    @connected.setter
+    def connected(self, value):
+        if value == self._connected:
+            return
+        self._connected = value
+        if not value:  # this client's unsequenced messages never reach the service
+            self.s.queue = [q for q in self.s.queue if q[0] is not self]
+            return
+        self.s.flush()  # (the local edits so far applied: their writes' handles are known)
+        for m in self.pending_remote:
+            self.process(m)
+        self.pending_remote = []
+        self.client_id = f"reconnected-{next(self.s.ids)}"
+        msgs, self.pending = self.pending, []
+        for contents, meta in msgs:  # reSubmitMessages -> SharedMatrix.reSubmitCore (matrix.ts:553-604)
+            self.resubmit(contents, meta)
+        self.log.start_collab(self.client_id)  # setConnectionState -> both vectors' startOrUpdateCollaboration
+
+    def resubmit(self, contents, meta):
+        target = contents.get("target")
+        if target is not None:  # rows / cols: regeneratePendingOp, then submitRowMessage / submitColMessage
+            first = self.log.regenerate_vector(target, contents)
+            self.s.flush()
+            self.s.submit(self, self.log.regenerated_vector_op(target, contents, first))
+            return
+        lseq = meta["localSeq"]
+        rh, ch = next((a, b) for a, b, q in self.log.local_meta if q == lseq)
+        p = self.log.pending.get_cell(rh, ch)
+        assert not (p is not None and p < lseq), "0x023"
+        if p == lseq:  # isLatestPendingWrite (matrix.ts:745-762)
+            ri = self.log.rebase_position("rows", contents["row"], meta["rowsRefSeq"], lseq)
+            ci = self.log.rebase_position("cols", contents["col"], meta["colsRefSeq"], lseq)
+            self.s.flush()
+            row, col = self.log.rebased("rows", ri), self.log.rebased("cols", ci)
+            if row >= 0 and col >= 0:  # sendSetCellOp with the original localSeq and refSeqs
+                self.s.submit(self, dict(contents, row=row, col=col), meta)
+                return
+        # not re-sent: no ACK will come for this write
+        self.log.local_meta = [e for e in self.log.local_meta if e[2] != lseq]
 
     def insert_rows(self, start, count):
         self._vector("rows", {"pos1": start, "seg": [count, U], "type": 0})
@@ -58,7 +117,8 @@ class MClient:
             msg = {"type": 2, "row": row, "col": col}
             if value is not None:  # (an undefined value is no JSON field)
                 msg["value"] = value
-            self.s.submit(self, msg)
+            # ISetOpMetadata (matrix.ts:299-305): the handles come with the write's record (CellMatrixLog.local_meta)
+            self.s.submit(self, msg, {"localSeq": self.log.local_seq, "rowsRefSeq": self.seq, "colsRefSeq": self.seq})
 
     def set_cells(self, row, col, col_count, values):  # setCells (matrix.ts:216-252)
         r, c = row, col
@@ -88,6 +148,7 @@ class MSession:
         self.queue = []
         self.seq = 0
         self.min_seq = {}
+        self.ids = itertools.count(1)
         self.clients = [MClient(self, n, k, attached) for k, n in enumerate(names)]
         self.eng = None
         if engine:
@@ -102,10 +163,13 @@ class MSession:
     def leaves(self, c, w):
         return self.eng.leaves(2 * c.k + w) if self.eng is not None else c.doc.select(w).leaves()
 
-    def submit(self, c, contents):  # MockContainerRuntime.submit -> factory.pushMessage (mocks.ts:216-240)
+    def submit(self, c, contents, meta=None):  # MockContainerRuntime.submit -> factory.pushMessage (mocks.ts:216-240)
+        c.pending.append((contents, meta))
+        if not c.connected:
+            return
         ref = c.seq
-        self.min_seq.setdefault(c.name, ref)
-        self.queue.append((c, contents, ref))
+        self.min_seq.setdefault(c.client_id, ref)
+        self.queue.append((c, contents, ref, c.client_id))
 
     def flush(self):
         if not any(c.log.ops for c in self.clients):
@@ -131,14 +195,13 @@ class MSession:
     def process_all(self):  # processAllMessages (mocks.ts:262-303)
         self.flush()
         while self.queue:
-            c, contents, ref = self.queue.pop(0)
-            self.min_seq[c.name] = ref
+            c, contents, ref, cid = self.queue.pop(0)
+            self.min_seq[cid] = ref
             self.seq += 1
             msg = {"type": "op", "sequenceNumber": self.seq, "referenceSequenceNumber": ref,
-                   "minimumSequenceNumber": min(self.min_seq.values()), "clientId": c.name, "contents": contents}
+                   "minimumSequenceNumber": min(self.min_seq.values()), "clientId": cid, "contents": contents}
             for x in self.clients:
-                x.log.message(json.loads(json.dumps(msg)), self.it)
-                x.seq = self.seq
+                x.process(msg)
         self.flush()
 
 
@@ -368,3 +431,106 @@ def test_local_client_summarize_mutate_after_load(engine):  # :274-305
     assert m2.extract() == [[0, 1], [10, 11], [2, 3]]
     m2.insert_cols(1, 1)
     assert m2.extract() == [[0, None, 1], [10, None, 11], [2, None, 3]]
+
+
+# ---------------------------------------------------------------- "Reconnection" (:612-880)
+class TwoR(Two):
+    """beforeEach of "Reconnection" (:643-659): two matrices on MockContainerRuntimeFactoryForReconnection; a
+    client's `connected` setter is its runtime's (disconnect drops its unsequenced messages, reconnect processes
+    the messages sequenced meanwhile, takes a new client id and resubmits every pending message)."""
+
+
+def resend_setcell_when_later_ops_shift(t, reconnects=1):  # :668-695 (reconnects=2: :697-729)
+    t.m1.insert_rows(0, 1)
+    t.m1.insert_cols(0, 1)
+    t.expect([[None]])
+    t.m1.set_cells(0, 0, 1, ["A"])
+    t.m1.insert_cols(0, 3)
+    for _ in range(reconnects):
+        t.m1.connected = False
+        t.m1.connected = True
+    t.expect([[None, None, None, "A"]])
+
+
+def resend_setcell_multiple_reconnects(t):  # :697-729
+    resend_setcell_when_later_ops_shift(t, 2)
+
+
+def resend_unacked_ops(t):  # :731-752
+    t.m1.insert_cols(0, 1)
+    t.m1.insert_rows(0, 1)
+    t.m1.connected = False
+    t.m1.connected = True
+    t.expect([[None]])
+    t.m2.set_cell(0, 0, "2nd")
+    t.m2.connected = False
+    t.m2.connected = True
+    t.expect([["2nd"]])
+
+
+def store_ops_while_disconnected(t):  # :754-779
+    t.m1.connected = False
+    t.m1.insert_cols(0, 1)
+    t.m1.insert_rows(0, 1)
+    t.m1.connected = True
+    t.expect([[None]])
+    t.m2.connected = False
+    t.m2.set_cell(0, 0, "2nd")
+    t.m2.connected = True
+    t.expect([["2nd"]])
+
+
+def omit_writes_to_recycled_handles(t):  # :808-825
+    t.m1.insert_rows(0, 2)
+    t.m1.insert_cols(0, 2)
+    t.m1.set_cells(0, 0, 2, [0, 1, 2, 3])
+    t.m1.remove_rows(1, 1)
+    t.m1.connected = False
+    t.m1.insert_rows(0, 1)
+    t.m1.set_cells(0, 0, 2, [28, 49])
+    t.m1.connected = True
+    t.expect([[28, 49], [0, 1]])
+
+
+def omit_not_yet_locally_deleted(t):  # :827-859
+    t.m1.insert_rows(0, 2)
+    t.m1.insert_cols(0, 4)
+    t.m1.set_cells(0, 0, 4, [0, 1, 2, 3, 4, 5, 6, 7])
+    t.m1.insert_rows(0, 1)
+    t.m1.set_cells(0, 0, 4, [61, 57, 7, 62])
+    t.m1.connected = False
+    t.m1.connected = True
+    t.expect([[61, 57, 7, 62], [0, 1, 2, 3], [4, 5, 6, 7]])
+    t.m1.set_cells(2, 3, 1, [65])
+    t.m1.connected = False
+    t.m1.remove_rows(0, 1)
+    t.m1.connected = True
+    t.expect([[0, 1, 2, 3], [4, 5, 6, 65]])
+
+
+def reset_handles_for_resubmitted_ops(t):  # :861-879
+    t.m1.insert_rows(0, 1)
+    t.m1.insert_cols(0, 1)
+    t.m1.set_cells(0, 0, 1, [0])
+    t.m2.insert_cols(0, 1)
+    t.m2.insert_rows(0, 1)
+    t.m2.set_cells(0, 0, 1, [90])
+    t.m2.connected = False
+    t.m2.connected = True
+    t.expect([[90, None], [None, 0]])
+
+
+RECONNECT = [resend_setcell_when_later_ops_shift, resend_setcell_multiple_reconnects, resend_unacked_ops,
+             store_ops_while_disconnected, omit_writes_to_recycled_handles, omit_not_yet_locally_deleted,
+             reset_handles_for_resubmitted_ops]
+
+
+@pytest.mark.parametrize("engine", KINDS)
+@pytest.mark.parametrize("case", RECONNECT, ids=[c.__name__ for c in RECONNECT])
+def test_reconnection(case, engine):
+    """The "Reconnection" cases (setCell(IFluidHandle), :781-806, compares handle objects and is not restated)."""
+    t = TwoR(engine)
+    case(t)
+    t.expect()  # afterEach (:661-666)
+    if engine:
+        assert t.s.checks > 0
