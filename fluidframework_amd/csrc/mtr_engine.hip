@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -151,6 +152,15 @@ struct mtr_engine {
     int32_t* h_pflags = nullptr;
     uint32_t h_pflags_n = 0;
     DevBuf<mtr_doc_desc> pdocs;  // the descriptors as uploaded (part_ready_kernel enables them)
+    // pipelined summaries (mtr_replay_pipelined): a part is summarized and downloaded once its documents are done
+    uint8_t* pipe_out = nullptr;
+    bool pipe_one_group = false;  // (set by mtr_replay_pipelined around its mtr_submit_pipelined)
+    int64_t pipe_cap = 0;
+    DevBuf<int32_t> pleft;                     // per part: documents with ops left (classify_kernel)
+    int32_t *h_pleft = nullptr, *d_pleft = nullptr;   // (mapped page-locked copy, its device address)
+    int64_t *h_psize = nullptr, *d_psize = nullptr;   // per document: summary sizes read back, then offsets
+    uint32_t h_pleft_n = 0, h_psize_n = 0;
+    std::vector<hipEvent_t> pdone_ev, psize_ev;     // per part: documents done, sizes read back
     // timing
     double t_apply = 0, t_summary = 0;
     double t_kernels = 0;  // sum of the apply launches' own durations (they overlap across lanes)
@@ -185,6 +195,12 @@ __global__ void cursor_reset_kernel(DocHdr* h, const mtr_doc_desc* docs, uint32_
 // dst[i] = src ? src[i] : 0 for i < n (one block): zeroing and reading back small counters without a DMA copy
 __global__ void words_kernel(int32_t* dst, const int32_t* src, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src ? src[i] : 0;
+    __threadfence_system();
+}
+
+// dst[i] = src[i] for i < n, 64-bit words (summary sizes to mapped host memory, offsets back)
+__global__ void words64_kernel(int64_t* dst, const int64_t* src, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
     __threadfence_system();
 }
 
@@ -255,7 +271,8 @@ constexpr int kClasses = 64;
 constexpr int kAllClasses = 2 * kClasses;
 __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t lo,
                                                       uint32_t hi, const uint32_t* dkind, const uint32_t* dpart,
-                                                      int32_t* cls, uint32_t* list, int class_leaves) {
+                                                      int32_t* cls, uint32_t* list, int class_leaves,
+                                                      int32_t* pleft = nullptr, uint32_t n_all = 0, uint32_t pparts = 0) {
     // block-local histogram in LDS, then one global atomic per (block, class): the per-document
     // atomics on a handful of addresses would serialise at the memory side
     __shared__ int lcnt[kAllClasses], lmax[kAllClasses], lheap[kAllClasses], lbase[kAllClasses];
@@ -284,6 +301,10 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
             atomicMax(&lmax[c], nseg);
             atomicMax(&lheap[c], heapn);
             atomicMax(&lrem, rem);
+            if (pleft) {  // (a pipelined run: this document's part still has ops left)
+                const uint32_t pp = uint32_t(((uint64_t(d) + 1) * pparts - 1) / n_all);  // part_lo[p] = n p / P
+                if (!pleft[pp]) atomicOr(&pleft[pp], 1);
+            }
         }
     }
     __syncthreads();
@@ -445,6 +466,12 @@ int mtr_engine_destroy(mtr_engine* e) {
         }
     for (auto& x : e->part_ev)
         if (x) (void)hipEventDestroy(x);
+    for (auto* v : {&e->pdone_ev, &e->psize_ev})
+        for (auto& x : *v)
+            if (x) (void)hipEventDestroy(x);
+    e->pleft.release();
+    if (e->h_pleft) (void)hipHostFree(e->h_pleft);
+    if (e->h_psize) (void)hipHostFree(e->h_psize);
     e->pflags.release();
     e->pdocs.release();
     if (e->h_pflags) (void)hipHostFree(e->h_pflags);
@@ -637,7 +664,15 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts) {
     for (uint32_t p = 0; p <= parts; p++) e->part_lo[p] = uint32_t(uint64_t(n) * p / parts);
     // two document groups (mtr_run's default above 4,096 documents), each with half the parts: the upload
     // alternates between them, so both start within the first two parts
-    e->pipe_groups = (n >= 4096u && parts >= 2) ? 2u : 1u;
+    // (mtr_replay_pipelined: one group unless MTR_PIPE_GROUPS=2 -- the group's documents run their rounds in
+    // lockstep, so its parts finish in the order they landed, a part's width apart, and their summaries and
+    // downloads stream out behind them; two groups finish at two times, the second's parts all together)
+    int pg = (n >= 4096u && parts >= 2) ? 2 : 1;
+    if (e->pipe_one_group) {
+        const char* v = std::getenv("MTR_PIPE_GROUPS");
+        pg = std::min(pg, v && *v ? std::max(1, std::atoi(v)) : 1);
+    }
+    e->pipe_groups = uint32_t(pg);
     const uint32_t half = (parts + 1) / 2;
     for (uint32_t q = 0; q < parts; q++) {
         const uint32_t p = e->pipe_groups == 2 ? ((q & 1) ? half + q / 2 : q / 2) : q;
@@ -664,6 +699,7 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts) {
 }
 
 static int run_impl(mtr_engine* e, int gen);
+static int summary_params(mtr_engine* e, SParams& P);
 
 int mtr_run(mtr_engine* e) { return run_impl(e, 0); }
 
@@ -808,6 +844,14 @@ static int run_impl(mtr_engine* e, int gen) {
     static const bool no_fixed_cap = std::getenv("MTR_NO_FIXED_CAP") != nullptr;
     // matrix pairs on one wave even when two could run them (tuning knob MTR_PAIR1)
     static const bool pair1 = std::getenv("MTR_PAIR1") != nullptr;
+    static const bool ptrace = std::getenv("MTR_PIPE_TRACE") != nullptr;  // (host timeline of a pipelined run)
+    const auto tr0 = std::chrono::steady_clock::now();
+    auto trace = [&](const char* what, int a, int b) {
+        if (ptrace)
+            std::fprintf(stderr, "pipe %8.3f ms %s %d %d\n",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count(),
+                         what, a, b);
+    };
     static const int slack_env = [] {
         const char* v = std::getenv("MTR_SLACK");
         return v ? std::max(0, std::atoi(v)) : -1;
@@ -846,6 +890,7 @@ static int run_impl(mtr_engine* e, int gen) {
                                            : (any_pair || (e->n_docs >= 4096u && e->n_docs <= 60000u) ? 128 : 64);
     // (a pipelined hand-over: its parts still landing; a group takes whole parts)
     const uint32_t PP = gen ? 0u : e->pipe_parts;
+    const bool psum = PP && e->pipe_out;  // (mtr_replay_pipelined)
     int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
     if (PP) G = std::min<int>(int(e->pipe_groups), int(PP));
     const int L = std::max(1, nlanes / G);  // lanes (streams) per group
@@ -871,14 +916,14 @@ static int run_impl(mtr_engine* e, int gen) {
     auto lanes_of = [&](int g) -> int {
         if (!PP) return L;
         const int base = G == 2 ? (g == 0 ? 2 : 1) : int(mtr_engine::kLanes) - 1;
-        if (G == 2 && g == 0) return base;  // (the copy stream is group 1's second lane)
+        if ((G == 2 && g == 0) || psum) return base;  // (the copy stream: group 1's second lane; summaries' stream)
         const hipError_t q = hipEventQuery(e->part_ev[e->pipe_last]);
         return q == hipSuccess ? base + 1 : base;
     };
     struct Grp {
         uint32_t lo = 0, hi = 0;
         bool done = false;
-        uint32_t p_hi = 0, waited = 0;  // pipelined: the group's parts [waited .. p_hi) not yet waited for
+        uint32_t p_lo = 0, p_hi = 0, waited = 0;  // pipelined: its parts [p_lo, p_hi), [waited, p_hi) not waited for
     };
     std::vector<Grp> grp(static_cast<size_t>(G));
     for (int g = 0; g < G; g++) {
@@ -886,6 +931,7 @@ static int run_impl(mtr_engine* e, int gen) {
         if (PP) {  // (mtr_submit_pipelined's split: two groups take [0, half) and [half, PP))
             const uint32_t half = (PP + 1) / 2;
             gr.waited = G == 2 && g == 1 ? half : 0u;
+            gr.p_lo = gr.waited;
             gr.p_hi = G == 2 && g == 0 ? half : PP;
             gr.lo = e->part_lo[gr.waited];
             gr.hi = e->part_lo[gr.p_hi];
@@ -906,15 +952,22 @@ static int run_impl(mtr_engine* e, int gen) {
     // classify group g (on its first lane) and read its class counts back
     auto classify = [&](int g) -> int {
         Grp& gr = grp[size_t(g)];
+        // (pipelined summaries: the parts that have landed by now count as waited for -- this classify sees all
+        // of their documents, so a part it finds with no ops left is done)
+        if (psum)
+            while (gr.waited < gr.p_hi && hipEventQuery(e->part_ev[gr.waited]) == hipSuccess) gr.waited++;
         hipStream_t st = lane_stream(g, 0);
         int32_t* dcls = e->cls.p + size_t(g) * ncls;
         // (the counters are zeroed and read back by kernels, the read-back into mapped page-locked memory: a DMA
         // copy would queue behind mtr_submit_pipelined's uploads on the copy engine)
         words_kernel<<<1, 256, 0, st>>>(dcls, nullptr, int(ncls));
+        if (psum) words_kernel<<<1, 256, 0, st>>>(e->pleft.p + gr.p_lo, nullptr, int(gr.p_hi - gr.p_lo));
         const uint32_t n = gr.hi - gr.lo;
         classify_kernel<<<(n + 255) / 256, 256, 0, st>>>(e->hdr.p, e->docs.p, gr.lo, gr.hi, e->dkind.p, e->dpart.p,
-                                                         dcls, e->dlist.p + size_t(kAllClasses) * gr.lo, class_leaves);
+                                                         dcls, e->dlist.p + size_t(kAllClasses) * gr.lo, class_leaves,
+                                                         psum ? e->pleft.p : nullptr, e->n_docs, PP);
         words_kernel<<<1, 256, 0, st>>>(e->d_cls + size_t(g) * ncls, dcls, int(ncls));
+        if (psum) words_kernel<<<1, 256, 0, st>>>(e->d_pleft + gr.p_lo, e->pleft.p + gr.p_lo, int(gr.p_hi - gr.p_lo));
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e->grp_cls[g], st));
         return 0;
@@ -1040,6 +1093,88 @@ static int run_impl(mtr_engine* e, int gen) {
         }
         return 0;
     };
+    // pipelined summaries (mtr_replay_pipelined): a part whose documents have no ops left is summarized on the copy
+    // stream -- the size pass, its sizes read back into mapped memory, the offsets (parts in order), the write pass
+    // and the blobs' download into the caller's buffer -- while the other parts still apply
+    SParams SP{};
+    std::vector<int> pstate;  // per part: 0 applying, 1 done (pdone_ev recorded), 2 sizing, 3 downloading
+    uint32_t next_size = 0, next_dl = 0;
+    int64_t pbase = 0;
+    int prc = 0;  // a summary pass's error: no more passes, the apply runs out, then run_impl returns it
+    if (psum) {
+        e->summarized = false;
+        if (summary_params(e, SP) || e->out.ensure(size_t(e->pipe_cap) + 16) || e->pleft.ensure(PP)) return -1;
+        SP.out = e->out.p;
+        if (e->h_pleft_n < PP) {
+            if (e->h_pleft) HIPCHK(hipHostFree(e->h_pleft));
+            HIPCHK(hipHostMalloc((void**)&e->h_pleft, size_t(PP) * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer((void**)&e->d_pleft, e->h_pleft, 0));
+            e->h_pleft_n = PP;
+        }
+        if (e->h_psize_n < e->n_docs) {
+            if (e->h_psize) HIPCHK(hipHostFree(e->h_psize));
+            HIPCHK(hipHostMalloc((void**)&e->h_psize, size_t(e->n_docs) * sizeof(int64_t),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer((void**)&e->d_psize, e->h_psize, 0));
+            e->h_psize_n = e->n_docs;
+        }
+        for (auto* v : {&e->pdone_ev, &e->psize_ev})
+            while (v->size() < PP) {
+                hipEvent_t x;
+                HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+                v->push_back(x);
+            }
+        pstate.assign(PP, 0);
+        e->h_size.assign(e->n_docs, 0);
+        e->h_off.assign(e->n_docs, 0);
+    }
+    auto pump = [&]() -> int {
+        if (prc) return 0;
+        while (next_size < PP && pstate[next_size] == 1) {  // size passes, parts in order
+            const uint32_t p = next_size++, lo = e->part_lo[p], hi = e->part_lo[p + 1];
+            HIPCHK(hipStreamWaitEvent(e->copy, e->pdone_ev[p], 0));
+            SP.doc_base = lo;
+            summary_size_kernel<<<hi - lo, 64, 0, e->copy>>>(SP);
+            words64_kernel<<<(hi - lo + 255) / 256, 256, 0, e->copy>>>(e->d_psize + lo, e->out_size.p + lo, hi - lo);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(e->psize_ev[p], e->copy));
+            pstate[p] = 2;
+            trace("size", int(p), 0);
+        }
+        while (next_dl < next_size) {  // offsets, write pass, download, parts in order
+            const hipError_t q = hipEventQuery(e->psize_ev[next_dl]);
+            if (q == hipErrorNotReady) break;
+            HIPCHK(q);
+            const uint32_t p = next_dl++, lo = e->part_lo[p], hi = e->part_lo[p + 1];
+            const int64_t base = pbase;
+            for (uint32_t d = lo; d < hi; d++) {
+                const int64_t z = e->h_psize[d];
+                if (z < 0) {
+                    set_err("document " + std::to_string(d) + " has more summary chunks than the engine's blob table");
+                    return MTR_ERR_CAPACITY;
+                }
+                e->h_size[d] = z;
+                e->h_off[d] = pbase;
+                e->h_psize[d] = pbase;  // (the offsets go back through the same mapped words)
+                pbase += z;
+            }
+            if (pbase > e->pipe_cap) {
+                set_err("mtr_replay_pipelined: the output buffer holds " + std::to_string(e->pipe_cap) + " bytes, the "
+                        "summaries need more");
+                return MTR_ERR_CAPACITY;
+            }
+            words64_kernel<<<(hi - lo + 255) / 256, 256, 0, e->copy>>>(e->out_off.p + lo, e->d_psize + lo, hi - lo);
+            SP.doc_base = lo;
+            summary_write_kernel<<<hi - lo, 64, 0, e->copy>>>(SP);
+            HIPCHK(hipGetLastError());
+            if (pbase > base)
+                HIPCHK(hipMemcpyAsync(e->pipe_out + base, e->out.p + base, size_t(pbase - base), hipMemcpyDeviceToHost,
+                                      e->copy));
+            pstate[p] = 3;
+            trace("download", int(p), int((pbase - base) >> 20));
+        }
+        return 0;
+    };
     // pipelined: a group classifies again once the next of its parts has landed (its lane 0 waits for it)
     auto wait_part = [&](int g) -> int {
         Grp& gr = grp[size_t(g)];
@@ -1063,21 +1198,36 @@ static int run_impl(mtr_engine* e, int gen) {
             HIPCHK(q);
             progressed = true;
             const int32_t* cls = e->h_cls + size_t(g) * ncls;
+            if (psum) {  // parts classified after they landed with no ops left: done (before this round's launches)
+                for (uint32_t p = gr.p_lo; p < gr.waited; p++)
+                    if (pstate[p] == 0 && e->h_pleft[p] == 0) {
+                        HIPCHK(hipEventRecord(e->pdone_ev[p], lane_stream(g, 0)));
+                        pstate[p] = 1;
+                        trace("done", int(p), g);
+                    }
+            }
             if (cls[0] <= 0) {
                 if (PP && gr.waited < gr.p_hi) {  // more of the group's documents are still landing
                     if (wait_part(g) || classify(g)) return -1;
                     continue;
                 }
                 gr.done = true;
+                trace("group-done", g, 0);
                 left--;
                 continue;
             }
+            trace("round", g, cls[0]);
             if (issue_round(g, stuck)) return -1;
             if (stuck) break;
             if (classify(g)) return -1;  // queued behind the round's launches
         }
         if (stuck) break;
+        if (psum) prc = pump();
         if (!progressed) std::this_thread::yield();
+    }
+    while (psum && !stuck && !prc && next_dl < PP) {  // the last parts' summaries
+        prc = pump();
+        if (next_dl < PP) std::this_thread::yield();
     }
     for (int g = 0; g < G; g++)
         if (g > 0) {  // join every group into the engine stream
@@ -1097,6 +1247,12 @@ static int run_impl(mtr_engine* e, int gen) {
     if (PP) {  // the parts' op-scan bits: a part holding records the pipelined path does not run was not started
         e->pipe_parts = 0;
         HIPCHK(hipStreamSynchronize(e->copy));
+        trace("end", int(prc), 0);
+        if (prc) return prc;
+        if (psum && !stuck) {
+            e->out_total = pbase;
+            e->summarized = true;
+        }
         for (uint32_t p = 0; p < PP; p++)
             if (e->h_pflags[p]) {
                 set_err("mtr_submit_pipelined: documents " + std::to_string(e->part_lo[p]) + ".." +
@@ -1109,8 +1265,35 @@ static int run_impl(mtr_engine* e, int gen) {
         set_err("document exceeds the leaf capacity");
         return MTR_ERR_CAPACITY;
     }
-    e->summarized = false;
+    if (!psum) e->summarized = false;
     return MTR_OK;
+}
+
+int64_t mtr_replay_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts, uint8_t* out, int64_t cap,
+                             int64_t* doc_off) {
+    const uint32_t n = b->n_docs;
+    e->pipe_one_group = true;
+    int rc = mtr_submit_pipelined(e, b, parts);
+    e->pipe_one_group = false;
+    if (rc != MTR_OK) return -1;
+    if (e->pipe_parts) {
+        e->pipe_out = out;
+        e->pipe_cap = cap;
+        rc = run_impl(e, 0);
+        e->pipe_out = nullptr;
+        if (rc != MTR_OK) return -1;
+        if (doc_off) {
+            for (uint32_t d = 0; d < n; d++) doc_off[d] = e->h_off[d];
+            doc_off[n] = e->out_total;
+        }
+        return e->out_total;
+    }
+    // (a batch the pipelined path does not take: mtr_submit's, then the ordinary summarize and download)
+    if (mtr_run(e) != MTR_OK || mtr_summarize(e) != MTR_OK) return -1;
+    const int64_t r = mtr_get_summaries(e, 0, n, out, cap, doc_off);
+    if (r < -1) set_err("mtr_replay_pipelined: the output buffer holds " + std::to_string(cap) + " bytes, the summaries "
+                        "need " + std::to_string(-r));
+    return r < 0 ? -1 : r;
 }
 
 __global__ void synth_init_kernel(mtr_synth_cfg cfg, mtr_synth_state* st, uint32_t n) {
@@ -1321,12 +1504,11 @@ int mtr_download_batch(mtr_engine* e, uint32_t lo, uint32_t hi, mtr_doc_desc* do
     return MTR_OK;
 }
 
-int mtr_summarize(mtr_engine* e) {
-    HIPCHK(hipSetDevice(e->device));
+// the summary kernels' parameters for every document of the batch (scratch buffers sized)
+static int summary_params(mtr_engine* e, SParams& P) {
     const uint32_t n = e->n_docs;
-    if (n == 0) return MTR_OK;
     if (e->out_size.ensure(n) || e->out_off.ensure(n) || e->out_hash.ensure(n)) return -1;
-    SParams P{};
+    P = SParams{};
     P.hdr = e->hdr.p;
     P.seg = e->seg.p;
     P.text = e->text.p;
@@ -1365,6 +1547,15 @@ int mtr_summarize(mtr_engine* e) {
         P.s_bytes = e->s_bytes.p;
         P.s_blob = e->s_blob.p;
     }
+    return 0;
+}
+
+int mtr_summarize(mtr_engine* e) {
+    HIPCHK(hipSetDevice(e->device));
+    const uint32_t n = e->n_docs;
+    if (n == 0) return MTR_OK;
+    SParams P;
+    if (summary_params(e, P)) return -1;
     HIPCHK(hipEventRecord(e->ev[2], e->stream));
     summary_size_kernel<<<n, 64, 0, e->stream>>>(P);
     HIPCHK(hipGetLastError());

@@ -32,6 +32,7 @@ struct SParams {
     int32_t segcap, tcap, pcap, rcap, rtab;
     int32_t snapshot_v1, chunk_size, new_length_calc;
     uint32_t n_docs;
+    uint32_t doc_base;  // the launch's blocks are documents doc_base + blockIdx.x (< n_docs)
     const mtr_doc_desc* docs;
     const uint32_t* key_off;
     const uint8_t* key_bytes;
@@ -884,13 +885,13 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
 #define MTR_SWPE 8
 #endif
 __global__ void __launch_bounds__(64) summary_size_kernel(SParams P) {
-    const uint32_t d = blockIdx.x;
+    const uint32_t d = P.doc_base + blockIdx.x;
     if (d >= P.n_docs) return;
     summary_size_doc(P, d);
 }
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTR_SWPE))) summary_write_kernel(SParams P) {
-    const uint32_t d = blockIdx.x;
+    const uint32_t d = P.doc_base + blockIdx.x;
     if (d >= P.n_docs) return;
     summary_write_doc(P, d);
 }

@@ -59,6 +59,8 @@ def lib():
         L.mtr_submit.restype = C.c_int
         L.mtr_submit_pipelined.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
         L.mtr_submit_pipelined.restype = C.c_int
+        L.mtr_replay_pipelined.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p]
+        L.mtr_replay_pipelined.restype = C.c_int64
         L.mtr_get_summary.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]
         L.mtr_get_summary.restype = C.c_int64
         L.mtr_summary_info.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
@@ -192,6 +194,19 @@ class Engine:
         arrays should be page-locked (Engine.download(..., pinned_memory=True)) for the copies to overlap."""
         self._batch = batch
         self._check(lib().mtr_submit_pipelined(self.h, C.addressof(batch.c), int(parts)), "mtr_submit_pipelined")
+
+    def replay_pipelined(self, batch, out, parts=16):
+        """mtr_replay_pipelined: upload, apply, summarize and download every document's summary records into
+        `out` (a u1 array, page-locked for the copies to overlap), pipelined over `parts` document ranges.
+        Returns (out, doc_off) like summaries()."""
+        self._batch = batch
+        n = int(batch.c.n_docs)
+        doc_off = np.zeros(n + 1, dtype="<i8")
+        r = lib().mtr_replay_pipelined(self.h, C.addressof(batch.c), int(parts), out.ctypes.data, out.size,
+                                       doc_off.ctypes.data)
+        if r < 0:
+            raise EngineError(f"mtr_replay_pipelined failed: {_err()}")
+        return out, doc_off
 
     def run(self):
         self._check(lib().mtr_run(self.h), "mtr_run")

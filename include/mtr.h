@@ -68,6 +68,17 @@ int mtr_submit(mtr_engine* e, const mtr_batch* b);
  * (each document's op records and text after the previous one's); parts <= 1 is mtr_submit. */
 int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts);
 
+/* The whole end-to-end hand-over in one call: mtr_submit_pipelined + mtr_run + mtr_summarize + mtr_get_summaries
+ * over every document, pipelined at both ends -- a range whose documents have no ops left is summarized and its
+ * records downloaded into `out` (cap bytes; page-locked for the copies to overlap) while the later ranges still
+ * upload and apply.  Writes doc_off[0..n_docs] (as mtr_get_summaries) and returns the byte count, or -1
+ * (mtr_last_error; MTR_ERR_CAPACITY text when cap is too small).  The summaries stay readable afterwards
+ * (mtr_get_summary, mtr_get_summaries, mtr_hashes).  A batch the pipelined path does not take (see
+ * mtr_submit_pipelined) runs the serial calls.  Replaces, for a summarizer, the applyMsg loop followed by
+ * summarizeCore (SURVEY 8d's end-to-end row). */
+int64_t mtr_replay_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts, uint8_t* out, int64_t cap,
+                             int64_t* doc_off);
+
 /* Apply the submitted ops (Client.applyMsg for each message, in order, per document). Async. */
 int mtr_run(mtr_engine* e);
 

@@ -251,6 +251,44 @@ def test_pipelined_submit_equals_serial_submit(n, parts):
     assert np.array_equal(eng.hashes(n), want)
 
 
+@pytest.mark.parametrize("n, parts", [(3000, 16), (5000, 7), (5000, 64)])
+def test_replay_pipelined_equals_serial_calls(n, parts):
+    """mtr_replay_pipelined (a range summarized and downloaded once its documents are done, while the later ranges
+    still upload and apply): byte for byte the records of mtr_submit + mtr_run + mtr_summarize + mtr_get_summaries,
+    the same hashes, the per-document reads still served afterwards; a buffer too small is refused."""
+    from fluidframework_amd.engine import EngineError, pinned
+    from fluidframework_amd.synth import make_cfg, tables
+
+    ops = 300
+    cfg = make_cfg(n, ops, writers=8, max_lag=32, seed=0x7e11 + parts)
+    eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
+                  prop_words=16384, remover_cells=4096, ops_per_launch=48)
+    eng.generate(cfg, tables(writers=8))
+    hb = eng.download(0, n, pinned_memory=True)
+    eng.reset()
+    eng.submit(hb)
+    eng.run()
+    eng.summarize()
+    want_h = eng.hashes(n).copy()
+    want, want_off = eng.summaries(0, n)
+    want = want[:int(want_off[-1])].copy()
+    out = pinned(want.size + 4096, "u1")
+    for _ in range(2):
+        eng.reset()
+        out[:] = 0
+        buf, off = eng.replay_pipelined(hb, out, parts)
+        assert eng.stats()["bad_docs"] == 0
+        assert np.array_equal(off, want_off)
+        assert np.array_equal(buf[:int(off[-1])], want)
+        assert np.array_equal(eng.hashes(n), want_h)
+        for d in (0, n // 2, n - 1):
+            again, again_off = eng.summaries(d, d + 1)
+            assert np.array_equal(again[:int(again_off[-1])], want[int(want_off[d]):int(want_off[d + 1])])
+    eng.reset()
+    with pytest.raises(EngineError, match="output buffer"):
+        eng.replay_pipelined(hb, pinned(want.size // 2, "u1"), parts)
+
+
 def test_pipelined_submit_refuses_records_beyond_remote_ops():
     """A part holding a record the pipelined path does not run (here MTR_F_DELTA) is not started: mtr_run returns
     MTR_ERR_UNSUPPORTED, and after mtr_reset the same batch through mtr_submit is applied in full."""
