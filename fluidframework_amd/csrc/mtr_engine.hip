@@ -160,7 +160,7 @@ struct mtr_engine {
     int32_t *h_pleft = nullptr, *d_pleft = nullptr;   // (mapped page-locked copy, its device address)
     int64_t *h_psize = nullptr, *d_psize = nullptr;   // per document: summary sizes read back, then offsets
     uint32_t h_pleft_n = 0, h_psize_n = 0;
-    std::vector<hipEvent_t> pdone_ev, psize_ev;     // per part: documents done, sizes read back
+    std::vector<hipEvent_t> pdone_ev, psize_ev, pwrite_ev;  // per part: documents done, sizes read back, written
     // timing
     double t_apply = 0, t_summary = 0;
     double t_kernels = 0;  // sum of the apply launches' own durations (they overlap across lanes)
@@ -466,7 +466,7 @@ int mtr_engine_destroy(mtr_engine* e) {
         }
     for (auto& x : e->part_ev)
         if (x) (void)hipEventDestroy(x);
-    for (auto* v : {&e->pdone_ev, &e->psize_ev})
+    for (auto* v : {&e->pdone_ev, &e->psize_ev, &e->pwrite_ev})
         for (auto& x : *v)
             if (x) (void)hipEventDestroy(x);
     e->pleft.release();
@@ -891,6 +891,14 @@ static int run_impl(mtr_engine* e, int gen) {
     // (a pipelined hand-over: its parts still landing; a group takes whole parts)
     const uint32_t PP = gen ? 0u : e->pipe_parts;
     const bool psum = PP && e->pipe_out;  // (mtr_replay_pipelined)
+    // ops per launch of a pipelined run: twice the engine's -- while parts are landing a round holds few documents,
+    // so its fixed costs (the launches' ramp and tail, the class read-back) weigh more per op; C3 end-to-end
+    // 270.1 -> 264.3 ms at 96 against 48, the device-resident rate unchanged (profiles/r06_e2e_sweep.json)
+    static const int pipe_k_env = [] {
+        const char* v = std::getenv("MTR_PIPE_K");
+        return v ? std::atoi(v) : 0;
+    }();
+    const int Kr = !PP ? K : pipe_k_env > 0 ? pipe_k_env : int(std::min<int64_t>(2 * int64_t(K), 0x7fffffff));
     int G = any_pair ? 1 : std::max(1, std::min<int>(g_want, int(e->n_docs)));
     if (PP) G = std::min<int>(int(e->pipe_groups), int(PP));
     const int L = std::max(1, nlanes / G);  // lanes (streams) per group
@@ -990,7 +998,7 @@ static int run_impl(mtr_engine* e, int gen) {
         const int Lr = lanes_of(g);
         const int32_t* cls = e->h_cls + size_t(g) * ncls;
         const uint32_t n = gr.hi - gr.lo;
-        const int k = std::min(K, cls[0]);
+        const int k = std::min(Kr, cls[0]);
         hipStream_t st0 = lane_stream(g, 0);
         HIPCHK(hipEventRecord(e->grp_fork[g], st0));
         int nl = 0;  // launches of this round
@@ -1118,7 +1126,7 @@ static int run_impl(mtr_engine* e, int gen) {
             HIPCHK(hipHostGetDevicePointer((void**)&e->d_psize, e->h_psize, 0));
             e->h_psize_n = e->n_docs;
         }
-        for (auto* v : {&e->pdone_ev, &e->psize_ev})
+        for (auto* v : {&e->pdone_ev, &e->psize_ev, &e->pwrite_ev})
             while (v->size() < PP) {
                 hipEvent_t x;
                 HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
@@ -1128,16 +1136,20 @@ static int run_impl(mtr_engine* e, int gen) {
         e->h_size.assign(e->n_docs, 0);
         e->h_off.assign(e->n_docs, 0);
     }
+    int left = G;  // groups still applying
+    // (the summary kernels run on the copy stream while the apply runs, on the idle engine stream once it is done,
+    // so the last parts' passes do not queue behind the downloads)
     auto pump = [&]() -> int {
         if (prc) return 0;
+        hipStream_t ks = left == 0 ? e->stream : e->copy;
         while (next_size < PP && pstate[next_size] == 1) {  // size passes, parts in order
             const uint32_t p = next_size++, lo = e->part_lo[p], hi = e->part_lo[p + 1];
-            HIPCHK(hipStreamWaitEvent(e->copy, e->pdone_ev[p], 0));
+            HIPCHK(hipStreamWaitEvent(ks, e->pdone_ev[p], 0));
             SP.doc_base = lo;
-            summary_size_kernel<<<hi - lo, 64, 0, e->copy>>>(SP);
-            words64_kernel<<<(hi - lo + 255) / 256, 256, 0, e->copy>>>(e->d_psize + lo, e->out_size.p + lo, hi - lo);
+            summary_size_kernel<<<hi - lo, 64, 0, ks>>>(SP);
+            words64_kernel<<<(hi - lo + 255) / 256, 256, 0, ks>>>(e->d_psize + lo, e->out_size.p + lo, hi - lo);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(e->psize_ev[p], e->copy));
+            HIPCHK(hipEventRecord(e->psize_ev[p], ks));
             pstate[p] = 2;
             trace("size", int(p), 0);
         }
@@ -1163,10 +1175,14 @@ static int run_impl(mtr_engine* e, int gen) {
                         "summaries need more");
                 return MTR_ERR_CAPACITY;
             }
-            words64_kernel<<<(hi - lo + 255) / 256, 256, 0, e->copy>>>(e->out_off.p + lo, e->d_psize + lo, hi - lo);
+            words64_kernel<<<(hi - lo + 255) / 256, 256, 0, ks>>>(e->out_off.p + lo, e->d_psize + lo, hi - lo);
             SP.doc_base = lo;
-            summary_write_kernel<<<hi - lo, 64, 0, e->copy>>>(SP);
+            summary_write_kernel<<<hi - lo, 64, 0, ks>>>(SP);
             HIPCHK(hipGetLastError());
+            if (ks != e->copy) {
+                HIPCHK(hipEventRecord(e->pwrite_ev[p], ks));
+                HIPCHK(hipStreamWaitEvent(e->copy, e->pwrite_ev[p], 0));
+            }
             if (pbase > base)
                 HIPCHK(hipMemcpyAsync(e->pipe_out + base, e->out.p + base, size_t(pbase - base), hipMemcpyDeviceToHost,
                                       e->copy));
@@ -1186,7 +1202,6 @@ static int run_impl(mtr_engine* e, int gen) {
     HIPCHK(hipEventRecord(e->ev[1], e->stream));  // (timing start: after the forks above)
     for (int g = 0; g < G; g++)
         if ((PP && wait_part(g)) || classify(g)) return -1;
-    int left = G;
     bool stuck = false;
     while (left > 0) {
         bool progressed = false;
