@@ -422,39 +422,63 @@ MTR_DI void unit_write(gptr<uint8_t> o, uint32_t p, uint32_t c, uint32_t n) {
     w.unit(c, hi);
 }
 // the body of spec [s, e) (pieces: leaf s and the kind-1 leaves after it, concatenated) by all
-// 64 lanes, one unit per lane per round: byte counts, a wave scan for offsets, then each lane
-// writes its unit (W).  Returns the body's byte count.
+// 64 lanes, one unit per lane per round over the concatenation -- a round spans pieces, which are
+// short (a few units each after the splits), so a round per piece left most lanes idle: byte
+// counts, a wave scan for offsets, then each lane writes its unit (W).  The pieces are taken 64 at
+// a time, one per lane; a unit's piece is found by a binary search over the lanes' piece starts.
+// Returns the body's byte count.
 template <bool W>
 MTR_DI int64_t wave_body(const SDoc& D, int s, int e, gptr<uint8_t> out) {
     const int ln = lane_id();
     int64_t nb = 0;
-    uint32_t prev = NOU;  // last unit of the previous non-empty piece
-    for (int k = s; k < e; k++) {
-        if (k != s && D.kind[k] != 1) continue;
-        const int L = int(uniu(D.len[k]));
-        if (L <= 0) continue;
-        const uint32_t t = uniu(D.text[k]);
-        uint32_t after = NOU;  // first unit of the next non-empty piece
-        for (int k2 = k + 1; k2 < e; k2++)
+    uint32_t prev = NOU;  // last unit of the body so far
+    for (int g0 = s; g0 < e; g0 += 64) {
+        const int k = g0 + ln;
+        int L = 0;
+        uint32_t t = 0;
+        if (k < e && (k == s || D.kind[k] == 1)) {
+            L = max(int(D.len[k]), 0);
+            t = D.text[k];
+        }
+        const int incl = wave_incl_scan(L);
+        const int T = rdlane(incl, 63);  // units of this group of pieces
+        if (T == 0) continue;
+        const int start = incl - L;
+        const uint64_t nz = __ballot(L > 0);
+        uint32_t after = NOU;  // first unit after this group's pieces
+        for (int k2 = g0 + 64; k2 < e; k2++)
             if (D.kind[k2] == 1 && uni(int(D.len[k2])) > 0) {
                 after = uniu(uint32_t(D.gtext[uniu(D.text[k2])]));
                 break;
             }
-        for (int u0 = 0; u0 < L; u0 += 64) {
+        for (int u0 = 0; u0 < T; u0 += 64) {
             const int i = u0 + ln;
-            const bool in = i < L;
-            const uint32_t c = in ? uint32_t(D.gtext[t + uint32_t(i)]) : NOU;
+            const bool in = i < T;
+            // unit i's piece: the last lane whose start is <= i (an empty piece shares the next one's start)
+            int j = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1) {
+                const int sc = __shfl(start, j + step);
+                if (sc <= i) j += step;
+            }
+            const int off = i - __shfl(start, j);
+            const uint32_t tj = uint32_t(__shfl(int(t), j));
+            const int Lj = __shfl(L, j);
+            const uint32_t c = in ? uint32_t(D.gtext[tj + uint32_t(off)]) : NOU;
+            // the unit after i when it is in the next piece of the group: that piece's first unit
+            const uint64_t up = j >= 63 ? 0ull : (nz & (~0ull << (j + 1)));
+            const uint32_t tn = uint32_t(__shfl(int(t), up ? first_lane(up) : 0));
             uint32_t pu = uint32_t(__shfl(int(c), max(ln - 1, 0)));
-            if (ln == 0) pu = u0 == 0 ? prev : uint32_t(D.gtext[t + uint32_t(u0 - 1)]);
+            if (ln == 0) pu = prev;
             uint32_t nu = uint32_t(__shfl(int(c), min(ln + 1, 63)));
-            if (i + 1 >= L) nu = after;
-            else if (ln == 63) nu = uint32_t(D.gtext[t + uint32_t(i + 1)]);
-            const int b = in ? unit_bytes(pu, c, nu) : 0;
-            const int incl = wave_incl_scan(b);
-            if (W && in && b) unit_write(out + (nb + incl - b), pu, c, nu);
-            nb += rdlane(incl, 63);
+            if (i + 1 >= T) nu = after;
+            else if (ln == 63) nu = off + 1 < Lj ? uint32_t(D.gtext[tj + uint32_t(off + 1)]) : uint32_t(D.gtext[tn]);
+            const int bts = in ? unit_bytes(pu, c, nu) : 0;
+            const int bi = wave_incl_scan(bts);
+            if (W && in && bts) unit_write(out + (nb + bi - bts), pu, c, nu);
+            nb += rdlane(bi, 63);
+            prev = uint32_t(rdlane(int(c), min(63, T - 1 - u0)));
         }
-        prev = uniu(uint32_t(D.gtext[t + uint32_t(L - 1)]));
     }
     return nb;
 }
