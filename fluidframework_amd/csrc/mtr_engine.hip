@@ -157,6 +157,7 @@ struct mtr_engine {
     bool pipe_one_group = false;  // (set by mtr_replay_pipelined around its mtr_submit_pipelined)
     int64_t pipe_cap = 0;
     DevBuf<int32_t> pleft;                     // per part: documents with ops left (classify_kernel)
+    DevBuf<uint32_t> dpart_lo;                 // the parts' first documents (+ n_docs), for classify_kernel
     int32_t *h_pleft = nullptr, *d_pleft = nullptr;   // (mapped page-locked copy, its device address)
     int64_t *h_psize = nullptr, *d_psize = nullptr;   // per document: summary sizes read back, then offsets
     uint32_t h_pleft_n = 0, h_psize_n = 0;
@@ -272,7 +273,8 @@ constexpr int kAllClasses = 2 * kClasses;
 __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mtr_doc_desc* docs, uint32_t lo,
                                                       uint32_t hi, const uint32_t* dkind, const uint32_t* dpart,
                                                       int32_t* cls, uint32_t* list, int class_leaves,
-                                                      int32_t* pleft = nullptr, uint32_t n_all = 0, uint32_t pparts = 0) {
+                                                      int32_t* pleft = nullptr, const uint32_t* plo = nullptr,
+                                                      uint32_t pparts = 0) {
     // block-local histogram in LDS, then one global atomic per (block, class): the per-document
     // atomics on a handful of addresses would serialise at the memory side
     __shared__ int lcnt[kAllClasses], lmax[kAllClasses], lheap[kAllClasses], lbase[kAllClasses];
@@ -302,7 +304,9 @@ __global__ void __launch_bounds__(256) classify_kernel(const DocHdr* h, const mt
             atomicMax(&lheap[c], heapn);
             atomicMax(&lrem, rem);
             if (pleft) {  // (a pipelined run: this document's part still has ops left)
-                const uint32_t pp = uint32_t(((uint64_t(d) + 1) * pparts - 1) / n_all);  // part_lo[p] = n p / P
+                uint32_t pp = 0;  // the last part whose first document is <= d
+                for (uint32_t step = 1u << (31 - __clz(int(pparts))); step > 0; step >>= 1)
+                    if (pp + step < pparts && plo[pp + step] <= d) pp += step;
                 if (!pleft[pp]) atomicOr(&pleft[pp], 1);
             }
         }
@@ -470,6 +474,7 @@ int mtr_engine_destroy(mtr_engine* e) {
         for (auto& x : *v)
             if (x) (void)hipEventDestroy(x);
     e->pleft.release();
+    e->dpart_lo.release();
     if (e->h_pleft) (void)hipHostFree(e->h_pleft);
     if (e->h_psize) (void)hipHostFree(e->h_psize);
     e->pflags.release();
@@ -673,6 +678,11 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts) {
         pg = std::min(pg, v && *v ? std::max(1, std::atoi(v)) : 1);
     }
     e->pipe_groups = uint32_t(pg);
+    // (a ramp -- the first two parts a quarter and a half of the others' size -- measured slower end to end:
+    // 263.5 against 260.9 ms on C3, profiles/r06_e2e_sweep.json)
+    if (e->dpart_lo.ensure(size_t(parts) + 1)) return -1;
+    HIPCHK(hipMemcpyAsync(e->dpart_lo.p, e->part_lo.data(), (size_t(parts) + 1) * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, e->stream));
     const uint32_t half = (parts + 1) / 2;
     for (uint32_t q = 0; q < parts; q++) {
         const uint32_t p = e->pipe_groups == 2 ? ((q & 1) ? half + q / 2 : q / 2) : q;
@@ -973,7 +983,7 @@ static int run_impl(mtr_engine* e, int gen) {
         const uint32_t n = gr.hi - gr.lo;
         classify_kernel<<<(n + 255) / 256, 256, 0, st>>>(e->hdr.p, e->docs.p, gr.lo, gr.hi, e->dkind.p, e->dpart.p,
                                                          dcls, e->dlist.p + size_t(kAllClasses) * gr.lo, class_leaves,
-                                                         psum ? e->pleft.p : nullptr, e->n_docs, PP);
+                                                         psum ? e->pleft.p : nullptr, e->dpart_lo.p, PP);
         words_kernel<<<1, 256, 0, st>>>(e->d_cls + size_t(g) * ncls, dcls, int(ncls));
         if (psum) words_kernel<<<1, 256, 0, st>>>(e->d_pleft + gr.p_lo, e->pleft.p + gr.p_lo, int(gr.p_hi - gr.p_lo));
         HIPCHK(hipGetLastError());
