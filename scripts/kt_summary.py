@@ -30,7 +30,7 @@ res = {
     "source": "rocprofv3 --kernel-trace --stats -- python3 bench.py " + " ".join(sys.argv[3:]),
     "timed_step_apply_launches": n,
     "avg_launch_ms_rocprof": sum(dur) / n,
-    "avg_launch_ms_bench_hip_events": bench["roofline"]["avg_launch_ms"],
+    "avg_launch_ms_bench_hip_events": bench["roofline"]["per_launch"]["avg_launch_ms"],
     "apply_span_ms_rocprof": (t1 - t0) / 1e6,
     "apply_wall_ms_bench": bench["roofline"].get("apply_wall_ms_per_step"),
     "bench_value_under_profiler": bench["value"],
