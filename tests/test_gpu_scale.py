@@ -289,6 +289,62 @@ def test_replay_pipelined_equals_serial_calls(n, parts):
         eng.replay_pipelined(hb, pinned(want.size // 2, "u1"), parts)
 
 
+@pytest.mark.parametrize("n, parts", [(5, 16), (40, 1), (40, 3)])
+def test_replay_pipelined_small_batches_and_serial_fallback(n, parts):
+    """mtr_replay_pipelined on batches the pipelined path splits into fewer ranges than asked (5 documents, 16 parts)
+    or does not split at all (parts = 1: the serial calls inside): the records of the serial calls."""
+    from fluidframework_amd.engine import pinned
+    from fluidframework_amd.synth import make_cfg, tables
+
+    ops = 200
+    cfg = make_cfg(n, ops, writers=4, max_lag=16, seed=0x5a11 + n + parts)
+    eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
+                  prop_words=16384, remover_cells=4096, ops_per_launch=48)
+    eng.generate(cfg, tables(writers=4))
+    hb = eng.download(0, n, pinned_memory=True)
+    eng.reset()
+    eng.submit(hb)
+    eng.run()
+    eng.summarize()
+    want, want_off = eng.summaries(0, n)
+    want = want[:int(want_off[-1])].copy()
+    eng.reset()
+    buf, off = eng.replay_pipelined(hb, pinned(want.size + 64, "u1"), parts)
+    assert eng.stats()["bad_docs"] == 0
+    assert np.array_equal(off, want_off)
+    assert np.array_equal(buf[:int(off[-1])], want)
+
+
+def test_replay_pipelined_refuses_records_beyond_remote_ops():
+    """A range holding a record the pipelined path does not run: mtr_replay_pipelined fails with
+    MTR_ERR_UNSUPPORTED's message, and after mtr_reset the serial calls apply the same batch in full."""
+    from fluidframework_amd.engine import EngineError, pinned
+    from fluidframework_amd.synth import make_cfg, tables, with_docs
+
+    n, ops = 400, 200
+    cfg = make_cfg(n, ops, writers=4, max_lag=16, seed=0xbeef)
+    eng = _engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
+                  prop_words=16384, remover_cells=4096, ops_per_launch=48)
+    eng.generate(cfg, tables(writers=8))
+    eng.reset()
+    eng.run()
+    eng.summarize()
+    want = eng.hashes(n).copy()
+    hb = eng.download(0, n)
+    ops_arr = hb.ops.copy()
+    ops_arr["flags"][int(hb.docs["op_begin"][123]) + 7] |= abi.F_DELTA
+    flagged = with_docs(tables(writers=8), hb.docs.copy(), ops_arr, hb.text)
+    eng.reset()
+    with pytest.raises(EngineError, match="beyond remote ops"):
+        eng.replay_pipelined(flagged, pinned(1 << 24, "u1"), 4)
+    eng.reset()
+    eng.submit(flagged)
+    eng.run()
+    eng.summarize()
+    assert eng.stats()["bad_docs"] == 0
+    assert np.array_equal(eng.hashes(n), want)
+
+
 def test_pipelined_submit_refuses_records_beyond_remote_ops():
     """A part holding a record the pipelined path does not run (here MTR_F_DELTA) is not started: mtr_run returns
     MTR_ERR_UNSUPPORTED, and after mtr_reset the same batch through mtr_submit is applied in full."""
