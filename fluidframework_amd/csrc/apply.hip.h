@@ -4856,18 +4856,21 @@ struct Eng {
                     }
                 }
                 wsync();
-                if (lru) {  // addToLRUSet for every touched leaf, in leaf order (one push per block)
+                if (lru) {  // addToLRUSet for every touched leaf, in leaf order: one step per leaf block (its
+                    // first touched leaf), the block's other touched leaves skipped by mask
                     const uint64_t fm = __ballot(in && bnd_of(mj) >= 1);
                     uint64_t todo = am;
                     while (todo) {
                         const int l = first_lane(todo);
-                        todo &= todo - 1;
                         const uint64_t below = fm & ((uint64_t(2) << l) - 1);
                         const int b = below ? base + last_lane(below) : block_start(L, base, 1);
                         if (b != last_blk) {
                             last_blk = b;
                             add_lru_block(L, s, b, uniu(L.uid[base + l]), seq);
                         }
+                        // the next block starts at the first block-start lane above l
+                        const uint64_t above = l == 63 ? 0 : (fm & (~uint64_t(0) << (l + 1)));
+                        todo = above ? (todo & (~uint64_t(0) << first_lane(above))) : 0;
                     }
                 }
             }

@@ -1273,11 +1273,6 @@ static int run_impl(mtr_engine* e, int gen) {
         e->pipe_parts = 0;
         HIPCHK(hipStreamSynchronize(e->copy));
         trace("end", int(prc), 0);
-        if (prc) return prc;
-        if (psum && !stuck) {
-            e->out_total = pbase;
-            e->summarized = true;
-        }
         for (uint32_t p = 0; p < PP; p++)
             if (e->h_pflags[p]) {
                 set_err("mtr_submit_pipelined: documents " + std::to_string(e->part_lo[p]) + ".." +
@@ -1285,6 +1280,11 @@ static int run_impl(mtr_engine* e, int gen) {
                         "local references or rare records); mtr_reset and submit the batch with mtr_submit");
                 return MTR_ERR_UNSUPPORTED;
             }
+        if (prc) return prc;  // (a summary pass's error: the batch is applied, the summaries are not built)
+        if (psum && !stuck) {
+            e->out_total = pbase;
+            e->summarized = true;
+        }
     }
     if (stuck) {
         set_err("document exceeds the leaf capacity");

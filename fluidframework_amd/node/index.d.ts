@@ -36,6 +36,14 @@ export class BatchReplayEngine {
 	flush(): void;
 	/** flush() on a libuv worker thread (napi_async_work); other calls on this engine throw until it settles. */
 	flushAsync(): Promise<void>;
+	/**
+	 * The summarizer's hand-over in one call (mtr_replay_pipelined): apply every queued message, build every
+	 * document's summary and download the records -- document d's is bytes[docOff[d], docOff[d + 1]): u32 blob
+	 * count, u32 blob lengths, the blobs (the same bytes summarize() returns as blob contents).  Batches of remote
+	 * messages go through the pipelined path in `parts` document ranges (pipelined: true); others take the serial
+	 * calls.  The per-client summarize() reads stay valid afterwards.
+	 */
+	replaySummaries(parts?: number): { bytes: Buffer; docOff: Float64Array; pipelined: boolean };
 }
 
 /** getContainingSegment's answer (client.ts:1065-1078); both fields undefined when no segment covers pos. */

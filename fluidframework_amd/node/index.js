@@ -855,6 +855,20 @@ class BatchReplayEngine {
         }
         this._afterRun();
     }
+    /**
+     * The summarizer's hand-over in one call (mtr_replay_pipelined through the addon's replaySummaries): every
+     * queued message applied, every document summarized and its records in host memory -- document d's record is
+     * bytes[docOff[d], docOff[d + 1]) = u32 blob count, u32 blob lengths, the blobs.  A batch of remote messages
+     * goes through the pipelined path (ranges applied as they land, summarized and downloaded as they finish;
+     * `pipelined` true), any other the serial calls.
+     */
+    replaySummaries(parts = 16) {
+        this._assertIdle();
+        const r = native().replaySummaries(this.h, this._batch(), parts);
+        this._afterRun();
+        this.summarized = true;
+        return r;
+    }
     async summarizeAllAsync() {  // every document's blobs, built on a worker thread
         await this.flushAsync();
         if (!this.summarized) {

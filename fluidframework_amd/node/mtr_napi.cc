@@ -8,7 +8,9 @@
 #include <node_api.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
+#include <map>
 #include <set>
 #include <string>
 #include <vector>
@@ -102,8 +104,18 @@ bool arr_prop(napi_env env, napi_value obj, const char* name, const T** p, size_
 }
 
 // (an engine with a job in flight is never finalized: the job holds a reference to its handle)
+// per engine: the page-locked buffer replaySummaries downloads into (mtr_host_alloc), grown on demand
+std::map<mtr_engine*, std::pair<uint8_t*, int64_t>> g_out;
+
 void finalize_engine(napi_env, void* data, void*) {
-    if (data) mtr_engine_destroy(static_cast<mtr_engine*>(data));
+    if (!data) return;
+    auto* e = static_cast<mtr_engine*>(data);
+    auto it = g_out.find(e);
+    if (it != g_out.end()) {
+        mtr_host_free(it->second.first);
+        g_out.erase(it);
+    }
+    mtr_engine_destroy(e);
 }
 
 // createEngine(maxDocs, {device, newLengthCalc, snapshotV1, chunkSize, maxSegments, heapEntries,
@@ -172,6 +184,94 @@ napi_value SubmitRun(napi_env env, napi_callback_info info) {
     if (mtr_run(e) != MTR_OK || mtr_sync(e) != MTR_OK) return throw_engine(env, "mtr_run");
     napi_value r;
     NAPI_CALL(env, napi_get_undefined(env, &r));
+    return r;
+}
+
+// replaySummaries(h, batch, parts) -> {bytes: Buffer, docOff: Float64Array}: the summarizer's whole hand-over
+// (mtr_replay_pipelined): upload, apply, summarize and every document's records in host memory, pipelined at both
+// ends; document d's record is bytes[docOff[d], docOff[d + 1]) = u32 blob count, u32 lengths, the blobs
+// (mtr_get_summaries' layout).  The records land in a page-locked buffer of the engine's, grown when a batch needs
+// more (that batch then takes the serial summarize + download), and are copied into the returned Buffer.  The
+// batch's arrays are the JS heap's: the upload is not overlapped unless they are page-locked.
+// whether mtr_submit_pipelined would start every range of the batch: no record its op scan refuses (op_scan_kernel
+// in mtr_engine.hip -- MTR_F_DELTA, reference records, the local-op path, rare records); a refused range would be
+// left unapplied while the others ran, so such a batch takes the serial calls here instead
+bool pipelinable(const mtr_batch& b) {
+    for (uint64_t i = 0; i < b.n_ops; i++) {
+        const mtr_op& op = b.ops[i];
+        const uint32_t t = op.type;
+        if ((op.flags & (MTR_F_DELTA | MTR_F_REL)) || t == MTR_OP_REF_CREATE || t == MTR_OP_REF_REMOVE ||
+            t == MTR_OP_REF_ACK || t == MTR_OP_REBASE_POS || t == MTR_OP_LSEQ || t == MTR_OP_ACK ||
+            t == MTR_OP_ROLLBACK || t == MTR_OP_REGENERATE || t == MTR_OP_RELPOS || t == MTR_OP_HANDLES ||
+            t == MTR_OP_LOCAL_SETCELL || (t >= MTR_OP_LOCAL_INSERT && t <= MTR_OP_LOCAL_ANNOTATE && op.seq == -1) ||
+            (t == MTR_OP_ANNOTATE && op.payload2 != 0) ||
+            ((op.flags & MTR_F_MARKER) && op.payload2 != 0 &&
+             (t == MTR_OP_INSERT || t == MTR_OP_LOCAL_INSERT || t == MTR_OP_LOAD)))
+            return false;
+    }
+    return true;
+}
+
+napi_value ReplaySummaries(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return nullptr;
+    mtr_engine* e = engine_of(env, argv[0]);
+    if (!e) return nullptr;
+    mtr_batch b{};
+    if (!parse_batch(env, argv[1], b)) return nullptr;
+    uint32_t parts = 16;
+    NAPI_CALL(env, napi_get_value_uint32(env, argv[2], &parts));
+    const uint32_t n = b.n_docs;
+    auto& buf = g_out[e];
+    if (!buf.first) {  // a first guess (64 MiB, or the batch's text at 16 bytes a unit): a larger need takes the
+        // serial download once and grows the buffer for the next call
+        buf.second = std::max<int64_t>(int64_t(64) << 20, int64_t(16) * int64_t(b.n_text) + 4096 * int64_t(n));
+        buf.first = static_cast<uint8_t*>(mtr_host_alloc(uint64_t(buf.second)));
+        if (!buf.first) {
+            g_out.erase(e);
+            return throw_engine(env, "mtr_host_alloc");
+        }
+    }
+    std::vector<int64_t> off64(size_t(n) + 1, 0);
+    const bool pipe = buf.first && pipelinable(b);
+    int64_t total = pipe ? mtr_replay_pipelined(e, &b, parts, buf.first, buf.second, off64.data()) : -1;
+    const bool piped = total >= 0;
+    if (total < 0) {
+        // a batch the pipelined path refuses, or a buffer too small (the batch is applied then)
+        if (pipe && std::string(mtr_last_error()).find("output buffer holds") == std::string::npos)
+            return throw_engine(env, "mtr_replay_pipelined");
+        if (!pipe) {
+            if (mtr_submit(e, &b) != MTR_OK || mtr_sync(e) != MTR_OK) return throw_engine(env, "mtr_submit");
+            if (mtr_run(e) != MTR_OK || mtr_sync(e) != MTR_OK) return throw_engine(env, "mtr_run");
+        }
+        if (mtr_summarize(e) != MTR_OK || mtr_sync(e) != MTR_OK) return throw_engine(env, "mtr_summarize");
+        const int64_t need = -mtr_get_summaries(e, 0, n, nullptr, 0, nullptr);
+        if (need < 0) return throw_engine(env, "mtr_get_summaries");
+        if (!buf.first || buf.second < need) {
+            if (buf.first) mtr_host_free(buf.first);
+            buf.second = need + need / 4 + 4096;
+            buf.first = static_cast<uint8_t*>(mtr_host_alloc(uint64_t(buf.second)));
+            if (!buf.first) {
+                g_out.erase(e);
+                return throw_engine(env, "mtr_host_alloc");
+            }
+        }
+        total = mtr_get_summaries(e, 0, n, buf.first, buf.second, off64.data());
+        if (total < 0) return throw_engine(env, "mtr_get_summaries");
+    }
+    std::vector<double> off(size_t(n) + 1, 0.0);
+    for (size_t d = 0; d <= n; d++) off[d] = double(off64[d]);
+    napi_value r, bytes, ab, doff, pv;
+    void* data = nullptr;
+    NAPI_CALL(env, napi_create_buffer_copy(env, size_t(total), buf.first, &data, &bytes));
+    NAPI_CALL(env, napi_create_arraybuffer(env, off.size() * sizeof(double), &data, &ab));
+    std::memcpy(data, off.data(), off.size() * sizeof(double));
+    NAPI_CALL(env, napi_create_typedarray(env, napi_float64_array, off.size(), ab, 0, &doff));
+    NAPI_CALL(env, napi_get_boolean(env, piped, &pv));
+    NAPI_CALL(env, napi_create_object(env, &r));
+    NAPI_CALL(env, napi_set_named_property(env, r, "bytes", bytes));
+    NAPI_CALL(env, napi_set_named_property(env, r, "docOff", doff));
+    NAPI_CALL(env, napi_set_named_property(env, r, "pipelined", pv));
     return r;
 }
 
@@ -622,7 +722,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"summarizeAsync", SummarizeAsync}, {"getContainingSegment", GetContainingSegment},
                {"getProps", GetProps}, {"getRefPositions", GetRefPositions}, {"getRefInfo", GetRefInfo},
                {"getRefStates", GetRefStates}, {"getLeaves", GetLeaves}, {"getRefKeys", GetRefKeys},
-               {"getViewLength", GetViewLength}};
+               {"getViewLength", GetViewLength}, {"replaySummaries", ReplaySummaries}};
     for (const auto& f : fns) {
         napi_value fn;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok ||

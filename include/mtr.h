@@ -72,7 +72,9 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts);
  * over every document, pipelined at both ends -- a range whose documents have no ops left is summarized and its
  * records downloaded into `out` (cap bytes; page-locked for the copies to overlap) while the later ranges still
  * upload and apply.  Writes doc_off[0..n_docs] (as mtr_get_summaries) and returns the byte count, or -1
- * (mtr_last_error; MTR_ERR_CAPACITY text when cap is too small).  The summaries stay readable afterwards
+ * (mtr_last_error).  When cap is too small the error text starts "mtr_replay_pipelined: the output buffer holds":
+ * the batch is then applied in full and mtr_summarize + mtr_get_summaries give its records.  The summaries stay
+ * readable afterwards
  * (mtr_get_summary, mtr_get_summaries, mtr_hashes).  A batch the pipelined path does not take (see
  * mtr_submit_pipelined) runs the serial calls.  Replaces, for a summarizer, the applyMsg loop followed by
  * summarizeCore (SURVEY 8d's end-to-end row). */

@@ -50,7 +50,7 @@ def test_addon_loads_and_fails_loudly_without_a_gpu():
                                            "docStatus", "stats", "reset", "setMatrix", "getDeltas",
                                            "submitRunAsync", "summarizeAsync", "getContainingSegment", "getProps",
                                            "getRefPositions", "getRefInfo", "getRefStates", "getLeaves",
-                                           "getRefKeys", "getViewLength"])
+                                           "getRefKeys", "getViewLength", "replaySummaries"])
     if lines[1] != "ENGINE":  # no HIP device here: construction must throw, never fall back
         assert lines[1].startswith("ERR mtr_engine_create")
 
@@ -154,6 +154,25 @@ def test_js_packer_matches_python_packer(pre):
     n_keys, n_vals = len(py.key_off) - 1, len(py.val_off) - 1
     assert np.array_equal(arr("keyIndex", "<u4")[:n_keys], py.key_index[:n_keys])
     assert np.array_equal(arr("valEq", "<u4")[:n_vals], py.val_eq[:n_vals])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [4, 16])
+def test_replay_summaries_through_node_host(parts):
+    """BatchReplayEngine.replaySummaries (mtr_replay_pipelined through the addon): the last group of every reference
+    log applied, summarized and downloaded in one call on an engine holding the earlier groups; the records equal
+    the oracle's blobs and the per-client summarize(), and the remote-message batch took the pipelined path."""
+    paths = replay_files()
+    _addon()
+    res = json.loads(_node([os.path.join(HERE, "node", "replay_summaries.js"), str(parts)] + paths, timeout=300))
+    assert res["checks"] == sum(len(load_replay(p)) for p in paths)
+    assert res["pipelined"] is True
+    b = _py_batch(paths)
+    for r in res["result"]:
+        orc = OracleDoc(options())
+        assert orc.apply(b, r["doc"]) == 0
+        assert [base64.b64decode(x) for x in r["blobs"]] == orc.summarize(b, r["doc"]), f"doc {r['doc']}"
+        assert r["same_as_summarize"]
 
 
 @pytest.mark.gpu
