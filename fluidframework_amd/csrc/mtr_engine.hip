@@ -132,7 +132,7 @@ struct mtr_engine {
     // summaries
     DevBuf<int64_t> out_size, out_off;
     DevBuf<uint8_t> s_kind;                       // summary scratch (size pass -> write pass)
-    DevBuf<uint32_t> s_start, s_len, s_bytes;
+    DevBuf<uint32_t> s_start, s_len, s_bytes, s_lb, s_fl;
     DevBuf<int32_t> s_blob;
     DevBuf<unsigned long long> out_hash;
     DevBuf<uint8_t> out;
@@ -449,6 +449,8 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->s_start.release();
     e->s_len.release();
     e->s_bytes.release();
+    e->s_lb.release();
+    e->s_fl.release();
     e->s_blob.release();
     e->out_off.release();
     e->out_hash.release();
@@ -1564,12 +1566,15 @@ static int summary_params(mtr_engine* e, SParams& P) {
         const size_t sc = size_t(P.segcap);
         P.maxb = int(std::min<int64_t>(int64_t(sc) + 1, std::max<int64_t>(int64_t(P.tcap) / std::max(1, P.chunk_size) + 4, 64)));
         if (e->s_kind.ensure(n * sc) || e->s_start.ensure(n * (sc + 1)) || e->s_len.ensure(n * sc) ||
-            e->s_bytes.ensure(n * sc) || e->s_blob.ensure(n * (4 + 4 * size_t(P.maxb))))
+            e->s_bytes.ensure(n * sc) || e->s_blob.ensure(n * (4 + 4 * size_t(P.maxb))) || e->s_lb.ensure(n * sc) ||
+            e->s_fl.ensure(n * sc))
             return -1;
         P.s_kind = e->s_kind.p;
         P.s_start = e->s_start.p;
         P.s_len = e->s_len.p;
         P.s_bytes = e->s_bytes.p;
+        P.s_lb = e->s_lb.p;
+        P.s_fl = e->s_fl.p;
         P.s_blob = e->s_blob.p;
     }
     return 0;
@@ -1581,6 +1586,15 @@ int mtr_summarize(mtr_engine* e) {
     if (n == 0) return MTR_OK;
     SParams P;
     if (summary_params(e, P)) return -1;
+    {  // (timing probes: MTR_SUM_DEBUG, summary.hip.h g_sdbg)
+        const char* v = std::getenv("MTR_SUM_DEBUG");
+        const int dbg = v ? std::atoi(v) : 0;
+        static int last = 0;
+        if (dbg != last) {
+            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_sdbg), &dbg, sizeof(int)));
+            last = dbg;
+        }
+    }
     HIPCHK(hipEventRecord(e->ev[2], e->stream));
     summary_size_kernel<<<n, 64, 0, e->stream>>>(P);
     HIPCHK(hipGetLastError());

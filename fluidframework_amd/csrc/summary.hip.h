@@ -47,6 +47,8 @@ struct SParams {
     uint32_t* s_start;  // [doc][segcap + 1]  first leaf of every spec (+ sentinel)
     uint32_t* s_len;    // [doc][segcap]      spec length (UTF-16 units)
     uint32_t* s_bytes;  // [doc][segcap]      spec JSON bytes
+    uint32_t* s_lb;     // [doc][segcap]      per leaf: its text's JSON string-body bytes, as a string of its own
+    uint32_t* s_fl;     // [doc][segcap]      per leaf: first unit | last unit << 16 (pairing across pieces)
     int32_t* s_blob;    // [doc][4 + 4 * maxb]: nspec, nblob, totalLength, ok; per blob start, count, length, bytes
     int32_t maxb;
     int64_t* out_size;       // size pass output
@@ -167,7 +169,7 @@ struct SDoc {
     gptr<const uint32_t> gprop, grm, grt;
     int rtmask;
     gptr<uint8_t> kind;
-    gptr<uint32_t> start, slen, sbytes;
+    gptr<uint32_t> start, slen, sbytes, lb, fl;
     gptr<int32_t> blob;
     int S, minseq, curseq, collab, local, newlen;
     int perm, hlen;  // PermutationVector: [length, start] specs, HandleTable of hlen words in the arena
@@ -192,6 +194,8 @@ MTR_DI SDoc sdoc(const SParams& P, uint32_t d, const DocHdr& h) {
     D.start = gp(P.s_start) + size_t(d) * (P.segcap + 1);
     D.slen = gp(P.s_len) + size_t(d) * P.segcap;
     D.sbytes = gp(P.s_bytes) + size_t(d) * P.segcap;
+    D.lb = gp(P.s_lb) + size_t(d) * P.segcap;
+    D.fl = gp(P.s_fl) + size_t(d) * P.segcap;
     D.blob = gp(P.s_blob) + size_t(d) * (4 + 4 * P.maxb);
     D.S = h.nseg;
     D.minseq = h.minseq;
@@ -286,9 +290,17 @@ MTR_DI void w_props(LW<W>& w, const SDoc& D, const SParams& P, uint32_t pr) {
     w.put('}');
 }
 
+// (timing probes only, MTR_SUM_DEBUG: bit 0 / 1 skip the size / write pass's lane-serial text, bit 2 the wave's
+// long bodies, bit 3 the blob digests -- the summaries are then wrong)
+__device__ int g_sdbg = 0;
+
 // the text of one leaf, 8 units per round of loads
 template <bool W>
 MTR_DI void w_units(LW<W>& w, const SDoc& D, uint32_t t, int n, int& hi) {
+    if (g_sdbg & (W ? 2 : 1)) {
+        w.n += n;
+        return;
+    }
     for (int u0 = 0; u0 < n; u0 += 8) {
         uint32_t b[8];
 #pragma unroll
@@ -429,6 +441,7 @@ MTR_DI void unit_write(gptr<uint8_t> o, uint32_t p, uint32_t c, uint32_t n) {
 // Returns the body's byte count.
 template <bool W>
 MTR_DI int64_t wave_body(const SDoc& D, int s, int e, gptr<uint8_t> out) {
+    if (g_sdbg & 4) return 0;
     const int ln = lane_id();
     int64_t nb = 0;
     uint32_t prev = NOU;  // last unit of the body so far
@@ -555,6 +568,7 @@ MTR_DI void w_blob_tail(LW<W>& w, const SDoc& D, int v1, int c, int nblob, int s
 }
 
 // ------------------------------------------------------------------ size pass
+constexpr int kLaneText = 32;  // a leaf's text up to this many units is counted by its lane, longer by the wave
 MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
     const DocHdr h = uni_struct(ld_struct<DocHdr>(gp(P.hdr) + d));
     const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
@@ -589,6 +603,52 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
         bool nl = false;  // last unit is '\n'
         if (kd == 1 && !mk && len > 0 && !D.perm)
             nl = (m & M_NLQ) ? D.gtext[tx + uint32_t(len) - 1] == u'\n' : (m & M_NL) != 0;
+        {  // the leaf's text as a JSON string body of its own (unit_bytes: a surrogate pairs with its neighbour
+            // inside the leaf; a pair split across two pieces of a spec is corrected in B), first and last unit.
+            // Short leaves one lane each, 8 units per round of loads; longer ones by the whole wave.
+            const bool tl = kd != 0 && !mk && len > 0 && !D.perm;
+            uint32_t lbv = 0, flv = 0;
+            if (tl && len <= kLaneText) {
+                uint32_t prev = NOU;
+                for (int u0 = 0; u0 < len; u0 += 8) {
+                    uint32_t b[9];
+#pragma unroll
+                    for (int q = 0; q < 9; q++) b[q] = u0 + q < len ? uint32_t(D.gtext[tx + uint32_t(u0 + q)]) : NOU;
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (u0 + q < len) lbv += uint32_t(unit_bytes(q ? b[q - 1] : prev, b[q], b[q + 1]));
+                    if (u0 == 0) flv = b[0];
+                    prev = b[7];
+                }
+                flv |= uint32_t(D.gtext[tx + uint32_t(len) - 1]) << 16;
+            }
+            for (uint64_t lm = __ballot(tl && len > kLaneText); lm; lm &= lm - 1) {
+                const int l = first_lane(lm);
+                const int L = rdlane(len, l);
+                const uint32_t t = uint32_t(rdlane(int(tx), l));
+                int64_t nb = 0;
+                uint32_t prev = NOU;
+                for (int u0 = 0; u0 < L; u0 += 64) {
+                    const int u = u0 + ln;
+                    const uint32_t c = u < L ? uint32_t(D.gtext[t + uint32_t(u)]) : NOU;
+                    uint32_t pu = uint32_t(__shfl(int(c), max(ln - 1, 0)));
+                    if (ln == 0) pu = prev;
+                    uint32_t nu = uint32_t(__shfl(int(c), min(ln + 1, 63)));
+                    if (u + 1 >= L) nu = NOU;
+                    else if (ln == 63) nu = uint32_t(D.gtext[t + uint32_t(u + 1)]);
+                    nb += rdlane(wave_incl_scan(u < L ? unit_bytes(pu, c, nu) : 0), 63);
+                    prev = uint32_t(rdlane(int(c), min(63, L - 1 - u0)));
+                }
+                if (ln == l) {
+                    lbv = uint32_t(nb);
+                    flv = uint32_t(D.gtext[t]) | (prev << 16);
+                }
+            }
+            if (in) {
+                D.lb[i] = lbv;
+                D.fl[i] = flv;
+            }
+        }
         const uint64_t ns = __ballot(kd != 0);
         const uint64_t below = ns & lanes_below();
         const int p = below ? last_lane(below) : -1;
@@ -662,31 +722,38 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
     if (ln == 0) D.start[nspec] = uint32_t(S);
     wsync();
 
-    // B. one lane per spec: length and JSON bytes
+    wsync();
+    // B. one lane per spec: length and JSON bytes -- a text body from its pieces' byte counts (A), less 8 bytes
+    // for each surrogate pair split across two pieces (two escaped halves, 12 bytes, become one 4-byte character)
     for (int g0 = 0; g0 < nspec; g0 += 64) {
         const int g = g0 + ln;
         if (g < nspec) {
             const int s = int(D.start[g]), e = int(D.start[g + 1]);
+            const bool txt = !D.perm && !(D.meta[s] & M_MARKER);
             int length = 0;
+            int64_t body = 0;
             if (D.kind[s] == 2) {
                 length = int(D.len[s]);
+                if (txt) body = D.lb[s];
             } else {
+                uint32_t lastu = NOU;  // last unit of the previous non-empty piece
                 for (int k = s; k < e; k++)
-                    if (k == s || D.kind[k] == 1) length += int(D.len[k]);
+                    if (k == s || D.kind[k] == 1) {
+                        const int lk = int(D.len[k]);
+                        length += lk;
+                        if (txt && lk > 0) {
+                            const uint32_t f = D.fl[k];
+                            body += D.lb[k];
+                            if (lastu != NOU && is_hi(lastu) && is_lo(f & 0xffffu)) body -= 8;
+                            lastu = f >> 16;
+                        }
+                    }
             }
             LW<false> w{(gptr<uint8_t>)nullptr, 0};
-            if (long_body(D, s, uint32_t(length))) w.skip = 0;  // counted by the wave below
+            if (txt) w.skip = body;
             w_spec(w, D, P, dd, s, e);
             D.slen[g] = uint32_t(length);
             D.sbytes[g] = uint32_t(w.n);
-        }
-        wsync();
-        const bool lb = g < nspec && long_body(D, int(D.start[g]), D.slen[g]);
-        for (uint64_t lm = __ballot(lb); lm; lm &= lm - 1) {  // long bodies: all lanes on one spec
-            const int l = first_lane(lm);
-            const int s = int(uniu(D.start[g0 + l])), e = int(uniu(D.start[g0 + l + 1]));
-            const int64_t nb = wave_body<false>(D, s, e, (gptr<uint8_t>)nullptr);
-            if (ln == l) D.sbytes[g] += uint32_t(nb);
         }
     }
     wsync();
@@ -773,6 +840,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
 
 // digest of one written blob (include/mtr_digest.h): one 8-byte word per lane per round
 MTR_DI uint64_t blob_digest(gptr<uint8_t> base, int64_t b0, int64_t blen) {
+    if (g_sdbg & 8) return 0;
     const int ln = lane_id();
     uint64_t sum = 0;
     const int64_t nw = (blen + 7) / 8;
@@ -796,6 +864,7 @@ MTR_DI uint64_t blob_digest(gptr<uint8_t> base, int64_t b0, int64_t blen) {
 
 // ------------------------------------------------------------------ write pass
 MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
+    if (g_sdbg & 16) return;
     const DocHdr h = uni_struct(ld_struct<DocHdr>(gp(P.hdr) + d));
     const mtr_doc_desc dd = uni_struct(ld_struct<mtr_doc_desc>(gp(P.docs) + d));
     SDoc D = sdoc(P, d, h);

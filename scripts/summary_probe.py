@@ -1,0 +1,18 @@
+import os, sys, json, time
+sys.path.insert(0, ".")
+from fluidframework_amd.engine import Engine
+from fluidframework_amd.synth import make_cfg, tables
+n, ops = 100000, 1000
+cfg = make_cfg(n, ops, writers=8, max_lag=32)
+eng = Engine(n, max_segments=2 * ops + 128, heap_entries=2 * ops + 128, text_units=2 * int(cfg.text_cap) + 1024,
+             prop_words=16384, remover_cells=4096, ops_per_launch=48)
+eng.generate(cfg, tables(writers=8))
+eng.reset(); eng.run(); eng.sync()
+res = {}
+for dbg in [0, 16, 2, 0]:
+    os.environ["MTR_SUM_DEBUG"] = str(dbg)
+    ts = []
+    for _ in range(3):
+        eng.summarize(); eng.sync(); ts.append(eng.timing()["summary_ms"])
+    res.setdefault(str(dbg), []).append(round(min(ts), 3))
+print(json.dumps(res), flush=True)
