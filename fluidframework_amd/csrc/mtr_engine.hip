@@ -132,7 +132,7 @@ struct mtr_engine {
     // summaries
     DevBuf<int64_t> out_size, out_off;
     DevBuf<uint8_t> s_kind;                       // summary scratch (size pass -> write pass)
-    DevBuf<uint32_t> s_start, s_len, s_bytes, s_lb, s_fl;
+    DevBuf<uint32_t> s_start, s_len, s_bytes, s_lb, s_fl, s_sid, s_bb;
     DevBuf<int32_t> s_blob;
     DevBuf<unsigned long long> out_hash;
     DevBuf<uint8_t> out;
@@ -451,6 +451,8 @@ int mtr_engine_destroy(mtr_engine* e) {
     e->s_bytes.release();
     e->s_lb.release();
     e->s_fl.release();
+    e->s_sid.release();
+    e->s_bb.release();
     e->s_blob.release();
     e->out_off.release();
     e->out_hash.release();
@@ -1567,7 +1569,7 @@ static int summary_params(mtr_engine* e, SParams& P) {
         P.maxb = int(std::min<int64_t>(int64_t(sc) + 1, std::max<int64_t>(int64_t(P.tcap) / std::max(1, P.chunk_size) + 4, 64)));
         if (e->s_kind.ensure(n * sc) || e->s_start.ensure(n * (sc + 1)) || e->s_len.ensure(n * sc) ||
             e->s_bytes.ensure(n * sc) || e->s_blob.ensure(n * (4 + 4 * size_t(P.maxb))) || e->s_lb.ensure(n * sc) ||
-            e->s_fl.ensure(n * sc))
+            e->s_fl.ensure(n * sc) || e->s_sid.ensure(n * sc) || e->s_bb.ensure(n * sc))
             return -1;
         P.s_kind = e->s_kind.p;
         P.s_start = e->s_start.p;
@@ -1575,6 +1577,8 @@ static int summary_params(mtr_engine* e, SParams& P) {
         P.s_bytes = e->s_bytes.p;
         P.s_lb = e->s_lb.p;
         P.s_fl = e->s_fl.p;
+        P.s_sid = e->s_sid.p;
+        P.s_bb = e->s_bb.p;
         P.s_blob = e->s_blob.p;
     }
     return 0;

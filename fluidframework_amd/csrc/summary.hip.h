@@ -49,6 +49,9 @@ struct SParams {
     uint32_t* s_bytes;  // [doc][segcap]      spec JSON bytes
     uint32_t* s_lb;     // [doc][segcap]      per leaf: its text's JSON string-body bytes, as a string of its own
     uint32_t* s_fl;     // [doc][segcap]      per leaf: first unit | last unit << 16 (pairing across pieces)
+    uint32_t* s_sid;    // [doc][segcap]      per leaf: the spec it belongs to (non-skipped leaves)
+    uint32_t* s_bb;     // [doc][segcap]      per spec: its text body's bytes (NONE32: no text body); the write
+                        //                    pass keeps the body's offset in s_len
     int32_t* s_blob;    // [doc][4 + 4 * maxb]: nspec, nblob, totalLength, ok; per blob start, count, length, bytes
     int32_t maxb;
     int64_t* out_size;       // size pass output
@@ -169,7 +172,7 @@ struct SDoc {
     gptr<const uint32_t> gprop, grm, grt;
     int rtmask;
     gptr<uint8_t> kind;
-    gptr<uint32_t> start, slen, sbytes, lb, fl;
+    gptr<uint32_t> start, slen, sbytes, lb, fl, sid, bb;
     gptr<int32_t> blob;
     int S, minseq, curseq, collab, local, newlen;
     int perm, hlen;  // PermutationVector: [length, start] specs, HandleTable of hlen words in the arena
@@ -196,6 +199,8 @@ MTR_DI SDoc sdoc(const SParams& P, uint32_t d, const DocHdr& h) {
     D.sbytes = gp(P.s_bytes) + size_t(d) * P.segcap;
     D.lb = gp(P.s_lb) + size_t(d) * P.segcap;
     D.fl = gp(P.s_fl) + size_t(d) * P.segcap;
+    D.sid = gp(P.s_sid) + size_t(d) * P.segcap;
+    D.bb = gp(P.s_bb) + size_t(d) * P.segcap;
     D.blob = gp(P.s_blob) + size_t(d) * (4 + 4 * P.maxb);
     D.S = h.nseg;
     D.minseq = h.minseq;
@@ -694,6 +699,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
         const bool st = kd == 2 || (kd == 1 && !link);
         const uint64_t sm = __ballot(st);
         if (st) D.start[nspec + __popcll(sm & lanes_below())] = uint32_t(i);
+        if (kd != 0) D.sid[i] = uint32_t(nspec + __popcll(sm & ((uint64_t(2) << ln) - 1)) - 1);
         nspec += __popcll(sm);
         if (ns) {  // carry: the last non-skipped leaf of this round
             const int q = last_lane(ns);
@@ -754,6 +760,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
             w_spec(w, D, P, dd, s, e);
             D.slen[g] = uint32_t(length);
             D.sbytes[g] = uint32_t(w.n);
+            D.bb[g] = txt ? uint32_t(body) : NONE32;
         }
     }
     wsync();
@@ -863,6 +870,124 @@ MTR_DI uint64_t blob_digest(gptr<uint8_t> base, int64_t b0, int64_t blen) {
 }
 
 // ------------------------------------------------------------------ write pass
+// one unit of a string body at w's position given its neighbours in the body (unit_bytes' bytes)
+MTR_DI void emit_unit(LW<true>& w, uint32_t p, uint32_t c, uint32_t n) {
+    if (is_lo(c) && p != NOU && is_hi(p)) return;
+    if (is_hi(c) && n != NOU && is_lo(n)) {
+        w.utf8(0x10000 + ((c - 0xD800) << 10) + (n - 0xDC00));
+        return;
+    }
+    if (is_hi(c) || is_lo(c)) {
+        w.hex4(c);
+        return;
+    }
+    int hi = -1;
+    w.unit(c, hi);
+}
+
+// the text bodies of every spec, one leaf (piece) a lane: a piece's place is its spec's body offset (kept in
+// D.slen by the wrapper pass) plus the bytes of the spec's earlier pieces -- the pieces' own counts (D.lb) less
+// the 2 / 6 bytes a surrogate pair split across two pieces saves at its high / low half
+MTR_DI void write_bodies(const SDoc& D, gptr<uint8_t> base) {
+    const int ln = lane_id();
+    const int S = D.S;
+    int cspec = -1;          // the spec of the last piece so far
+    int coff = 0;            // bytes of that spec's body written so far
+    uint32_t clast = NOU;    // the last unit of the last piece so far
+    for (int b0 = 0; b0 < S; b0 += 64) {
+        const int i = b0 + ln;
+        const bool in = i < S;
+        const int ic = min(i, S - 1);
+        const uint32_t kd = D.kind[ic];
+        const uint32_t m = D.meta[ic];
+        const int len = int(D.len[ic]);
+        const bool piece = in && kd != 0 && !(m & M_MARKER);
+        const int sid = piece ? int(D.sid[ic]) : -1;
+        const bool tl = piece && len > 0;  // (an empty piece writes nothing and breaks no pair)
+        const uint32_t f = tl ? D.fl[ic] : 0u;
+        const uint32_t first = tl ? (f & 0xffffu) : NOU, last = tl ? (f >> 16) : NOU;
+        const uint64_t pm = __ballot(tl);
+        if (!pm) continue;
+        // neighbours in the same spec: the previous / next text piece
+        const uint64_t pb = pm & lanes_below();
+        const int pl = pb ? last_lane(pb) : -1;
+        const int psid = __shfl(sid, max(pl, 0));
+        const uint32_t plast = uint32_t(__shfl(int(last), max(pl, 0)));
+        uint32_t prevu = NOU;
+        if (pl >= 0) prevu = psid == sid ? plast : NOU;
+        else prevu = cspec == sid ? clast : NOU;
+        const uint64_t pa = ln == 63 ? 0ull : (pm & (~uint64_t(0) << (ln + 1)));
+        const int nl = pa ? first_lane(pa) : 0;
+        const int nsid = __shfl(sid, nl);
+        const uint32_t nfirst = uint32_t(__shfl(int(first), nl));
+        uint32_t nextu = NOU;
+        if (pa) {
+            nextu = nsid == sid ? nfirst : NOU;
+        } else if (tl) {  // the window's last piece: the next text piece after the window, if in the same spec
+            for (int k = b0 + 64; k < S; k++) {
+                if (D.kind[k] == 0 || int(D.len[k]) <= 0) continue;
+                if ((D.meta[k] & M_MARKER) || int(D.sid[k]) != sid) break;
+                nextu = D.fl[k] & 0xffffu;
+                break;
+            }
+        }
+        const int ab = tl ? int(D.lb[ic]) - (is_hi(last) && nextu != NOU && is_lo(nextu) ? 2 : 0) -
+                                (is_lo(first) && prevu != NOU && is_hi(prevu) ? 6 : 0)
+                          : 0;
+        // the bytes of the spec's earlier pieces: a scan restarted at each spec's first piece in the window
+        const int incl = wave_incl_scan(ab);
+        const uint64_t heads = __ballot(tl && (pl < 0 ? true : psid != sid));  // a spec's first piece here
+        const uint64_t hu = heads & ((uint64_t(2) << ln) - 1);
+        const int hl = hu ? last_lane(hu) : 0;
+        const int hbase = __shfl(incl - ab, hl);
+        const int hsid = __shfl(sid, hl);
+        const int off = incl - ab - hbase + (hsid == cspec ? coff : 0);
+        if (tl && len <= kLaneText) {
+            LW<true> w{base, int64_t(D.slen[sid]) + off};
+            uint32_t p = prevu;
+            const uint32_t t = D.text[ic];
+            for (int u0 = 0; u0 < len; u0 += 8) {
+                uint32_t bu[9];
+#pragma unroll
+                for (int q = 0; q < 9; q++) bu[q] = u0 + q < len ? uint32_t(D.gtext[t + uint32_t(u0 + q)]) : nextu;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (u0 + q < len) emit_unit(w, q ? bu[q - 1] : p, bu[q], bu[q + 1]);
+                p = bu[7];
+            }
+        }
+        for (uint64_t lm = __ballot(tl && len > kLaneText); lm; lm &= lm - 1) {  // long pieces: the wave
+            const int l = first_lane(lm);
+            const int L = rdlane(len, l);
+            const uint32_t t = uniu(D.text[b0 + l]);
+            const int64_t at = int64_t(uniu(D.slen[rdlane(sid, l)])) + rdlane(off, l);
+            const uint32_t pv = uint32_t(rdlane(int(prevu), l)), nx = uint32_t(rdlane(int(nextu), l));
+            uint32_t prev = pv;
+            int64_t nb = 0;
+            for (int u0 = 0; u0 < L; u0 += 64) {
+                const int u = u0 + ln;
+                const bool uin = u < L;
+                const uint32_t c = uin ? uint32_t(D.gtext[t + uint32_t(u)]) : NOU;
+                uint32_t pu = uint32_t(__shfl(int(c), max(ln - 1, 0)));
+                if (ln == 0) pu = prev;
+                uint32_t nu = uint32_t(__shfl(int(c), min(ln + 1, 63)));
+                if (u + 1 >= L) nu = nx;
+                else if (ln == 63) nu = uint32_t(D.gtext[t + uint32_t(u + 1)]);
+                const int bts = uin ? unit_bytes(pu, c, nu) : 0;
+                const int bi = wave_incl_scan(bts);
+                if (uin && bts) unit_write(base + (at + nb + bi - bts), pu, c, nu);
+                nb += rdlane(bi, 63);
+                prev = uint32_t(rdlane(int(c), min(63, L - 1 - u0)));
+            }
+        }
+        // carry: the window's last text piece
+        const int q = last_lane(pm);
+        cspec = rdlane(sid, q);
+        coff = rdlane(off, q) + rdlane(ab, q);
+        clast = uint32_t(rdlane(int(last), q));
+    }
+}
+
 MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
     if (g_sdbg & 16) return;
     const DocHdr h = uni_struct(ld_struct<DocHdr>(gp(P.hdr) + d));
@@ -882,8 +1007,9 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
         base[2] = uint8_t(nall >> 16);
         base[3] = uint8_t(nall >> 24);
     }
-    int64_t pos = 4 + 4 * int64_t(nall);
-    uint64_t hsh = mtr_dg_begin(uint64_t(nall));
+    const int64_t pos0 = 4 + 4 * int64_t(nall);
+    int64_t pos = pos0;
+    // the blobs' wrappers and specs, each spec's text body left as a gap (its offset kept in D.slen)
     for (int c = 0; c < nblob; c++) {
         const int bs = uni(D.blob[4 + 4 * c + 0]), bc = uni(D.blob[4 + 4 * c + 1]), bl = uni(D.blob[4 + 4 * c + 2]);
         const int64_t b0 = pos;
@@ -897,26 +1023,14 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
             const bool act = g < bs + bc;
             const int x = act ? int(D.sbytes[g]) + (g > bs ? 1 : 0) : 0;
             const int incl = wave_incl_scan(x);
-            int64_t body_at = -1;
             if (act) {
                 LW<true> w{base, pos + incl - x};
                 if (g > bs) w.put(',');
                 const int s = int(D.start[g]), e = int(D.start[g + 1]);
-                if (long_body(D, s, D.slen[g])) {  // lay out around the body, which the wave writes
-                    LW<false> c{(gptr<uint8_t>)nullptr, 0};
-                    c.skip = 0;
-                    w_spec(c, D, P, dd, s, e);
-                    w.skip = int64_t(D.sbytes[g]) - c.n;
-                }
+                const uint32_t bb = D.bb[g];
+                if (bb != NONE32) w.skip = int64_t(bb);
                 w_spec(w, D, P, dd, s, e);
-                body_at = w.body_at;
-            }
-            wsync();
-            for (uint64_t lm = __ballot(body_at >= 0); lm; lm &= lm - 1) {
-                const int l = first_lane(lm);
-                const int s = int(uniu(D.start[g0 + l])), e = int(uniu(D.start[g0 + l + 1]));
-                const uint32_t lo = uint32_t(rdlane(uint32_t(body_at), l)), hi = uint32_t(rdlane(uint32_t(body_at >> 32), l));
-                wave_body<true>(D, s, e, base + int64_t((uint64_t(hi) << 32) | lo));
+                if (bb != NONE32) D.slen[g] = uint32_t(w.body_at);
             }
             pos += rdlane(incl, 63);
         }
@@ -931,9 +1045,20 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
             base[4 + 4 * c + 1] = uint8_t(blen >> 8);
             base[4 + 4 * c + 2] = uint8_t(blen >> 16);
             base[4 + 4 * c + 3] = uint8_t(blen >> 24);
+            D.blob[4 + 4 * c + 3] = int32_t(blen);
         }
-        wsync();
-        hsh = mtr_dg_next(hsh, blob_digest(base, b0, blen));
+    }
+    wsync();
+    if (!D.perm) write_bodies(D, base);
+    wsync();
+    uint64_t hsh = mtr_dg_begin(uint64_t(nall));
+    {
+        int64_t b0 = pos0;
+        for (int c = 0; c < nblob; c++) {
+            const int64_t blen = uni(D.blob[4 + 4 * c + 3]);
+            hsh = mtr_dg_next(hsh, blob_digest(base, b0, blen));
+            b0 += blen;
+        }
     }
     if (D.perm) {  // handleTable blob: "[h0,h1,...]" (HandleTable.getSummaryContent, handletable.ts:84)
         const gptr<const int32_t> ht = (gptr<const int32_t>)D.gtext;

@@ -24,6 +24,37 @@ def _engine(n_docs, **kw):
     return Engine(n_docs, **caps)
 
 
+@pytest.mark.parametrize("v1, chunk", [(True, 10000), (True, 300), (False, 10000), (False, 200)])
+def test_summary_bodies_split_pairs_and_long_pieces(v1, chunk):
+    """The summary passes' text bodies counted and written a piece (leaf) at a time: every document's blobs equal
+    the oracle's (SnapshotV1 and legacy, one blob and many) for texts dense in surrogate pairs (40 % of inserts end
+    with one, and splits land between the halves, so pairs straddle pieces of a coalesced spec) and inserts of up
+    to 100 units (pieces longer than one lane's share, written by the wave)."""
+    from oracle.oracle import OracleDoc, options
+    from fluidframework_amd.synth import make_cfg, tables
+
+    n, ops = 160, 500
+    cfg = make_cfg(n, ops, writers=8, max_lag=32, max_text=100, nonbmp_permille=400, newline_permille=3,
+                   seed=0x5a77 + chunk + int(v1))
+    eng = _engine(n, snapshot_v1=v1, chunk_size=chunk, max_segments=2 * ops + 128, heap_entries=2 * ops + 128,
+                  text_units=2 * int(cfg.text_cap) + 1024, prop_words=16384, remover_cells=4096, ops_per_launch=48)
+    eng.generate(cfg, tables(writers=8))
+    eng.reset()
+    eng.run()
+    eng.summarize()
+    assert eng.stats()["bad_docs"] == 0
+    hb = eng.download(0, n)
+    n_multi = 0
+    for d in range(n):
+        orc = OracleDoc(options(snapshot_v1=v1, chunk_size=chunk))
+        assert orc.apply(hb, d) == 0
+        want = orc.summarize(hb, d)
+        assert eng.summary(d) == want, f"doc {d}"
+        n_multi += len(want) > 1
+    if chunk < 1000:
+        assert n_multi > 0
+
+
 def test_bulk_summaries_equal_per_document_reads():
     from fluidframework_amd.engine import Engine, lib, pinned
     from fluidframework_amd.synth import make_cfg, tables
