@@ -845,6 +845,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
     }
 }
 
+typedef uint64_t u64_ua __attribute__((aligned(1)));
 // digest of one written blob (include/mtr_digest.h): one 8-byte word per lane per round
 MTR_DI uint64_t blob_digest(gptr<uint8_t> base, int64_t b0, int64_t blen) {
     if (g_sdbg & 8) return 0;
@@ -855,9 +856,13 @@ MTR_DI uint64_t blob_digest(gptr<uint8_t> base, int64_t b0, int64_t blen) {
         const int64_t j = j0 + ln;
         if (j < nw) {
             uint64_t wv = 0;
+            if (8 * j + 8 <= blen) {  // (one unaligned 8-byte load: the engine's code runs in unaligned access mode)
+                wv = *(gptr<const u64_ua>)(base + (b0 + 8 * j));
+            } else {
 #pragma unroll
-            for (int q = 0; q < 8; q++)
-                if (8 * j + q < blen) wv |= uint64_t(base[b0 + 8 * j + q]) << (8 * q);
+                for (int q = 0; q < 8; q++)
+                    if (8 * j + q < blen) wv |= uint64_t(base[b0 + 8 * j + q]) << (8 * q);
+            }
             sum += mtr_dg_word(wv, uint64_t(j));
         }
     }
