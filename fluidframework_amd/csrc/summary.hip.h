@@ -83,7 +83,14 @@ struct LW {
     }
     MTR_DI void bytes(gptr<const uint8_t> s, uint32_t k) {
         if (W)
-            for (uint32_t i = 0; i < k; i++) p[n + i] = s[i];
+            for (uint32_t i0 = 0; i0 < k; i0 += 8) {  // 8 loads in flight, then their stores
+                uint8_t b[8];
+#pragma unroll
+                for (uint32_t q = 0; q < 8; q++) b[q] = i0 + q < k ? s[i0 + q] : 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 8; q++)
+                    if (i0 + q < k) p[n + i0 + q] = b[q];
+            }
         n += k;
     }
     MTR_DI void num(int64_t v) {
@@ -894,6 +901,7 @@ MTR_DI void emit_unit(LW<true>& w, uint32_t p, uint32_t c, uint32_t n) {
 // D.slen by the wrapper pass) plus the bytes of the spec's earlier pieces -- the pieces' own counts (D.lb) less
 // the 2 / 6 bytes a surrogate pair split across two pieces saves at its high / low half
 MTR_DI void write_bodies(const SDoc& D, gptr<uint8_t> base) {
+    if (g_sdbg & 32) return;
     const int ln = lane_id();
     const int S = D.S;
     int cspec = -1;          // the spec of the last piece so far
@@ -955,9 +963,21 @@ MTR_DI void write_bodies(const SDoc& D, gptr<uint8_t> base) {
                 uint32_t bu[9];
 #pragma unroll
                 for (int q = 0; q < 9; q++) bu[q] = u0 + q < len ? uint32_t(D.gtext[t + uint32_t(u0 + q)]) : nextu;
+                bool plain = u0 + 8 <= len;  // eight plain ASCII units: one unaligned 8-byte store
+                uint64_t x = 0;
 #pragma unroll
-                for (int q = 0; q < 8; q++)
-                    if (u0 + q < len) emit_unit(w, q ? bu[q - 1] : p, bu[q], bu[q + 1]);
+                for (int q = 0; q < 8; q++) {
+                    plain = plain && bu[q] >= 0x20u && bu[q] < 0x80u && bu[q] != '"' && bu[q] != '\\';
+                    x |= uint64_t(bu[q] & 0xffu) << (8 * q);
+                }
+                if (plain) {
+                    *(gptr<u64_ua>)(w.p + w.n) = x;
+                    w.n += 8;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (u0 + q < len) emit_unit(w, q ? bu[q - 1] : p, bu[q], bu[q + 1]);
+                }
                 p = bu[7];
             }
         }
