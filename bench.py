@@ -107,7 +107,7 @@ def parse(argv=None):
                     help="N>1: documents of its own shard each rank checks against the oracle after the timed "
                          "region (default: about 4M messages' worth; one per host thread for C5)")
     ap.add_argument("--pipe-parts", type=int, default=16,
-                    help="end-to-end leg: document ranges of the pipelined hand-over (mtr_submit_pipelined)")
+                    help="end-to-end leg: document ranges of the pipelined hand-over (mtr_replay_pipelined)")
     ap.add_argument("--master-port", type=int, default=0, help="--gpus N launcher: rendezvous port (default: a free one)")
     ap.add_argument("--traffic-file", default=None,
                     help="PMC summary of this config (default: profiles/traffic_r06_final.json for C3, traffic_r06_c5.json "
