@@ -303,7 +303,8 @@ MTR_DI void w_props(LW<W>& w, const SDoc& D, const SParams& P, uint32_t pr) {
 }
 
 // (timing probes only, MTR_SUM_DEBUG: bit 0 / 1 skip the size / write pass's lane-serial text, bit 2 the wave's
-// long bodies, bit 3 the blob digests -- the summaries are then wrong)
+// long bodies, bit 3 the blob digests, bit 4 the write pass, bit 5 its bodies, bit 6 the size pass's per-leaf text
+// counts, bit 7 its per-spec pass -- the summaries are then wrong; bits 6 and 7 only with bit 4)
 __device__ int g_sdbg = 0;
 
 // the text of one leaf, 8 units per round of loads
@@ -618,7 +619,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
         {  // the leaf's text as a JSON string body of its own (unit_bytes: a surrogate pairs with its neighbour
             // inside the leaf; a pair split across two pieces of a spec is corrected in B), first and last unit.
             // Short leaves one lane each, 8 units per round of loads; longer ones by the whole wave.
-            const bool tl = kd != 0 && !mk && len > 0 && !D.perm;
+            const bool tl = kd != 0 && !mk && len > 0 && !D.perm && !(g_sdbg & 64);
             uint32_t lbv = 0, flv = 0;
             if (tl && len <= kLaneText) {
                 uint32_t prev = NOU;
@@ -738,7 +739,7 @@ MTR_DI void summary_size_doc(const SParams& P, uint32_t d) {
     wsync();
     // B. one lane per spec: length and JSON bytes -- a text body from its pieces' byte counts (A), less 8 bytes
     // for each surrogate pair split across two pieces (two escaped halves, 12 bytes, become one 4-byte character)
-    for (int g0 = 0; g0 < nspec; g0 += 64) {
+    for (int g0 = 0; g0 < nspec && !(g_sdbg & 128); g0 += 64) {
         const int g = g0 + ln;
         if (g < nspec) {
             const int s = int(D.start[g]), e = int(D.start[g + 1]);
