@@ -4,14 +4,17 @@
 // but the last flushed as usual (texts checked against resultText), the last applied, summarized and downloaded in
 // one call.  Prints each document's record (u32 blob count, u32 lengths, blobs) as base64 blobs, whether the
 // pipelined path ran, and the texts checked afterwards, for the Python test to compare with the CPU oracle.
-// usage: node replay_summaries.js <parts> <replay.json.gz> [...]
+// mode "local": document 0 also queues a pending local insert before the call, so the batch holds a record the
+// pipelined path refuses and the addon takes the serial calls (V1 summaries leave the unacked insert out).
+// usage: node replay_summaries.js <parts> <remote|local> <replay.json.gz> [...]
 const fs = require('fs');
 const zlib = require('zlib');
 const path = require('path');
 const m = require(path.join(__dirname, '..', '..', 'fluidframework_amd', 'node', 'index.js'));
 
 const parts = Number(process.argv[2]);
-const files = process.argv.slice(3);
+const mode = process.argv[3];
+const files = process.argv.slice(4);
 const all = files.map((f) => JSON.parse(zlib.gunzipSync(fs.readFileSync(f)).toString('utf8')));
 const engine = new m.BatchReplayEngine(files.length, { snapshotV1: 1, maxSegments: 8192, heapEntries: 8192,
     textUnits: 1 << 18, propWords: 1 << 18, removerCells: 1 << 14, opsPerLaunch: 64 });
@@ -26,9 +29,12 @@ let checks = 0;
 let rec = null;
 for (let gi = 0; gi < nGroups; gi++) {
     all.forEach((groups, d) => { if (gi < groups.length) for (const msg of groups[gi].msgs) clients[d].applyMsg(msg); });
-    if (gi === nGroups - 1) rec = engine.replaySummaries(parts);
+    if (gi === nGroups - 1) {
+        if (mode === 'local') clients[0].insertTextLocal(0, 'xyz');
+        rec = engine.replaySummaries(parts);
+    }
     all.forEach((groups, d) => {
-        if (gi >= groups.length) return;
+        if (gi >= groups.length || (mode === 'local' && d === 0 && gi === nGroups - 1)) return;
         if (clients[d].getText() !== groups[gi].resultText) throw new Error(`doc ${d} group ${gi}: text differs`);
         checks++;
     });
