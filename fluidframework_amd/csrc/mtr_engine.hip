@@ -1301,6 +1301,12 @@ static int run_impl(mtr_engine* e, int gen) {
 int64_t mtr_replay_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts, uint8_t* out, int64_t cap,
                              int64_t* doc_off) {
     const uint32_t n = b->n_docs;
+    // a range of fewer than ~3,000 documents keeps too few in flight while the ranges land (one document group, every
+    // round small): C2's 10,000 documents in 2 / 4 / 8 / 16 ranges measured 490 / 472 / 482 / 476 ms end to end
+    // against 464 ms for the serial calls, C3's 100,000 in 16 ranges 258 against 322 ms (profiles/r06_e2e_sweep.json)
+    const char* mpd = std::getenv("MTR_PIPE_MIN_PART_DOCS");
+    const uint32_t min_part_docs = mpd ? uint32_t(std::max(0, std::atoi(mpd))) : 3000u;
+    if (parts > 1 && n / parts < min_part_docs) parts = 1;  // (mtr_submit_pipelined: parts <= 1 is mtr_submit)
     e->pipe_one_group = true;
     int rc = mtr_submit_pipelined(e, b, parts);
     e->pipe_one_group = false;

@@ -76,7 +76,8 @@ int mtr_submit_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts);
  * the batch is then applied in full and mtr_summarize + mtr_get_summaries give its records.  The summaries stay
  * readable afterwards
  * (mtr_get_summary, mtr_get_summaries, mtr_hashes).  A batch the pipelined path does not take (see
- * mtr_submit_pipelined) runs the serial calls.  Replaces, for a summarizer, the applyMsg loop followed by
+ * mtr_submit_pipelined), or whose ranges would hold fewer than 3,000 documents each (MTR_PIPE_MIN_PART_DOCS), runs
+ * the serial calls.  Replaces, for a summarizer, the applyMsg loop followed by
  * summarizeCore (SURVEY 8d's end-to-end row). */
 int64_t mtr_replay_pipelined(mtr_engine* e, const mtr_batch* b, uint32_t parts, uint8_t* out, int64_t cap,
                              int64_t* doc_off);

@@ -283,12 +283,15 @@ def test_pipelined_submit_equals_serial_submit(n, parts):
 
 
 @pytest.mark.parametrize("n, parts", [(3000, 16), (5000, 7), (5000, 64)])
-def test_replay_pipelined_equals_serial_calls(n, parts):
+def test_replay_pipelined_equals_serial_calls(n, parts, monkeypatch):
     """mtr_replay_pipelined (a range summarized and downloaded once its documents are done, while the later ranges
     still upload and apply): byte for byte the records of mtr_submit + mtr_run + mtr_summarize + mtr_get_summaries,
-    the same hashes, the per-document reads still served afterwards; a buffer too small is refused."""
+    the same hashes, the per-document reads still served afterwards; a buffer too small is refused.  (Ranges of any
+    size: MTR_PIPE_MIN_PART_DOCS=0 -- by default ranges under 3,000 documents take the serial calls.)"""
     from fluidframework_amd.engine import EngineError, pinned
     from fluidframework_amd.synth import make_cfg, tables
+
+    monkeypatch.setenv("MTR_PIPE_MIN_PART_DOCS", "0")
 
     ops = 300
     cfg = make_cfg(n, ops, writers=8, max_lag=32, seed=0x7e11 + parts)
@@ -320,12 +323,18 @@ def test_replay_pipelined_equals_serial_calls(n, parts):
         eng.replay_pipelined(hb, pinned(want.size // 2, "u1"), parts)
 
 
-@pytest.mark.parametrize("n, parts", [(5, 16), (40, 1), (40, 3)])
-def test_replay_pipelined_small_batches_and_serial_fallback(n, parts):
+@pytest.mark.parametrize("n, parts, force", [(5, 16, True), (40, 1, True), (40, 3, True), (4000, 16, False)])
+def test_replay_pipelined_small_batches_and_serial_fallback(n, parts, force, monkeypatch):
     """mtr_replay_pipelined on batches the pipelined path splits into fewer ranges than asked (5 documents, 16 parts)
-    or does not split at all (parts = 1: the serial calls inside): the records of the serial calls."""
+    or does not split at all (parts = 1; or, by default, ranges under 3,000 documents: the serial calls inside): the
+    records of the serial calls."""
     from fluidframework_amd.engine import pinned
     from fluidframework_amd.synth import make_cfg, tables
+
+    if force:
+        monkeypatch.setenv("MTR_PIPE_MIN_PART_DOCS", "0")
+    else:
+        monkeypatch.delenv("MTR_PIPE_MIN_PART_DOCS", raising=False)
 
     ops = 200
     cfg = make_cfg(n, ops, writers=4, max_lag=16, seed=0x5a11 + n + parts)
@@ -346,11 +355,13 @@ def test_replay_pipelined_small_batches_and_serial_fallback(n, parts):
     assert np.array_equal(buf[:int(off[-1])], want)
 
 
-def test_replay_pipelined_refuses_records_beyond_remote_ops():
+def test_replay_pipelined_refuses_records_beyond_remote_ops(monkeypatch):
     """A range holding a record the pipelined path does not run: mtr_replay_pipelined fails with
     MTR_ERR_UNSUPPORTED's message, and after mtr_reset the serial calls apply the same batch in full."""
     from fluidframework_amd.engine import EngineError, pinned
     from fluidframework_amd.synth import make_cfg, tables, with_docs
+
+    monkeypatch.setenv("MTR_PIPE_MIN_PART_DOCS", "0")
 
     n, ops = 400, 200
     cfg = make_cfg(n, ops, writers=4, max_lag=16, seed=0xbeef)

@@ -158,11 +158,13 @@ def test_js_packer_matches_python_packer(pre):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("parts, mode", [(4, "remote"), (16, "remote"), (16, "local")])
-def test_replay_summaries_through_node_host(parts, mode):
+def test_replay_summaries_through_node_host(parts, mode, monkeypatch):
     """BatchReplayEngine.replaySummaries (mtr_replay_pipelined through the addon): the last group of every reference
     log applied, summarized and downloaded in one call on an engine holding the earlier groups; the records equal
     the oracle's blobs and the per-client summarize().  The remote-message batch takes the pipelined path; with a
-    pending local insert queued (a record the pipelined path refuses) the addon takes the serial calls."""
+    pending local insert queued (a record the pipelined path refuses) the addon takes the serial calls.  (30
+    documents: MTR_PIPE_MIN_PART_DOCS=0 keeps the engine from taking the serial calls for ranges this small.)"""
+    monkeypatch.setenv("MTR_PIPE_MIN_PART_DOCS", "0")
     paths = replay_files()
     _addon()
     res = json.loads(_node([os.path.join(HERE, "node", "replay_summaries.js"), str(parts), mode] + paths, timeout=300))
