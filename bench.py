@@ -110,12 +110,13 @@ def parse(argv=None):
                     help="end-to-end leg: document ranges of the pipelined hand-over (mtr_replay_pipelined)")
     ap.add_argument("--master-port", type=int, default=0, help="--gpus N launcher: rendezvous port (default: a free one)")
     ap.add_argument("--traffic-file", default=None,
-                    help="PMC summary of this config (default: profiles/traffic_r06_final.json for C3, traffic_r06_c5.json "
-                         "for C5, traffic_r06_c4.json for C4, traffic_r06_c2.json for C2, traffic_r01.json else)")
+                    help="PMC summary of this config (default: profiles/traffic_r06_final.json for C3, traffic_r06_c5_final.json "
+                         "for C5, traffic_r06_c4_final.json for C4, traffic_r06_c2_final.json for C2, traffic_r01.json "
+                         "else)")
     a = ap.parse_args(argv)
     if a.traffic_file is None:
-        name = {"C2": "traffic_r06_c2.json", "C3": "traffic_r06_final.json", "C4": "traffic_r06_c4.json",
-                "C5": "traffic_r06_c5.json"}.get(
+        name = {"C2": "traffic_r06_c2_final.json", "C3": "traffic_r06_final.json", "C4": "traffic_r06_c4_final.json",
+                "C5": "traffic_r06_c5_final.json"}.get(
             a.config, "traffic_r01.json")
         a.traffic_file = os.path.join(ROOT, "profiles", name)
     for k, v in PRESETS[a.config].items():
