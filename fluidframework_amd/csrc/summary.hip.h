@@ -60,6 +60,12 @@ struct SParams {
     unsigned long long* out_hash;
 };
 
+// (timing probes only, MTR_SUM_DEBUG: bit 0 / 1 skip the size / write pass's lane-serial text, bit 2 the wave's
+// long bodies, bit 3 the blob digests, bit 4 the write pass, bit 5 its bodies, bit 6 the size pass's per-leaf text
+// counts, bit 7 its per-spec pass, bit 8 the write pass's property sets -- the summaries are then wrong; bits 6 and 7
+// only with bit 4)
+__device__ int g_sdbg = 0;
+
 // ------------------------------------------------------------------ one lane's JSON writer
 template <bool W>
 struct LW {
@@ -285,6 +291,7 @@ MTR_DI void w_client(LW<W>& w, const SParams& P, const mtr_doc_desc& dd, uint32_
 
 template <bool W>
 MTR_DI void w_props(LW<W>& w, const SDoc& D, const SParams& P, uint32_t pr) {
+    if (W && (g_sdbg & 256)) return;  // (probe: the write pass's property sets; positions then drift)
     w.put('{');
     pr &= PN_MASK;  // (the index may carry MTR_PROPS_NEVER)
     const uint32_t n = D.gprop[pr];
@@ -302,10 +309,6 @@ MTR_DI void w_props(LW<W>& w, const SDoc& D, const SParams& P, uint32_t pr) {
     w.put('}');
 }
 
-// (timing probes only, MTR_SUM_DEBUG: bit 0 / 1 skip the size / write pass's lane-serial text, bit 2 the wave's
-// long bodies, bit 3 the blob digests, bit 4 the write pass, bit 5 its bodies, bit 6 the size pass's per-leaf text
-// counts, bit 7 its per-spec pass -- the summaries are then wrong; bits 6 and 7 only with bit 4)
-__device__ int g_sdbg = 0;
 
 // the text of one leaf, 8 units per round of loads
 template <bool W>
