@@ -1131,7 +1131,7 @@ MTR_DI void summary_write_doc(const SParams& P, uint32_t d) {
 #ifndef MTR_SWPE
 #define MTR_SWPE 8
 #endif
-__global__ void __launch_bounds__(64) summary_size_kernel(SParams P) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTR_SWPE))) summary_size_kernel(SParams P) {
     const uint32_t d = P.doc_base + blockIdx.x;
     if (d >= P.n_docs) return;
     summary_size_doc(P, d);
